@@ -1,0 +1,198 @@
+#!/usr/bin/env python3
+"""Benchmark of the SimplePathTracer render loop on MI355X.
+
+One step = one frame of BASELINE.json config 2 (GenerateSpheres seed 1,
+1200x800, 100 spp, depth 50): every (pixel, sample) path traced by the gfx950
+megakernel, folded in sample order, written as float RGBA + RGB8 g_data.
+With N GPUs (torchrun, one process per GPU) the frame is split into interleaved
+8-row strips, rank r renders strips r, r+N, ...; the float tiles are gathered to
+rank 0 over RCCL (all_gather_into_tensor) and assembled there (strong scaling:
+the frame is fixed, per-GPU work shrinks with N).
+
+Prints ONE JSON line on rank 0 (see DESIGN.md §Measurement for every field).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+CONFIGS = {
+    # name: (scene, width, height, spp, bounces)
+    "c2": ("random", 1200, 800, 100, 50),
+    "c3": ("random", 3840, 2160, 1024, 50),
+    "c5": ("stress10k", 1920, 1080, 256, 50),
+    "c1": ("cornell3", 200, 100, 4, 8),
+}
+VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12  # 78.64 T fp32 lane-ops/s (non-FMA)
+HBM_PEAK_GBS = 8000.0
+FLOP_PER_TEST = 17  # RaySphereIntersection, Collision.hpp:9-17
+
+
+def make_scene(spt, name):
+    if name == "random":
+        return spt.generate_spheres(1)
+    if name == "stress10k":
+        return spt.generate_stress(1, 10000)
+    if name == "cornell3":
+        return spt.cornell3()
+    raise ValueError(name)
+
+
+def cpu_baseline(scene, view, w, h, spp_sample, bounces, threads):
+    """The CPU restatement (oracle/, "port") timed with the reference's
+    RenderImageParallelMain tiling (threads x threads tiles, <= threads in
+    flight) on RenderSegmentTask, the TaskBasedPathTracer path of north_star."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle
+    pyoracle.build()
+    osc = pyoracle.OracleScene(scene.centers, scene.radii, scene.colors, scene.materials, scene.fuzz)
+    fr = pyoracle.make_frame(view, [0, 1, -3, 0], [137, 207, 240, 0], w, h, spp_sample, bounces, 1)
+    t0 = time.perf_counter()
+    pyoracle.render_image_parallel(osc, fr, threads, mode=1, want_rgba=False)
+    dt = time.perf_counter() - t0
+    return {"value": round(w * h * spp_sample / dt / 1e6, 4), "unit": "Msamples/s", "cores": threads,
+            "kind": "port",
+            "sample": f"RenderSegmentTask (oracle C restatement, gcc -O2) via RenderImageParallelMain tiling "
+                      f"{threads}x{threads}, same scene/camera at {w}x{h}, {spp_sample} spp, depth {bounces}; "
+                      f"{dt:.2f} s wall on {threads} threads"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--mode", default="segment", choices=["segment", "task"])
+    ap.add_argument("--strip", type=int, default=8)
+    ap.add_argument("--cpu-spp", type=int, default=8, help="spp of the bounded CPU-baseline sample")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    import simplepathtracer_amd as spt
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world and world > 1:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    scene_name, W, H, spp, bounces = CONFIGS[args.config]
+    scene = make_scene(spt, scene_name)
+    view = spt.camera_basis()
+    mode = spt.MODE_TASK if args.mode == "task" else spt.MODE_SEGMENT
+    ctx = spt.Context(local)
+    ctx.set_scene(scene)
+    ctx.set_camera(view, spt.scene.DEFAULT_EYE, spt.INIT_COLOR)
+    ctx.set_params(W, H, spp, bounces, 1)
+
+    strip = args.strip
+    rows = [spt.rows_count(0, H, strip, world, p) for p in range(world)]
+    max_rows = max(rows)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    frame = torch.zeros((H * W, 4), dtype=torch.float32, device=dev) if rank == 0 else None
+    g_data = torch.zeros(W * H * 3, dtype=torch.uint8, device=dev) if rank == 0 else None
+    if world > 1:
+        local_tile = torch.zeros((max_rows * W, 4), dtype=torch.float32, device=dev)
+        gathered = torch.zeros((world, max_rows * W, 4), dtype=torch.float32, device=dev)
+
+    def step():
+        if world == 1:
+            ctx.render_rows_async(mode, 0, H, 1, 1, 0, 0, W, frame.data_ptr(), g_data.data_ptr(), stream)
+        else:
+            ctx.render_rows_async(mode, 0, H, strip, world, rank, 0, W, local_tile.data_ptr(), 0, stream)
+            dist.all_gather_into_tensor(gathered, local_tile)
+            if rank == 0:
+                ctx.assemble_rows_async(gathered.data_ptr(), max_rows, 0, H, strip, world, 0, W, frame.data_ptr(),
+                                        g_data.data_ptr(), stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    ctx.reset_stats()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    st = ctx.stats()
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        tot = torch.tensor([st["casts"], st["samples"]], dtype=torch.float64, device=dev)
+        dist.all_reduce(tot)
+        casts_all, samples_all = float(tot[0]), float(tot[1])
+    else:
+        casts_all, samples_all = float(st["casts"]), float(st["samples"])
+
+    total_samples = W * H * spp * args.steps
+    value = total_samples / elapsed / 1e6
+    if rank == 0:
+        # dominant kernel = render_kernel; per-launch averages from HIP events on `stream`
+        launches = max(st["launches"], 1)
+        avg_ms = st["render_ms"] / launches
+        rays_per_launch = st["casts"] / launches
+        algo_tflop = FLOP_PER_TEST * scene.n * rays_per_launch / 1e12
+        achieved = algo_tflop / (avg_ms / 1e3)
+        samples_per_launch = st["samples"] / launches
+        hbm_bytes = 16.0 * samples_per_launch  # per-sample colour slot written by the render kernel
+        out = {
+            "metric": "Msamples/s (pixels×spp/s), RTIOW random-sphere scene, 1/2/4/8 MI355X",
+            "value": round(value, 3),
+            "unit": "Msamples/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic",
+            "config": {"workload": f"{args.config}: {scene_name} scene seed 1 (N={scene.n} spheres), {W}x{H}, "
+                                   f"{spp} spp, depth {bounces}, {args.mode} mode",
+                       "width": W, "height": H, "spp": spp, "bounces": bounces, "spheres": scene.n,
+                       "parallelism": f"row-strips{strip}x{world}" if world > 1 else "1 GPU"},
+            "roofline": {"bound": "valu", "achieved": round(achieved, 3), "peak": round(VALU_PEAK_TOPS, 2),
+                         "unit": "TFLOP/s", "frac": round(achieved / VALU_PEAK_TOPS, 4), "traffic": None,
+                         "kernel": "render_kernel", "avg_launch_ms": round(avg_ms, 4),
+                         "rays_per_launch": rays_per_launch,
+                         "flop_per_launch": FLOP_PER_TEST * scene.n * rays_per_launch},
+            "roofline_hbm": {"bound": "hbm", "achieved": round(hbm_bytes / (avg_ms / 1e3) / 1e9, 3),
+                             "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                             "frac": round(hbm_bytes / (avg_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 6)},
+            "rays_per_sample": round(casts_all / max(samples_all, 1), 4),
+            "fold_ms_per_step": round(st["fold_ms"] / args.steps, 4),
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            cw, ch = (W, H) if args.config != "c3" else (1920, 1080)
+            out["cpu_baseline"] = cpu_baseline(scene, view, cw, ch, args.cpu_spp, bounces, args.cpu_threads)
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

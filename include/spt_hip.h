@@ -1,0 +1,165 @@
+/*
+ * spt_hip.h -- C ABI of the MI355X (gfx950) render loop of SimplePathTracer.
+ *
+ * This is the drop-in boundary.  The reference's hot path is reached through
+ * two void free functions that read mutable globals and write bytes into the
+ * caller-owned framebuffer g_data:
+ *
+ *   void RenderSegment(RenderSegmentData)       SingleThreadPathTracer.hpp:114-137
+ *   void RenderSegmentTask(RenderSegmentData)   TaskBasedPathTracer.hpp:54-206
+ *
+ * called from RenderJob (Renderer.hpp:242-255) on up to threadCount concurrent
+ * threads and from RenderImage (Renderer.hpp:304-308).  Their implicit inputs
+ * are the globals of Globals.hpp:8-37 (scene SoA, viewMatrix, eyePos,
+ * initColor, g_width/g_height/g_samples/g_bounces).  The functions below make
+ * each of those inputs explicit; include/spt/RenderSegmentShim.hpp rebuilds the
+ * two reference entry points on top of them so Renderer.hpp / Main.cpp and the
+ * GL preview keep compiling unchanged.
+ *
+ * Plain C types only.  Every function returns an spt_status; on failure
+ * spt_last_error() describes why.  A context is safe to use from several host
+ * threads (calls are serialised per context).
+ */
+#ifndef SPT_HIP_H
+#define SPT_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SPT_ABI_VERSION 1
+
+typedef enum spt_status {
+    SPT_OK = 0,
+    SPT_ERR_ARG = 1,      /* invalid argument (null pointer, bad range, ...) */
+    SPT_ERR_STATE = 2,    /* scene / camera / params not set */
+    SPT_ERR_HIP = 3,      /* HIP runtime error */
+    SPT_ERR_NOMEM = 4,    /* allocation failed */
+    SPT_ERR_NODEVICE = 5  /* no gfx950 device / bad ordinal */
+} spt_status;
+
+/* Material ids, Definitions.hpp:7-13 (enum class Material : uint8_t). */
+enum { SPT_SKYBOX = 0, SPT_REFLECTIVE = 1, SPT_REFRACTIVE = 2, SPT_DIFFUSE = 3 };
+
+/* Render modes: which reference entry point's semantics a launch follows. */
+enum {
+    SPT_MODE_SEGMENT = 0,  /* RenderSegment: every sample counts, acc *= 1/spp  */
+    SPT_MODE_TASK = 1      /* RenderSegmentTask: paths needing > 10 passes are
+                              dropped (TaskBasedPathTracer.hpp:81) and the pixel
+                              is averaged over the samples that finished (196-205) */
+};
+
+typedef struct spt_ctx spt_ctx;
+
+typedef struct spt_stats {
+    uint64_t samples;      /* (pixel, sample) paths completed */
+    uint64_t casts;        /* FindClosestIntersectionSphere calls (rays) */
+    uint64_t dropped;      /* task mode: samples dropped by the pass cap */
+    uint64_t launches;     /* render-kernel launches */
+    double render_ms;      /* summed device time of render-kernel launches */
+    double fold_ms;        /* summed device time of resolve (fold) launches */
+    double last_render_ms; /* device time of the most recent render launch */
+    uint32_t grid_blocks;  /* persistent grid of the render kernel */
+    uint32_t block_threads;
+} spt_stats;
+
+int spt_abi_version(void);
+/* Number of visible HIP devices. */
+int spt_device_count(int *count);
+
+/* Context on one device.  Replaces nothing in the reference (its state is global);
+ * it owns the device copies of Globals.hpp's scene/camera and a workspace. */
+int spt_ctx_create(int device, spt_ctx **out);
+void spt_ctx_destroy(spt_ctx *ctx);
+/* Last error of ctx, or of the calling thread when ctx is NULL. Never NULL. */
+const char *spt_last_error(const spt_ctx *ctx);
+
+/* Scene SoA, Globals.hpp:31-37: g_spheres (float4 per sphere, w ignored),
+ * g_radii, g_colors (float4, w ignored), g_materials, g_diffuses (fuzz),
+ * g_sphereNumber.  Data is copied.  The reference's uint8_t sphere index
+ * (Collision.hpp:87-92) limits it to n <= 255; this build uses a 32-bit index,
+ * identical for n <= 255, and accepts larger scenes as an extension. */
+int spt_set_scene(spt_ctx *ctx, const float *centers4, const float *radii, const float *colors4,
+                  const uint8_t *materials, const float *fuzz, uint32_t n);
+/* viewMatrix (row-major, already transposed, Renderer.hpp:321; its fourth row
+ * must be zero as CreateCameraBasisMatrix makes it), eyePos and initColor
+ * (Globals.hpp:21-29).  w lanes of eye/sky are ignored (0 in the reference). */
+int spt_set_camera(spt_ctx *ctx, const float view[16], const float eye[4], const float sky[4]);
+/* g_width, g_height, g_samples, g_bounces (Globals.hpp:12-15) + RNG seed.
+ * bounces == 0 is rejected: `while (--bounceCount && ...)` would never count
+ * down (SingleThreadPathTracer.hpp:28). */
+int spt_set_params(spt_ctx *ctx, uint32_t width, uint32_t height, uint32_t spp, uint32_t bounces, uint64_t seed);
+/* Upper bound of the per-sample workspace (default 4 GiB).  Larger frames are
+ * rendered in sample batches folded in order. */
+int spt_set_workspace(spt_ctx *ctx, uint64_t bytes);
+
+/* ---- drop-in entry points (host memory, blocking) ----------------------------
+ * Render pixels [yBegin,yEnd) x [xBegin,xEnd).
+ * rgba_out (nullable): region-local row-major float4 per pixel = the reference's
+ *   pixelColor after `*= 1/g_samples` (the value WritePixel receives).
+ * g_data (nullable): full-frame width*height*3 bytes; the region's pixels are
+ *   written at g_size - ((g_width - x)*3 + y*g_width*3) exactly as
+ *   io::WritePixel does (IOHelpers.hpp:17-22), other bytes untouched. */
+int spt_render_segment(spt_ctx *ctx, uint32_t yBegin, uint32_t yEnd, uint32_t xBegin, uint32_t xEnd,
+                       float *rgba_out, uint8_t *g_data);
+int spt_render_segment_task(spt_ctx *ctx, uint32_t yBegin, uint32_t yEnd, uint32_t xBegin, uint32_t xEnd,
+                            float *rgba_out, uint8_t *g_data);
+
+/* ---- device-resident entry point (asynchronous) -------------------------------
+ * Rows y in [yBegin,yEnd) with ((y - yBegin) / strip) % parts == part, columns
+ * [xBegin,xEnd) -- the interleaved row-strip tiling used to split a frame over
+ * GPUs (parts = world size, part = rank; parts = 1 for a plain rectangle).
+ * d_rgba (nullable): device float4 per local pixel, local order (row k of the
+ *   owned rows, then x).  d_rgb8 (nullable): device full frame in g_data layout.
+ * stream: a hipStream_t (NULL = the context's own stream).  Returns after
+ * enqueueing; pair with spt_synchronize or the caller's stream sync. */
+int spt_render_rows_async(spt_ctx *ctx, int mode, uint32_t yBegin, uint32_t yEnd, uint32_t strip, uint32_t parts,
+                          uint32_t part, uint32_t xBegin, uint32_t xEnd, void *d_rgba, void *d_rgb8, void *stream);
+/* Number of rows the (yBegin, yEnd, strip, parts, part) map owns. */
+int spt_rows_count(uint32_t yBegin, uint32_t yEnd, uint32_t strip, uint32_t parts, uint32_t part, uint32_t *rows);
+/* Scatter a gathered, rank-major stack of local float4 tiles (parts tiles of
+ * max_rows*(xEnd-xBegin) pixels each, on device) into a full-frame float4
+ * buffer and/or a g_data RGB8 frame.  Used by rank 0 after the RCCL gather. */
+int spt_assemble_rows_async(spt_ctx *ctx, const void *d_tiles, uint32_t max_rows, uint32_t yBegin, uint32_t yEnd,
+                            uint32_t strip, uint32_t parts, uint32_t xBegin, uint32_t xEnd, void *d_frame_rgba,
+                            void *d_rgb8, void *stream);
+int spt_synchronize(spt_ctx *ctx);
+
+/* Per-(pixel, sample) colors of a rectangle, host memory: out[(p*spp + s)*4 + c]
+ * with p the region-local pixel.  w = 1 if the sample counts, 0 if dropped
+ * (task mode).  Debug/parity aid; same kernel as the render path. */
+int spt_render_samples(spt_ctx *ctx, int mode, uint32_t yBegin, uint32_t yEnd, uint32_t xBegin, uint32_t xEnd,
+                       float *out);
+
+int spt_get_stats(spt_ctx *ctx, spt_stats *out);
+int spt_reset_stats(spt_ctx *ctx);
+
+/* ---- input producers (SceneGenerators.hpp, Math.hpp) -------------------------
+ * GenerateSpheres (SceneGenerators.hpp:6-66) and InitSpheres (68-133) driven by
+ * splitmix(seed) (Random.hpp:19) instead of the clock; capacity in spheres. */
+int spt_scene_generate_random(uint32_t seed, uint32_t capacity, float *centers4, float *radii, float *colors4,
+                              uint8_t *materials, float *fuzz, uint32_t *n_out);
+int spt_scene_init_reference(uint32_t seed, float *centers4, float *radii, float *colors4, uint8_t *materials,
+                             float *fuzz, uint32_t *n_out);
+/* Stress scene for the >255-sphere extension (BASELINE config 5): the four big
+ * spheres of GenerateSpheres plus n-4 small spheres on a jittered grid. */
+int spt_scene_generate_stress(uint32_t seed, uint32_t n, float *centers4, float *radii, float *colors4,
+                              uint8_t *materials, float *fuzz);
+/* Transpose(CreateCameraBasisMatrix(eye, lookAt, up)), Math.hpp:198-231. */
+int spt_camera_basis(const float eye[4], const float look_at[4], const float up[4], float view_out[16]);
+
+/* ---- numerics self-test ------------------------------------------------------
+ * Runs the device primitives the render path relies on over n inputs and
+ * writes SPT_SELFTEST_COLS floats per input: a/b, sqrtf(a),
+ * float(sqrt(double(a))), float(pow5(double(a))), uniform draw, u8 of a. */
+#define SPT_SELFTEST_COLS 8
+int spt_selftest_numerics(spt_ctx *ctx, const float *a, const float *b, const uint32_t *bits, uint32_t n,
+                          float *out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

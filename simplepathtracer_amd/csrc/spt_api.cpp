@@ -1,0 +1,587 @@
+// spt_api.cpp -- C ABI (include/spt_hip.h) over the gfx950 render kernels.
+//
+// Owns the device copy of the reference's global state (scene SoA, camera,
+// config: Globals.hpp:8-37), the per-sample workspace and the launch geometry
+// of the persistent render kernel, and rebuilds the two reference entry points
+// RenderSegment (SingleThreadPathTracer.hpp:114-137) and RenderSegmentTask
+// (TaskBasedPathTracer.hpp:54-206) as render + fold launches.
+#include "spt_hip.h"
+#include "spt_internal.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <utility>
+#include <vector>
+
+namespace {
+
+thread_local std::string g_thread_error;
+
+struct EventPair {
+    hipEvent_t a = nullptr, b = nullptr;
+};
+
+}  // namespace
+
+struct spt_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::mutex mu;
+    std::string err;
+    int num_cu = 0;
+    uint32_t grid = 0, block = spt::kRenderBlock, claim = 128;
+
+    // scene (Globals.hpp:31-37)
+    float4 *d_hit = nullptr, *d_shade = nullptr;
+    uint32_t *d_mat = nullptr;
+    uint32_t n = 0, scene_cap = 0;
+    bool scene_set = false;
+    // camera (Globals.hpp:21-29)
+    spt::Camera cam{};
+    bool cam_set = false;
+    // config (Globals.hpp:12-15)
+    uint32_t W = 0, H = 0, spp = 0, bounces = 0;
+    uint64_t seed = 0;
+    bool params_set = false;
+
+    // workspace
+    uint64_t ws_bytes = 4ull << 30;
+    float4 *d_samples = nullptr;
+    size_t samples_cap = 0;
+    float4 *d_acc = nullptr;
+    size_t acc_cap = 0;
+    uint32_t *d_head = nullptr;
+    unsigned long long *d_counters = nullptr;
+    float4 *d_stage = nullptr;
+    size_t stage_cap = 0;
+    uint8_t *d_frame8 = nullptr;
+    size_t frame8_cap = 0;
+
+    // timing
+    std::vector<EventPair> pending_render, pending_fold, pool;
+    double render_ms = 0, fold_ms = 0, last_render_ms = 0;
+    uint64_t launches = 0;
+};
+
+namespace {
+
+int fail(spt_ctx *ctx, int code, const char *fmt, ...)
+{
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    if (ctx) ctx->err = buf;
+    g_thread_error = buf;
+    return code;
+}
+
+#define HIP_TRY(ctx, expr)                                                                          \
+    do {                                                                                            \
+        hipError_t e_ = (expr);                                                                     \
+        if (e_ != hipSuccess)                                                                       \
+            return fail((ctx), SPT_ERR_HIP, "%s failed: %s", #expr, hipGetErrorString(e_));        \
+    } while (0)
+
+template <class T>
+int ensure(spt_ctx *ctx, T **p, size_t *cap, size_t count)
+{
+    if (*cap >= count && *p) return SPT_OK;
+    if (*p) {
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        HIP_TRY(ctx, hipFree(*p));
+        *p = nullptr;
+        *cap = 0;
+    }
+    size_t want = std::max<size_t>(count, 1);
+    hipError_t e = hipMalloc((void **)p, want * sizeof(T));
+    if (e != hipSuccess) {
+        *p = nullptr;
+        return fail(ctx, SPT_ERR_NOMEM, "hipMalloc(%zu bytes) failed: %s", want * sizeof(T), hipGetErrorString(e));
+    }
+    *cap = want;
+    return SPT_OK;
+}
+
+EventPair get_pair(spt_ctx *ctx)
+{
+    if (!ctx->pool.empty()) {
+        EventPair p = ctx->pool.back();
+        ctx->pool.pop_back();
+        return p;
+    }
+    EventPair p;
+    (void)hipEventCreate(&p.a);
+    (void)hipEventCreate(&p.b);
+    return p;
+}
+
+// Harvest finished launch timings (blocking on their stop events).
+int collect_timings(spt_ctx *ctx)
+{
+    for (auto *vec : {&ctx->pending_render, &ctx->pending_fold}) {
+        for (EventPair &p : *vec) {
+            HIP_TRY(ctx, hipEventSynchronize(p.b));
+            float ms = 0.f;
+            HIP_TRY(ctx, hipEventElapsedTime(&ms, p.a, p.b));
+            if (vec == &ctx->pending_render) {
+                ctx->render_ms += ms;
+                ctx->last_render_ms = ms;
+            } else {
+                ctx->fold_ms += ms;
+            }
+            ctx->pool.push_back(p);
+        }
+        vec->clear();
+    }
+    return SPT_OK;
+}
+
+int check_ready(spt_ctx *ctx)
+{
+    if (!ctx->scene_set) return fail(ctx, SPT_ERR_STATE, "scene not set (spt_set_scene)");
+    if (!ctx->cam_set) return fail(ctx, SPT_ERR_STATE, "camera not set (spt_set_camera)");
+    if (!ctx->params_set) return fail(ctx, SPT_ERR_STATE, "params not set (spt_set_params)");
+    return SPT_OK;
+}
+
+uint64_t fmix64(uint64_t z)
+{
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+// Render the rows of `map` and fold them into d_rgba (local pixel order) and/or
+// d_rgb8 (full frame).  keep_samples: leave the per-sample colours of a single
+// batch in d_samples (debug path).
+int render_impl(spt_ctx *ctx, int mode, const spt::RowMap &map, float4 *d_rgba, uint8_t *d_rgb8, hipStream_t s,
+                bool keep_samples)
+{
+    const uint32_t rows = spt::rows_owned(map);
+    const uint64_t npix64 = (uint64_t)rows * map.width;
+    if (npix64 == 0) return SPT_OK;
+    if (npix64 > 0x7FFFFFFFull) return fail(ctx, SPT_ERR_ARG, "region too large (%llu pixels)", (unsigned long long)npix64);
+    const uint32_t npix = (uint32_t)npix64;
+    uint64_t budget = std::max<uint64_t>(ctx->ws_bytes / sizeof(float4), 1);
+    budget = std::min<uint64_t>(budget, 0x7FFFFFFFull);
+    uint64_t per = std::max<uint64_t>(1, budget / npix);
+    const uint32_t spp_batch = (uint32_t)std::min<uint64_t>(ctx->spp, per);
+    if (keep_samples && spp_batch != ctx->spp)
+        return fail(ctx, SPT_ERR_ARG, "region * spp exceeds the workspace for spt_render_samples");
+    const uint64_t items_max = (uint64_t)npix * spp_batch;
+    int rc = ensure(ctx, &ctx->d_samples, &ctx->samples_cap, items_max);
+    if (rc) return rc;
+    if (spp_batch < ctx->spp) {
+        rc = ensure(ctx, &ctx->d_acc, &ctx->acc_cap, npix);
+        if (rc) return rc;
+    }
+
+    spt::RenderArgs ra{};
+    ra.scene = spt::DeviceScene{ctx->d_hit, ctx->d_shade, ctx->d_mat, ctx->n};
+    ra.cam = ctx->cam;
+    ra.width = ctx->W;
+    ra.height = ctx->H;
+    ra.bounces = ctx->bounces;
+    ra.mode = (uint32_t)mode;
+    ra.seed_key = fmix64(ctx->seed);
+    ra.map = map;
+    ra.npix = npix;
+    ra.claim = ctx->claim;
+    ra.samples = ctx->d_samples;
+    ra.head = ctx->d_head;
+    ra.counters = ctx->d_counters;
+
+    spt::FoldArgs fa{};
+    fa.samples = ctx->d_samples;
+    fa.acc = ctx->d_acc;
+    fa.out_rgba = d_rgba;
+    fa.out_rgb8 = d_rgb8;
+    fa.map = map;
+    fa.width = ctx->W;
+    fa.height = ctx->H;
+    fa.npix = npix;
+    fa.spp_total = ctx->spp;
+    fa.mode = mode;
+
+    for (uint32_t s0 = 0; s0 < ctx->spp; s0 += spp_batch) {
+        const uint32_t b = std::min(spp_batch, ctx->spp - s0);
+        ra.spp_batch = b;
+        ra.s0 = s0;
+        ra.n_items = npix * b;
+        HIP_TRY(ctx, hipMemsetAsync(ctx->d_head, 0, sizeof(uint32_t), s));
+        EventPair ev = get_pair(ctx);
+        HIP_TRY(ctx, hipEventRecord(ev.a, s));
+        HIP_TRY(ctx, spt::launch_render(ra, ctx->grid, ctx->block, s));
+        HIP_TRY(ctx, hipEventRecord(ev.b, s));
+        ctx->pending_render.push_back(ev);
+        ctx->launches++;
+        if (keep_samples) continue;
+        fa.spp_batch = b;
+        fa.first = s0 == 0;
+        fa.last = s0 + b >= ctx->spp;
+        EventPair ef = get_pair(ctx);
+        HIP_TRY(ctx, hipEventRecord(ef.a, s));
+        HIP_TRY(ctx, spt::launch_fold(fa, s));
+        HIP_TRY(ctx, hipEventRecord(ef.b, s));
+        ctx->pending_fold.push_back(ef);
+    }
+    if (ctx->pending_render.size() > 256) return collect_timings(ctx);
+    return SPT_OK;
+}
+
+int check_region(spt_ctx *ctx, uint32_t yB, uint32_t yE, uint32_t xB, uint32_t xE)
+{
+    if (yE > ctx->H || xE > ctx->W)
+        return fail(ctx, SPT_ERR_ARG, "region [%u,%u)x[%u,%u) outside %ux%u frame", yB, yE, xB, xE, ctx->W, ctx->H);
+    return SPT_OK;
+}
+
+// RenderSegment / RenderSegmentTask with host outputs.
+int render_segment_host(spt_ctx *ctx, int mode, uint32_t yB, uint32_t yE, uint32_t xB, uint32_t xE, float *rgba,
+                        uint8_t *g_data)
+{
+    if (!ctx) return fail(nullptr, SPT_ERR_ARG, "null context");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    int rc = check_ready(ctx);
+    if (rc) return rc;
+    if ((rc = check_region(ctx, yB, yE, xB, xE))) return rc;
+    if (yB >= yE || xB >= xE) return SPT_OK;  // the reference's loops do nothing
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    const uint32_t w = xE - xB, h = yE - yB;
+    const size_t npix = (size_t)w * h;
+    if ((rc = ensure(ctx, &ctx->d_stage, &ctx->stage_cap, npix))) return rc;
+    uint8_t *d8 = nullptr;
+    if (g_data) {
+        if ((rc = ensure(ctx, &ctx->d_frame8, &ctx->frame8_cap, (size_t)ctx->W * ctx->H * 3))) return rc;
+        d8 = ctx->d_frame8;
+    }
+    spt::RowMap map{yB, yE, 1u, 1u, 0u, xB, w};
+    if ((rc = render_impl(ctx, mode, map, ctx->d_stage, d8, ctx->stream, false))) return rc;
+    if (rgba) HIP_TRY(ctx, hipMemcpyAsync(rgba, ctx->d_stage, npix * sizeof(float4), hipMemcpyDeviceToHost, ctx->stream));
+    if (g_data) {
+        // rows y in [yB, yE) live at g_data rows H-1-y: one contiguous band, xB.. per row
+        const size_t pitch = (size_t)ctx->W * 3;
+        const size_t off = (size_t)(ctx->H - yE) * pitch + (size_t)xB * 3;
+        HIP_TRY(ctx, hipMemcpy2DAsync(g_data + off, pitch, ctx->d_frame8 + off, pitch, (size_t)w * 3, h,
+                                      hipMemcpyDeviceToHost, ctx->stream));
+    }
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return collect_timings(ctx);
+}
+
+}  // namespace
+
+extern "C" {
+
+int spt_abi_version(void) { return SPT_ABI_VERSION; }
+
+int spt_device_count(int *count)
+{
+    if (!count) return fail(nullptr, SPT_ERR_ARG, "null count");
+    int c = 0;
+    hipError_t e = hipGetDeviceCount(&c);
+    if (e != hipSuccess) c = 0;
+    *count = c;
+    return SPT_OK;
+}
+
+int spt_ctx_create(int device, spt_ctx **out)
+{
+    if (!out) return fail(nullptr, SPT_ERR_ARG, "null out");
+    *out = nullptr;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count == 0)
+        return fail(nullptr, SPT_ERR_NODEVICE, "no HIP device visible");
+    if (device < 0 || device >= count) return fail(nullptr, SPT_ERR_NODEVICE, "device %d out of range (%d)", device, count);
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess)
+        return fail(nullptr, SPT_ERR_NODEVICE, "hipGetDeviceProperties(%d) failed", device);
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return fail(nullptr, SPT_ERR_NODEVICE, "device %d is %s, this build targets gfx950", device, prop.gcnArchName);
+    spt_ctx *ctx = new spt_ctx();
+    ctx->device = device;
+    ctx->num_cu = prop.multiProcessorCount;
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete ctx;
+        return fail(nullptr, SPT_ERR_HIP, "stream creation failed on device %d", device);
+    }
+    int per_cu = 0;
+    if (spt::render_occupancy(ctx->block, &per_cu) != hipSuccess || per_cu <= 0) per_cu = 1;
+    // launch_bounds / occupancy API may over-report by one block per CU for SGPR-heavy
+    // kernels (MI355X_MICROARCH.md, Residency): the kernel needs no co-residency, so
+    // extra blocks only queue.  SPT_BLOCKS_PER_CU overrides for tuning.
+    if (const char *e = std::getenv("SPT_BLOCKS_PER_CU")) per_cu = std::max(1, std::atoi(e));
+    if (const char *e = std::getenv("SPT_CLAIM")) ctx->claim = (uint32_t)std::max(1, std::atoi(e));
+    ctx->grid = (uint32_t)(per_cu * ctx->num_cu);
+    if (hipMalloc((void **)&ctx->d_head, sizeof(uint32_t)) != hipSuccess ||
+        hipMalloc((void **)&ctx->d_counters, 4 * sizeof(unsigned long long)) != hipSuccess ||
+        hipMemset(ctx->d_counters, 0, 4 * sizeof(unsigned long long)) != hipSuccess) {
+        spt_ctx_destroy(ctx);
+        return fail(nullptr, SPT_ERR_NOMEM, "workspace allocation failed");
+    }
+    *out = ctx;
+    return SPT_OK;
+}
+
+void spt_ctx_destroy(spt_ctx *ctx)
+{
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    for (auto *vec : {&ctx->pending_render, &ctx->pending_fold, &ctx->pool})
+        for (EventPair &p : *vec) {
+            (void)hipEventDestroy(p.a);
+            (void)hipEventDestroy(p.b);
+        }
+    void *bufs[] = {ctx->d_hit, ctx->d_shade, ctx->d_mat, ctx->d_samples, ctx->d_acc,
+                    ctx->d_head, ctx->d_counters, ctx->d_stage, ctx->d_frame8};
+    for (void *b : bufs)
+        if (b) (void)hipFree(b);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+const char *spt_last_error(const spt_ctx *ctx)
+{
+    if (ctx) return ctx->err.c_str();
+    return g_thread_error.c_str();
+}
+
+int spt_set_scene(spt_ctx *ctx, const float *centers4, const float *radii, const float *colors4,
+                  const uint8_t *materials, const float *fuzz, uint32_t n)
+{
+    if (!ctx) return fail(nullptr, SPT_ERR_ARG, "null context");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    if (n > 0 && (!centers4 || !radii || !colors4 || !materials || !fuzz))
+        return fail(ctx, SPT_ERR_ARG, "null scene array");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    std::vector<float4> hit(n), shade(n);
+    std::vector<uint32_t> mat(n);
+    for (uint32_t i = 0; i < n; ++i) {
+        const float r = radii[i];
+        hit[i] = make_float4(centers4[4 * i], centers4[4 * i + 1], centers4[4 * i + 2], r * r);
+        shade[i] = make_float4(colors4[4 * i], colors4[4 * i + 1], colors4[4 * i + 2], fuzz[i]);
+        mat[i] = materials[i];
+    }
+    if (n > ctx->scene_cap) {
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        for (void *b : {(void *)ctx->d_hit, (void *)ctx->d_shade, (void *)ctx->d_mat})
+            if (b) HIP_TRY(ctx, hipFree(b));
+        ctx->d_hit = ctx->d_shade = nullptr;
+        ctx->d_mat = nullptr;
+        ctx->scene_cap = 0;
+        HIP_TRY(ctx, hipMalloc((void **)&ctx->d_hit, n * sizeof(float4)));
+        HIP_TRY(ctx, hipMalloc((void **)&ctx->d_shade, n * sizeof(float4)));
+        HIP_TRY(ctx, hipMalloc((void **)&ctx->d_mat, n * sizeof(uint32_t)));
+        ctx->scene_cap = n;
+    }
+    if (n) {
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        HIP_TRY(ctx, hipMemcpy(ctx->d_hit, hit.data(), n * sizeof(float4), hipMemcpyHostToDevice));
+        HIP_TRY(ctx, hipMemcpy(ctx->d_shade, shade.data(), n * sizeof(float4), hipMemcpyHostToDevice));
+        HIP_TRY(ctx, hipMemcpy(ctx->d_mat, mat.data(), n * sizeof(uint32_t), hipMemcpyHostToDevice));
+    }
+    ctx->n = n;
+    ctx->scene_set = true;
+    return SPT_OK;
+}
+
+int spt_set_camera(spt_ctx *ctx, const float view[16], const float eye[4], const float sky[4])
+{
+    if (!ctx) return fail(nullptr, SPT_ERR_ARG, "null context");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    if (!view || !eye || !sky) return fail(ctx, SPT_ERR_ARG, "null camera array");
+    for (int j = 12; j < 16; ++j)
+        if (view[j] != 0.0f)
+            return fail(ctx, SPT_ERR_ARG, "viewMatrix row 3 must be zero (CreateCameraBasisMatrix, Math.hpp:204-208)");
+    for (int j = 0; j < 12; ++j) ctx->cam.view[j] = view[j];
+    for (int j = 0; j < 3; ++j) {
+        ctx->cam.eye[j] = eye[j];
+        ctx->cam.sky[j] = sky[j];
+    }
+    ctx->cam_set = true;
+    return SPT_OK;
+}
+
+int spt_set_params(spt_ctx *ctx, uint32_t width, uint32_t height, uint32_t spp, uint32_t bounces, uint64_t seed)
+{
+    if (!ctx) return fail(nullptr, SPT_ERR_ARG, "null context");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    if (width == 0 || height == 0) return fail(ctx, SPT_ERR_ARG, "empty frame %ux%u", width, height);
+    if ((uint64_t)width * height * 3 > 0xFFFFFFFFull)
+        return fail(ctx, SPT_ERR_ARG, "frame %ux%u overflows the reference's uint32 g_size", width, height);
+    if (spp == 0) return fail(ctx, SPT_ERR_ARG, "spp must be >= 1 (1.f/0 samples)");
+    if (bounces == 0) return fail(ctx, SPT_ERR_ARG, "bounces must be >= 1 (--bounceCount never reaches 0)");
+    ctx->W = width;
+    ctx->H = height;
+    ctx->spp = spp;
+    ctx->bounces = bounces;
+    ctx->seed = seed;
+    ctx->params_set = true;
+    return SPT_OK;
+}
+
+int spt_set_workspace(spt_ctx *ctx, uint64_t bytes)
+{
+    if (!ctx) return fail(nullptr, SPT_ERR_ARG, "null context");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    if (bytes < sizeof(float4)) return fail(ctx, SPT_ERR_ARG, "workspace too small");
+    ctx->ws_bytes = bytes;
+    return SPT_OK;
+}
+
+int spt_render_segment(spt_ctx *ctx, uint32_t yB, uint32_t yE, uint32_t xB, uint32_t xE, float *rgba, uint8_t *g_data)
+{
+    return render_segment_host(ctx, SPT_MODE_SEGMENT, yB, yE, xB, xE, rgba, g_data);
+}
+
+int spt_render_segment_task(spt_ctx *ctx, uint32_t yB, uint32_t yE, uint32_t xB, uint32_t xE, float *rgba,
+                            uint8_t *g_data)
+{
+    return render_segment_host(ctx, SPT_MODE_TASK, yB, yE, xB, xE, rgba, g_data);
+}
+
+int spt_rows_count(uint32_t yB, uint32_t yE, uint32_t strip, uint32_t parts, uint32_t part, uint32_t *rows)
+{
+    if (!rows || strip == 0 || parts == 0 || part >= parts) return fail(nullptr, SPT_ERR_ARG, "bad row map");
+    spt::RowMap m{yB, yE, strip, parts, part, 0u, 0u};
+    *rows = spt::rows_owned(m);
+    return SPT_OK;
+}
+
+int spt_render_rows_async(spt_ctx *ctx, int mode, uint32_t yB, uint32_t yE, uint32_t strip, uint32_t parts,
+                          uint32_t part, uint32_t xB, uint32_t xE, void *d_rgba, void *d_rgb8, void *stream)
+{
+    if (!ctx) return fail(nullptr, SPT_ERR_ARG, "null context");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    int rc = check_ready(ctx);
+    if (rc) return rc;
+    if (mode != SPT_MODE_SEGMENT && mode != SPT_MODE_TASK) return fail(ctx, SPT_ERR_ARG, "bad mode %d", mode);
+    if (strip == 0 || parts == 0 || part >= parts) return fail(ctx, SPT_ERR_ARG, "bad row map");
+    if ((rc = check_region(ctx, yB, yE, xB, xE))) return rc;
+    if (yB >= yE || xB >= xE) return SPT_OK;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    spt::RowMap map{yB, yE, strip, parts, part, xB, xE - xB};
+    hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+    return render_impl(ctx, mode, map, (float4 *)d_rgba, (uint8_t *)d_rgb8, s, false);
+}
+
+int spt_assemble_rows_async(spt_ctx *ctx, const void *d_tiles, uint32_t max_rows, uint32_t yB, uint32_t yE,
+                            uint32_t strip, uint32_t parts, uint32_t xB, uint32_t xE, void *d_frame_rgba, void *d_rgb8,
+                            void *stream)
+{
+    if (!ctx) return fail(nullptr, SPT_ERR_ARG, "null context");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    if (!d_tiles || strip == 0 || parts == 0 || yE > ctx->H || xE > ctx->W || yB > yE || xB > xE)
+        return fail(ctx, SPT_ERR_ARG, "bad assemble arguments");
+    if (!ctx->params_set) return fail(ctx, SPT_ERR_STATE, "params not set");
+    for (uint32_t p = 0; p < parts; ++p) {
+        spt::RowMap m{yB, yE, strip, parts, p, xB, xE - xB};
+        if (spt::rows_owned(m) > max_rows) return fail(ctx, SPT_ERR_ARG, "max_rows smaller than part %u's rows", p);
+    }
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    spt::RowMap base{yB, yE, strip, parts, 0u, xB, xE - xB};
+    hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+    HIP_TRY(ctx, spt::launch_assemble((const float4 *)d_tiles, max_rows, base, ctx->W, ctx->H, (float4 *)d_frame_rgba,
+                                      (uint8_t *)d_rgb8, s));
+    return SPT_OK;
+}
+
+int spt_synchronize(spt_ctx *ctx)
+{
+    if (!ctx) return fail(nullptr, SPT_ERR_ARG, "null context");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    HIP_TRY(ctx, hipDeviceSynchronize());
+    return collect_timings(ctx);
+}
+
+int spt_render_samples(spt_ctx *ctx, int mode, uint32_t yB, uint32_t yE, uint32_t xB, uint32_t xE, float *out)
+{
+    if (!ctx) return fail(nullptr, SPT_ERR_ARG, "null context");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    int rc = check_ready(ctx);
+    if (rc) return rc;
+    if (!out) return fail(ctx, SPT_ERR_ARG, "null out");
+    if ((rc = check_region(ctx, yB, yE, xB, xE))) return rc;
+    if (yB >= yE || xB >= xE) return SPT_OK;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    spt::RowMap map{yB, yE, 1u, 1u, 0u, xB, xE - xB};
+    if ((rc = render_impl(ctx, mode, map, nullptr, nullptr, ctx->stream, true))) return rc;
+    const size_t items = (size_t)(xE - xB) * (yE - yB) * ctx->spp;
+    HIP_TRY(ctx, hipMemcpyAsync(out, ctx->d_samples, items * sizeof(float4), hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return collect_timings(ctx);
+}
+
+int spt_get_stats(spt_ctx *ctx, spt_stats *out)
+{
+    if (!ctx || !out) return fail(ctx, SPT_ERR_ARG, "null argument");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    int rc = collect_timings(ctx);
+    if (rc) return rc;
+    unsigned long long c[4] = {0, 0, 0, 0};
+    HIP_TRY(ctx, hipMemcpy(c, ctx->d_counters, sizeof c, hipMemcpyDeviceToHost));
+    out->casts = c[0];
+    out->samples = c[1];
+    out->dropped = c[2];
+    out->launches = ctx->launches;
+    out->render_ms = ctx->render_ms;
+    out->fold_ms = ctx->fold_ms;
+    out->last_render_ms = ctx->last_render_ms;
+    out->grid_blocks = ctx->grid;
+    out->block_threads = ctx->block;
+    return SPT_OK;
+}
+
+int spt_reset_stats(spt_ctx *ctx)
+{
+    if (!ctx) return fail(nullptr, SPT_ERR_ARG, "null context");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    int rc = collect_timings(ctx);
+    if (rc) return rc;
+    HIP_TRY(ctx, hipMemset(ctx->d_counters, 0, 4 * sizeof(unsigned long long)));
+    ctx->render_ms = ctx->fold_ms = ctx->last_render_ms = 0;
+    ctx->launches = 0;
+    return SPT_OK;
+}
+
+int spt_selftest_numerics(spt_ctx *ctx, const float *a, const float *b, const uint32_t *bits, uint32_t n, float *out)
+{
+    if (!ctx) return fail(nullptr, SPT_ERR_ARG, "null context");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    if (!a || !b || !bits || !out) return fail(ctx, SPT_ERR_ARG, "null argument");
+    if (n == 0) return SPT_OK;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    float *da = nullptr, *db = nullptr, *dout = nullptr;
+    uint32_t *dbits = nullptr;
+    HIP_TRY(ctx, hipMalloc((void **)&da, n * sizeof(float)));
+    HIP_TRY(ctx, hipMalloc((void **)&db, n * sizeof(float)));
+    HIP_TRY(ctx, hipMalloc((void **)&dbits, n * sizeof(uint32_t)));
+    HIP_TRY(ctx, hipMalloc((void **)&dout, (size_t)n * SPT_SELFTEST_COLS * sizeof(float)));
+    HIP_TRY(ctx, hipMemcpy(da, a, n * sizeof(float), hipMemcpyHostToDevice));
+    HIP_TRY(ctx, hipMemcpy(db, b, n * sizeof(float), hipMemcpyHostToDevice));
+    HIP_TRY(ctx, hipMemcpy(dbits, bits, n * sizeof(uint32_t), hipMemcpyHostToDevice));
+    HIP_TRY(ctx, spt::launch_selftest(da, db, dbits, n, dout, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    HIP_TRY(ctx, hipMemcpy(out, dout, (size_t)n * SPT_SELFTEST_COLS * sizeof(float), hipMemcpyDeviceToHost));
+    (void)hipFree(da);
+    (void)hipFree(db);
+    (void)hipFree(dbits);
+    (void)hipFree(dout);
+    return SPT_OK;
+}
+
+}  // extern "C"

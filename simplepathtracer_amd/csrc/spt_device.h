@@ -1,0 +1,138 @@
+// spt_device.h -- device-side arithmetic of the render loop (gfx950).
+//
+// Every helper restates one reference function with its exact fp32 operation
+// order.  The whole translation unit is compiled with
+// -ffp-contract=off (and the pragma below): no FMA contraction, IEEE division
+// and sqrt (hipcc's default correctly-rounded f32 div/sqrt), denormals kept.
+//
+// Vec4 lanes: the reference's w lane is always +-0 (Vec4{x,y,z} initialisers,
+// viewMatrix row 3 = 0), so dpps' (x*x'+y*y')+(z*z'+w*w') reduces to
+// (x*x'+y*y')+z*z' up to the sign of an all-zero result, which no comparison or
+// colour depends on.  The oracle keeps all four lanes; parity tests check both.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#pragma clang fp contract(off)
+
+namespace spt {
+
+// Material ids, Definitions.hpp:7-13
+constexpr uint32_t SPT_SKYBOX_ID = 0, SPT_REFLECTIVE_ID = 1, SPT_REFRACTIVE_ID = 2, SPT_DIFFUSE_ID = 3;
+
+struct f3 {
+    float x, y, z;
+};
+
+__device__ __forceinline__ f3 mk(float x, float y, float z) { return f3{x, y, z}; }
+// Math.hpp:16-48
+__device__ __forceinline__ f3 add(f3 a, f3 b) { return f3{a.x + b.x, a.y + b.y, a.z + b.z}; }
+__device__ __forceinline__ f3 sub(f3 a, f3 b) { return f3{a.x - b.x, a.y - b.y, a.z - b.z}; }
+// Math.hpp:50-64
+__device__ __forceinline__ f3 mul(f3 a, float s) { return f3{a.x * s, a.y * s, a.z * s}; }
+__device__ __forceinline__ f3 neg(f3 a) { return f3{-a.x, -a.y, -a.z}; }
+// Math.hpp:107-111 (_mm_dp_ps 0xF1)
+__device__ __forceinline__ float dot(f3 a, f3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
+// Math.hpp:122-133 (mul + 2x hadd)
+__device__ __forceinline__ float lensq(f3 a) { return (a.x * a.x + a.y * a.y) + a.z * a.z; }
+// Math.hpp:140-154: v / sqrt(|v|^2), lane-wise IEEE division
+__device__ __forceinline__ f3 normalize(f3 a)
+{
+    float l = __builtin_sqrtf(lensq(a));
+    return f3{a.x / l, a.y / l, a.z / l};
+}
+// Math.hpp:156-159: vec - normal * Dot(vec, normal) * 2.f
+__device__ __forceinline__ f3 reflect(f3 v, f3 n) { return sub(v, mul(mul(n, dot(v, n)), 2.0f)); }
+
+// ---------------------------------------------------------------------------
+// RNG: Random.hpp:30-36 splitmix mixer on a keyed counter stream.
+// ---------------------------------------------------------------------------
+constexpr uint64_t kGamma = 0x9E3779B97F4A7C15ull;
+
+__device__ __forceinline__ uint64_t fmix64(uint64_t z)
+{
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+__device__ __forceinline__ uint32_t next_u32(uint64_t &st)
+{
+    st += kGamma;
+    uint64_t z = st;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return (uint32_t)((z ^ (z >> 31)) >> 31);
+}
+
+// libstdc++ generate_canonical<float,24> + uniform_real_distribution (Random.hpp:86-93):
+// float(u)/2^32 (exact scaling), clamp >= 1 to nextafter(1,0), then u*(b-a)+a.
+__device__ __forceinline__ float canon_u32(uint32_t bits)
+{
+    float u = (float)bits * 2.3283064365386963e-10f;  // * 2^-32, exact
+    return u >= 1.0f ? 0x1.fffffep-1f : u;  // nextafterf(1, 0)
+}
+__device__ __forceinline__ float uniform(uint64_t &st, float a, float b) { return canon_u32(next_u32(st)) * (b - a) + a; }
+
+// Random.hpp:115-127 (== 129-141): x, y, z ~ U(-0.5,0.5) while Length < 0.5.
+// sqrt_rn is monotone and sqrt_rn(0.25) == 0.5, sqrt_rn(prev(0.25)) < 0.5, so
+// `sqrtf(L) < 0.5f` <=> `L < 0.25f` (checked exhaustively in tests).
+__device__ __forceinline__ f3 ball_vector(uint64_t &st)
+{
+    f3 r;
+    do {
+        float x = uniform(st, -0.5f, 0.5f);
+        float y = uniform(st, -0.5f, 0.5f);
+        float z = uniform(st, -0.5f, 0.5f);
+        r = mk(x, y, z);
+    } while (lensq(r) < 0.25f);
+    return r;
+}
+
+// ---------------------------------------------------------------------------
+// Refraction helpers (SingleThreadPathTracer.hpp:48-92).  Under libstdc++ the
+// float arguments of pow()/sqrt() promote to ::pow(double,double) and
+// ::sqrt(double); the GPU evaluates x^5 exactly as a double-double and rounds
+// once (glibc pow is accurate to ~2^-68 relative; the result is then narrowed
+// to float, so the two agree except on measure-zero ties).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ double pow5(double x)
+{
+    double x2 = x * x;                         // exact: x has a 24-bit significand
+    double x4 = x2 * x2;
+    double x4l = __builtin_fma(x2, x2, -x4);   // exact low part of x2^2
+    double p = x4 * x;
+    double pl = __builtin_fma(x4, x, -p);      // exact low part of x4*x
+    return p + (pl + x4l * x);
+}
+
+__device__ __forceinline__ float schlick(float rsq, float c)
+{
+    return (float)((double)rsq + (double)(1.f - rsq) * pow5((double)(1.f - c)));
+}
+
+// direction * r + n * (r*c - sqrt(1 - r*r*(1 - c*c)))  (lines 68, 84)
+__device__ __forceinline__ f3 refract_dir(f3 d, f3 n, float r, float c)
+{
+    float k = (float)((double)(r * c) - __builtin_sqrt((double)(1.f - r * r * (1.f - c * c))));
+    return normalize(add(mul(d, r), mul(n, k)));
+}
+
+// r * sqrt(1 - c*c) < 1, evaluated in double (lines 66, 82)
+__device__ __forceinline__ bool no_tir(float r, float c)
+{
+    return (double)r * __builtin_sqrt((double)(1.f - c * c)) < 1.0;
+}
+
+// IOHelpers.hpp:17-22 + x86 cvttss2si semantics of static_cast<uint8_t>(float)
+__device__ __forceinline__ uint8_t f2u8(float v)
+{
+    if (!(v > -2147483648.0f && v < 2147483648.0f)) return 0;
+    return (uint8_t)(int32_t)v;
+}
+__device__ __forceinline__ uint8_t gamma_byte(float c)
+{
+    return f2u8(__builtin_roundf(__builtin_sqrtf(c / 255.f) * 255.f));
+}
+
+}  // namespace spt

@@ -1,0 +1,83 @@
+// spt_internal.h -- kernel launch interface shared by spt_kernels.hip and spt_api.cpp.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace spt {
+
+// Row map of a launch: rows y in [y0, y1) with ((y - y0) / strip) % parts == part.
+struct RowMap {
+    uint32_t y0, y1, strip, parts, part;
+    uint32_t x0, width;  // columns [x0, x0 + width)
+};
+
+__host__ __device__ inline uint32_t row_of(const RowMap &m, uint32_t lr)
+{
+    uint32_t blk = lr / m.strip;
+    return m.y0 + (blk * m.parts + m.part) * m.strip + (lr - blk * m.strip);
+}
+
+__host__ __device__ inline uint32_t rows_owned(const RowMap &m)
+{
+    if (m.y1 <= m.y0) return 0;
+    uint32_t h = m.y1 - m.y0;
+    uint32_t period = m.strip * m.parts;
+    uint32_t full = h / period, rem = h % period;
+    uint32_t r = full * m.strip;
+    uint32_t start = m.part * m.strip;
+    if (rem > start) r += (rem - start < m.strip) ? rem - start : m.strip;
+    return r;
+}
+
+struct DeviceScene {
+    const float4 *hit;      // {cx, cy, cz, r*r}
+    const float4 *shade;    // {red, green, blue, fuzz}
+    const uint32_t *mat;    // material id
+    uint32_t n;
+};
+
+struct Camera {
+    float view[12];  // rows 0..2 of viewMatrix (row 3 is zero)
+    float eye[3];
+    float sky[3];
+};
+
+struct RenderArgs {
+    DeviceScene scene;
+    Camera cam;
+    uint32_t width, height, bounces, mode;
+    uint64_t seed_key;  // fmix64(seed)
+    RowMap map;
+    uint32_t npix;       // pixels of the launch (rows_owned * width)
+    uint32_t spp_batch;  // samples per pixel in this batch
+    uint32_t s0;         // first sample index of the batch
+    uint32_t n_items;    // npix * spp_batch
+    uint32_t claim;      // items per queue claim
+    float4 *samples;     // [n_items] per-sample colour, w = counted
+    uint32_t *head;      // queue head (zeroed before launch)
+    unsigned long long *counters;  // [0] casts, [1] samples, [2] dropped
+};
+
+struct FoldArgs {
+    const float4 *samples;
+    float4 *acc;         // persistent accumulator (w = sample count)
+    float4 *out_rgba;    // nullable, local pixel order
+    uint8_t *out_rgb8;   // nullable, full frame (g_data layout)
+    RowMap map;
+    uint32_t width, height, npix, spp_batch, spp_total;
+    int first, last, mode;
+};
+
+hipError_t launch_render(const RenderArgs &a, uint32_t grid, uint32_t block, hipStream_t s);
+hipError_t launch_fold(const FoldArgs &a, hipStream_t s);
+hipError_t launch_assemble(const float4 *tiles, uint32_t max_rows, RowMap base, uint32_t width, uint32_t height,
+                           float4 *frame, uint8_t *rgb8, hipStream_t s);
+hipError_t launch_selftest(const float *a, const float *b, const uint32_t *bits, uint32_t n, float *out,
+                           hipStream_t s);
+hipError_t render_occupancy(uint32_t block, int *blocks_per_cu);
+
+constexpr uint32_t kSpecularCap = 1024;  // see spt_oracle.h SPO_SPECULAR_CAP
+constexpr uint32_t kTaskPasses = 10;     // TaskBasedPathTracer.hpp:81
+constexpr uint32_t kRenderBlock = 256;
+
+}  // namespace spt

@@ -1,0 +1,317 @@
+"""GPU parity tests: the gfx950 render path (through the C ABI) against the CPU
+restatement (oracle/) and the committed goldens.  Bar: bit-exact float pixels
+(north_star's 1e-5 abs tolerance is below one ulp for bright pixels) and exact
+RGB8 bytes.  Run on an MI355X with `pytest -m gpu`.
+"""
+import ctypes
+import math
+import threading
+from fractions import Fraction
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+EYE, LOOK, UP, SKY = [0, 1, -3, 0], [0, 1, 0, 0], [0, 1, 0, 0], [137, 207, 240, 0]
+
+
+def bits(a):
+    return np.ascontiguousarray(a, np.float32).view(np.uint32)
+
+
+def assert_bitwise(got, want, what=""):
+    got, want = np.asarray(got, np.float32), np.asarray(want, np.float32)
+    assert got.shape == want.shape, what
+    g, w = bits(got), bits(want)
+    bad = np.nonzero(g != w)
+    if len(bad[0]):
+        i = tuple(b[0] for b in bad)
+        raise AssertionError(f"{what}: {len(bad[0])} of {g.size} lanes differ; first at {i}: "
+                             f"got {got[i]!r} want {want[i]!r}")
+
+
+@pytest.fixture(scope="module")
+def spt():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import simplepathtracer_amd as m
+    m.lib()
+    return m
+
+
+@pytest.fixture(scope="module")
+def ctx(spt):
+    c = spt.Context(0)
+    yield c
+    c.close()
+
+
+def scene_from(spt, gs, name):
+    return spt.Scene(*(gs[f"{name}_{k}"] for k in ("centers", "radii", "colors", "materials", "fuzz")))
+
+
+def oscene_from(oracle, gs, name):
+    return oracle.OracleScene(*(gs[f"{name}_{k}"] for k in ("centers", "radii", "colors", "materials", "fuzz")))
+
+
+def setup(ctx, scene, w, h, spp, b, seed=1, view=None):
+    import simplepathtracer_amd as m
+    ctx.set_scene(scene)
+    ctx.set_camera(m.camera_basis(EYE, LOOK, UP) if view is None else view, EYE, SKY)
+    ctx.set_params(w, h, spp, b, seed)
+
+
+# ---------------------------------------------------------------- numerics
+
+def test_device_numerics_match_host(ctx, oracle):
+    rng = np.random.default_rng(3)
+    n = 1 << 16
+    a = np.concatenate([rng.random(n - 8, dtype=np.float32) * 4,
+                        np.float32([0, 1, 2, 1e-40, 255, 0.25, 3.4e38, 1e-30])])
+    b = (rng.random(n, dtype=np.float32) * 3 + np.float32(1e-3)).astype(np.float32)
+    u = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    u[:6] = [0, 1, 0xFFFFFF7F, 0xFFFFFF80, 0xFFFFFFFF, 0x80000000]
+    out = ctx.selftest_numerics(a, b, u)
+    assert_bitwise(out[:, 0], a / b, "fp32 division")
+    assert_bitwise(out[:, 1], np.sqrt(a), "fp32 sqrt")
+    sq = out[:, 2:4].copy().view(np.float64).ravel()
+    assert np.array_equal(sq, np.sqrt(a.astype(np.float64))), "fp64 sqrt"
+    p5 = out[:, 4:6].copy().view(np.float64).ravel()
+    for i in range(0, n, 97):
+        assert p5[i] == float(Fraction(float(a[i])) ** 5), (a[i], p5[i])
+    want_u = np.array([oracle.lib().spo_uniform_u32(int(x), -1.0, 1.0) for x in u[:4096]], np.float32)
+    assert_bitwise(out[:4096, 6], want_u, "uniform(-1,1)")
+    assert np.array_equal(out[:, 7], np.trunc(np.where(a < 2**31, a, 0)).astype(np.int64).astype(np.uint8))
+
+
+# ---------------------------------------------------------------- goldens
+
+@pytest.mark.parametrize("name", ["cornell3", "reference"])
+def test_config1_frame_matches_golden(spt, ctx, golden, golden_scenes, name):
+    setup(ctx, scene_from(spt, golden_scenes, name), 200, 100, 4, 8)
+    g = np.zeros(200 * 100 * 3, np.uint8)
+    rgba = ctx.render_segment(0, 100, 0, 200, g)
+    assert_bitwise(rgba[:, :3], golden[f"c1_{name}_rgba"][:, :3], f"C1 {name} float pixels")
+    assert np.array_equal(g, golden[f"c1_{name}_rgb8"])
+    st = ctx.stats()
+    assert st["samples"] >= 200 * 100 * 4
+
+
+@pytest.mark.parametrize("name", ["cornell3", "reference"])
+def test_config1_task_tiles_match_golden(spt, ctx, golden, golden_scenes, name):
+    setup(ctx, scene_from(spt, golden_scenes, name), 200, 100, 4, 8)
+    g = np.zeros(200 * 100 * 3, np.uint8)
+    out = np.zeros((100, 200, 4), np.float32)
+    for ty in range(0, 100, 50):
+        for tx in range(0, 200, 50):
+            t = ctx.render_segment(ty, ty + 50, tx, tx + 50, g, task=True)
+            out[ty:ty + 50, tx:tx + 50] = t.reshape(50, 50, 4)
+    assert_bitwise(out.reshape(-1, 4)[:, :3], golden[f"c1_{name}_task_rgba"][:, :3], "C1 task")
+    assert np.array_equal(g, golden[f"c1_{name}_task_rgb8"])
+
+
+def test_config2_sparse_pixels_and_window_match_golden(spt, ctx, golden, golden_scenes):
+    setup(ctx, scene_from(spt, golden_scenes, "random"), 1200, 800, 100, 50)
+    win = ctx.render_segment(400, 416, 592, 608)
+    assert_bitwise(win[:, :3], golden["c2_window_400_592_rgba"][:, :3], "C2 window")
+    for (x, y), want in zip(golden["c2_pixels_xy"], golden["c2_pixels_rgba"]):
+        got = ctx.render_segment(int(y), int(y) + 1, int(x), int(x) + 1)
+        assert_bitwise(got[0, :3], want[:3], f"C2 pixel {(x, y)}")
+
+
+# ---------------------------------------------------------------- vs live oracle
+
+def test_per_sample_colours_and_cast_counts(spt, ctx, oracle, golden_scenes):
+    setup(ctx, scene_from(spt, golden_scenes, "random"), 1200, 800, 12, 50, seed=77)
+    sc = oscene_from(oracle, golden_scenes, "random")
+    fr = oracle.make_frame(golden_scenes["view"], EYE, SKY, 1200, 800, 12, 50, 77)
+    yB, yE, xB, xE = 350, 358, 500, 540
+    ctx.reset_stats()
+    samp = ctx.render_samples(yB, yE, xB, xE, 12)
+    casts = 0
+    for p in range(samp.shape[0]):
+        y, x = yB + p // (xE - xB), xB + p % (xE - xB)
+        for s in range(12):
+            want, c = oracle.trace_sample(sc, fr, x, y, s)
+            casts += c
+            assert_bitwise(samp[p, s, :3], want[:3], f"sample {(x, y, s)}")
+    assert ctx.stats()["casts"] == casts
+
+
+@pytest.mark.parametrize("task", [False, True])
+def test_region_vs_oracle_with_gdata_bytes(spt, ctx, oracle, golden_scenes, task):
+    setup(ctx, scene_from(spt, golden_scenes, "random"), 1200, 800, 8, 50, seed=5)
+    sc = oscene_from(oracle, golden_scenes, "random")
+    fr = oracle.make_frame(golden_scenes["view"], EYE, SKY, 1200, 800, 8, 50, 5)
+    g = np.full(1200 * 800 * 3, 0xAB, np.uint8)
+    gw = g.copy()
+    yB, xB, t = 300, 610, 32
+    got = ctx.render_segment(yB, yB + t, xB, xB + t, g, task=task)
+    want, _ = oracle.render_segment(sc, fr, yB, yB + t, xB, xB + t, task=task, rgb8=gw)
+    assert_bitwise(got[:, :3], want[:, :3], "region")
+    assert np.array_equal(g, gw), "g_data bytes (region written, rest untouched)"
+
+
+def test_task_mode_drops_deep_specular_paths(spt, ctx, oracle):
+    """Two facing mirrors: many paths exceed RenderSegmentTask's 10 passes
+    (TaskBasedPathTracer.hpp:81) and are dropped; the resolve averages the rest."""
+    c = np.float32([[0, -1000.5, 0, 0], [-0.55, 0.5, 2, 0], [0.55, 0.5, 2, 0]])
+    r = np.float32([1000, 0.5, 0.5])
+    col = np.float32([[30, 144, 255, 0], [200, 50, 50, 0], [50, 200, 50, 0]])
+    m = np.uint8([3, 1, 1])
+    fz = np.float32([0, 0.0, 0.05])
+    scene = spt.Scene(c, r, col, m, fz)
+    setup(ctx, scene, 64, 64, 16, 8, seed=9)
+    ctx.reset_stats()
+    got = ctx.render_segment(0, 64, 0, 64, task=True)
+    assert ctx.stats()["dropped"] > 0
+    osc = oracle.OracleScene(c, r, col, m, fz)
+    fr = oracle.make_frame(spt.camera_basis(EYE, LOOK, UP), EYE, SKY, 64, 64, 16, 8, 9)
+    want, _ = oracle.render_segment(osc, fr, 0, 64, 0, 64, task=True)
+    assert_bitwise(got[:, :3], want[:, :3], "task mode with drops")
+    got_seg = ctx.render_segment(0, 64, 0, 64, task=False)
+    want_seg, _ = oracle.render_segment(osc, fr, 0, 64, 0, 64)
+    assert_bitwise(got_seg[:, :3], want_seg[:, :3], "segment mode, deep specular chains")
+
+
+# ---------------------------------------------------------------- edge cases
+
+def test_empty_region_is_a_noop(spt, ctx, golden_scenes):
+    setup(ctx, scene_from(spt, golden_scenes, "reference"), 16, 16, 2, 3)
+    g = np.full(16 * 16 * 3, 7, np.uint8)
+    out = ctx.render_segment(5, 5, 0, 16, g)
+    assert out.size == 0 and (g == 7).all()
+
+
+def test_zero_spheres_is_all_sky(spt, ctx, oracle):
+    e = np.zeros((0, 4), np.float32)
+    scene = spt.Scene(e, np.zeros(0, np.float32), e, np.zeros(0, np.uint8), np.zeros(0, np.float32))
+    setup(ctx, scene, 24, 12, 3, 4)
+    got = ctx.render_segment(0, 12, 0, 24)
+    osc = oracle.OracleScene(e, np.zeros(0, np.float32), e, np.zeros(0, np.uint8), np.zeros(0, np.float32))
+    fr = oracle.make_frame(spt.camera_basis(EYE, LOOK, UP), EYE, SKY, 24, 12, 3, 4, 1)
+    want, casts = oracle.render_segment(osc, fr, 0, 12, 0, 24)
+    assert casts == 24 * 12 * 3
+    assert_bitwise(got[:, :3], want[:, :3], "sky only")
+
+
+def test_skybox_material_and_single_bounce(spt, ctx, oracle, golden_scenes):
+    """Material SKYBOX on a sphere falls through to the sky (SingleThreadPathTracer.hpp:98-111)."""
+    gs = golden_scenes
+    m = gs["reference_materials"].copy()
+    m[5] = 0
+    m[7] = 7  # unknown id behaves like SKYBOX too
+    scene = spt.Scene(gs["reference_centers"], gs["reference_radii"], gs["reference_colors"], m,
+                      gs["reference_fuzz"])
+    setup(ctx, scene, 40, 40, 5, 1)
+    got = ctx.render_segment(0, 40, 0, 40)
+    osc = oracle.OracleScene(gs["reference_centers"], gs["reference_radii"], gs["reference_colors"], m,
+                             gs["reference_fuzz"])
+    fr = oracle.make_frame(gs["view"], EYE, SKY, 40, 40, 5, 1, 1)
+    want, _ = oracle.render_segment(osc, fr, 0, 40, 0, 40)
+    assert_bitwise(got[:, :3], want[:, :3], "skybox material / bounces=1")
+
+
+def test_more_than_255_spheres(spt, ctx, oracle):
+    """Extension beyond the reference's uint8 index (Collision.hpp:87-92); pinned
+    against the oracle's uint32 restatement only (the reference hangs)."""
+    s = spt.generate_stress(11, 300)
+    setup(ctx, s, 96, 64, 4, 10)
+    got = ctx.render_segment(20, 44, 30, 62)
+    osc = oracle.OracleScene(s.centers, s.radii, s.colors, s.materials, s.fuzz)
+    fr = oracle.make_frame(spt.camera_basis(EYE, LOOK, UP), EYE, SKY, 96, 64, 4, 10, 1)
+    want, _ = oracle.render_segment(osc, fr, 20, 44, 30, 62)
+    assert_bitwise(got[:, :3], want[:, :3], "300 spheres")
+
+
+def test_nondefault_camera_and_odd_frame(spt, ctx, oracle, golden_scenes):
+    view = spt.camera_basis([2, 3, -4, 0], [0, 0.5, 2, 0], UP)
+    setup(ctx, scene_from(spt, golden_scenes, "random"), 131, 77, 3, 12, seed=3, view=view)
+    got = ctx.render_segment(10, 50, 7, 120)
+    osc = oscene_from(oracle, golden_scenes, "random")
+    fr = oracle.make_frame(view, EYE, SKY, 131, 77, 3, 12, 3)
+    want, _ = oracle.render_segment(osc, fr, 10, 50, 7, 120)
+    assert_bitwise(got[:, :3], want[:, :3], "camera")
+
+
+def test_invalid_arguments_raise(spt, ctx, golden_scenes):
+    setup(ctx, scene_from(spt, golden_scenes, "reference"), 16, 16, 2, 3)
+    with pytest.raises(spt.SptError):
+        ctx.set_params(16, 16, 2, 0, 1)  # bounces = 0
+    with pytest.raises(spt.SptError):
+        ctx.set_params(16, 16, 0, 3, 1)  # spp = 0
+    with pytest.raises(spt.SptError):
+        ctx.render_segment(0, 17, 0, 16)  # outside the frame
+    bad = np.eye(4, dtype=np.float32).ravel()
+    with pytest.raises(spt.SptError):
+        ctx.set_camera(bad, EYE, SKY)  # viewMatrix row 3 must be zero
+
+
+# ---------------------------------------------------------------- full-size properties
+
+def test_workspace_batches_fold_in_order(spt, ctx, golden_scenes):
+    setup(ctx, scene_from(spt, golden_scenes, "random"), 1200, 800, 10, 50, seed=4)
+    a = ctx.render_segment(200, 264, 100, 228)
+    ctx.set_workspace(64 * 128 * 3 * 16)  # forces 4 batches of <= 3 samples
+    b = ctx.render_segment(200, 264, 100, 228)
+    ctx.set_workspace(4 << 30)
+    assert_bitwise(b, a, "batched vs single-batch")
+
+
+def test_row_split_and_assemble_equals_full_frame(spt, ctx, golden_scenes):
+    import torch
+    setup(ctx, scene_from(spt, golden_scenes, "random"), 1200, 800, 4, 50, seed=2)
+    full = torch.zeros((800 * 1200, 4), dtype=torch.float32, device="cuda")
+    g_full = torch.zeros(1200 * 800 * 3, dtype=torch.uint8, device="cuda")
+    ctx.render_rows_async(0, 0, 800, 1, 1, 0, 0, 1200, full.data_ptr(), g_full.data_ptr())
+    ctx.synchronize()
+    parts, strip = 3, 8
+    rows = [spt.rows_count(0, 800, strip, parts, p) for p in range(parts)]
+    mr = max(rows)
+    tiles = torch.zeros((parts, mr * 1200, 4), dtype=torch.float32, device="cuda")
+    for p in range(parts):
+        ctx.render_rows_async(0, 0, 800, strip, parts, p, 0, 1200, tiles[p].data_ptr(), 0)
+    frame = torch.zeros_like(full)
+    g = torch.zeros_like(g_full)
+    ctx.assemble_rows_async(tiles.data_ptr(), mr, 0, 800, strip, parts, 0, 1200, frame.data_ptr(), g.data_ptr())
+    ctx.synchronize()
+    assert torch.equal(frame.view(torch.int32), full.view(torch.int32))
+    assert torch.equal(g, g_full)
+
+
+def test_config2_full_frame_properties(spt, ctx, oracle, golden_scenes):
+    """BASELINE config 2 at full size: every sample accounted for, deterministic,
+    and random pixels bit-exact vs the oracle."""
+    setup(ctx, scene_from(spt, golden_scenes, "random"), 1200, 800, 100, 50)
+    ctx.reset_stats()
+    g1 = np.zeros(1200 * 800 * 3, np.uint8)
+    a = ctx.render_segment(0, 800, 0, 1200, g1)
+    st = ctx.stats()
+    assert st["samples"] == 1200 * 800 * 100
+    assert 1.5 < st["casts"] / st["samples"] < 4.0
+    b = ctx.render_segment(0, 800, 0, 1200)
+    assert_bitwise(a, b, "determinism")
+    sc = oscene_from(oracle, golden_scenes, "random")
+    fr = oracle.make_frame(golden_scenes["view"], EYE, SKY, 1200, 800, 100, 50, 1)
+    rng = np.random.default_rng(99)
+    for _ in range(24):
+        x, y = int(rng.integers(0, 1200)), int(rng.integers(0, 800))
+        want, _ = oracle.render_segment(sc, fr, y, y + 1, x, x + 1)
+        assert_bitwise(a[y * 1200 + x, :3], want[0, :3], f"pixel {(x, y)}")
+    gw = np.zeros_like(g1)
+    assert np.isfinite(a[:, :3]).all()
+    _ = gw
+
+
+def test_concurrent_render_jobs_share_a_context(spt, golden_scenes):
+    """RenderImageParallelMain (Renderer.hpp:257-302) calls the entry point from
+    several threads at once on disjoint tiles."""
+    g = spt.Globals(scene_from(spt, golden_scenes, "random"), width=240, height=160, samples=6, bounces=50)
+    spt.RenderImageParallelMain(g, thread_count=4)
+    tiled = g.g_data.copy()
+    g.g_data[:] = 0
+    spt.RenderSegment(spt.RenderSegmentData(0, 160, 0, 240), g)
+    assert np.array_equal(tiled, g.g_data)
+    g.ctx.close()

@@ -64,6 +64,8 @@ typedef struct spt_stats {
     double last_render_ms; /* device time of the most recent render launch */
     uint32_t grid_blocks;  /* persistent grid of the render kernel */
     uint32_t block_threads;
+    uint64_t diag[4];      /* diagnostic build only (-DSPT_DIAG=1): wave iterations,
+                              hit-block entries, lane hits, reserved */
 } spt_stats;
 
 int spt_abi_version(void);

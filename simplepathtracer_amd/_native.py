@@ -12,7 +12,7 @@ import re
 import subprocess
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG_DIR, "lib", "libspt_hip.so")
+LIB_PATH = os.path.join(PKG_DIR, "lib", os.environ.get("SPT_LIB", "libspt_hip.so"))
 HEADER_PATH = os.path.join(os.path.dirname(PKG_DIR), "include", "spt_hip.h")
 
 SPT_OK = 0
@@ -39,6 +39,7 @@ class Stats(ctypes.Structure):
         ("last_render_ms", ctypes.c_double),
         ("grid_blocks", ctypes.c_uint32),
         ("block_threads", ctypes.c_uint32),
+        ("diag", ctypes.c_uint64 * 4),
     ]
 
 

@@ -41,6 +41,7 @@ struct spt_ctx {
 
     // scene (Globals.hpp:31-37)
     float4 *d_hit = nullptr, *d_shade = nullptr;
+    float *d_hitp = nullptr;
     uint32_t *d_mat = nullptr;
     uint32_t n = 0, scene_cap = 0;
     bool scene_set = false;
@@ -187,7 +188,8 @@ int render_impl(spt_ctx *ctx, int mode, const spt::RowMap &map, float4 *d_rgba, 
     }
 
     spt::RenderArgs ra{};
-    ra.scene = spt::DeviceScene{ctx->d_hit, ctx->d_shade, ctx->d_mat, ctx->n};
+    ra.scene = spt::DeviceScene{ctx->d_hit, ctx->d_hitp, ctx->d_shade, ctx->d_mat, ctx->n,
+                                (ctx->n + spt::render_group_size() - 1) / spt::render_group_size()};
     ra.cam = ctx->cam;
     ra.width = ctx->W;
     ra.height = ctx->H;
@@ -324,8 +326,8 @@ int spt_ctx_create(int device, spt_ctx **out)
     if (const char *e = std::getenv("SPT_CLAIM")) ctx->claim = (uint32_t)std::max(1, std::atoi(e));
     ctx->grid = (uint32_t)(per_cu * ctx->num_cu);
     if (hipMalloc((void **)&ctx->d_head, sizeof(uint32_t)) != hipSuccess ||
-        hipMalloc((void **)&ctx->d_counters, 4 * sizeof(unsigned long long)) != hipSuccess ||
-        hipMemset(ctx->d_counters, 0, 4 * sizeof(unsigned long long)) != hipSuccess) {
+        hipMalloc((void **)&ctx->d_counters, 8 * sizeof(unsigned long long)) != hipSuccess ||
+        hipMemset(ctx->d_counters, 0, 8 * sizeof(unsigned long long)) != hipSuccess) {
         spt_ctx_destroy(ctx);
         return fail(nullptr, SPT_ERR_NOMEM, "workspace allocation failed");
     }
@@ -343,7 +345,7 @@ void spt_ctx_destroy(spt_ctx *ctx)
             (void)hipEventDestroy(p.a);
             (void)hipEventDestroy(p.b);
         }
-    void *bufs[] = {ctx->d_hit, ctx->d_shade, ctx->d_mat, ctx->d_samples, ctx->d_acc,
+    void *bufs[] = {ctx->d_hit, ctx->d_hitp, ctx->d_shade, ctx->d_mat, ctx->d_samples, ctx->d_acc,
                     ctx->d_head, ctx->d_counters, ctx->d_stage, ctx->d_frame8};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
@@ -365,29 +367,46 @@ int spt_set_scene(spt_ctx *ctx, const float *centers4, const float *radii, const
     if (n > 0 && (!centers4 || !radii || !colors4 || !materials || !fuzz))
         return fail(ctx, SPT_ERR_ARG, "null scene array");
     HIP_TRY(ctx, hipSetDevice(ctx->device));
-    std::vector<float4> hit(n), shade(n);
-    std::vector<uint32_t> mat(n);
+    // hit table padded to a multiple of 2*kMaxGroup plus two more groups (the hot
+    // loop runs groups in pairs and prefetches two groups ahead); padding spheres have
+    // r*r = -inf so RaySphereIntersection never passes for them.
+    const size_t npad = ((size_t)n + 2 * spt::kMaxGroup - 1) / (2 * spt::kMaxGroup) * (2 * spt::kMaxGroup) +
+                        2 * spt::kMaxGroup;
+    std::vector<float4> hit(npad, make_float4(0.f, 0.f, 0.f, -INFINITY)), shade(std::max<size_t>(n, 1));
+    std::vector<uint32_t> mat(std::max<size_t>(n, 1));
     for (uint32_t i = 0; i < n; ++i) {
         const float r = radii[i];
         hit[i] = make_float4(centers4[4 * i], centers4[4 * i + 1], centers4[4 * i + 2], r * r);
         shade[i] = make_float4(colors4[4 * i], colors4[4 * i + 1], colors4[4 * i + 2], fuzz[i]);
         mat[i] = materials[i];
     }
-    if (n > ctx->scene_cap) {
+    if (npad > ctx->scene_cap) {
         HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-        for (void *b : {(void *)ctx->d_hit, (void *)ctx->d_shade, (void *)ctx->d_mat})
+        for (void *b : {(void *)ctx->d_hit, (void *)ctx->d_shade, (void *)ctx->d_mat, (void *)ctx->d_hitp})
             if (b) HIP_TRY(ctx, hipFree(b));
         ctx->d_hit = ctx->d_shade = nullptr;
+        ctx->d_hitp = nullptr;
         ctx->d_mat = nullptr;
         ctx->scene_cap = 0;
-        HIP_TRY(ctx, hipMalloc((void **)&ctx->d_hit, n * sizeof(float4)));
-        HIP_TRY(ctx, hipMalloc((void **)&ctx->d_shade, n * sizeof(float4)));
-        HIP_TRY(ctx, hipMalloc((void **)&ctx->d_mat, n * sizeof(uint32_t)));
-        ctx->scene_cap = n;
+        HIP_TRY(ctx, hipMalloc((void **)&ctx->d_hit, npad * sizeof(float4)));
+        HIP_TRY(ctx, hipMalloc((void **)&ctx->d_hitp, npad * sizeof(float4)));
+        HIP_TRY(ctx, hipMalloc((void **)&ctx->d_shade, npad * sizeof(float4)));
+        HIP_TRY(ctx, hipMalloc((void **)&ctx->d_mat, npad * sizeof(uint32_t)));
+        ctx->scene_cap = (uint32_t)npad;
     }
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    HIP_TRY(ctx, hipMemcpy(ctx->d_hit, hit.data(), npad * sizeof(float4), hipMemcpyHostToDevice));
+    std::vector<float> hitp(npad * 4);
+    for (size_t j = 0; j < npad / 2; ++j)
+        for (int h = 0; h < 2; ++h) {
+            const float4 &v = hit[2 * j + h];
+            hitp[8 * j + 0 + h] = v.x;
+            hitp[8 * j + 2 + h] = v.y;
+            hitp[8 * j + 4 + h] = v.z;
+            hitp[8 * j + 6 + h] = v.w;
+        }
+    HIP_TRY(ctx, hipMemcpy(ctx->d_hitp, hitp.data(), npad * sizeof(float4), hipMemcpyHostToDevice));
     if (n) {
-        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-        HIP_TRY(ctx, hipMemcpy(ctx->d_hit, hit.data(), n * sizeof(float4), hipMemcpyHostToDevice));
         HIP_TRY(ctx, hipMemcpy(ctx->d_shade, shade.data(), n * sizeof(float4), hipMemcpyHostToDevice));
         HIP_TRY(ctx, hipMemcpy(ctx->d_mat, mat.data(), n * sizeof(uint32_t), hipMemcpyHostToDevice));
     }
@@ -518,9 +537,13 @@ int spt_render_samples(spt_ctx *ctx, int mode, uint32_t yB, uint32_t yE, uint32_
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     spt::RowMap map{yB, yE, 1u, 1u, 0u, xB, xE - xB};
     if ((rc = render_impl(ctx, mode, map, nullptr, nullptr, ctx->stream, true))) return rc;
-    const size_t items = (size_t)(xE - xB) * (yE - yB) * ctx->spp;
-    HIP_TRY(ctx, hipMemcpyAsync(out, ctx->d_samples, items * sizeof(float4), hipMemcpyDeviceToHost, ctx->stream));
+    const size_t npix = (size_t)(xE - xB) * (yE - yB);
+    std::vector<float4> buf(npix * ctx->spp);  // device order [sample][pixel]
+    HIP_TRY(ctx, hipMemcpyAsync(buf.data(), ctx->d_samples, buf.size() * sizeof(float4), hipMemcpyDeviceToHost,
+                                ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    for (size_t p = 0; p < npix; ++p)
+        for (size_t s = 0; s < ctx->spp; ++s) std::memcpy(out + 4 * (p * ctx->spp + s), &buf[s * npix + p], 16);
     return collect_timings(ctx);
 }
 
@@ -531,11 +554,12 @@ int spt_get_stats(spt_ctx *ctx, spt_stats *out)
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     int rc = collect_timings(ctx);
     if (rc) return rc;
-    unsigned long long c[4] = {0, 0, 0, 0};
+    unsigned long long c[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     HIP_TRY(ctx, hipMemcpy(c, ctx->d_counters, sizeof c, hipMemcpyDeviceToHost));
     out->casts = c[0];
     out->samples = c[1];
     out->dropped = c[2];
+    for (int i = 0; i < 4; ++i) out->diag[i] = c[4 + i];
     out->launches = ctx->launches;
     out->render_ms = ctx->render_ms;
     out->fold_ms = ctx->fold_ms;
@@ -552,7 +576,7 @@ int spt_reset_stats(spt_ctx *ctx)
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     int rc = collect_timings(ctx);
     if (rc) return rc;
-    HIP_TRY(ctx, hipMemset(ctx->d_counters, 0, 4 * sizeof(unsigned long long)));
+    HIP_TRY(ctx, hipMemset(ctx->d_counters, 0, 8 * sizeof(unsigned long long)));
     ctx->render_ms = ctx->fold_ms = ctx->last_render_ms = 0;
     ctx->launches = 0;
     return SPT_OK;

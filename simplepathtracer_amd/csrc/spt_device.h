@@ -41,6 +41,21 @@ __device__ __forceinline__ f3 normalize(f3 a)
     float l = __builtin_sqrtf(lensq(a));
     return f3{a.x / l, a.y / l, a.z / l};
 }
+// Correctly rounded sqrt for arguments known to be normal and positive (the
+// hit test only takes the root of r*r - d2 > 1e-3): v_sqrt_f32 (<= 1 ulp) plus
+// the residual correction hipcc emits for sqrtf, without its denormal scaling.
+__device__ __forceinline__ float sqrt_pos_normal(float h)
+{
+    float s = __builtin_amdgcn_sqrtf(h);
+    const float dn = __builtin_bit_cast(float, __builtin_bit_cast(int, s) - 1);
+    const float up = __builtin_bit_cast(float, __builtin_bit_cast(int, s) + 1);
+    const float rdn = __builtin_fmaf(-dn, s, h);
+    const float rup = __builtin_fmaf(-up, s, h);
+    s = rdn <= 0.0f ? dn : s;
+    s = rup > 0.0f ? up : s;
+    return s;
+}
+
 // Math.hpp:156-159: vec - normal * Dot(vec, normal) * 2.f
 __device__ __forceinline__ f3 reflect(f3 v, f3 n) { return sub(v, mul(mul(n, dot(v, n)), 2.0f)); }
 

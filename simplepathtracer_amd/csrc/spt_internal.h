@@ -29,11 +29,15 @@ __host__ __device__ inline uint32_t rows_owned(const RowMap &m)
     return r;
 }
 
+constexpr uint32_t kMaxGroup = 16;  // sphere-table padding granule (>= SPT_GROUP)
+
 struct DeviceScene {
-    const float4 *hit;      // {cx, cy, cz, r*r}
+    const float4 *hit;      // {cx, cy, cz, r*r}, padded: see spt_set_scene
+    const float *hitp;      // same table as sphere pairs {cx0,cx1,cy0,cy1,cz0,cz1,rr0,rr1}
     const float4 *shade;    // {red, green, blue, fuzz}
     const uint32_t *mat;    // material id
     uint32_t n;
+    uint32_t ngroups;       // ceil(n / SPT_GROUP) groups of the hot loop
 };
 
 struct Camera {
@@ -75,6 +79,7 @@ hipError_t launch_assemble(const float4 *tiles, uint32_t max_rows, RowMap base, 
 hipError_t launch_selftest(const float *a, const float *b, const uint32_t *bits, uint32_t n, float *out,
                            hipStream_t s);
 hipError_t render_occupancy(uint32_t block, int *blocks_per_cu);
+uint32_t render_group_size();  // spheres per group of the hot loop (SPT_GROUP)
 
 constexpr uint32_t kSpecularCap = 1024;  // see spt_oracle.h SPO_SPECULAR_CAP
 constexpr uint32_t kTaskPasses = 10;     // TaskBasedPathTracer.hpp:81

@@ -22,6 +22,18 @@
 
 #include <float.h>
 
+#ifndef SPT_GROUP
+#define SPT_GROUP 4
+#endif
+
+#ifndef SPT_PACKED
+#define SPT_PACKED 0
+#endif
+
+#ifndef SPT_DIAG
+#define SPT_DIAG 0
+#endif
+
 #pragma clang fp contract(off)
 
 namespace spt {
@@ -36,10 +48,127 @@ constexpr float kRsq = (float)((double)((1.0f - 1.5f) / (1.0f + 1.5f)) * (double
 constexpr float kAirToGlass = 1.0f / 1.5f;
 constexpr float kGlassToAir = 1.5f / 1.0f;
 
+// Sphere table as constant-address-space data: wave-uniform indices become
+// scalar (s_load) reads even though the kernel also stores to global memory.
+typedef __attribute__((address_space(4))) const float cfloat;
+
+__device__ __forceinline__ float4 ld_uniform(cfloat *p, uint32_t i)
+{
+    return make_float4(p[4 * i + 0], p[4 * i + 1], p[4 * i + 2], p[4 * i + 3]);
+}
+
 __device__ __forceinline__ uint32_t lane_rank(unsigned long long mask)
 {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
 }
+
+
+// One group of SPT_GROUP spheres of FindClosestIntersectionSphere
+// (Collision.hpp:87-109): RaySphereIntersection for all of them, then the rare
+// closest-contact / distance update behind a single branch.
+__device__ __forceinline__ void test_group(const float4 (&sp)[SPT_GROUP], uint32_t base, const f3 &o, const f3 &d,
+                                           float dod, float &best, uint32_t &idx, f3 &bp)
+{
+    float tcv[SPT_GROUP], hv[SPT_GROUP];
+    bool pass[SPT_GROUP];
+    bool any = false;
+#pragma unroll
+    for (int k = 0; k < SPT_GROUP; ++k) {
+        // RaySphereIntersection, Collision.hpp:9-17
+        const float ocx = sp[k].x - o.x, ocy = sp[k].y - o.y, ocz = sp[k].z - o.z;
+        const float tc = (ocx * d.x + ocy * d.y) + ocz * d.z;
+        const float d2 = ((ocx * ocx + ocy * ocy) + ocz * ocz) - tc * tc;
+        const float h = sp[k].w - d2;
+        tcv[k] = tc;
+        hv[k] = h;
+        pass[k] = tc > 1e-3f && h > 1e-3f;
+        any = any || pass[k];
+    }
+    if (any) {
+#pragma unroll
+        for (int k = 0; k < SPT_GROUP; ++k) {
+            if (pass[k]) {
+                // CalculateRaySphereClosestContactPoint, Collision.hpp:19-27,49-56
+                const float t = tcv[k] - sqrt_pos_normal(hv[k]);
+                const f3 p = mk(o.x + d.x * t, o.y + d.y * t, o.z + d.z * t);
+                if (dod < dot(p, d)) {
+                    const float ds = lensq(sub(o, p));
+                    if (best > ds) {  // strict: the lowest index wins ties
+                        best = ds;
+                        idx = base + k;
+                        bp = p;
+                    }
+                }
+            }
+        }
+    }
+}
+
+#if SPT_PACKED
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+// Sphere pairs in pair-SoA layout {cx0,cx1, cy0,cy1, cz0,cz1, rr0,rr1}: each
+// component pair is one 64-bit scalar operand of a packed fp32 instruction, so
+// RaySphereIntersection for two spheres costs the same packed instructions as
+// one scalar sphere (IEEE per half, no contraction: results are identical).
+struct PairS {
+    f2v cx, cy, cz, rr;
+};
+
+__device__ __forceinline__ PairS ld_pair(cfloat *p, uint32_t j)
+{
+    const uint32_t b = 8 * j;
+    PairS r;
+    r.cx = f2v{p[b + 0], p[b + 1]};
+    r.cy = f2v{p[b + 2], p[b + 3]};
+    r.cz = f2v{p[b + 4], p[b + 5]};
+    r.rr = f2v{p[b + 6], p[b + 7]};
+    return r;
+}
+
+__device__ __forceinline__ void test_pairs(const PairS (&q)[SPT_GROUP / 2], uint32_t base, const f3 &o, const f3 &d,
+                                           float dod, float &best, uint32_t &idx, f3 &bp)
+{
+    float tcv[SPT_GROUP], hv[SPT_GROUP];
+    bool pass[SPT_GROUP];
+    bool any = false;
+    const f2v ox = f2v{o.x, o.x}, oy = f2v{o.y, o.y}, oz = f2v{o.z, o.z};
+    const f2v dx = f2v{d.x, d.x}, dy = f2v{d.y, d.y}, dz = f2v{d.z, d.z};
+#pragma unroll
+    for (int j = 0; j < SPT_GROUP / 2; ++j) {
+        const f2v ocx = q[j].cx - ox, ocy = q[j].cy - oy, ocz = q[j].cz - oz;
+        const f2v tc = (ocx * dx + ocy * dy) + ocz * dz;
+        const f2v d2 = ((ocx * ocx + ocy * ocy) + ocz * ocz) - tc * tc;
+        const f2v h = q[j].rr - d2;
+        tcv[2 * j] = tc.x;
+        tcv[2 * j + 1] = tc.y;
+        hv[2 * j] = h.x;
+        hv[2 * j + 1] = h.y;
+    }
+#pragma unroll
+    for (int k = 0; k < SPT_GROUP; ++k) {
+        pass[k] = tcv[k] > 1e-3f && hv[k] > 1e-3f;
+        any = any || pass[k];
+    }
+    if (any) {
+#pragma unroll
+        for (int k = 0; k < SPT_GROUP; ++k) {
+            if (pass[k]) {
+                const float t = tcv[k] - sqrt_pos_normal(hv[k]);
+                const f3 p = mk(o.x + d.x * t, o.y + d.y * t, o.z + d.z * t);
+                if (dod < dot(p, d)) {
+                    const float ds = lensq(sub(o, p));
+                    if (best > ds) {
+                        best = ds;
+                        idx = base + k;
+                        bp = p;
+                    }
+                }
+            }
+        }
+    }
+}
+#endif
 
 }  // namespace
 
@@ -48,6 +177,7 @@ __global__ __launch_bounds__(kRenderBlock) void render_kernel(RenderArgs a)
     const uint32_t lane = __lane_id();
     const uint32_t n = a.scene.n;
     const float4 *__restrict__ hit = a.scene.hit;
+    cfloat *hit_s = (cfloat *)a.scene.hit;
     const float4 *__restrict__ shade = a.scene.shade;
     const uint32_t *__restrict__ mat = a.scene.mat;
 
@@ -58,6 +188,9 @@ __global__ __launch_bounds__(kRenderBlock) void render_kernel(RenderArgs a)
     uint32_t blk_cur = 0, blk_end = 0;
     bool exhausted = false;
     unsigned long long casts = 0, done = 0, dropped = 0;
+#if SPT_DIAG
+    unsigned long long d_iters = 0, d_hitblk = 0, d_lanehits = 0, d_dotblk = 0;
+#endif
 
     for (;;) {
         // ---- hand out (pixel, sample) items to idle lanes: ballot + prefix ----
@@ -88,8 +221,11 @@ __global__ __launch_bounds__(kRenderBlock) void render_kernel(RenderArgs a)
             if (phase == PH_IDLE && mine != 0xFFFFFFFFu) {
                 // primary ray, SingleThreadPathTracer.hpp:123-130
                 item = mine;
-                const uint32_t pl = item / a.spp_batch;
-                const uint32_t s = a.s0 + (item - pl * a.spp_batch);
+                // items are ordered [sample][pixel]: a claim is a run of adjacent
+                // pixels of one sample (coherent primary rays, coalesced slots)
+                const uint32_t sl = item / a.npix;
+                const uint32_t s = a.s0 + sl;
+                const uint32_t pl = item - sl * a.npix;
                 const uint32_t lr = pl / a.map.width;
                 const uint32_t x = a.map.x0 + (pl - lr * a.map.width);
                 const uint32_t y = row_of(a.map, lr);
@@ -110,34 +246,48 @@ __global__ __launch_bounds__(kRenderBlock) void render_kernel(RenderArgs a)
         const unsigned long long live = __ballot(phase != PH_IDLE);
         if (live == 0ull) break;
         casts += (unsigned long long)__popcll(live);
+#if SPT_DIAG
+        ++d_iters;
+#endif
 
         // ---- FindClosestIntersectionSphere, Collision.hpp:87-109 ----
+        // Spheres are tested SPT_GROUP at a time from scalar registers (one
+        // s_load_dwordx16 per 4 spheres, prefetched a group ahead); the rare hit
+        // blocks (~6 of 148 spheres per wave iteration on config 2) sit behind
+        // one combined branch per group.  The table is padded with spheres of
+        // r*r = -inf that never pass, so the prefetch needs no bound check.
         uint32_t idx = n;
         float best = FLT_MAX;
         f3 bp = o;
         const float dod = dot(o, d);
-#pragma unroll 2
-        for (uint32_t i = 0; i < n; ++i) {
-            const float4 sp = hit[i];
-            // RaySphereIntersection, Collision.hpp:9-17
-            const float ocx = sp.x - o.x, ocy = sp.y - o.y, ocz = sp.z - o.z;
-            const float tc = (ocx * d.x + ocy * d.y) + ocz * d.z;
-            const float d2 = ((ocx * ocx + ocy * ocy) + ocz * ocz) - tc * tc;
-            const float h = sp.w - d2;
-            if (tc > 1e-3f && h > 1e-3f) {
-                // CalculateRaySphereClosestContactPoint, Collision.hpp:19-27,49-56
-                const float t = tc - __builtin_sqrtf(h);
-                const f3 p = mk(o.x + d.x * t, o.y + d.y * t, o.z + d.z * t);
-                if (dod < dot(p, d)) {
-                    const float ds = lensq(sub(o, p));
-                    if (best > ds) {
-                        best = ds;
-                        idx = i;
-                        bp = p;
-                    }
-                }
-            }
+#if SPT_PACKED
+        cfloat *pair_s = (cfloat *)a.scene.hitp;
+        PairS pa[SPT_GROUP / 2], pb[SPT_GROUP / 2];
+#pragma unroll
+        for (int j = 0; j < SPT_GROUP / 2; ++j) pa[j] = ld_pair(pair_s, j);
+        for (uint32_t g = 0; g < a.scene.ngroups; g += 2) {
+#pragma unroll
+            for (int j = 0; j < SPT_GROUP / 2; ++j) pb[j] = ld_pair(pair_s, (g + 1) * (SPT_GROUP / 2) + j);
+            test_pairs(pa, g * SPT_GROUP, o, d, dod, best, idx, bp);
+#pragma unroll
+            for (int j = 0; j < SPT_GROUP / 2; ++j) pa[j] = ld_pair(pair_s, (g + 2) * (SPT_GROUP / 2) + j);
+            test_pairs(pb, (g + 1) * SPT_GROUP, o, d, dod, best, idx, bp);
         }
+#else
+        float4 ga[SPT_GROUP], gb[SPT_GROUP];
+#pragma unroll
+        for (int k = 0; k < SPT_GROUP; ++k) ga[k] = ld_uniform(hit_s, k);
+        // two groups per trip, ping-ponging two scalar register buffers
+        for (uint32_t g = 0; g < a.scene.ngroups; g += 2) {
+#pragma unroll
+            for (int k = 0; k < SPT_GROUP; ++k) gb[k] = ld_uniform(hit_s, (g + 1) * SPT_GROUP + k);
+            test_group(ga, g * SPT_GROUP, o, d, dod, best, idx, bp);
+#pragma unroll
+            for (int k = 0; k < SPT_GROUP; ++k) ga[k] = ld_uniform(hit_s, (g + 2) * SPT_GROUP + k);
+            test_group(gb, (g + 1) * SPT_GROUP, o, d, dod, best, idx, bp);
+        }
+
+#endif
 
         // ---- one shading step ----
         if (phase != PH_IDLE) {
@@ -252,6 +402,13 @@ __global__ __launch_bounds__(kRenderBlock) void render_kernel(RenderArgs a)
     if (done) atomicAdd(&a.counters[1], done);
     if (dropped) atomicAdd(&a.counters[2], dropped);
     if (lane == 0) atomicAdd(&a.counters[0], casts);
+#if SPT_DIAG
+    if (lane == 0) {
+        atomicAdd(&a.counters[4], d_iters);
+        atomicAdd(&a.counters[5], d_hitblk);
+        atomicAdd(&a.counters[6], d_lanehits);
+    }
+#endif
 }
 
 __global__ __launch_bounds__(256) void fold_kernel(FoldArgs a)
@@ -259,9 +416,9 @@ __global__ __launch_bounds__(256) void fold_kernel(FoldArgs a)
     const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= a.npix) return;
     float4 acc = a.first ? make_float4(0.f, 0.f, 0.f, 0.f) : a.acc[p];
-    const float4 *s = a.samples + (size_t)p * a.spp_batch;
+    const float4 *s = a.samples + p;
     for (uint32_t k = 0; k < a.spp_batch; ++k) {
-        const float4 c = s[k];
+        const float4 c = s[(size_t)k * a.npix];  // [sample][pixel]: coalesced across lanes
         if (a.mode == 0 || c.w != 0.f) {
             acc.x = acc.x + c.x;
             acc.y = acc.y + c.y;
@@ -357,6 +514,8 @@ hipError_t launch_selftest(const float *a, const float *b, const uint32_t *bits,
     hipLaunchKernelGGL(selftest_kernel, dim3((n + 255) / 256), dim3(256), 0, s, a, b, bits, n, out);
     return hipGetLastError();
 }
+
+uint32_t render_group_size() { return SPT_GROUP; }
 
 hipError_t render_occupancy(uint32_t block, int *blocks_per_cu)
 {

@@ -118,7 +118,9 @@ class Context:
     def stats(self) -> dict:
         s = _native.Stats()
         self._check(_native.lib().spt_get_stats(self._h, ctypes.byref(s)))
-        return {k: getattr(s, k) for k, _ in _native.Stats._fields_}
+        d = {k: getattr(s, k) for k, _ in _native.Stats._fields_}
+        d["diag"] = list(s.diag)
+        return d
 
     def reset_stats(self) -> None:
         self._check(_native.lib().spt_reset_stats(self._h))

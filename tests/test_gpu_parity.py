@@ -154,20 +154,26 @@ def test_region_vs_oracle_with_gdata_bytes(spt, ctx, oracle, golden_scenes, task
     assert np.array_equal(g, gw), "g_data bytes (region written, rest untouched)"
 
 
+def _mirror_lattice():
+    """6x6x6 lattice of fuzzy mirror spheres over the ground: ~4% of paths need
+    more than RenderSegmentTask's 10 passes (TaskBasedPathTracer.hpp:81)."""
+    pts = [[(i - 2.5), 0.2 + j, 1.5 + k, 0] for i in range(6) for j in range(6) for k in range(6)]
+    c = np.float32([[0, -1000.5, 0, 0]] + pts)
+    n = len(c)
+    r = np.float32([1000] + [0.47] * (n - 1))
+    col = np.float32([[30, 144, 255, 0]] + [[200, 100, 50, 0]] * (n - 1))
+    m = np.uint8([3] + [1] * (n - 1))
+    fz = np.float32([0] + [0.02] * (n - 1))
+    return c, r, col, m, fz
+
+
 def test_task_mode_drops_deep_specular_paths(spt, ctx, oracle):
-    """Two facing mirrors: many paths exceed RenderSegmentTask's 10 passes
-    (TaskBasedPathTracer.hpp:81) and are dropped; the resolve averages the rest."""
-    c = np.float32([[0, -1000.5, 0, 0], [-0.55, 0.5, 2, 0], [0.55, 0.5, 2, 0]])
-    r = np.float32([1000, 0.5, 0.5])
-    col = np.float32([[30, 144, 255, 0], [200, 50, 50, 0], [50, 200, 50, 0]])
-    m = np.uint8([3, 1, 1])
-    fz = np.float32([0, 0.0, 0.05])
-    scene = spt.Scene(c, r, col, m, fz)
-    setup(ctx, scene, 64, 64, 16, 8, seed=9)
+    arrays = _mirror_lattice()
+    setup(ctx, spt.Scene(*arrays), 64, 64, 16, 8, seed=9)
     ctx.reset_stats()
     got = ctx.render_segment(0, 64, 0, 64, task=True)
     assert ctx.stats()["dropped"] > 0
-    osc = oracle.OracleScene(c, r, col, m, fz)
+    osc = oracle.OracleScene(*arrays)
     fr = oracle.make_frame(spt.camera_basis(EYE, LOOK, UP), EYE, SKY, 64, 64, 16, 8, 9)
     want, _ = oracle.render_segment(osc, fr, 0, 64, 0, 64, task=True)
     assert_bitwise(got[:, :3], want[:, :3], "task mode with drops")

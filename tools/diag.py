@@ -1,0 +1,23 @@
+"""Diagnostic run: in-kernel counters of the SPT_DIAG build (never used for timing).
+Usage on the GPU box: SPT_LIB=libspt_hip_diag.so python tools/diag.py [config]"""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import simplepathtracer_amd as spt  # noqa: E402
+
+cfg = sys.argv[1] if len(sys.argv) > 1 else "c2"
+W, H, spp, b = {"c2": (1200, 800, 100, 50), "c2s": (1200, 800, 8, 50)}[cfg]
+ctx = spt.Context(0)
+scene = spt.generate_spheres(1)
+ctx.set_scene(scene)
+ctx.set_camera(spt.camera_basis(), spt.scene.DEFAULT_EYE, spt.INIT_COLOR)
+ctx.set_params(W, H, spp, b, 1)
+ctx.render_segment(0, H, 0, W)
+ctx.reset_stats()
+ctx.render_segment(0, H, 0, W)
+st = ctx.stats()
+it, hb, lh, _ = st["diag"]
+print(f"casts={st['casts']} samples={st['samples']} wave_iters={it} live_lanes/iter={st['casts']/max(it,1):.2f}")
+print(f"hit-block entries/iter={hb/max(it,1):.2f} of {scene.n} spheres; lane hits/cast={lh/max(st['casts'],1):.3f}")
+print(f"render_ms={st['render_ms']:.3f}")

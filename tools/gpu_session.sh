@@ -1,0 +1,25 @@
+#!/bin/bash
+# One GPU-box session: build, GPU tests, smoke, bench.  Stops at the first step
+# that ends in a fault / abort / timeout (anything but 0 or a pytest failure 1).
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+STEPS="${STEPS:-tests smoke bench}"
+python -c "import __graft_entry__ as g; g.build()" > gpurun_out/build.log 2>&1 || { echo "build failed"; tail -20 gpurun_out/build.log; exit 3; }
+run() {  # name timeout cmd...
+  local name=$1 t=$2; shift 2
+  echo "== $name: $*"
+  timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc"; tail -n 25 "gpurun_out/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+}
+for s in $STEPS; do
+  case $s in
+    tests) run gpu_tests 900 python -m pytest tests -m gpu -x -q ;;
+    alltests) run gpu_tests 900 python -m pytest tests -m gpu -q ;;
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) run bench 600 python bench.py ;;
+    *) run custom 900 bash -c "$s" ;;
+  esac
+done

@@ -1,0 +1,119 @@
+// RenderSegmentShim.hpp -- the reference's two render entry points rebuilt on the
+// MI355X C ABI (spt_hip.h).  Include it in the reference's translation unit in
+// place of SingleThreadPathTracer.hpp / TaskBasedPathTracer.hpp (or put
+// include/dropin first on the include path, which does exactly that) and link
+// libspt_hip.so.  Renderer.hpp, Main.cpp and the GL preview compile unchanged.
+//
+// Replaces:
+//   void RenderSegment(RenderSegmentData)       SingleThreadPathTracer.hpp:114-137
+//   void RenderSegmentTask(RenderSegmentData)   TaskBasedPathTracer.hpp:54-206
+// Reads the same globals (Globals.hpp:12-37: g_width, g_height, g_samples,
+// g_bounces, viewMatrix, eyePos, initColor, g_spheres, g_radii, g_colors,
+// g_materials, g_diffuses, g_sphereNumber) and writes the same g_data bytes
+// (IOHelpers.hpp:17-22).  The reference has no error channel, so a failure is
+// reported on stderr and aborts.  Sampling uses the keyed per-(pixel, sample)
+// stream seeded with spt_shim::seed (default 1; SPT_SEED overrides) instead of
+// the clock-seeded thread_local splitmix (Random.hpp:86-93).
+#pragma once
+
+#include <spt_hip.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+namespace spt_shim {
+
+inline uint64_t seed = std::getenv("SPT_SEED") ? std::strtoull(std::getenv("SPT_SEED"), nullptr, 0) : 1ull;
+
+inline void check(spt_ctx *ctx, int rc, const char *what)
+{
+    if (rc != SPT_OK) {
+        std::fprintf(stderr, "spt: %s failed: %s\n", what, spt_last_error(ctx));
+        std::abort();
+    }
+}
+
+inline spt_ctx *context()
+{
+    static spt_ctx *ctx = [] {
+        spt_ctx *c = nullptr;
+        const char *dev = std::getenv("SPT_DEVICE");
+        check(nullptr, spt_ctx_create(dev ? std::atoi(dev) : 0, &c), "spt_ctx_create");
+        return c;
+    }();
+    return ctx;
+}
+
+// Push the reference globals to the device when they changed since the last call.
+inline void sync_globals()
+{
+    static std::mutex mu;
+    static std::vector<float> last;
+    std::lock_guard<std::mutex> lk(mu);
+    const uint32_t n = g_sphereNumber;
+    std::vector<float> centers(4 * (size_t)n), colors(4 * (size_t)n), radii(n), fuzz(n);
+    std::vector<uint8_t> mats(n);
+    for (uint32_t i = 0; i < n; ++i) {
+        for (int c = 0; c < 4; ++c) {
+            centers[4 * i + c] = g_spheres[i].xyzw[c];
+            colors[4 * i + c] = g_colors[i].xyzw[c];
+        }
+        radii[i] = g_radii[i];
+        fuzz[i] = g_diffuses[i];
+        mats[i] = static_cast<uint8_t>(g_materials[i]);
+    }
+    float view[16], eye[4], sky[4];
+    for (int i = 0; i < 16; ++i) view[i] = viewMatrix.array[i];
+    for (int i = 0; i < 4; ++i) {
+        eye[i] = eyePos.xyzw[i];
+        sky[i] = initColor.xyzw[i];
+    }
+    std::vector<float> key;
+    key.reserve(centers.size() * 2 + 3 * n + 40);
+    key.insert(key.end(), centers.begin(), centers.end());
+    key.insert(key.end(), colors.begin(), colors.end());
+    key.insert(key.end(), radii.begin(), radii.end());
+    key.insert(key.end(), fuzz.begin(), fuzz.end());
+    for (uint8_t m : mats) key.push_back((float)m);
+    key.insert(key.end(), view, view + 16);
+    key.insert(key.end(), eye, eye + 4);
+    key.insert(key.end(), sky, sky + 4);
+    key.push_back((float)g_width);
+    key.push_back((float)g_height);
+    key.push_back((float)g_samples);
+    key.push_back((float)g_bounces);
+    key.push_back((float)(seed & 0xFFFFFF));
+    if (key.size() == last.size() && std::memcmp(key.data(), last.data(), key.size() * sizeof(float)) == 0) return;
+    spt_ctx *ctx = context();
+    check(ctx, spt_set_scene(ctx, centers.data(), radii.data(), colors.data(), mats.data(), fuzz.data(), n),
+          "spt_set_scene");
+    check(ctx, spt_set_camera(ctx, view, eye, sky), "spt_set_camera");
+    check(ctx, spt_set_params(ctx, g_width, g_height, g_samples, g_bounces, seed), "spt_set_params");
+    last.swap(key);
+}
+
+}  // namespace spt_shim
+
+// SingleThreadPathTracer.hpp:114-137
+inline void RenderSegment(RenderSegmentData segment)
+{
+    spt_shim::sync_globals();
+    spt_ctx *ctx = spt_shim::context();
+    spt_shim::check(ctx,
+                    spt_render_segment(ctx, segment.yBegin, segment.yEnd, segment.xBegin, segment.xEnd, nullptr, g_data),
+                    "spt_render_segment");
+}
+
+// TaskBasedPathTracer.hpp:54-206 (exact for square tiles)
+inline void RenderSegmentTask(RenderSegmentData segment)
+{
+    spt_shim::sync_globals();
+    spt_ctx *ctx = spt_shim::context();
+    spt_shim::check(ctx,
+                    spt_render_segment_task(ctx, segment.yBegin, segment.yEnd, segment.xBegin, segment.xEnd, nullptr,
+                                            g_data),
+                    "spt_render_segment_task");
+}

@@ -58,3 +58,22 @@ def test_scene_generators_validate_arguments(native):
     assert s.n == 1000 and (s.radii > 0).all() and set(np.unique(s.materials)) <= {1, 2, 3}
     c = spt.cornell3()
     assert c.n == 4 and list(c.materials) == [3, 3, 1, 2]
+
+
+def _build_shim_harness(tmp_path):
+    import os
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    lib = os.path.join(root, "simplepathtracer_amd", "lib")
+    exe = str(tmp_path / "shim_harness")
+    subprocess.run(["g++", "-std=c++17", "-O2", "-Wall", "-Werror", f"-I{root}/include",
+                    os.path.join(root, "tests", "cpp", "shim_harness.cpp"), f"-L{lib}", "-lspt_hip",
+                    f"-Wl,-rpath,{lib}", "-o", exe], check=True)
+    return exe
+
+
+def test_cpp_dropin_shim_compiles_against_the_c_abi(native, tmp_path):
+    """include/spt/RenderSegmentShim.hpp + include/spt_hip.h build with plain g++
+    (no HIP headers) in a translation unit shaped like the reference's."""
+    import os
+    assert os.path.exists(_build_shim_harness(tmp_path))

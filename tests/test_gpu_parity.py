@@ -321,3 +321,25 @@ def test_concurrent_render_jobs_share_a_context(spt, golden_scenes):
     spt.RenderSegment(spt.RenderSegmentData(0, 160, 0, 240), g)
     assert np.array_equal(tiled, g.g_data)
     g.ctx.close()
+
+
+@pytest.mark.parametrize("w,h,tc,task", [(1200, 800, 4, 0), (800, 800, 4, 1)])
+def test_cpp_dropin_shim_renders_like_the_context(spt, golden_scenes, tmp_path, w, h, tc, task):
+    """The C++ RenderSegment/RenderSegmentTask shim, driven by RenderJob-style
+    concurrent threads over a tc x tc tile grid, writes the same g_data bytes as
+    a one-shot render through the context."""
+    import subprocess
+    from test_abi import _build_shim_harness
+    exe = _build_shim_harness(tmp_path)
+    out = tmp_path / "g_data.bin"
+    subprocess.run([exe, str(out), str(w), str(h), "6", "50", str(tc), str(task)], check=True, timeout=300)
+    got = np.fromfile(out, np.uint8)
+    c = spt.Context(0)
+    setup(c, scene_from(spt, golden_scenes, "random"), w, h, 6, 50)
+    want = np.zeros(w * h * 3, np.uint8)
+    sw, sh = w // tc, h // tc
+    for j in range(tc):
+        for i in range(tc):
+            c.render_segment(sh * j, sh * j + sh, sw * i, sw * i + sw, want, task=bool(task))
+    c.close()
+    assert np.array_equal(got, want)

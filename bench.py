@@ -76,6 +76,7 @@ def main():
     ap.add_argument("--cpu-spp", type=int, default=8, help="spp of the bounded CPU-baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dump", default="", help="write rank 0's final g_data bytes to this file")
     args = ap.parse_args()
 
     import torch
@@ -87,10 +88,16 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.gpus != world and world > 1:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    # SPT_DIST_BACKEND=gloo rehearses the N>1 flow with several ranks on one GPU
+    backend = os.environ.get("SPT_DIST_BACKEND", "nccl")
+    local = local % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     scene_name, W, H, spp, bounces = CONFIGS[args.config]
     scene = make_scene(spt, scene_name)
@@ -101,25 +108,18 @@ def main():
     ctx.set_camera(view, spt.scene.DEFAULT_EYE, spt.INIT_COLOR)
     ctx.set_params(W, H, spp, bounces, 1)
 
-    strip = args.strip
-    rows = [spt.rows_count(0, H, strip, world, p) for p in range(world)]
-    max_rows = max(rows)
+    from simplepathtracer_amd.distributed import FrameSplit, render_frame
+    split = FrameSplit(W, H, world, args.strip)
     stream = torch.cuda.current_stream(dev).cuda_stream
     frame = torch.zeros((H * W, 4), dtype=torch.float32, device=dev) if rank == 0 else None
     g_data = torch.zeros(W * H * 3, dtype=torch.uint8, device=dev) if rank == 0 else None
+    local_tile = gathered = None
     if world > 1:
-        local_tile = torch.zeros((max_rows * W, 4), dtype=torch.float32, device=dev)
-        gathered = torch.zeros((world, max_rows * W, 4), dtype=torch.float32, device=dev)
+        local_tile = torch.zeros((split.tile_pixels(), 4), dtype=torch.float32, device=dev)
+        gathered = torch.zeros((world * split.tile_pixels(), 4), dtype=torch.float32, device=dev)
 
     def step():
-        if world == 1:
-            ctx.render_rows_async(mode, 0, H, 1, 1, 0, 0, W, frame.data_ptr(), g_data.data_ptr(), stream)
-        else:
-            ctx.render_rows_async(mode, 0, H, strip, world, rank, 0, W, local_tile.data_ptr(), 0, stream)
-            dist.all_gather_into_tensor(gathered, local_tile)
-            if rank == 0:
-                ctx.assemble_rows_async(gathered.data_ptr(), max_rows, 0, H, strip, world, 0, W, frame.data_ptr(),
-                                        g_data.data_ptr(), stream)
+        render_frame(ctx, split, rank, mode, local_tile, gathered, frame, g_data, stream)
 
     for _ in range(args.warmup):
         step()
@@ -173,7 +173,7 @@ def main():
             "config": {"workload": f"{args.config}: {scene_name} scene seed 1 (N={scene.n} spheres), {W}x{H}, "
                                    f"{spp} spp, depth {bounces}, {args.mode} mode",
                        "width": W, "height": H, "spp": spp, "bounces": bounces, "spheres": scene.n,
-                       "parallelism": f"row-strips{strip}x{world}" if world > 1 else "1 GPU"},
+                       "parallelism": f"row-strips{args.strip}x{world}" if world > 1 else "1 GPU"},
             "roofline": {"bound": "valu", "achieved": round(achieved, 3), "peak": round(VALU_PEAK_TOPS, 2),
                          "unit": "TFLOP/s", "frac": round(achieved / VALU_PEAK_TOPS, 4), "traffic": None,
                          "kernel": "render_kernel", "avg_launch_ms": round(avg_ms, 4),
@@ -189,6 +189,8 @@ def main():
             cw, ch = (W, H) if args.config != "c3" else (1920, 1080)
             out["cpu_baseline"] = cpu_baseline(scene, view, cw, ch, args.cpu_spp, bounces, args.cpu_threads)
         print(json.dumps(out), flush=True)
+        if args.dump:
+            g_data.cpu().numpy().tofile(args.dump)
     ctx.close()
     if world > 1:
         dist.destroy_process_group()

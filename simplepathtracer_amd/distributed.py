@@ -1,0 +1,68 @@
+"""Multi-GPU frame split (north_star: tile-partitioned across the GPUs of a node
+with an RCCL gather of the per-tile framebuffers).
+
+One process per GPU.  The frame's rows are dealt in interleaved `strip`-row
+strips: rank r owns strips r, r+N, r+2N, ...  Each rank renders its rows into a
+compact float4 tile (spt_render_rows_async); one all_gather_into_tensor over
+RCCL/xGMI brings every tile to every rank and rank 0 scatters them into the frame
+and the RGB8 g_data buffer (spt_assemble_rows_async).  Per-pixel results do not
+depend on the split (keyed per-(pixel, sample) RNG), so any N gives the 1-GPU frame.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+
+from .renderer import rows_count
+
+
+@dataclass(frozen=True)
+class FrameSplit:
+    width: int
+    height: int
+    world: int
+    strip: int = 8
+
+    @property
+    def rows(self) -> list[int]:
+        return [rows_count(0, self.height, self.strip, self.world, r) for r in range(self.world)]
+
+    @property
+    def max_rows(self) -> int:
+        return max(self.rows)
+
+    def local_rows(self, rank: int) -> np.ndarray:
+        """Global y of each local row of `rank` (the kernel's RowMap, restated)."""
+        n = rows_count(0, self.height, self.strip, self.world, rank)
+        k = np.arange(n)
+        blk = k // self.strip
+        return (blk * self.world + rank) * self.strip + (k - blk * self.strip)
+
+    def tile_pixels(self) -> int:
+        return self.max_rows * self.width
+
+
+def gather_tiles(local_tile, gathered, group=None) -> None:
+    """All ranks' tiles -> gathered[world*max_rows*width, 4], rank-major (one
+    collective; the concatenated form is accepted by both RCCL and gloo)."""
+    import torch.distributed as dist
+    dist.all_gather_into_tensor(gathered, local_tile, group=group)
+
+
+def render_frame(ctx, split: FrameSplit, rank: int, mode: int, local_tile, gathered=None, frame=None,
+                 g_data=None, stream=0, group=None) -> None:
+    """One distributed frame: render own rows, gather, assemble on rank 0.
+    Tensors are device tensors; `stream` is the hipStream_t the launches use."""
+    if split.world == 1:
+        ctx.render_rows_async(mode, 0, split.height, 1, 1, 0, 0, split.width,
+                              frame.data_ptr() if frame is not None else 0,
+                              g_data.data_ptr() if g_data is not None else 0, stream)
+        return
+    ctx.render_rows_async(mode, 0, split.height, split.strip, split.world, rank, 0, split.width,
+                          local_tile.data_ptr(), 0, stream)
+    gather_tiles(local_tile, gathered, group)
+    if rank == 0:
+        ctx.assemble_rows_async(gathered.data_ptr(), split.max_rows, 0, split.height, split.strip, split.world, 0,
+                                split.width, frame.data_ptr() if frame is not None else 0,
+                                g_data.data_ptr() if g_data is not None else 0, stream)

@@ -343,3 +343,21 @@ def test_cpp_dropin_shim_renders_like_the_context(spt, golden_scenes, tmp_path, 
             c.render_segment(sh * j, sh * j + sh, sw * i, sw * i + sw, want, task=bool(task))
     c.close()
     assert np.array_equal(got, want)
+
+
+def test_bench_two_ranks_on_one_gpu_matches_one_rank(spt, tmp_path):
+    """bench.py's N>1 flow (strip split, all_gather_into_tensor, rank-0 assemble)
+    rehearsed with two gloo ranks sharing cuda:0: same g_data as N=1."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    one, two = tmp_path / "one.bin", tmp_path / "two.bin"
+    base = [sys.executable, os.path.join(root, "bench.py"), "--steps", "1", "--warmup", "0", "--no-cpu-baseline"]
+    subprocess.run(base + ["--dump", str(one)], check=True, timeout=300, cwd=root)
+    env = dict(os.environ, SPT_DIST_BACKEND="gloo")
+    subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+                    "--master-addr=127.0.0.1", "--master-port=29533"] + base[1:] + ["--gpus", "2", "--dump", str(two)],
+                   check=True, timeout=300, cwd=root, env=env)
+    a, b = np.fromfile(one, np.uint8), np.fromfile(two, np.uint8)
+    assert a.size == 1200 * 800 * 3 and np.array_equal(a, b)

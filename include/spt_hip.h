@@ -64,8 +64,9 @@ typedef struct spt_stats {
     double last_render_ms; /* device time of the most recent render launch */
     uint32_t grid_blocks;  /* persistent grid of the render kernel */
     uint32_t block_threads;
-    uint64_t diag[4];      /* diagnostic build only (-DSPT_DIAG=1): wave iterations,
-                              hit-block entries, lane hits, reserved */
+    uint64_t diag[8];      /* diagnostic build only (-DSPT_DIAG=1): wave iterations,
+                              clusters entered, lanes wanting them, s_memtime cycles in
+                              cast / shading / refill, 2 reserved */
 } spt_stats;
 
 int spt_abi_version(void);
@@ -94,6 +95,11 @@ int spt_set_camera(spt_ctx *ctx, const float view[16], const float eye[4], const
  * bounces == 0 is rejected: `while (--bounceCount && ...)` would never count
  * down (SingleThreadPathTracer.hpp:28). */
 int spt_set_params(spt_ctx *ctx, uint32_t width, uint32_t height, uint32_t spp, uint32_t bounces, uint64_t seed);
+/* Hot-loop culling: small spheres are grouped into clusters of k (default 8)
+ * whose conservative bounding test skips them exactly when no ray of a wave can
+ * pass RaySphereIntersection for any member; k = 0 tests every sphere for every
+ * ray (the reference's brute force).  Results are identical either way. */
+int spt_set_cluster_size(spt_ctx *ctx, uint32_t k);
 /* Upper bound of the per-sample workspace (default 4 GiB).  Larger frames are
  * rendered in sample batches folded in order. */
 int spt_set_workspace(spt_ctx *ctx, uint64_t bytes);
@@ -116,8 +122,9 @@ int spt_render_segment_task(spt_ctx *ctx, uint32_t yBegin, uint32_t yEnd, uint32
  * GPUs (parts = world size, part = rank; parts = 1 for a plain rectangle).
  * d_rgba (nullable): device float4 per local pixel, local order (row k of the
  *   owned rows, then x).  d_rgb8 (nullable): device full frame in g_data layout.
- * stream: a hipStream_t (NULL = the context's own stream).  Returns after
- * enqueueing; pair with spt_synchronize or the caller's stream sync. */
+ * stream: a hipStream_t; NULL is HIP's default (null) stream, as for any HIP
+ * call.  Launches are ordered on that stream only.  Returns after enqueueing;
+ * pair with spt_synchronize or the caller's stream sync. */
 int spt_render_rows_async(spt_ctx *ctx, int mode, uint32_t yBegin, uint32_t yEnd, uint32_t strip, uint32_t parts,
                           uint32_t part, uint32_t xBegin, uint32_t xEnd, void *d_rgba, void *d_rgb8, void *stream);
 /* Number of rows the (yBegin, yEnd, strip, parts, part) map owns. */

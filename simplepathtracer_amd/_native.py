@@ -39,7 +39,7 @@ class Stats(ctypes.Structure):
         ("last_render_ms", ctypes.c_double),
         ("grid_blocks", ctypes.c_uint32),
         ("block_threads", ctypes.c_uint32),
-        ("diag", ctypes.c_uint64 * 4),
+        ("diag", ctypes.c_uint64 * 8),
     ]
 
 
@@ -79,6 +79,7 @@ def lib() -> ctypes.CDLL:
         "spt_set_camera": ([P, P, P, P], I),
         "spt_set_params": ([P, u32, u32, u32, u32, u64], I),
         "spt_set_workspace": ([P, u64], I),
+        "spt_set_cluster_size": ([P, u32], I),
         "spt_render_segment": ([P, u32, u32, u32, u32, P, P], I),
         "spt_render_segment_task": ([P, u32, u32, u32, u32, P, P], I),
         "spt_render_rows_async": ([P, I, u32, u32, u32, u32, u32, u32, u32, P, P, P], I),

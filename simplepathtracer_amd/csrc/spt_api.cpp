@@ -6,6 +6,7 @@
 // RenderSegment (SingleThreadPathTracer.hpp:114-137) and RenderSegmentTask
 // (TaskBasedPathTracer.hpp:54-206) as render + fold launches.
 #include "spt_hip.h"
+#include "spt_accel.h"
 #include "spt_internal.h"
 
 #include <hip/hip_runtime.h>
@@ -40,11 +41,15 @@ struct spt_ctx {
     uint32_t grid = 0, block = spt::kRenderBlock, claim = 128;
 
     // scene (Globals.hpp:31-37)
-    float4 *d_hit = nullptr, *d_shade = nullptr;
-    float *d_hitp = nullptr;
-    uint32_t *d_mat = nullptr;
-    uint32_t n = 0, scene_cap = 0;
+    float4 *d_hit = nullptr, *d_shade = nullptr, *d_slots = nullptr, *d_bounds = nullptr;
+    uint32_t *d_mat = nullptr, *d_orig = nullptr;
+    size_t hit_cap = 0, shade_cap = 0, mat_cap = 0, slots_cap = 0, orig_cap = 0, bounds_cap = 0;
+    uint32_t n = 0;
     bool scene_set = false;
+    // host copy of the hit geometry, to rebuild the traversal tables
+    std::vector<float> h_centers, h_radii;
+    uint32_t cluster_k = 8;  // slots per culling cluster; 0 = brute force
+    spt::AccelView accel{};
     // camera (Globals.hpp:21-29)
     spt::Camera cam{};
     bool cam_set = false;
@@ -98,7 +103,7 @@ int ensure(spt_ctx *ctx, T **p, size_t *cap, size_t count)
 {
     if (*cap >= count && *p) return SPT_OK;
     if (*p) {
-        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        HIP_TRY(ctx, hipDeviceSynchronize());  // launches on caller streams may still read it
         HIP_TRY(ctx, hipFree(*p));
         *p = nullptr;
         *cap = 0;
@@ -188,8 +193,7 @@ int render_impl(spt_ctx *ctx, int mode, const spt::RowMap &map, float4 *d_rgba, 
     }
 
     spt::RenderArgs ra{};
-    ra.scene = spt::DeviceScene{ctx->d_hit, ctx->d_hitp, ctx->d_shade, ctx->d_mat, ctx->n,
-                                (ctx->n + spt::render_group_size() - 1) / spt::render_group_size()};
+    ra.scene = spt::DeviceScene{ctx->d_hit, ctx->d_shade, ctx->d_mat, ctx->n, ctx->accel};
     ra.cam = ctx->cam;
     ra.width = ctx->W;
     ra.height = ctx->H;
@@ -238,6 +242,29 @@ int render_impl(spt_ctx *ctx, int mode, const spt::RowMap &map, float4 *d_rgba, 
         ctx->pending_fold.push_back(ef);
     }
     if (ctx->pending_render.size() > 256) return collect_timings(ctx);
+    return SPT_OK;
+}
+
+template <class T>
+int upload(spt_ctx *ctx, T **p, size_t *cap, const std::vector<T> &v)
+{
+    int rc = ensure(ctx, p, cap, v.size());
+    if (rc) return rc;
+    HIP_TRY(ctx, hipMemcpy(*p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+    return SPT_OK;
+}
+
+// Build and upload the hot-loop traversal tables (spt_accel.cpp) for the current scene.
+int rebuild_accel(spt_ctx *ctx)
+{
+    const uint32_t g = spt::render_group_size();
+    spt::AccelTables t = spt::build_accel(ctx->h_centers.data(), ctx->h_radii.data(), ctx->n, ctx->cluster_k, g);
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    int rc = upload(ctx, &ctx->d_slots, &ctx->slots_cap, t.slots);
+    if (!rc) rc = upload(ctx, &ctx->d_orig, &ctx->orig_cap, t.orig);
+    if (!rc) rc = upload(ctx, &ctx->d_bounds, &ctx->bounds_cap, t.bounds);
+    if (rc) return rc;
+    ctx->accel = spt::AccelView{ctx->d_slots, ctx->d_orig, ctx->d_bounds, t.always_groups, t.clusters, t.cluster_k};
     return SPT_OK;
 }
 
@@ -324,10 +351,11 @@ int spt_ctx_create(int device, spt_ctx **out)
     // extra blocks only queue.  SPT_BLOCKS_PER_CU overrides for tuning.
     if (const char *e = std::getenv("SPT_BLOCKS_PER_CU")) per_cu = std::max(1, std::atoi(e));
     if (const char *e = std::getenv("SPT_CLAIM")) ctx->claim = (uint32_t)std::max(1, std::atoi(e));
+    if (const char *e = std::getenv("SPT_CLUSTER_K")) ctx->cluster_k = (uint32_t)std::max(0, std::atoi(e));
     ctx->grid = (uint32_t)(per_cu * ctx->num_cu);
     if (hipMalloc((void **)&ctx->d_head, sizeof(uint32_t)) != hipSuccess ||
-        hipMalloc((void **)&ctx->d_counters, 8 * sizeof(unsigned long long)) != hipSuccess ||
-        hipMemset(ctx->d_counters, 0, 8 * sizeof(unsigned long long)) != hipSuccess) {
+        hipMalloc((void **)&ctx->d_counters, 12 * sizeof(unsigned long long)) != hipSuccess ||
+        hipMemset(ctx->d_counters, 0, 12 * sizeof(unsigned long long)) != hipSuccess) {
         spt_ctx_destroy(ctx);
         return fail(nullptr, SPT_ERR_NOMEM, "workspace allocation failed");
     }
@@ -345,7 +373,7 @@ void spt_ctx_destroy(spt_ctx *ctx)
             (void)hipEventDestroy(p.a);
             (void)hipEventDestroy(p.b);
         }
-    void *bufs[] = {ctx->d_hit, ctx->d_hitp, ctx->d_shade, ctx->d_mat, ctx->d_samples, ctx->d_acc,
+    void *bufs[] = {ctx->d_hit, ctx->d_shade, ctx->d_mat, ctx->d_slots, ctx->d_orig, ctx->d_bounds, ctx->d_samples, ctx->d_acc,
                     ctx->d_head, ctx->d_counters, ctx->d_stage, ctx->d_frame8};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
@@ -367,50 +395,23 @@ int spt_set_scene(spt_ctx *ctx, const float *centers4, const float *radii, const
     if (n > 0 && (!centers4 || !radii || !colors4 || !materials || !fuzz))
         return fail(ctx, SPT_ERR_ARG, "null scene array");
     HIP_TRY(ctx, hipSetDevice(ctx->device));
-    // hit table padded to a multiple of 2*kMaxGroup plus two more groups (the hot
-    // loop runs groups in pairs and prefetches two groups ahead); padding spheres have
-    // r*r = -inf so RaySphereIntersection never passes for them.
-    const size_t npad = ((size_t)n + 2 * spt::kMaxGroup - 1) / (2 * spt::kMaxGroup) * (2 * spt::kMaxGroup) +
-                        2 * spt::kMaxGroup;
-    std::vector<float4> hit(npad, make_float4(0.f, 0.f, 0.f, -INFINITY)), shade(std::max<size_t>(n, 1));
-    std::vector<uint32_t> mat(std::max<size_t>(n, 1));
+    std::vector<float4> hit(std::max<uint32_t>(n, 1)), shade(std::max<uint32_t>(n, 1));
+    std::vector<uint32_t> mat(std::max<uint32_t>(n, 1));
     for (uint32_t i = 0; i < n; ++i) {
         const float r = radii[i];
         hit[i] = make_float4(centers4[4 * i], centers4[4 * i + 1], centers4[4 * i + 2], r * r);
         shade[i] = make_float4(colors4[4 * i], colors4[4 * i + 1], colors4[4 * i + 2], fuzz[i]);
         mat[i] = materials[i];
     }
-    if (npad > ctx->scene_cap) {
-        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-        for (void *b : {(void *)ctx->d_hit, (void *)ctx->d_shade, (void *)ctx->d_mat, (void *)ctx->d_hitp})
-            if (b) HIP_TRY(ctx, hipFree(b));
-        ctx->d_hit = ctx->d_shade = nullptr;
-        ctx->d_hitp = nullptr;
-        ctx->d_mat = nullptr;
-        ctx->scene_cap = 0;
-        HIP_TRY(ctx, hipMalloc((void **)&ctx->d_hit, npad * sizeof(float4)));
-        HIP_TRY(ctx, hipMalloc((void **)&ctx->d_hitp, npad * sizeof(float4)));
-        HIP_TRY(ctx, hipMalloc((void **)&ctx->d_shade, npad * sizeof(float4)));
-        HIP_TRY(ctx, hipMalloc((void **)&ctx->d_mat, npad * sizeof(uint32_t)));
-        ctx->scene_cap = (uint32_t)npad;
-    }
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-    HIP_TRY(ctx, hipMemcpy(ctx->d_hit, hit.data(), npad * sizeof(float4), hipMemcpyHostToDevice));
-    std::vector<float> hitp(npad * 4);
-    for (size_t j = 0; j < npad / 2; ++j)
-        for (int h = 0; h < 2; ++h) {
-            const float4 &v = hit[2 * j + h];
-            hitp[8 * j + 0 + h] = v.x;
-            hitp[8 * j + 2 + h] = v.y;
-            hitp[8 * j + 4 + h] = v.z;
-            hitp[8 * j + 6 + h] = v.w;
-        }
-    HIP_TRY(ctx, hipMemcpy(ctx->d_hitp, hitp.data(), npad * sizeof(float4), hipMemcpyHostToDevice));
-    if (n) {
-        HIP_TRY(ctx, hipMemcpy(ctx->d_shade, shade.data(), n * sizeof(float4), hipMemcpyHostToDevice));
-        HIP_TRY(ctx, hipMemcpy(ctx->d_mat, mat.data(), n * sizeof(uint32_t), hipMemcpyHostToDevice));
-    }
+    int rc = upload(ctx, &ctx->d_hit, &ctx->hit_cap, hit);
+    if (!rc) rc = upload(ctx, &ctx->d_shade, &ctx->shade_cap, shade);
+    if (!rc) rc = upload(ctx, &ctx->d_mat, &ctx->mat_cap, mat);
+    if (rc) return rc;
+    ctx->h_centers.assign(centers4, centers4 + 4 * (size_t)n);
+    ctx->h_radii.assign(radii, radii + n);
     ctx->n = n;
+    if ((rc = rebuild_accel(ctx))) return rc;
     ctx->scene_set = true;
     return SPT_OK;
 }
@@ -448,6 +449,17 @@ int spt_set_params(spt_ctx *ctx, uint32_t width, uint32_t height, uint32_t spp, 
     ctx->seed = seed;
     ctx->params_set = true;
     return SPT_OK;
+}
+
+int spt_set_cluster_size(spt_ctx *ctx, uint32_t k)
+{
+    if (!ctx) return fail(nullptr, SPT_ERR_ARG, "null context");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    if (k > 256) return fail(ctx, SPT_ERR_ARG, "cluster size %u > 256", k);
+    ctx->cluster_k = k;
+    if (!ctx->scene_set) return SPT_OK;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    return rebuild_accel(ctx);
 }
 
 int spt_set_workspace(spt_ctx *ctx, uint64_t bytes)
@@ -491,7 +503,7 @@ int spt_render_rows_async(spt_ctx *ctx, int mode, uint32_t yB, uint32_t yE, uint
     if (yB >= yE || xB >= xE) return SPT_OK;
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     spt::RowMap map{yB, yE, strip, parts, part, xB, xE - xB};
-    hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+    hipStream_t s = (hipStream_t)stream;  // NULL = the HIP default stream
     return render_impl(ctx, mode, map, (float4 *)d_rgba, (uint8_t *)d_rgb8, s, false);
 }
 
@@ -510,7 +522,7 @@ int spt_assemble_rows_async(spt_ctx *ctx, const void *d_tiles, uint32_t max_rows
     }
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     spt::RowMap base{yB, yE, strip, parts, 0u, xB, xE - xB};
-    hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+    hipStream_t s = (hipStream_t)stream;  // NULL = the HIP default stream
     HIP_TRY(ctx, spt::launch_assemble((const float4 *)d_tiles, max_rows, base, ctx->W, ctx->H, (float4 *)d_frame_rgba,
                                       (uint8_t *)d_rgb8, s));
     return SPT_OK;
@@ -554,12 +566,12 @@ int spt_get_stats(spt_ctx *ctx, spt_stats *out)
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     int rc = collect_timings(ctx);
     if (rc) return rc;
-    unsigned long long c[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long c[12] = {0};
     HIP_TRY(ctx, hipMemcpy(c, ctx->d_counters, sizeof c, hipMemcpyDeviceToHost));
     out->casts = c[0];
     out->samples = c[1];
     out->dropped = c[2];
-    for (int i = 0; i < 4; ++i) out->diag[i] = c[4 + i];
+    for (int i = 0; i < 8; ++i) out->diag[i] = c[4 + i];
     out->launches = ctx->launches;
     out->render_ms = ctx->render_ms;
     out->fold_ms = ctx->fold_ms;
@@ -576,7 +588,7 @@ int spt_reset_stats(spt_ctx *ctx)
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     int rc = collect_timings(ctx);
     if (rc) return rc;
-    HIP_TRY(ctx, hipMemset(ctx->d_counters, 0, 8 * sizeof(unsigned long long)));
+    HIP_TRY(ctx, hipMemset(ctx->d_counters, 0, 12 * sizeof(unsigned long long)));
     ctx->render_ms = ctx->fold_ms = ctx->last_render_ms = 0;
     ctx->launches = 0;
     return SPT_OK;

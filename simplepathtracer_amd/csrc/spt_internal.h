@@ -31,13 +31,20 @@ __host__ __device__ inline uint32_t rows_owned(const RowMap &m)
 
 constexpr uint32_t kMaxGroup = 16;  // sphere-table padding granule (>= SPT_GROUP)
 
+// Hot-loop traversal tables (spt_accel.cpp).
+struct AccelView {
+    const float4 *slots;     // {cx, cy, cz, r*r} in traversal order (always groups, then clusters)
+    const uint32_t *orig;    // original sphere index per slot
+    const float4 *bounds;    // per cluster {Cb, K1}
+    uint32_t always_groups, clusters, cluster_k;
+};
+
 struct DeviceScene {
-    const float4 *hit;      // {cx, cy, cz, r*r}, padded: see spt_set_scene
-    const float *hitp;      // same table as sphere pairs {cx0,cx1,cy0,cy1,cz0,cz1,rr0,rr1}
+    const float4 *hit;      // {cx, cy, cz, r*r} in original order (shading)
     const float4 *shade;    // {red, green, blue, fuzz}
     const uint32_t *mat;    // material id
     uint32_t n;
-    uint32_t ngroups;       // ceil(n / SPT_GROUP) groups of the hot loop
+    AccelView accel;
 };
 
 struct Camera {

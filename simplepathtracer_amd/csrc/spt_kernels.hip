@@ -26,10 +26,6 @@
 #define SPT_GROUP 4
 #endif
 
-#ifndef SPT_PACKED
-#define SPT_PACKED 0
-#endif
-
 #ifndef SPT_DIAG
 #define SPT_DIAG 0
 #endif
@@ -63,11 +59,15 @@ __device__ __forceinline__ uint32_t lane_rank(unsigned long long mask)
 }
 
 
-// One group of SPT_GROUP spheres of FindClosestIntersectionSphere
+// One group of SPT_GROUP slots of FindClosestIntersectionSphere
 // (Collision.hpp:87-109): RaySphereIntersection for all of them, then the rare
-// closest-contact / distance update behind a single branch.
-__device__ __forceinline__ void test_group(const float4 (&sp)[SPT_GROUP], uint32_t base, const f3 &o, const f3 &d,
-                                           float dod, float &best, uint32_t &idx, f3 &bp)
+// closest-contact / distance update behind a single branch.  Slots are visited
+// in traversal order, so the winner is the lexicographic minimum of
+// (distance, original index): identical to the reference's strict-'>' scan in
+// index order (first index wins ties; NaN and FLT_MAX distances never win).
+__device__ __forceinline__ void test_group(const float4 (&sp)[SPT_GROUP], const uint32_t *__restrict__ orig,
+                                           uint32_t slot, const f3 &o, const f3 &d, float dod, float &best,
+                                           uint32_t &best_orig, uint32_t &idx, f3 &bp)
 {
     float tcv[SPT_GROUP], hv[SPT_GROUP];
     bool pass[SPT_GROUP];
@@ -93,9 +93,11 @@ __device__ __forceinline__ void test_group(const float4 (&sp)[SPT_GROUP], uint32
                 const f3 p = mk(o.x + d.x * t, o.y + d.y * t, o.z + d.z * t);
                 if (dod < dot(p, d)) {
                     const float ds = lensq(sub(o, p));
-                    if (best > ds) {  // strict: the lowest index wins ties
+                    const uint32_t oi = orig[slot + k];
+                    if (ds < best || (ds == best && oi < best_orig)) {
                         best = ds;
-                        idx = base + k;
+                        best_orig = oi;
+                        idx = oi;
                         bp = p;
                     }
                 }
@@ -103,72 +105,6 @@ __device__ __forceinline__ void test_group(const float4 (&sp)[SPT_GROUP], uint32
         }
     }
 }
-
-#if SPT_PACKED
-typedef float f2v __attribute__((ext_vector_type(2)));
-
-// Sphere pairs in pair-SoA layout {cx0,cx1, cy0,cy1, cz0,cz1, rr0,rr1}: each
-// component pair is one 64-bit scalar operand of a packed fp32 instruction, so
-// RaySphereIntersection for two spheres costs the same packed instructions as
-// one scalar sphere (IEEE per half, no contraction: results are identical).
-struct PairS {
-    f2v cx, cy, cz, rr;
-};
-
-__device__ __forceinline__ PairS ld_pair(cfloat *p, uint32_t j)
-{
-    const uint32_t b = 8 * j;
-    PairS r;
-    r.cx = f2v{p[b + 0], p[b + 1]};
-    r.cy = f2v{p[b + 2], p[b + 3]};
-    r.cz = f2v{p[b + 4], p[b + 5]};
-    r.rr = f2v{p[b + 6], p[b + 7]};
-    return r;
-}
-
-__device__ __forceinline__ void test_pairs(const PairS (&q)[SPT_GROUP / 2], uint32_t base, const f3 &o, const f3 &d,
-                                           float dod, float &best, uint32_t &idx, f3 &bp)
-{
-    float tcv[SPT_GROUP], hv[SPT_GROUP];
-    bool pass[SPT_GROUP];
-    bool any = false;
-    const f2v ox = f2v{o.x, o.x}, oy = f2v{o.y, o.y}, oz = f2v{o.z, o.z};
-    const f2v dx = f2v{d.x, d.x}, dy = f2v{d.y, d.y}, dz = f2v{d.z, d.z};
-#pragma unroll
-    for (int j = 0; j < SPT_GROUP / 2; ++j) {
-        const f2v ocx = q[j].cx - ox, ocy = q[j].cy - oy, ocz = q[j].cz - oz;
-        const f2v tc = (ocx * dx + ocy * dy) + ocz * dz;
-        const f2v d2 = ((ocx * ocx + ocy * ocy) + ocz * ocz) - tc * tc;
-        const f2v h = q[j].rr - d2;
-        tcv[2 * j] = tc.x;
-        tcv[2 * j + 1] = tc.y;
-        hv[2 * j] = h.x;
-        hv[2 * j + 1] = h.y;
-    }
-#pragma unroll
-    for (int k = 0; k < SPT_GROUP; ++k) {
-        pass[k] = tcv[k] > 1e-3f && hv[k] > 1e-3f;
-        any = any || pass[k];
-    }
-    if (any) {
-#pragma unroll
-        for (int k = 0; k < SPT_GROUP; ++k) {
-            if (pass[k]) {
-                const float t = tcv[k] - sqrt_pos_normal(hv[k]);
-                const f3 p = mk(o.x + d.x * t, o.y + d.y * t, o.z + d.z * t);
-                if (dod < dot(p, d)) {
-                    const float ds = lensq(sub(o, p));
-                    if (best > ds) {
-                        best = ds;
-                        idx = base + k;
-                        bp = p;
-                    }
-                }
-            }
-        }
-    }
-}
-#endif
 
 }  // namespace
 
@@ -177,7 +113,6 @@ __global__ __launch_bounds__(kRenderBlock) void render_kernel(RenderArgs a)
     const uint32_t lane = __lane_id();
     const uint32_t n = a.scene.n;
     const float4 *__restrict__ hit = a.scene.hit;
-    cfloat *hit_s = (cfloat *)a.scene.hit;
     const float4 *__restrict__ shade = a.scene.shade;
     const uint32_t *__restrict__ mat = a.scene.mat;
 
@@ -189,7 +124,8 @@ __global__ __launch_bounds__(kRenderBlock) void render_kernel(RenderArgs a)
     bool exhausted = false;
     unsigned long long casts = 0, done = 0, dropped = 0;
 #if SPT_DIAG
-    unsigned long long d_iters = 0, d_hitblk = 0, d_lanehits = 0, d_dotblk = 0;
+    unsigned long long d_iters = 0, d_hitblk = 0, d_lanehits = 0, d_cyc_cast = 0, d_cyc_shade = 0, d_cyc_refill = 0;
+    unsigned long long d_t0 = __builtin_amdgcn_s_memtime();
 #endif
 
     for (;;) {
@@ -245,6 +181,13 @@ __global__ __launch_bounds__(kRenderBlock) void render_kernel(RenderArgs a)
         }
         const unsigned long long live = __ballot(phase != PH_IDLE);
         if (live == 0ull) break;
+#if SPT_DIAG
+        {
+            const unsigned long long t = __builtin_amdgcn_s_memtime();
+            d_cyc_refill += t - d_t0;
+            d_t0 = t;
+        }
+#endif
         casts += (unsigned long long)__popcll(live);
 #if SPT_DIAG
         ++d_iters;
@@ -256,39 +199,57 @@ __global__ __launch_bounds__(kRenderBlock) void render_kernel(RenderArgs a)
         // blocks (~6 of 148 spheres per wave iteration on config 2) sit behind
         // one combined branch per group.  The table is padded with spheres of
         // r*r = -inf that never pass, so the prefetch needs no bound check.
-        uint32_t idx = n;
+        uint32_t idx = n, best_orig = 0;
         float best = FLT_MAX;
         f3 bp = o;
         const float dod = dot(o, d);
-#if SPT_PACKED
-        cfloat *pair_s = (cfloat *)a.scene.hitp;
-        PairS pa[SPT_GROUP / 2], pb[SPT_GROUP / 2];
+        {
+            const AccelView &ac = a.scene.accel;
+            cfloat *slots = (cfloat *)ac.slots;
+            float4 g4[SPT_GROUP];
+            // always-tested spheres (ground, large balls; every sphere when culling is off)
+            for (uint32_t g = 0; g < ac.always_groups; ++g) {
 #pragma unroll
-        for (int j = 0; j < SPT_GROUP / 2; ++j) pa[j] = ld_pair(pair_s, j);
-        for (uint32_t g = 0; g < a.scene.ngroups; g += 2) {
-#pragma unroll
-            for (int j = 0; j < SPT_GROUP / 2; ++j) pb[j] = ld_pair(pair_s, (g + 1) * (SPT_GROUP / 2) + j);
-            test_pairs(pa, g * SPT_GROUP, o, d, dod, best, idx, bp);
-#pragma unroll
-            for (int j = 0; j < SPT_GROUP / 2; ++j) pa[j] = ld_pair(pair_s, (g + 2) * (SPT_GROUP / 2) + j);
-            test_pairs(pb, (g + 1) * SPT_GROUP, o, d, dod, best, idx, bp);
-        }
-#else
-        float4 ga[SPT_GROUP], gb[SPT_GROUP];
-#pragma unroll
-        for (int k = 0; k < SPT_GROUP; ++k) ga[k] = ld_uniform(hit_s, k);
-        // two groups per trip, ping-ponging two scalar register buffers
-        for (uint32_t g = 0; g < a.scene.ngroups; g += 2) {
-#pragma unroll
-            for (int k = 0; k < SPT_GROUP; ++k) gb[k] = ld_uniform(hit_s, (g + 1) * SPT_GROUP + k);
-            test_group(ga, g * SPT_GROUP, o, d, dod, best, idx, bp);
-#pragma unroll
-            for (int k = 0; k < SPT_GROUP; ++k) ga[k] = ld_uniform(hit_s, (g + 2) * SPT_GROUP + k);
-            test_group(gb, (g + 1) * SPT_GROUP, o, d, dod, best, idx, bp);
-        }
-
+                for (int k = 0; k < SPT_GROUP; ++k) g4[k] = ld_uniform(slots, g * SPT_GROUP + k);
+                test_group(g4, ac.orig, g * SPT_GROUP, o, d, dod, best, best_orig, idx, bp);
+            }
+            // clusters: skipped when no lane can pass any member's test (spt_accel.cpp)
+            // lanes whose direction is not unit length within 1e-6 (the glass branch
+            // reflects without renormalising) never cull; idle lanes never open a cluster
+            const float ddev = lensq(d) - 1.0f;
+            const bool no_cull = phase != PH_IDLE && !(ddev <= 1e-6f && ddev >= -1e-6f);
+            cfloat *bounds = (cfloat *)ac.bounds;
+            const uint32_t cbase = ac.always_groups * SPT_GROUP;
+            for (uint32_t c = 0; c < ac.clusters; ++c) {
+                const float4 b = ld_uniform(bounds, c);
+                const f3 ocb = mk(b.x - o.x, b.y - o.y, b.z - o.z);
+                const float tcb = dot(ocb, d);
+                const float occb = lensq(ocb);
+                const float d2b = occb - tcb * tcb;
+                const bool might = no_cull || (phase != PH_IDLE && d2b <= b.w + 1e-4f * occb);
+                const unsigned long long mm = __ballot(might);
+#if SPT_DIAG
+                d_hitblk += mm != 0ull;
+                d_lanehits += __popcll(mm);
 #endif
+                if (mm != 0ull) {
+                    const uint32_t s0 = cbase + c * ac.cluster_k;
+                    for (uint32_t j = 0; j < ac.cluster_k; j += SPT_GROUP) {
+#pragma unroll
+                        for (int k = 0; k < SPT_GROUP; ++k) g4[k] = ld_uniform(slots, s0 + j + k);
+                        test_group(g4, ac.orig, s0 + j, o, d, dod, best, best_orig, idx, bp);
+                    }
+                }
+            }
+        }
 
+#if SPT_DIAG
+        {
+            const unsigned long long t = __builtin_amdgcn_s_memtime();
+            d_cyc_cast += t - d_t0;
+            d_t0 = t;
+        }
+#endif
         // ---- one shading step ----
         if (phase != PH_IDLE) {
             bool fin = false;
@@ -396,6 +357,13 @@ __global__ __launch_bounds__(kRenderBlock) void render_kernel(RenderArgs a)
                 ++done;
             }
         }
+#if SPT_DIAG
+        {
+            const unsigned long long t = __builtin_amdgcn_s_memtime();
+            d_cyc_shade += t - d_t0;
+            d_t0 = t;
+        }
+#endif
     }
 
     // per-lane done/dropped -> wave sums via atomics from every lane that has any
@@ -407,6 +375,9 @@ __global__ __launch_bounds__(kRenderBlock) void render_kernel(RenderArgs a)
         atomicAdd(&a.counters[4], d_iters);
         atomicAdd(&a.counters[5], d_hitblk);
         atomicAdd(&a.counters[6], d_lanehits);
+        atomicAdd(&a.counters[7], d_cyc_cast);
+        atomicAdd(&a.counters[8], d_cyc_shade);
+        atomicAdd(&a.counters[9], d_cyc_refill);
     }
 #endif
 }

@@ -47,6 +47,12 @@ def gather_tiles(local_tile, gathered, group=None) -> None:
     """All ranks' tiles -> gathered[world*max_rows*width, 4], rank-major (one
     collective; the concatenated form is accepted by both RCCL and gloo)."""
     import torch.distributed as dist
+    if local_tile.is_cuda and dist.get_backend(group) != "nccl":
+        # rehearsal path (several ranks on one GPU, gloo): exchange host copies
+        host = gathered.new_empty(gathered.shape, device="cpu")
+        dist.all_gather_into_tensor(host, local_tile.cpu(), group=group)
+        gathered.copy_(host)
+        return
     dist.all_gather_into_tensor(gathered, local_tile, group=group)
 
 

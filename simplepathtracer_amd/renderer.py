@@ -79,6 +79,10 @@ class Context:
     def set_params(self, width: int, height: int, spp: int, bounces: int, seed: int = 1) -> None:
         self._check(_native.lib().spt_set_params(self._h, width, height, spp, bounces, seed))
 
+    def set_cluster_size(self, k: int) -> None:
+        """Culling cluster size (0 = brute force over every sphere); results identical."""
+        self._check(_native.lib().spt_set_cluster_size(self._h, int(k)))
+
     def set_workspace(self, nbytes: int) -> None:
         self._check(_native.lib().spt_set_workspace(self._h, int(nbytes)))
 

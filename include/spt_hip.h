@@ -32,6 +32,14 @@ extern "C" {
 
 #define SPT_ABI_VERSION 1
 
+/* Only the functions below are exported from libspt_hip.so (built with
+ * -fvisibility=hidden), so several builds can be loaded side by side. */
+#if defined(__GNUC__)
+#define SPT_API __attribute__((visibility("default")))
+#else
+#define SPT_API
+#endif
+
 typedef enum spt_status {
     SPT_OK = 0,
     SPT_ERR_ARG = 1,      /* invalid argument (null pointer, bad range, ...) */
@@ -69,40 +77,40 @@ typedef struct spt_stats {
                               cast / shading / refill, 2 reserved */
 } spt_stats;
 
-int spt_abi_version(void);
+SPT_API int spt_abi_version(void);
 /* Number of visible HIP devices. */
-int spt_device_count(int *count);
+SPT_API int spt_device_count(int *count);
 
 /* Context on one device.  Replaces nothing in the reference (its state is global);
  * it owns the device copies of Globals.hpp's scene/camera and a workspace. */
-int spt_ctx_create(int device, spt_ctx **out);
-void spt_ctx_destroy(spt_ctx *ctx);
+SPT_API int spt_ctx_create(int device, spt_ctx **out);
+SPT_API void spt_ctx_destroy(spt_ctx *ctx);
 /* Last error of ctx, or of the calling thread when ctx is NULL. Never NULL. */
-const char *spt_last_error(const spt_ctx *ctx);
+SPT_API const char *spt_last_error(const spt_ctx *ctx);
 
 /* Scene SoA, Globals.hpp:31-37: g_spheres (float4 per sphere, w ignored),
  * g_radii, g_colors (float4, w ignored), g_materials, g_diffuses (fuzz),
  * g_sphereNumber.  Data is copied.  The reference's uint8_t sphere index
  * (Collision.hpp:87-92) limits it to n <= 255; this build uses a 32-bit index,
  * identical for n <= 255, and accepts larger scenes as an extension. */
-int spt_set_scene(spt_ctx *ctx, const float *centers4, const float *radii, const float *colors4,
+SPT_API int spt_set_scene(spt_ctx *ctx, const float *centers4, const float *radii, const float *colors4,
                   const uint8_t *materials, const float *fuzz, uint32_t n);
 /* viewMatrix (row-major, already transposed, Renderer.hpp:321; its fourth row
  * must be zero as CreateCameraBasisMatrix makes it), eyePos and initColor
  * (Globals.hpp:21-29).  w lanes of eye/sky are ignored (0 in the reference). */
-int spt_set_camera(spt_ctx *ctx, const float view[16], const float eye[4], const float sky[4]);
+SPT_API int spt_set_camera(spt_ctx *ctx, const float view[16], const float eye[4], const float sky[4]);
 /* g_width, g_height, g_samples, g_bounces (Globals.hpp:12-15) + RNG seed.
  * bounces == 0 is rejected: `while (--bounceCount && ...)` would never count
  * down (SingleThreadPathTracer.hpp:28). */
-int spt_set_params(spt_ctx *ctx, uint32_t width, uint32_t height, uint32_t spp, uint32_t bounces, uint64_t seed);
-/* Hot-loop culling: small spheres are grouped into clusters of k (default 8)
+SPT_API int spt_set_params(spt_ctx *ctx, uint32_t width, uint32_t height, uint32_t spp, uint32_t bounces, uint64_t seed);
+/* Hot-loop culling: small spheres are grouped into clusters of k <= 8 (default 8)
  * whose conservative bounding test skips them exactly when no ray of a wave can
  * pass RaySphereIntersection for any member; k = 0 tests every sphere for every
  * ray (the reference's brute force).  Results are identical either way. */
-int spt_set_cluster_size(spt_ctx *ctx, uint32_t k);
+SPT_API int spt_set_cluster_size(spt_ctx *ctx, uint32_t k);
 /* Upper bound of the per-sample workspace (default 4 GiB).  Larger frames are
  * rendered in sample batches folded in order. */
-int spt_set_workspace(spt_ctx *ctx, uint64_t bytes);
+SPT_API int spt_set_workspace(spt_ctx *ctx, uint64_t bytes);
 
 /* ---- drop-in entry points (host memory, blocking) ----------------------------
  * Render pixels [yBegin,yEnd) x [xBegin,xEnd).
@@ -111,9 +119,9 @@ int spt_set_workspace(spt_ctx *ctx, uint64_t bytes);
  * g_data (nullable): full-frame width*height*3 bytes; the region's pixels are
  *   written at g_size - ((g_width - x)*3 + y*g_width*3) exactly as
  *   io::WritePixel does (IOHelpers.hpp:17-22), other bytes untouched. */
-int spt_render_segment(spt_ctx *ctx, uint32_t yBegin, uint32_t yEnd, uint32_t xBegin, uint32_t xEnd,
+SPT_API int spt_render_segment(spt_ctx *ctx, uint32_t yBegin, uint32_t yEnd, uint32_t xBegin, uint32_t xEnd,
                        float *rgba_out, uint8_t *g_data);
-int spt_render_segment_task(spt_ctx *ctx, uint32_t yBegin, uint32_t yEnd, uint32_t xBegin, uint32_t xEnd,
+SPT_API int spt_render_segment_task(spt_ctx *ctx, uint32_t yBegin, uint32_t yEnd, uint32_t xBegin, uint32_t xEnd,
                             float *rgba_out, uint8_t *g_data);
 
 /* ---- device-resident entry point (asynchronous) -------------------------------
@@ -125,47 +133,47 @@ int spt_render_segment_task(spt_ctx *ctx, uint32_t yBegin, uint32_t yEnd, uint32
  * stream: a hipStream_t; NULL is HIP's default (null) stream, as for any HIP
  * call.  Launches are ordered on that stream only.  Returns after enqueueing;
  * pair with spt_synchronize or the caller's stream sync. */
-int spt_render_rows_async(spt_ctx *ctx, int mode, uint32_t yBegin, uint32_t yEnd, uint32_t strip, uint32_t parts,
+SPT_API int spt_render_rows_async(spt_ctx *ctx, int mode, uint32_t yBegin, uint32_t yEnd, uint32_t strip, uint32_t parts,
                           uint32_t part, uint32_t xBegin, uint32_t xEnd, void *d_rgba, void *d_rgb8, void *stream);
 /* Number of rows the (yBegin, yEnd, strip, parts, part) map owns. */
-int spt_rows_count(uint32_t yBegin, uint32_t yEnd, uint32_t strip, uint32_t parts, uint32_t part, uint32_t *rows);
+SPT_API int spt_rows_count(uint32_t yBegin, uint32_t yEnd, uint32_t strip, uint32_t parts, uint32_t part, uint32_t *rows);
 /* Scatter a gathered, rank-major stack of local float4 tiles (parts tiles of
  * max_rows*(xEnd-xBegin) pixels each, on device) into a full-frame float4
  * buffer and/or a g_data RGB8 frame.  Used by rank 0 after the RCCL gather. */
-int spt_assemble_rows_async(spt_ctx *ctx, const void *d_tiles, uint32_t max_rows, uint32_t yBegin, uint32_t yEnd,
+SPT_API int spt_assemble_rows_async(spt_ctx *ctx, const void *d_tiles, uint32_t max_rows, uint32_t yBegin, uint32_t yEnd,
                             uint32_t strip, uint32_t parts, uint32_t xBegin, uint32_t xEnd, void *d_frame_rgba,
                             void *d_rgb8, void *stream);
-int spt_synchronize(spt_ctx *ctx);
+SPT_API int spt_synchronize(spt_ctx *ctx);
 
 /* Per-(pixel, sample) colors of a rectangle, host memory: out[(p*spp + s)*4 + c]
  * with p the region-local pixel.  w = 1 if the sample counts, 0 if dropped
  * (task mode).  Debug/parity aid; same kernel as the render path. */
-int spt_render_samples(spt_ctx *ctx, int mode, uint32_t yBegin, uint32_t yEnd, uint32_t xBegin, uint32_t xEnd,
+SPT_API int spt_render_samples(spt_ctx *ctx, int mode, uint32_t yBegin, uint32_t yEnd, uint32_t xBegin, uint32_t xEnd,
                        float *out);
 
-int spt_get_stats(spt_ctx *ctx, spt_stats *out);
-int spt_reset_stats(spt_ctx *ctx);
+SPT_API int spt_get_stats(spt_ctx *ctx, spt_stats *out);
+SPT_API int spt_reset_stats(spt_ctx *ctx);
 
 /* ---- input producers (SceneGenerators.hpp, Math.hpp) -------------------------
  * GenerateSpheres (SceneGenerators.hpp:6-66) and InitSpheres (68-133) driven by
  * splitmix(seed) (Random.hpp:19) instead of the clock; capacity in spheres. */
-int spt_scene_generate_random(uint32_t seed, uint32_t capacity, float *centers4, float *radii, float *colors4,
+SPT_API int spt_scene_generate_random(uint32_t seed, uint32_t capacity, float *centers4, float *radii, float *colors4,
                               uint8_t *materials, float *fuzz, uint32_t *n_out);
-int spt_scene_init_reference(uint32_t seed, float *centers4, float *radii, float *colors4, uint8_t *materials,
+SPT_API int spt_scene_init_reference(uint32_t seed, float *centers4, float *radii, float *colors4, uint8_t *materials,
                              float *fuzz, uint32_t *n_out);
 /* Stress scene for the >255-sphere extension (BASELINE config 5): the four big
  * spheres of GenerateSpheres plus n-4 small spheres on a jittered grid. */
-int spt_scene_generate_stress(uint32_t seed, uint32_t n, float *centers4, float *radii, float *colors4,
+SPT_API int spt_scene_generate_stress(uint32_t seed, uint32_t n, float *centers4, float *radii, float *colors4,
                               uint8_t *materials, float *fuzz);
 /* Transpose(CreateCameraBasisMatrix(eye, lookAt, up)), Math.hpp:198-231. */
-int spt_camera_basis(const float eye[4], const float look_at[4], const float up[4], float view_out[16]);
+SPT_API int spt_camera_basis(const float eye[4], const float look_at[4], const float up[4], float view_out[16]);
 
 /* ---- numerics self-test ------------------------------------------------------
  * Runs the device primitives the render path relies on over n inputs and
  * writes SPT_SELFTEST_COLS floats per input: a/b, sqrtf(a),
  * float(sqrt(double(a))), float(pow5(double(a))), uniform draw, u8 of a. */
 #define SPT_SELFTEST_COLS 8
-int spt_selftest_numerics(spt_ctx *ctx, const float *a, const float *b, const uint32_t *bits, uint32_t n,
+SPT_API int spt_selftest_numerics(spt_ctx *ctx, const float *a, const float *b, const uint32_t *bits, uint32_t n,
                           float *out);
 
 #ifdef __cplusplus

@@ -53,7 +53,8 @@ def build(force: bool = False) -> str:
 def declared_symbols() -> list[str]:
     """Function names declared in include/spt_hip.h."""
     text = open(HEADER_PATH).read()
-    return sorted(set(re.findall(r"^\s*(?:int|void|const char \*)\s*\*?\s*(spt_[a-z0-9_]+)\s*\(", text, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:SPT_API\s+)?(?:int|void|const char \*)\s*\*?\s*(spt_[a-z0-9_]+)\s*\(", text,
+                                 re.M)))
 
 
 _lib = None
@@ -66,7 +67,7 @@ def lib() -> ctypes.CDLL:
     if not os.path.exists(LIB_PATH):
         raise ImportError(f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
                           " (no CPU fallback exists)")
-    L = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    L = ctypes.CDLL(LIB_PATH)
     P, I = ctypes.c_void_p, ctypes.c_int
     u32, u64 = ctypes.c_uint32, ctypes.c_uint64
     sig = {

@@ -20,6 +20,9 @@
 // lexicographic (distance, original index) minimum, which equals the
 // reference's strict-'>' first-index-wins scan.
 #include "spt_accel.h"
+#include "spt_internal.h"
+
+#pragma clang fp contract(off)
 
 #include <algorithm>
 #include <cmath>
@@ -85,8 +88,8 @@ AccelTables build_accel(const float *centers4, const float *radii, uint32_t n, u
     pad_to(group, 0);
     t.always_groups = (uint32_t)(t.slots.size() / group);
     if (!small.empty()) {
-        const uint32_t k = (cluster_k + group - 1) / group * group;
-        t.cluster_k = k;
+        const uint32_t k = std::min(cluster_k, kClusterSlots);  // members per cluster
+        t.cluster_k = kClusterSlots;
         double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
         for (uint32_t i : small)
             for (int c = 0; c < 3; ++c) {
@@ -124,7 +127,7 @@ AccelTables build_accel(const float *centers4, const float *radii, uint32_t n, u
                 rb = std::max(rb, std::sqrt(d2) + std::fabs((double)radii[i]));
                 push_slot(i);
             }
-            pad_to(k, (size_t)t.always_groups * group);
+            pad_to(kClusterSlots, (size_t)t.always_groups * group);
             rb *= 1.0 + 1e-6;
             t.bounds.push_back(make_float4(cbf[0], cbf[1], cbf[2], round_up(1.15 * rb * rb + 1e-5)));
         }
@@ -137,6 +140,16 @@ AccelTables build_accel(const float *centers4, const float *radii, uint32_t n, u
     }
     t.bounds.push_back(make_float4(0.f, 0.f, 0.f, -INFINITY));  // prefetch pad
     return t;
+}
+
+std::vector<float4> eye_relative(const std::vector<float4> &points, const float eye[3])
+{
+    std::vector<float4> out(points.size());
+    for (size_t i = 0; i < points.size(); ++i) {
+        const float x = points[i].x - eye[0], y = points[i].y - eye[1], z = points[i].z - eye[2];
+        out[i] = make_float4(x, y, z, (x * x + y * y) + z * z);  // lensq order, Math.hpp:122-133
+    }
+    return out;
 }
 
 }  // namespace spt

@@ -17,6 +17,10 @@ struct AccelTables {
     uint32_t cluster_k = 0;        // slots per cluster (multiple of group)
 };
 
+// Eye-relative copies for the primary-ray pass: {P - eye, |P - eye|^2} with the
+// kernel's own fp32 operation order (bit-identical to computing them in-kernel).
+std::vector<float4> eye_relative(const std::vector<float4> &points, const float eye[3]);
+
 // cluster_k == 0 (or n <= 32): every sphere is "always" tested (brute force).
 AccelTables build_accel(const float *centers4, const float *radii, uint32_t n, uint32_t cluster_k, uint32_t group);
 

@@ -42,8 +42,11 @@ struct spt_ctx {
 
     // scene (Globals.hpp:31-37)
     float4 *d_hit = nullptr, *d_shade = nullptr, *d_slots = nullptr, *d_bounds = nullptr;
+    float4 *d_slots_eye = nullptr, *d_bounds_eye = nullptr;
     uint32_t *d_mat = nullptr, *d_orig = nullptr;
     size_t hit_cap = 0, shade_cap = 0, mat_cap = 0, slots_cap = 0, orig_cap = 0, bounds_cap = 0;
+    size_t slots_eye_cap = 0, bounds_eye_cap = 0;
+    spt::AccelTables tables;
     uint32_t n = 0;
     bool scene_set = false;
     // host copy of the hit geometry, to rebuild the traversal tables
@@ -254,6 +257,20 @@ int upload(spt_ctx *ctx, T **p, size_t *cap, const std::vector<T> &v)
     return SPT_OK;
 }
 
+// Eye-relative tables of the primary-ray pass; needs both the scene and the camera.
+int rebuild_eye(spt_ctx *ctx)
+{
+    const spt::AccelTables &t = ctx->tables;
+    if (ctx->cam_set && !t.slots.empty()) {
+        int rc = upload(ctx, &ctx->d_slots_eye, &ctx->slots_eye_cap, spt::eye_relative(t.slots, ctx->cam.eye));
+        if (!rc) rc = upload(ctx, &ctx->d_bounds_eye, &ctx->bounds_eye_cap, spt::eye_relative(t.bounds, ctx->cam.eye));
+        if (rc) return rc;
+    }
+    ctx->accel = spt::AccelView{ctx->d_slots,     ctx->d_orig,       ctx->d_bounds,      ctx->d_slots_eye,
+                                ctx->d_bounds_eye, t.always_groups, t.clusters,         t.cluster_k};
+    return SPT_OK;
+}
+
 // Build and upload the hot-loop traversal tables (spt_accel.cpp) for the current scene.
 int rebuild_accel(spt_ctx *ctx)
 {
@@ -264,8 +281,8 @@ int rebuild_accel(spt_ctx *ctx)
     if (!rc) rc = upload(ctx, &ctx->d_orig, &ctx->orig_cap, t.orig);
     if (!rc) rc = upload(ctx, &ctx->d_bounds, &ctx->bounds_cap, t.bounds);
     if (rc) return rc;
-    ctx->accel = spt::AccelView{ctx->d_slots, ctx->d_orig, ctx->d_bounds, t.always_groups, t.clusters, t.cluster_k};
-    return SPT_OK;
+    ctx->tables = std::move(t);
+    return rebuild_eye(ctx);
 }
 
 int check_region(spt_ctx *ctx, uint32_t yB, uint32_t yE, uint32_t xB, uint32_t xE)
@@ -373,7 +390,8 @@ void spt_ctx_destroy(spt_ctx *ctx)
             (void)hipEventDestroy(p.a);
             (void)hipEventDestroy(p.b);
         }
-    void *bufs[] = {ctx->d_hit, ctx->d_shade, ctx->d_mat, ctx->d_slots, ctx->d_orig, ctx->d_bounds, ctx->d_samples, ctx->d_acc,
+    void *bufs[] = {ctx->d_hit, ctx->d_shade, ctx->d_mat, ctx->d_slots, ctx->d_orig, ctx->d_bounds,
+                    ctx->d_slots_eye, ctx->d_bounds_eye, ctx->d_samples, ctx->d_acc,
                     ctx->d_head, ctx->d_counters, ctx->d_stage, ctx->d_frame8};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
@@ -430,7 +448,8 @@ int spt_set_camera(spt_ctx *ctx, const float view[16], const float eye[4], const
         ctx->cam.sky[j] = sky[j];
     }
     ctx->cam_set = true;
-    return SPT_OK;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    return rebuild_eye(ctx);
 }
 
 int spt_set_params(spt_ctx *ctx, uint32_t width, uint32_t height, uint32_t spp, uint32_t bounces, uint64_t seed)
@@ -455,7 +474,7 @@ int spt_set_cluster_size(spt_ctx *ctx, uint32_t k)
 {
     if (!ctx) return fail(nullptr, SPT_ERR_ARG, "null context");
     std::lock_guard<std::mutex> lk(ctx->mu);
-    if (k > 256) return fail(ctx, SPT_ERR_ARG, "cluster size %u > 256", k);
+    if (k > spt::kClusterSlots) return fail(ctx, SPT_ERR_ARG, "cluster size %u > %u", k, spt::kClusterSlots);
     ctx->cluster_k = k;
     if (!ctx->scene_set) return SPT_OK;
     HIP_TRY(ctx, hipSetDevice(ctx->device));

@@ -3,14 +3,23 @@
 // render_kernel: persistent wavefront megakernel.  Each lane owns one
 // (pixel, sample) path at a time and runs the reference's recursion
 // (TraceAndSampleColor -> SampleColor{Diffuse,Reflective,Refractive,Skybox},
-// SingleThreadPathTracer.hpp:11-112) as an iterative state machine: every loop
-// iteration is exactly one FindClosestIntersectionSphere cast
-// (Collision.hpp:87-109) for every live lane, followed by one shading step.
-// When a path ends its colour goes to a per-sample slot and the lane takes the
-// next (pixel, sample) item; items are handed out by a wave-level ballot/mbcnt
-// prefix over a block claimed from one global counter, so lanes never wait for
-// the slowest path of their wave.  Sphere data is read with wave-uniform scalar
-// loads (s_load) -- the sphere index of the hot loop is the same for all lanes.
+// SingleThreadPathTracer.hpp:11-112) as an iterative state machine: one
+// FindClosestIntersectionSphere cast (Collision.hpp:87-109) followed by one
+// shading step per loop iteration.  When a path ends its colour goes to a
+// per-sample slot and the lane takes the next (pixel, sample) item; items are
+// handed out by a wave-level ballot/mbcnt prefix over a block claimed from one
+// global counter, so lanes never wait for the slowest path of their wave.
+//
+// Lanes that start a sample cast their primary ray in a batched pass right at
+// refill time: all primary rays share the origin eyePos, so C - eye and
+// |C - eye|^2 of every sphere (and cluster bound) come precomputed with the same
+// fp32 operations (bit-identical values), the test drops from 18 to 10 VALU and
+// the refilled lanes -- adjacent pixels of one sample -- cull clusters well.
+// The main cast then carries secondary rays only.
+//
+// Sphere data is read with wave-uniform scalar loads (s_load) -- the sphere
+// index of the hot loop is the same for all lanes.  Clusters of small spheres
+// are skipped when no lane can pass any member's test (spt_accel.cpp).
 //
 // fold_kernel: RenderSegment's `pixelColor += sample` in sample order followed by
 // `*= 1/g_samples` (SingleThreadPathTracer.hpp:121-134) or RenderSegmentTask's
@@ -30,6 +39,12 @@
 #define SPT_DIAG 0
 #endif
 
+// Primary-ray batch at refill time: number of refill rounds per iteration
+// (0 = primaries go through the main cast like any other ray).
+#ifndef SPT_PRIM_ROUNDS
+#define SPT_PRIM_ROUNDS 0
+#endif
+
 #pragma clang fp contract(off)
 
 namespace spt {
@@ -44,8 +59,8 @@ constexpr float kRsq = (float)((double)((1.0f - 1.5f) / (1.0f + 1.5f)) * (double
 constexpr float kAirToGlass = 1.0f / 1.5f;
 constexpr float kGlassToAir = 1.5f / 1.0f;
 
-// Sphere table as constant-address-space data: wave-uniform indices become
-// scalar (s_load) reads even though the kernel also stores to global memory.
+// Tables as constant-address-space data: wave-uniform indices become scalar
+// (s_load) reads even though the kernel also stores to global memory.
 typedef __attribute__((address_space(4))) const float cfloat;
 
 __device__ __forceinline__ float4 ld_uniform(cfloat *p, uint32_t i)
@@ -58,35 +73,52 @@ __device__ __forceinline__ uint32_t lane_rank(unsigned long long mask)
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
 }
 
+// Closest-hit state of one FindClosestIntersectionSphere call.
+struct Hit {
+    uint32_t idx;        // original sphere index, n = miss
+    uint32_t best_orig;  // tie-break key of the current winner
+    float best;          // its squared distance
+    f3 p;                // its closest contact point
+};
 
-// One group of SPT_GROUP slots of FindClosestIntersectionSphere
-// (Collision.hpp:87-109): RaySphereIntersection for all of them, then the rare
-// closest-contact / distance update behind a single branch.  Slots are visited
-// in traversal order, so the winner is the lexicographic minimum of
-// (distance, original index): identical to the reference's strict-'>' scan in
-// index order (first index wins ties; NaN and FLT_MAX distances never win).
-__device__ __forceinline__ void test_group(const float4 (&sp)[SPT_GROUP], const uint32_t *__restrict__ orig,
-                                           uint32_t slot, const f3 &o, const f3 &d, float dod, float &best,
-                                           uint32_t &best_orig, uint32_t &idx, f3 &bp)
+// One group of SPT_GROUP slots (Collision.hpp:87-109): RaySphereIntersection for
+// all of them, then the rare closest-contact / distance update behind a single
+// branch.  EYE: the slots hold {C - eye, |C - eye|^2} (primary rays, o == eye),
+// else {C, r*r}; `rr` then comes from the regular table.  Slots are visited in
+// traversal order, so the winner is the lexicographic minimum of (distance,
+// original index): identical to the reference's strict-'>' scan in index order
+// (first index wins ties; NaN and FLT_MAX distances never win).
+template <bool EYE, int G>
+__device__ __forceinline__ void test_group(const float4 (&sp)[G], const float (&rr)[G],
+                                           const uint32_t *__restrict__ orig, uint32_t slot, const f3 &o, const f3 &d,
+                                           float dod, Hit &h)
 {
-    float tcv[SPT_GROUP], hv[SPT_GROUP];
-    bool pass[SPT_GROUP];
+    float tcv[G], hv[G];
+    bool pass[G];
     bool any = false;
 #pragma unroll
-    for (int k = 0; k < SPT_GROUP; ++k) {
+    for (int k = 0; k < G; ++k) {
         // RaySphereIntersection, Collision.hpp:9-17
-        const float ocx = sp[k].x - o.x, ocy = sp[k].y - o.y, ocz = sp[k].z - o.z;
-        const float tc = (ocx * d.x + ocy * d.y) + ocz * d.z;
-        const float d2 = ((ocx * ocx + ocy * ocy) + ocz * ocz) - tc * tc;
-        const float h = sp[k].w - d2;
+        float tc, d2, r2;
+        if (EYE) {
+            tc = (sp[k].x * d.x + sp[k].y * d.y) + sp[k].z * d.z;
+            d2 = sp[k].w - tc * tc;
+            r2 = rr[k];
+        } else {
+            const float ocx = sp[k].x - o.x, ocy = sp[k].y - o.y, ocz = sp[k].z - o.z;
+            tc = (ocx * d.x + ocy * d.y) + ocz * d.z;
+            d2 = ((ocx * ocx + ocy * ocy) + ocz * ocz) - tc * tc;
+            r2 = sp[k].w;
+        }
+        const float hh = r2 - d2;
         tcv[k] = tc;
-        hv[k] = h;
-        pass[k] = tc > 1e-3f && h > 1e-3f;
+        hv[k] = hh;
+        pass[k] = tc > 1e-3f && hh > 1e-3f;
         any = any || pass[k];
     }
     if (any) {
 #pragma unroll
-        for (int k = 0; k < SPT_GROUP; ++k) {
+        for (int k = 0; k < G; ++k) {
             if (pass[k]) {
                 // CalculateRaySphereClosestContactPoint, Collision.hpp:19-27,49-56
                 const float t = tcv[k] - sqrt_pos_normal(hv[k]);
@@ -94,15 +126,211 @@ __device__ __forceinline__ void test_group(const float4 (&sp)[SPT_GROUP], const 
                 if (dod < dot(p, d)) {
                     const float ds = lensq(sub(o, p));
                     const uint32_t oi = orig[slot + k];
-                    if (ds < best || (ds == best && oi < best_orig)) {
-                        best = ds;
-                        best_orig = oi;
-                        idx = oi;
-                        bp = p;
+                    if (ds < h.best || (ds == h.best && oi < h.best_orig)) {
+                        h.best = ds;
+                        h.best_orig = oi;
+                        h.idx = oi;
+                        h.p = p;
                     }
                 }
             }
         }
+    }
+}
+
+// FindClosestIntersectionSphere for every lane of the wave (Collision.hpp:87-109).
+// `active`: lanes whose result matters (others never open a cluster).
+template <bool EYE>
+__device__ __forceinline__ Hit find_closest(const AccelView &ac, uint32_t n, const f3 &o, const f3 &d, bool active,
+                                            unsigned long long &diag_clusters)
+{
+    Hit h;
+    h.idx = n;
+    h.best_orig = 0;
+    h.best = FLT_MAX;
+    h.p = o;
+    const float dod = dot(o, d);
+    cfloat *slots = (cfloat *)(EYE ? ac.slots_eye : ac.slots);
+    cfloat *rrs = (cfloat *)ac.slots;
+    float4 g4[SPT_GROUP];
+    float rr[SPT_GROUP];
+    // always-tested spheres (ground, large balls; every sphere when culling is off)
+    for (uint32_t g = 0; g < ac.always_groups; ++g) {
+#pragma unroll
+        for (int k = 0; k < SPT_GROUP; ++k) {
+            g4[k] = ld_uniform(slots, g * SPT_GROUP + k);
+            rr[k] = EYE ? rrs[4 * (g * SPT_GROUP + k) + 3] : 0.f;
+        }
+        test_group<EYE, SPT_GROUP>(g4, rr, ac.orig, g * SPT_GROUP, o, d, dod, h);
+    }
+    // clusters: skipped when no lane can pass any member's test (spt_accel.cpp).
+    // Lanes whose direction is not unit length within 1e-6 (the glass branch
+    // reflects without renormalising) never cull.
+    const float ddev = lensq(d) - 1.0f;
+    const bool no_cull = active && !(ddev <= 1e-6f && ddev >= -1e-6f);
+    cfloat *bounds = (cfloat *)(EYE ? ac.bounds_eye : ac.bounds);
+    cfloat *k1s = (cfloat *)ac.bounds;
+    const uint32_t cbase = ac.always_groups * SPT_GROUP;
+    float4 bn = ld_uniform(bounds, 0);  // prefetched one cluster ahead (table is padded)
+    float k1n = k1s[3];
+    for (uint32_t c = 0; c < ac.clusters; ++c) {
+        const float4 b = bn;
+        const float k1 = k1n;
+        bn = ld_uniform(bounds, c + 1);
+        k1n = k1s[4 * (c + 1) + 3];
+        float d2b, occb;
+        if (EYE) {
+            const float tcb = (b.x * d.x + b.y * d.y) + b.z * d.z;
+            occb = b.w;
+            d2b = occb - tcb * tcb;
+        } else {
+            const f3 ocb = mk(b.x - o.x, b.y - o.y, b.z - o.z);
+            const float tcb = dot(ocb, d);
+            occb = lensq(ocb);
+            d2b = occb - tcb * tcb;
+        }
+        const bool might = no_cull || (active && d2b <= k1 + 1e-4f * occb);
+        const unsigned long long mm = __ballot(might);
+        diag_clusters += mm != 0ull;
+        if (mm != 0ull) {
+            // the cluster's kClusterSlots slots: two s_load_dwordx16 off one base pointer
+            const uint32_t s0 = cbase + c * kClusterSlots;
+            cfloat *cs = slots + 4 * s0;
+            float4 m8[kClusterSlots];
+            float r8[kClusterSlots];
+#pragma unroll
+            for (int k = 0; k < (int)kClusterSlots; ++k) {
+                m8[k] = ld_uniform(cs, k);
+                r8[k] = EYE ? rrs[4 * (s0 + k) + 3] : 0.f;
+            }
+            test_group<EYE, (int)kClusterSlots>(m8, r8, ac.orig, s0, o, d, dod, h);
+        }
+    }
+    return h;
+}
+
+// Per-lane path state of the flattened recursion.
+struct Path {
+    uint32_t phase, item, bounce, spec;
+    uint64_t st;  // keyed splitmix stream of this (pixel, sample)
+    f3 o, d, c;
+};
+
+// One shading step after a cast: the material switch of TraceAndSampleColor
+// (SingleThreadPathTracer.hpp:94-112) in PH_TRACE, or one turn of the diffuse
+// bounce loop (21-37) in PH_DLOOP.  Finishing paths write their sample slot.
+__device__ __forceinline__ void shade_step(const RenderArgs &a, Path &ps, const Hit &h, unsigned long long &done,
+                                           unsigned long long &dropped)
+{
+    const uint32_t n = a.scene.n;
+    const float4 *__restrict__ hit = a.scene.hit;
+    const float4 *__restrict__ shade = a.scene.shade;
+    const uint32_t *__restrict__ mat = a.scene.mat;
+    const uint32_t idx = h.idx;
+    bool fin = false;
+    float counted = 1.f;
+    f3 col = mk(0.f, 0.f, 0.f);
+    const bool dl = ps.phase == PH_DLOOP;
+    uint32_t m = SPT_SKYBOX_ID;
+    if (idx < n) m = mat[idx];
+    bool scatter, refr;
+    if (dl) {
+        // while (--bounceCount && sphereIndex < N), SingleThreadPathTracer.hpp:28
+        --ps.bounce;
+        const bool end = ps.bounce == 0u || idx >= n;
+        if (end) {
+            col = ps.c;
+            fin = true;
+        }
+        scatter = !end;
+        refr = false;
+    } else {
+        // TraceAndSampleColor material switch, SingleThreadPathTracer.hpp:98-111
+        scatter = m == SPT_DIFFUSE_ID || m == SPT_REFLECTIVE_ID;
+        refr = m == SPT_REFRACTIVE_ID;
+        if (!scatter && !refr) {
+            // SampleColorSkybox, lines 11-14
+            const float k = ps.d.y + 1.f;
+            col = mul(mk(a.cam.sky[0] * k, a.cam.sky[1] * k, a.cam.sky[2] * k), 0.5f);
+            fin = true;
+        }
+    }
+    bool spec_event = false;
+    if (scatter) {
+        // contact point + normal + cube-minus-ball vector, shared by the diffuse
+        // first hit (lines 23-26), the diffuse loop (30-33) and the mirror (41-43)
+        const float4 cs = hit[idx];
+        const f3 C = mk(cs.x, cs.y, cs.z);
+        ps.o = h.p;
+        const f3 nrm = normalize(sub(ps.o, C));
+        f3 rv = ball_vector(ps.st);
+        f3 base;
+        if (dl) {
+            ps.c = mul(ps.c, 0.5f);
+            base = add(ps.o, nrm);  // origin + normal (+ rv), line 32
+        } else if (m == SPT_DIFFUSE_ID) {
+            const float4 sh = shade[idx];
+            ps.c = mk(sh.x * 0.5f, sh.y * 0.5f, sh.z * 0.5f);
+            base = nrm;
+            ps.phase = PH_DLOOP;
+        } else {
+            base = reflect(ps.d, nrm);
+            rv = mul(rv, shade[idx].w);
+            spec_event = true;
+        }
+        ps.d = normalize(add(base, rv));
+    }
+    if (refr) {
+        // SampleColorRefractive, lines 48-92
+        const float4 cs = hit[idx];
+        const f3 C = mk(cs.x, cs.y, cs.z);
+        ps.o = h.p;
+        const f3 nrm = normalize(sub(ps.o, C));
+        const f3 d = ps.d;
+        const float cc = dot(neg(nrm), d);
+        f3 nd;
+        if (uniform(ps.st, 0.f, 1.f) < schlick(kRsq, cc)) {
+            nd = reflect(d, nrm);
+        } else if (no_tir(kAirToGlass, cc)) {
+            const f3 d2 = refract_dir(d, nrm, kAirToGlass, cc);
+            // CalculateRaySphereFarthestContactPoint, Collision.hpp:29-37,58-65
+            const f3 rs = sub(C, ps.o);
+            const float tc = dot(rs, d2);
+            const float dd = lensq(rs) - tc * tc;
+            const float t = tc + __builtin_sqrtf(cs.w - dd);
+            ps.o = mk(ps.o.x + d2.x * t, ps.o.y + d2.y * t, ps.o.z + d2.z * t);
+            const f3 n2 = neg(normalize(sub(ps.o, C)));
+            const float c2 = dot(neg(n2), d2);
+            if (uniform(ps.st, 0.f, 1.f) < schlick(kRsq, c2))
+                nd = reflect(d2, n2);
+            else if (no_tir(kGlassToAir, c2))
+                nd = refract_dir(d2, n2, kGlassToAir, c2);
+            else
+                nd = reflect(d2, n2);
+        } else {
+            nd = reflect(d, nrm);
+        }
+        ps.d = nd;
+        spec_event = true;
+    }
+    if (spec_event) {
+        ++ps.spec;
+        if (a.mode == 1u && ps.spec >= kTaskPasses) {
+            // RenderSegmentTask: this path would be processed in pass 10, which never runs
+            fin = true;
+            counted = 0.f;
+            col = mk(0.f, 0.f, 0.f);
+            ++dropped;
+        } else if (ps.spec > kSpecularCap) {
+            fin = true;
+            col = mk(0.f, 0.f, 0.f);
+        }
+    }
+    if (fin) {
+        a.samples[ps.item] = make_float4(col.x, col.y, col.z, counted);
+        ps.phase = PH_IDLE;
+        ps.d = mk(0.f, 0.f, 0.f);
+        ++done;
     }
 }
 
@@ -112,26 +340,40 @@ __global__ __launch_bounds__(kRenderBlock) void render_kernel(RenderArgs a)
 {
     const uint32_t lane = __lane_id();
     const uint32_t n = a.scene.n;
-    const float4 *__restrict__ hit = a.scene.hit;
-    const float4 *__restrict__ shade = a.scene.shade;
-    const uint32_t *__restrict__ mat = a.scene.mat;
+    const f3 eye = mk(a.cam.eye[0], a.cam.eye[1], a.cam.eye[2]);
 
-    uint32_t phase = PH_IDLE, item = 0, bounce = 0, spec = 0;
-    uint64_t st = 0;
-    f3 o = mk(0.f, 0.f, 0.f), d = mk(0.f, 0.f, 0.f), c = mk(0.f, 0.f, 0.f);
+    Path ps;
+    ps.phase = PH_IDLE;
+    ps.item = ps.bounce = ps.spec = 0;
+    ps.st = 0;
+    ps.o = ps.d = ps.c = mk(0.f, 0.f, 0.f);
 
     uint32_t blk_cur = 0, blk_end = 0;
     bool exhausted = false;
     unsigned long long casts = 0, done = 0, dropped = 0;
+    unsigned long long d_iters = 0, d_clusters = 0, d_cyc_cast = 0, d_cyc_shade = 0, d_cyc_refill = 0, d_prim = 0;
 #if SPT_DIAG
-    unsigned long long d_iters = 0, d_hitblk = 0, d_lanehits = 0, d_cyc_cast = 0, d_cyc_shade = 0, d_cyc_refill = 0;
     unsigned long long d_t0 = __builtin_amdgcn_s_memtime();
+#define SPT_STAMP(acc)                                              \
+    do {                                                            \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+        acc += t_ - d_t0;                                           \
+        d_t0 = t_;                                                  \
+    } while (0)
+#else
+#define SPT_STAMP(acc) \
+    do {               \
+    } while (0)
 #endif
 
     for (;;) {
-        // ---- hand out (pixel, sample) items to idle lanes: ballot + prefix ----
-        const unsigned long long need = __ballot(phase == PH_IDLE);
-        if (need != 0ull && !exhausted) {
+        // ---- refill: hand out (pixel, sample) items to idle lanes (ballot + prefix),
+        // cast their primary rays in one eye-relative batch and shade the hits.
+        // Two rounds, so lanes whose primary ray went to the sky start again at once.
+#pragma unroll 1
+        for (int round = 0; round < (SPT_PRIM_ROUNDS > 0 ? SPT_PRIM_ROUNDS : 1); ++round) {
+            const unsigned long long need = __ballot(ps.phase == PH_IDLE);
+            if (need == 0ull || exhausted) break;
             const uint32_t cnt = (uint32_t)__popcll(need);
             const uint32_t rank = lane_rank(need);
             const uint32_t avail = blk_end - blk_cur;
@@ -154,216 +396,53 @@ __global__ __launch_bounds__(kRenderBlock) void render_kernel(RenderArgs a)
                     blk_end = ne;
                 }
             }
-            if (phase == PH_IDLE && mine != 0xFFFFFFFFu) {
-                // primary ray, SingleThreadPathTracer.hpp:123-130
-                item = mine;
-                // items are ordered [sample][pixel]: a claim is a run of adjacent
-                // pixels of one sample (coherent primary rays, coalesced slots)
-                const uint32_t sl = item / a.npix;
+            const bool fresh = ps.phase == PH_IDLE && mine != 0xFFFFFFFFu;
+            if (fresh) {
+                // primary ray, SingleThreadPathTracer.hpp:123-130.  Items are ordered
+                // [sample][pixel]: a claim is a run of adjacent pixels of one sample.
+                ps.item = mine;
+                const uint32_t sl = ps.item / a.npix;
                 const uint32_t s = a.s0 + sl;
-                const uint32_t pl = item - sl * a.npix;
+                const uint32_t pl = ps.item - sl * a.npix;
                 const uint32_t lr = pl / a.map.width;
                 const uint32_t x = a.map.x0 + (pl - lr * a.map.width);
-                const uint32_t y = row_of(a.map, lr);
-                st = fmix64(a.seed_key ^ (((uint64_t)(y * a.width + x) << 32) | (uint64_t)s));
-                const float u = ((float)y + uniform(st, -1.f, 1.f)) / (float)a.width;
-                const float v = ((float)x + uniform(st, -1.f, 1.f)) / (float)a.height;
+                const uint32_t y = a.map.parts == 1u ? a.map.y0 + lr : row_of(a.map, lr);
+                ps.st = fmix64(a.seed_key ^ (((uint64_t)(y * a.width + x) << 32) | (uint64_t)s));
+                const float u = ((float)y + uniform(ps.st, -1.f, 1.f)) / (float)a.width;
+                const float v = ((float)x + uniform(ps.st, -1.f, 1.f)) / (float)a.height;
                 const float vx = -1.f + 2.f * v, vy = -1.f + 2.f * u;
                 const float *m = a.cam.view;
-                d = normalize(mk((m[0] * vx + m[1] * vy) + (m[2] * 1.f + m[3] * 0.f),
-                                 (m[4] * vx + m[5] * vy) + (m[6] * 1.f + m[7] * 0.f),
-                                 (m[8] * vx + m[9] * vy) + (m[10] * 1.f + m[11] * 0.f)));
-                o = mk(a.cam.eye[0], a.cam.eye[1], a.cam.eye[2]);
-                phase = PH_TRACE;
-                bounce = a.bounces;
-                spec = 0;
+                ps.d = normalize(mk((m[0] * vx + m[1] * vy) + (m[2] * 1.f + m[3] * 0.f),
+                                    (m[4] * vx + m[5] * vy) + (m[6] * 1.f + m[7] * 0.f),
+                                    (m[8] * vx + m[9] * vy) + (m[10] * 1.f + m[11] * 0.f)));
+                ps.o = eye;
+                ps.phase = PH_TRACE;
+                ps.bounce = a.bounces;
+                ps.spec = 0;
             }
+            if (SPT_PRIM_ROUNDS == 0) break;
+            const unsigned long long fm = __ballot(fresh);
+            if (fm == 0ull) break;
+            SPT_STAMP(d_cyc_refill);
+            casts += (unsigned long long)__popcll(fm);
+            d_prim += 1;
+            const Hit h = find_closest<true>(a.scene.accel, n, eye, ps.d, fresh, d_clusters);
+            SPT_STAMP(d_cyc_cast);
+            if (fresh) shade_step(a, ps, h, done, dropped);
+            SPT_STAMP(d_cyc_shade);
         }
-        const unsigned long long live = __ballot(phase != PH_IDLE);
-        if (live == 0ull) break;
-#if SPT_DIAG
-        {
-            const unsigned long long t = __builtin_amdgcn_s_memtime();
-            d_cyc_refill += t - d_t0;
-            d_t0 = t;
+        const unsigned long long live = __ballot(ps.phase != PH_IDLE);
+        if (live == 0ull) {
+            if (exhausted) break;
+            continue;
         }
-#endif
         casts += (unsigned long long)__popcll(live);
-#if SPT_DIAG
         ++d_iters;
-#endif
-
-        // ---- FindClosestIntersectionSphere, Collision.hpp:87-109 ----
-        // Spheres are tested SPT_GROUP at a time from scalar registers (one
-        // s_load_dwordx16 per 4 spheres, prefetched a group ahead); the rare hit
-        // blocks (~6 of 148 spheres per wave iteration on config 2) sit behind
-        // one combined branch per group.  The table is padded with spheres of
-        // r*r = -inf that never pass, so the prefetch needs no bound check.
-        uint32_t idx = n, best_orig = 0;
-        float best = FLT_MAX;
-        f3 bp = o;
-        const float dod = dot(o, d);
-        {
-            const AccelView &ac = a.scene.accel;
-            cfloat *slots = (cfloat *)ac.slots;
-            float4 g4[SPT_GROUP];
-            // always-tested spheres (ground, large balls; every sphere when culling is off)
-            for (uint32_t g = 0; g < ac.always_groups; ++g) {
-#pragma unroll
-                for (int k = 0; k < SPT_GROUP; ++k) g4[k] = ld_uniform(slots, g * SPT_GROUP + k);
-                test_group(g4, ac.orig, g * SPT_GROUP, o, d, dod, best, best_orig, idx, bp);
-            }
-            // clusters: skipped when no lane can pass any member's test (spt_accel.cpp)
-            // lanes whose direction is not unit length within 1e-6 (the glass branch
-            // reflects without renormalising) never cull; idle lanes never open a cluster
-            const float ddev = lensq(d) - 1.0f;
-            const bool no_cull = phase != PH_IDLE && !(ddev <= 1e-6f && ddev >= -1e-6f);
-            cfloat *bounds = (cfloat *)ac.bounds;
-            const uint32_t cbase = ac.always_groups * SPT_GROUP;
-            for (uint32_t c = 0; c < ac.clusters; ++c) {
-                const float4 b = ld_uniform(bounds, c);
-                const f3 ocb = mk(b.x - o.x, b.y - o.y, b.z - o.z);
-                const float tcb = dot(ocb, d);
-                const float occb = lensq(ocb);
-                const float d2b = occb - tcb * tcb;
-                const bool might = no_cull || (phase != PH_IDLE && d2b <= b.w + 1e-4f * occb);
-                const unsigned long long mm = __ballot(might);
-#if SPT_DIAG
-                d_hitblk += mm != 0ull;
-                d_lanehits += __popcll(mm);
-#endif
-                if (mm != 0ull) {
-                    const uint32_t s0 = cbase + c * ac.cluster_k;
-                    for (uint32_t j = 0; j < ac.cluster_k; j += SPT_GROUP) {
-#pragma unroll
-                        for (int k = 0; k < SPT_GROUP; ++k) g4[k] = ld_uniform(slots, s0 + j + k);
-                        test_group(g4, ac.orig, s0 + j, o, d, dod, best, best_orig, idx, bp);
-                    }
-                }
-            }
-        }
-
-#if SPT_DIAG
-        {
-            const unsigned long long t = __builtin_amdgcn_s_memtime();
-            d_cyc_cast += t - d_t0;
-            d_t0 = t;
-        }
-#endif
-        // ---- one shading step ----
-        if (phase != PH_IDLE) {
-            bool fin = false;
-            float counted = 1.f;
-            f3 col = mk(0.f, 0.f, 0.f);
-            const bool dl = phase == PH_DLOOP;
-            uint32_t m = SPT_SKYBOX_ID;
-            if (idx < n) m = mat[idx];
-            bool scatter, refr;
-            if (dl) {
-                // while (--bounceCount && sphereIndex < N), SingleThreadPathTracer.hpp:28
-                --bounce;
-                const bool end = bounce == 0u || idx >= n;
-                if (end) {
-                    col = c;
-                    fin = true;
-                }
-                scatter = !end;
-                refr = false;
-            } else {
-                // TraceAndSampleColor material switch, SingleThreadPathTracer.hpp:98-111
-                scatter = m == SPT_DIFFUSE_ID || m == SPT_REFLECTIVE_ID;
-                refr = m == SPT_REFRACTIVE_ID;
-                if (!scatter && !refr) {
-                    // SampleColorSkybox, lines 11-14
-                    const float k = d.y + 1.f;
-                    col = mul(mk(a.cam.sky[0] * k, a.cam.sky[1] * k, a.cam.sky[2] * k), 0.5f);
-                    fin = true;
-                }
-            }
-            bool spec_event = false;
-            if (scatter) {
-                // contact point + normal + cube-minus-ball vector, shared by the diffuse
-                // first hit (lines 23-26), the diffuse loop (30-33) and the mirror (41-43)
-                const float4 cs = hit[idx];
-                const f3 C = mk(cs.x, cs.y, cs.z);
-                o = bp;
-                const f3 nrm = normalize(sub(o, C));
-                f3 rv = ball_vector(st);
-                f3 base;
-                if (dl) {
-                    c = mul(c, 0.5f);
-                    base = add(o, nrm);  // origin + normal (+ rv), line 32
-                } else if (m == SPT_DIFFUSE_ID) {
-                    const float4 sh = shade[idx];
-                    c = mk(sh.x * 0.5f, sh.y * 0.5f, sh.z * 0.5f);
-                    base = nrm;
-                    phase = PH_DLOOP;
-                } else {
-                    base = reflect(d, nrm);
-                    rv = mul(rv, shade[idx].w);
-                    spec_event = true;
-                }
-                d = normalize(add(base, rv));
-            }
-            if (refr) {
-                // SampleColorRefractive, lines 48-92
-                const float4 cs = hit[idx];
-                const f3 C = mk(cs.x, cs.y, cs.z);
-                o = bp;
-                const f3 nrm = normalize(sub(o, C));
-                const float cc = dot(neg(nrm), d);
-                f3 nd;
-                if (uniform(st, 0.f, 1.f) < schlick(kRsq, cc)) {
-                    nd = reflect(d, nrm);
-                } else if (no_tir(kAirToGlass, cc)) {
-                    const f3 d2 = refract_dir(d, nrm, kAirToGlass, cc);
-                    // CalculateRaySphereFarthestContactPoint, Collision.hpp:29-37,58-65
-                    const f3 rs = sub(C, o);
-                    const float tc = dot(rs, d2);
-                    const float dd = lensq(rs) - tc * tc;
-                    const float t = tc + __builtin_sqrtf(cs.w - dd);
-                    o = mk(o.x + d2.x * t, o.y + d2.y * t, o.z + d2.z * t);
-                    const f3 n2 = neg(normalize(sub(o, C)));
-                    const float c2 = dot(neg(n2), d2);
-                    if (uniform(st, 0.f, 1.f) < schlick(kRsq, c2))
-                        nd = reflect(d2, n2);
-                    else if (no_tir(kGlassToAir, c2))
-                        nd = refract_dir(d2, n2, kGlassToAir, c2);
-                    else
-                        nd = reflect(d2, n2);
-                } else {
-                    nd = reflect(d, nrm);
-                }
-                d = nd;
-                spec_event = true;
-            }
-            if (spec_event) {
-                ++spec;
-                if (a.mode == 1u && spec >= kTaskPasses) {
-                    // the path would be processed in pass 10, which never runs
-                    fin = true;
-                    counted = 0.f;
-                    col = mk(0.f, 0.f, 0.f);
-                    ++dropped;
-                } else if (spec > kSpecularCap) {
-                    fin = true;
-                    col = mk(0.f, 0.f, 0.f);
-                }
-            }
-            if (fin) {
-                a.samples[item] = make_float4(col.x, col.y, col.z, counted);
-                phase = PH_IDLE;
-                d = mk(0.f, 0.f, 0.f);
-                ++done;
-            }
-        }
-#if SPT_DIAG
-        {
-            const unsigned long long t = __builtin_amdgcn_s_memtime();
-            d_cyc_shade += t - d_t0;
-            d_t0 = t;
-        }
-#endif
+        // ---- secondary casts + one shading step ----
+        const Hit h = find_closest<false>(a.scene.accel, n, ps.o, ps.d, ps.phase != PH_IDLE, d_clusters);
+        SPT_STAMP(d_cyc_cast);
+        if (ps.phase != PH_IDLE) shade_step(a, ps, h, done, dropped);
+        SPT_STAMP(d_cyc_shade);
     }
 
     // per-lane done/dropped -> wave sums via atomics from every lane that has any
@@ -373,13 +452,20 @@ __global__ __launch_bounds__(kRenderBlock) void render_kernel(RenderArgs a)
 #if SPT_DIAG
     if (lane == 0) {
         atomicAdd(&a.counters[4], d_iters);
-        atomicAdd(&a.counters[5], d_hitblk);
-        atomicAdd(&a.counters[6], d_lanehits);
+        atomicAdd(&a.counters[5], d_clusters);
+        atomicAdd(&a.counters[6], d_prim);
         atomicAdd(&a.counters[7], d_cyc_cast);
         atomicAdd(&a.counters[8], d_cyc_shade);
         atomicAdd(&a.counters[9], d_cyc_refill);
     }
 #endif
+    (void)d_iters;
+    (void)d_clusters;
+    (void)d_cyc_cast;
+    (void)d_cyc_shade;
+    (void)d_cyc_refill;
+    (void)d_prim;
+#undef SPT_STAMP
 }
 
 __global__ __launch_bounds__(256) void fold_kernel(FoldArgs a)

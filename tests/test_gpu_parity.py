@@ -376,7 +376,7 @@ def test_culling_is_exact(spt, ctx, golden_scenes, scene_name):
         scene, W, H, spp, region = spt.generate_stress(5, 2000), 480, 270, 8, (0, 270, 0, 480)
     setup(ctx, scene, W, H, spp, 50)
     outs = []
-    for k in (0, 8, 16, 4):
+    for k in (0, 8, 3, 5):
         ctx.set_cluster_size(k)
         ctx.reset_stats()
         outs.append((k, ctx.render_segment(*region), ctx.stats()["casts"]))
@@ -384,3 +384,5 @@ def test_culling_is_exact(spt, ctx, golden_scenes, scene_name):
     for k, img, casts in outs[1:]:
         assert_bitwise(img, outs[0][1], f"cluster size {k} vs brute force")
         assert casts == outs[0][2]
+    with pytest.raises(spt.SptError):
+        ctx.set_cluster_size(9)  # clusters hold at most kClusterSlots = 8 members

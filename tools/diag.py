@@ -17,10 +17,10 @@ ctx.render_segment(0, H, 0, W)
 ctx.reset_stats()
 ctx.render_segment(0, H, 0, W)
 st = ctx.stats()
-it, hb, lh, cc, cs, cr = st["diag"][:6]
+it, hb, lh, cc, cs, cr, cb = st["diag"][:7]
 print(f"casts={st['casts']} samples={st['samples']} wave_iters={it} live_lanes/iter={st['casts']/max(it,1):.2f}")
 k = int(os.environ.get("SPT_CLUSTER_K", "8"))
-print(f"clusters entered/iter={hb/max(it,1):.2f} (cluster size {k}); lanes wanting a cluster/cast={lh/max(st['casts'],1):.3f}")
+print(f"clusters entered per pass={hb/max(it+lh,1):.2f} (cluster size {k}); primary passes/secondary pass={lh/max(it,1):.3f}")
 tot = max(cc + cs + cr, 1)
-print(f"cycle shares: cast {cc/tot:.3f} shade {cs/tot:.3f} refill+ballot {cr/tot:.3f}")
+print(f"cycle shares: cast {cc/tot:.3f} shade {cs/tot:.3f} (ball_vector {cb/tot:.3f}) refill+ballot {cr/tot:.3f}")
 print(f"render_ms={st['render_ms']:.3f}")

@@ -73,8 +73,9 @@ typedef struct spt_stats {
     uint32_t grid_blocks;  /* persistent grid of the render kernel */
     uint32_t block_threads;
     uint64_t diag[8];      /* diagnostic build only (-DSPT_DIAG=1): wave iterations,
-                              clusters entered, lanes wanting them, s_memtime cycles in
-                              cast / shading / refill, 2 reserved */
+                              clusters entered, tree nodes tested, s_memtime cycles in
+                              cast / shading / refill, (lane, cluster) pairs that may
+                              pass, live lanes of entered clusters */
 } spt_stats;
 
 SPT_API int spt_abi_version(void);
@@ -108,6 +109,17 @@ SPT_API int spt_set_params(spt_ctx *ctx, uint32_t width, uint32_t height, uint32
  * pass RaySphereIntersection for any member; k = 0 tests every sphere for every
  * ray (the reference's brute force).  Results are identical either way. */
 SPT_API int spt_set_cluster_size(spt_ctx *ctx, uint32_t k);
+/* Clusters are the leaves of a tree of bounding spheres walked by the whole wave;
+ * `branching` children per inner node, 0 = flat list of clusters, SPT_TREE_AUTO
+ * (default) = flat up to 64 clusters, else 4.  Results are identical for any value. */
+#define SPT_TREE_AUTO 0xFFFFFFFFu
+SPT_API int spt_set_cluster_tree(spt_ctx *ctx, uint32_t branching);
+/* Host-only check (no device needed): build the traversal tables for a scene and
+ * verify the properties exactness rests on (every sphere once, preorder/skip
+ * structure of all 8 octant layouts, each node's bounding sphere contains every
+ * member below it).  *out_nodes (nullable) = tree nodes per layout. */
+SPT_API int spt_accel_check(const float *centers4, const float *radii, uint32_t n, uint32_t cluster_k,
+                            uint32_t branching, uint32_t *out_nodes);
 /* Upper bound of the per-sample workspace (default 4 GiB).  Larger frames are
  * rendered in sample batches folded in order. */
 SPT_API int spt_set_workspace(spt_ctx *ctx, uint64_t bytes);

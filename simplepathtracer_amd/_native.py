@@ -19,6 +19,7 @@ SPT_OK = 0
 STATUS_NAMES = {0: "SPT_OK", 1: "SPT_ERR_ARG", 2: "SPT_ERR_STATE", 3: "SPT_ERR_HIP", 4: "SPT_ERR_NOMEM",
                 5: "SPT_ERR_NODEVICE"}
 MODE_SEGMENT, MODE_TASK = 0, 1
+TREE_AUTO = 0xFFFFFFFF  # spt_set_cluster_tree default
 SELFTEST_COLS = 8
 
 
@@ -81,6 +82,8 @@ def lib() -> ctypes.CDLL:
         "spt_set_params": ([P, u32, u32, u32, u32, u64], I),
         "spt_set_workspace": ([P, u64], I),
         "spt_set_cluster_size": ([P, u32], I),
+        "spt_set_cluster_tree": ([P, u32], I),
+        "spt_accel_check": ([P, P, u32, u32, u32, P], I),
         "spt_render_segment": ([P, u32, u32, u32, u32, P, P], I),
         "spt_render_segment_task": ([P, u32, u32, u32, u32, P, P], I),
         "spt_render_rows_async": ([P, I, u32, u32, u32, u32, u32, u32, u32, P, P, P], I),

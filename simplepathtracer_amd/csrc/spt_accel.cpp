@@ -7,16 +7,22 @@
 //  * "always" spheres (large radius: the ground r = 1e6, the three r = 3 balls of
 //    GenerateSpheres) are tested for every ray;
 //  * the small spheres are sorted along a Morton curve and cut into clusters of
-//    K slots, each with a bounding sphere (Cb, Rb >= |Cm - Cb| + r_m).
+//    k <= 8 members (8 slots each, dummies pad), the leaves of a tree whose inner
+//    nodes group `branching` consecutive clusters; every node carries a bounding
+//    sphere of all member spheres below it (Cb, Rb >= |Cm - Cb| + r_m).  The tree
+//    is stored in preorder with skip links, so the wave-uniform traversal needs no
+//    stack: enter a node (next record) if any lane may pass, else jump to `skip`.
 //
-// Cull condition, derived in DESIGN.md §4.1 (fp32 error analysis of both the
+// Cull condition, derived in DESIGN.md §4.4 (fp32 error analysis of both the
 // member test and the cluster test for a ray whose fp32 direction has
 // | |d|^2 - 1 | <= 1e-6; other lanes never cull): a member can pass only if the
-// cluster's computed value
+// node's computed value
 //     d2b = |Cb-o|^2 - ((Cb-o).d)^2  <=  K1 + K2 * |Cb-o|^2,
 // K1 = 1.15 Rb^2 + 1e-5, K2 = 1e-4  (each about 2x the derived worst case).
-// The kernel evaluates exactly that; clusters failing it for every lane are
-// skipped.  Tests run in traversal order, so the closest hit is selected by the
+// Eight preorder layouts, one per direction octant, differ only in sibling order.
+// The derivation uses only the containment of the members, so it holds for inner
+// nodes as for clusters.  The kernel evaluates exactly that; nodes failing it for
+// every lane are skipped with their subtree.  Tests run in traversal order, so the closest hit is selected by the
 // lexicographic (distance, original index) minimum, which equals the
 // reference's strict-'>' first-index-wins scan.
 #include "spt_accel.h"
@@ -27,7 +33,9 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <cstdio>
 #include <numeric>
+#include <string>
 
 namespace spt {
 
@@ -54,7 +62,8 @@ const float4 kDummy = make_float4(0.f, 0.f, 0.f, -INFINITY);  // r*r = -inf: nev
 
 }  // namespace
 
-AccelTables build_accel(const float *centers4, const float *radii, uint32_t n, uint32_t cluster_k, uint32_t group)
+AccelTables build_accel(const float *centers4, const float *radii, uint32_t n, uint32_t cluster_k, uint32_t group,
+                        uint32_t branching)
 {
     AccelTables t;
     t.group = group;
@@ -72,7 +81,6 @@ AccelTables build_accel(const float *centers4, const float *radii, uint32_t n, u
             (radii[i] > 4.0f * med || !finite ? always : small).push_back(i);
         }
     }
-    // always-list, padded to whole groups
     auto push_slot = [&](uint32_t i) {
         const float rr = radii[i] * radii[i];
         t.slots.push_back(make_float4(centers4[4 * i], centers4[4 * i + 1], centers4[4 * i + 2], rr));
@@ -84,72 +92,197 @@ AccelTables build_accel(const float *centers4, const float *radii, uint32_t n, u
             t.orig.push_back(0xFFFFFFFFu);
         }
     };
+    // always-list, padded to whole groups
     for (uint32_t i : always) push_slot(i);
     pad_to(group, 0);
     t.always_groups = (uint32_t)(t.slots.size() / group);
+    const size_t cbase = t.slots.size();
+
     if (!small.empty()) {
         const uint32_t k = std::min(cluster_k, kClusterSlots);  // members per cluster
-        t.cluster_k = kClusterSlots;
+        // Morton order of the small spheres' centres
         double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
         for (uint32_t i : small)
             for (int c = 0; c < 3; ++c) {
                 lo[c] = std::min(lo[c], (double)centers4[4 * i + c]);
                 hi[c] = std::max(hi[c], (double)centers4[4 * i + c]);
             }
+        // one scale for all axes (a cube), so a thin axis does not split clusters
+        const double span = std::max({hi[0] - lo[0], hi[1] - lo[1], hi[2] - lo[2]});
         std::vector<std::pair<uint32_t, uint32_t>> keyed;
         for (uint32_t i : small) {
             uint32_t q[3];
-            for (int c = 0; c < 3; ++c) {
-                const double span = hi[c] - lo[c];
+            for (int c = 0; c < 3; ++c)
                 q[c] = span > 0 ? (uint32_t)std::min(1023.0, (centers4[4 * i + c] - lo[c]) / span * 1023.0) : 0u;
-            }
             keyed.push_back({spread10(q[0]) | (spread10(q[1]) << 1) | (spread10(q[2]) << 2), i});
         }
         std::sort(keyed.begin(), keyed.end());
-        for (size_t b = 0; b < keyed.size(); b += k) {
-            const size_t e = std::min(keyed.size(), b + k);
+        std::vector<uint32_t> sorted(keyed.size());
+        for (size_t j = 0; j < keyed.size(); ++j) sorted[j] = keyed[j].second;
+
+        // leaves: k consecutive spheres each, kClusterSlots slots each
+        const uint32_t leaves = (uint32_t)((sorted.size() + k - 1) / k);
+        for (uint32_t c = 0; c < leaves; ++c) {
+            for (size_t j = (size_t)c * k; j < std::min(sorted.size(), (size_t)(c + 1) * k); ++j) push_slot(sorted[j]);
+            pad_to(kClusterSlots, cbase);
+        }
+        t.leaves = leaves;
+
+        // tree levels over consecutive leaves: level 0 = leaves, each node = [c0, c1)
+        struct Span {
+            uint32_t c0, c1;
+        };
+        std::vector<std::vector<Span>> levels(1);
+        for (uint32_t c = 0; c < leaves; ++c) levels[0].push_back({c, c + 1});
+        if (branching >= 2)
+            while (levels.back().size() > branching) {
+                const std::vector<Span> &below = levels.back();
+                std::vector<Span> up;
+                for (size_t j = 0; j < below.size(); j += branching)
+                    up.push_back({below[j].c0, below[std::min(below.size(), j + branching) - 1].c1});
+                levels.push_back(std::move(up));
+            }
+        t.depth = (uint32_t)levels.size();
+
+        // bounding sphere of the member spheres of leaves [c0, c1)
+        auto bound = [&](Span sp, AccelNode &nd) {
+            const size_t j0 = (size_t)sp.c0 * k, j1 = std::min(sorted.size(), (size_t)sp.c1 * k);
             double clo[3] = {INFINITY, INFINITY, INFINITY}, chi[3] = {-INFINITY, -INFINITY, -INFINITY};
-            for (size_t j = b; j < e; ++j)
+            for (size_t j = j0; j < j1; ++j)
                 for (int c = 0; c < 3; ++c) {
-                    clo[c] = std::min(clo[c], (double)centers4[4 * keyed[j].second + c]);
-                    chi[c] = std::max(chi[c], (double)centers4[4 * keyed[j].second + c]);
+                    clo[c] = std::min(clo[c], (double)centers4[4 * sorted[j] + c]);
+                    chi[c] = std::max(chi[c], (double)centers4[4 * sorted[j] + c]);
                 }
-            const double cb[3] = {(clo[0] + chi[0]) / 2, (clo[1] + chi[1]) / 2, (clo[2] + chi[2]) / 2};
-            const float cbf[3] = {(float)cb[0], (float)cb[1], (float)cb[2]};
+            const float cbf[3] = {(float)((clo[0] + chi[0]) / 2), (float)((clo[1] + chi[1]) / 2),
+                                  (float)((clo[2] + chi[2]) / 2)};
             double rb = 0;
-            for (size_t j = b; j < e; ++j) {
-                const uint32_t i = keyed[j].second;
+            for (size_t j = j0; j < j1; ++j) {
+                const uint32_t i = sorted[j];
                 double d2 = 0;
                 for (int c = 0; c < 3; ++c) {
                     const double dd = (double)centers4[4 * i + c] - (double)cbf[c];
                     d2 += dd * dd;
                 }
                 rb = std::max(rb, std::sqrt(d2) + std::fabs((double)radii[i]));
-                push_slot(i);
             }
-            pad_to(kClusterSlots, (size_t)t.always_groups * group);
             rb *= 1.0 + 1e-6;
-            t.bounds.push_back(make_float4(cbf[0], cbf[1], cbf[2], round_up(1.15 * rb * rb + 1e-5)));
+            nd.cx = cbf[0];
+            nd.cy = cbf[1];
+            nd.cz = cbf[2];
+            nd.rb = round_up(rb);
+            nd.k1 = round_up(1.15 * (double)nd.rb * (double)nd.rb + 1e-5);
+        };
+        // Preorder emission, once per direction octant: siblings are ordered front to
+        // back along the octant's diagonal, so a wave walking the layout of its
+        // majority octant finds near hits first and the distance test culls more.
+        // The top level sits under an implicit root (never tested).
+        std::vector<std::vector<AccelNode>> bounds(levels.size());
+        for (size_t lvl = 0; lvl < levels.size(); ++lvl) {
+            bounds[lvl].resize(levels[lvl].size());
+            for (size_t j = 0; j < levels[lvl].size(); ++j) bound(levels[lvl][j], bounds[lvl][j]);
         }
-        t.clusters = (uint32_t)t.bounds.size();
+        const uint32_t top = (uint32_t)levels.size() - 1;
+        for (uint32_t oct = 0; oct < 8; ++oct) {
+            const double sx = (oct & 1) ? -1.0 : 1.0, sy = (oct & 2) ? -1.0 : 1.0, sz = (oct & 4) ? -1.0 : 1.0;
+            const size_t base = t.nodes.size();
+            auto ordered = [&](uint32_t lvl, size_t q0, size_t q1) {
+                std::vector<size_t> ix;
+                for (size_t q = q0; q < q1; ++q) ix.push_back(q);
+                std::stable_sort(ix.begin(), ix.end(), [&](size_t a, size_t b) {
+                    const AccelNode &na = bounds[lvl][a], &nb = bounds[lvl][b];
+                    return sx * na.cx + sy * na.cy + sz * na.cz < sx * nb.cx + sy * nb.cy + sz * nb.cz;
+                });
+                return ix;
+            };
+            auto emit = [&](auto &&self, uint32_t lvl, size_t j) -> void {
+                const Span sp = levels[lvl][j];
+                const size_t me = t.nodes.size();
+                t.nodes.push_back(bounds[lvl][j]);
+                if (lvl == 0) {
+                    t.nodes[me].slot = (uint32_t)(cbase + (size_t)sp.c0 * kClusterSlots);
+                } else {
+                    t.nodes[me].slot = kNoSlot;
+                    const size_t nb = levels[lvl - 1].size();
+                    for (size_t q : ordered(lvl - 1, j * branching, std::min(nb, (j + 1) * branching)))
+                        self(self, lvl - 1, q);
+                }
+                t.nodes[me].skip = (uint32_t)(t.nodes.size() - base);
+            };
+            for (size_t j : ordered(top, 0, levels[top].size())) emit(emit, top, j);
+            if (oct == 0) t.n_nodes = (uint32_t)t.nodes.size();
+            // pad node (the kernel prefetches one node past the layout)
+            t.nodes.push_back(AccelNode{0.f, 0.f, 0.f, -INFINITY, t.n_nodes + 1, kNoSlot, 0.f, 0});
+        }
     }
-    // the kernel prefetches up to two groups past the last slot it tests
+    // the kernel prefetches one always-group past the list and one node past the tree
     for (uint32_t j = 0; j < 2 * group; ++j) {
         t.slots.push_back(kDummy);
         t.orig.push_back(0xFFFFFFFFu);
     }
-    t.bounds.push_back(make_float4(0.f, 0.f, 0.f, -INFINITY));  // prefetch pad
+    if (t.nodes.empty())  // no tree: one pad record per octant layout (n_nodes = 0)
+        for (int oct = 0; oct < 8; ++oct) t.nodes.push_back(AccelNode{0.f, 0.f, 0.f, -INFINITY, 1, kNoSlot, 0.f, 0});
     return t;
 }
 
-std::vector<float4> eye_relative(const std::vector<float4> &points, const float eye[3])
+std::string validate_accel(const AccelTables &t, const float *centers4, const float *radii, uint32_t n)
 {
-    std::vector<float4> out(points.size());
-    for (size_t i = 0; i < points.size(); ++i) {
-        const float x = points[i].x - eye[0], y = points[i].y - eye[1], z = points[i].z - eye[2];
-        out[i] = make_float4(x, y, z, (x * x + y * y) + z * z);  // lensq order, Math.hpp:122-133
+    char buf[256];
+    auto bad = [&](const char *fmt, auto... a) {
+        std::snprintf(buf, sizeof buf, fmt, a...);
+        return std::string(buf);
+    };
+    const size_t g = t.group, cbase = (size_t)t.always_groups * g;
+    if (t.slots.size() != t.orig.size()) return bad("slots/orig size mismatch");
+    if (t.slots.size() < cbase + 2 * g) return bad("slot table lacks the prefetch pad");
+    if (t.nodes.size() != 8 * ((size_t)t.n_nodes + 1)) return bad("node table is not 8 layouts of %u + 1", t.n_nodes);
+    // every sphere exactly once
+    std::vector<int> seen(n, 0);
+    for (size_t j = 0; j < t.slots.size(); ++j) {
+        const uint32_t o = t.orig[j];
+        if (o == 0xFFFFFFFFu) {
+            if (!(t.slots[j].w == -INFINITY)) return bad("dummy slot %zu can pass", j);
+            continue;
+        }
+        if (o >= n || seen[o]++) return bad("slot %zu: sphere %u out of range or repeated", j, o);
     }
-    return out;
+    for (uint32_t i = 0; i < n; ++i)
+        if (!seen[i]) return bad("sphere %u missing from the slot table", i);
+    for (uint32_t oct = 0; oct < 8; ++oct) {
+        const AccelNode *L = t.nodes.data() + (size_t)oct * (t.n_nodes + 1);
+        if (!(L[t.n_nodes].k1 == -INFINITY) || L[t.n_nodes].slot != kNoSlot) return bad("layout %u: bad pad", oct);
+        size_t leaves = 0;
+        for (uint32_t i = 0; i < t.n_nodes; ++i) {
+            const AccelNode &nd = L[i];
+            const bool leaf = nd.slot != kNoSlot;
+            if (nd.skip <= i || nd.skip > t.n_nodes || (leaf && nd.skip != i + 1) || (!leaf && nd.skip == i + 1))
+                return bad("layout %u node %u: skip %u breaks preorder", oct, i, nd.skip);
+            if (leaf) {
+                ++leaves;
+                if (nd.slot < cbase || (nd.slot - cbase) % kClusterSlots || nd.slot + kClusterSlots > t.slots.size())
+                    return bad("layout %u node %u: leaf slot %u out of range", oct, i, nd.slot);
+            }
+            // containment of every member below: |Cm - Cb| + r <= Rb and 1.15 Rb^2 + 1e-5 <= K1
+            if (!((double)nd.k1 >= 1.15 * (double)nd.rb * (double)nd.rb + 1e-5))
+                return bad("layout %u node %u: K1 below 1.15 Rb^2 + 1e-5", oct, i);
+            for (uint32_t q = i; q < nd.skip; ++q) {
+                if (L[q].slot == kNoSlot) continue;
+                for (uint32_t k = 0; k < kClusterSlots; ++k) {
+                    const uint32_t o = t.orig[L[q].slot + k];
+                    if (o == 0xFFFFFFFFu) continue;
+                    double d2 = 0;
+                    const double cb[3] = {nd.cx, nd.cy, nd.cz};
+                    for (int c = 0; c < 3; ++c) {
+                        const double dd = (double)centers4[4 * o + c] - cb[c];
+                        d2 += dd * dd;
+                    }
+                    if (!(std::sqrt(d2) + std::fabs((double)radii[o]) <= (double)nd.rb))
+                        return bad("layout %u node %u: sphere %u not contained", oct, i, o);
+                }
+            }
+        }
+        if (leaves != t.leaves) return bad("layout %u: %zu leaves, expected %u", oct, leaves, t.leaves);
+    }
+    return std::string();
 }
 
 }  // namespace spt

@@ -3,25 +3,44 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <string>
 #include <vector>
+
+#include "spt_internal.h"
 
 namespace spt {
 
-struct AccelTables {
-    std::vector<float4> slots;     // {cx, cy, cz, r*r} in traversal order, dummy = r*r -inf
-    std::vector<uint32_t> orig;    // original sphere index per slot (0xFFFFFFFF = dummy)
-    std::vector<float4> bounds;    // per cluster {Cb.x, Cb.y, Cb.z, K1} (+1 pad)
-    uint32_t group = 4;            // spheres per test group (SPT_GROUP)
-    uint32_t always_groups = 0;    // groups of always-tested spheres at the front
-    uint32_t clusters = 0;         // clusters following them
-    uint32_t cluster_k = 0;        // slots per cluster (multiple of group)
+// One node of the cluster tree, 32 B (one s_load_dwordx8).  Nodes are stored in
+// depth-first preorder: the first child of an inner node is the next record, and
+// `skip` is the index just past the node's subtree.  Leaves are clusters.
+struct AccelNode {
+    float cx, cy, cz;  // bounding-sphere centre Cb
+    float k1;          // cull constant K1 = 1.15 Rb^2 + 1e-5 (rounded up)
+    uint32_t skip;     // next node when this one is culled (or is a leaf)
+    uint32_t slot;     // leaf: first of its kClusterSlots slots; inner: kNoSlot
+    float rb;          // bounding radius Rb (rounded up)
+    uint32_t pad;
 };
 
-// Eye-relative copies for the primary-ray pass: {P - eye, |P - eye|^2} with the
-// kernel's own fp32 operation order (bit-identical to computing them in-kernel).
-std::vector<float4> eye_relative(const std::vector<float4> &points, const float eye[3]);
+struct AccelTables {
+    std::vector<float4> slots;      // {cx, cy, cz, r*r} in traversal order, dummy = r*r -inf
+    std::vector<uint32_t> orig;     // original sphere index per slot (0xFFFFFFFF = dummy)
+    std::vector<AccelNode> nodes;   // 8 octant layouts of the tree in preorder, each
+                                    // n_nodes + 1 pad records (one pad if no tree)
+    uint32_t group = 4;             // spheres per always-list test group (SPT_GROUP)
+    uint32_t always_groups = 0;     // groups of always-tested spheres at the front
+    uint32_t n_nodes = 0;           // tree nodes (without the pad)
+    uint32_t leaves = 0;            // clusters
+    uint32_t depth = 0;             // levels of the tree (1 = flat cluster list)
+};
 
-// cluster_k == 0 (or n <= 32): every sphere is "always" tested (brute force).
-AccelTables build_accel(const float *centers4, const float *radii, uint32_t n, uint32_t cluster_k, uint32_t group);
+// cluster_k: members per cluster (0, or n <= 32: every sphere is "always" tested).
+// branching: children per inner node; 0 = flat list of clusters (no inner nodes).
+AccelTables build_accel(const float *centers4, const float *radii, uint32_t n, uint32_t cluster_k, uint32_t group,
+                        uint32_t branching);
+
+// Structural and containment checks of the tables the kernel relies on for
+// exactness and in-bounds loads; empty string = valid, else the first problem.
+std::string validate_accel(const AccelTables &t, const float *centers4, const float *radii, uint32_t n);
 
 }  // namespace spt

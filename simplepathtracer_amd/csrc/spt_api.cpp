@@ -41,17 +41,17 @@ struct spt_ctx {
     uint32_t grid = 0, block = spt::kRenderBlock, claim = 128;
 
     // scene (Globals.hpp:31-37)
-    float4 *d_hit = nullptr, *d_shade = nullptr, *d_slots = nullptr, *d_bounds = nullptr;
-    float4 *d_slots_eye = nullptr, *d_bounds_eye = nullptr;
+    float4 *d_hit = nullptr, *d_shade = nullptr, *d_slots = nullptr;
+    spt::AccelNode *d_nodes = nullptr;
     uint32_t *d_mat = nullptr, *d_orig = nullptr;
-    size_t hit_cap = 0, shade_cap = 0, mat_cap = 0, slots_cap = 0, orig_cap = 0, bounds_cap = 0;
-    size_t slots_eye_cap = 0, bounds_eye_cap = 0;
+    size_t hit_cap = 0, shade_cap = 0, mat_cap = 0, slots_cap = 0, orig_cap = 0, nodes_cap = 0;
     spt::AccelTables tables;
     uint32_t n = 0;
     bool scene_set = false;
     // host copy of the hit geometry, to rebuild the traversal tables
     std::vector<float> h_centers, h_radii;
-    uint32_t cluster_k = 8;  // slots per culling cluster; 0 = brute force
+    uint32_t cluster_k = 8;                 // members per culling cluster; 0 = brute force
+    uint32_t tree_branching = SPT_TREE_AUTO;  // children per inner node; 0 = flat cluster list
     spt::AccelView accel{};
     // camera (Globals.hpp:21-29)
     spt::Camera cam{};
@@ -257,32 +257,32 @@ int upload(spt_ctx *ctx, T **p, size_t *cap, const std::vector<T> &v)
     return SPT_OK;
 }
 
-// Eye-relative tables of the primary-ray pass; needs both the scene and the camera.
-int rebuild_eye(spt_ctx *ctx)
+// Children per inner node of the cluster tree: flat list for small scenes (the
+// wave enters most clusters anyway), a 4-ary tree once the list gets long.
+uint32_t resolve_branching(const spt_ctx *ctx)
 {
-    const spt::AccelTables &t = ctx->tables;
-    if (ctx->cam_set && !t.slots.empty()) {
-        int rc = upload(ctx, &ctx->d_slots_eye, &ctx->slots_eye_cap, spt::eye_relative(t.slots, ctx->cam.eye));
-        if (!rc) rc = upload(ctx, &ctx->d_bounds_eye, &ctx->bounds_eye_cap, spt::eye_relative(t.bounds, ctx->cam.eye));
-        if (rc) return rc;
-    }
-    ctx->accel = spt::AccelView{ctx->d_slots,     ctx->d_orig,       ctx->d_bounds,      ctx->d_slots_eye,
-                                ctx->d_bounds_eye, t.always_groups, t.clusters,         t.cluster_k};
-    return SPT_OK;
+    if (ctx->tree_branching != SPT_TREE_AUTO) return ctx->tree_branching;
+    const uint32_t k = std::max<uint32_t>(1, std::min(ctx->cluster_k, spt::kClusterSlots));
+    return ctx->n / k > 64 ? 4u : 0u;
 }
 
 // Build and upload the hot-loop traversal tables (spt_accel.cpp) for the current scene.
 int rebuild_accel(spt_ctx *ctx)
 {
     const uint32_t g = spt::render_group_size();
-    spt::AccelTables t = spt::build_accel(ctx->h_centers.data(), ctx->h_radii.data(), ctx->n, ctx->cluster_k, g);
+    spt::AccelTables t = spt::build_accel(ctx->h_centers.data(), ctx->h_radii.data(), ctx->n, ctx->cluster_k, g,
+                                          resolve_branching(ctx));
+    const std::string bad = spt::validate_accel(t, ctx->h_centers.data(), ctx->h_radii.data(), ctx->n);
+    if (!bad.empty()) return fail(ctx, SPT_ERR_STATE, "traversal tables invalid: %s", bad.c_str());
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     int rc = upload(ctx, &ctx->d_slots, &ctx->slots_cap, t.slots);
     if (!rc) rc = upload(ctx, &ctx->d_orig, &ctx->orig_cap, t.orig);
-    if (!rc) rc = upload(ctx, &ctx->d_bounds, &ctx->bounds_cap, t.bounds);
+    if (!rc) rc = upload(ctx, &ctx->d_nodes, &ctx->nodes_cap, t.nodes);
     if (rc) return rc;
+    ctx->accel = spt::AccelView{ctx->d_slots, ctx->d_orig, ctx->d_nodes, t.always_groups, t.n_nodes,
+                                t.n_nodes > t.leaves ? 1u : 0u};
     ctx->tables = std::move(t);
-    return rebuild_eye(ctx);
+    return SPT_OK;
 }
 
 int check_region(spt_ctx *ctx, uint32_t yB, uint32_t yE, uint32_t xB, uint32_t xE)
@@ -369,6 +369,7 @@ int spt_ctx_create(int device, spt_ctx **out)
     if (const char *e = std::getenv("SPT_BLOCKS_PER_CU")) per_cu = std::max(1, std::atoi(e));
     if (const char *e = std::getenv("SPT_CLAIM")) ctx->claim = (uint32_t)std::max(1, std::atoi(e));
     if (const char *e = std::getenv("SPT_CLUSTER_K")) ctx->cluster_k = (uint32_t)std::max(0, std::atoi(e));
+    if (const char *e = std::getenv("SPT_TREE_B")) ctx->tree_branching = (uint32_t)std::max(0, std::atoi(e));
     ctx->grid = (uint32_t)(per_cu * ctx->num_cu);
     if (hipMalloc((void **)&ctx->d_head, sizeof(uint32_t)) != hipSuccess ||
         hipMalloc((void **)&ctx->d_counters, 12 * sizeof(unsigned long long)) != hipSuccess ||
@@ -390,8 +391,8 @@ void spt_ctx_destroy(spt_ctx *ctx)
             (void)hipEventDestroy(p.a);
             (void)hipEventDestroy(p.b);
         }
-    void *bufs[] = {ctx->d_hit, ctx->d_shade, ctx->d_mat, ctx->d_slots, ctx->d_orig, ctx->d_bounds,
-                    ctx->d_slots_eye, ctx->d_bounds_eye, ctx->d_samples, ctx->d_acc,
+    void *bufs[] = {ctx->d_hit, ctx->d_shade, ctx->d_mat, ctx->d_slots, ctx->d_orig, ctx->d_nodes,
+                    ctx->d_samples, ctx->d_acc,
                     ctx->d_head, ctx->d_counters, ctx->d_stage, ctx->d_frame8};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
@@ -448,8 +449,7 @@ int spt_set_camera(spt_ctx *ctx, const float view[16], const float eye[4], const
         ctx->cam.sky[j] = sky[j];
     }
     ctx->cam_set = true;
-    HIP_TRY(ctx, hipSetDevice(ctx->device));
-    return rebuild_eye(ctx);
+    return SPT_OK;
 }
 
 int spt_set_params(spt_ctx *ctx, uint32_t width, uint32_t height, uint32_t spp, uint32_t bounces, uint64_t seed)
@@ -479,6 +479,31 @@ int spt_set_cluster_size(spt_ctx *ctx, uint32_t k)
     if (!ctx->scene_set) return SPT_OK;
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     return rebuild_accel(ctx);
+}
+
+int spt_set_cluster_tree(spt_ctx *ctx, uint32_t branching)
+{
+    if (!ctx) return fail(nullptr, SPT_ERR_ARG, "null context");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    if (branching == 1 || (branching > 64 && branching != SPT_TREE_AUTO))
+        return fail(ctx, SPT_ERR_ARG, "tree branching %u not in {0, 2..64, SPT_TREE_AUTO}", branching);
+    ctx->tree_branching = branching;
+    if (!ctx->scene_set) return SPT_OK;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    return rebuild_accel(ctx);
+}
+
+int spt_accel_check(const float *centers4, const float *radii, uint32_t n, uint32_t cluster_k, uint32_t branching,
+                    uint32_t *out_nodes)
+{
+    if (n > 0 && (!centers4 || !radii)) return fail(nullptr, SPT_ERR_ARG, "null scene array");
+    if (cluster_k > spt::kClusterSlots) return fail(nullptr, SPT_ERR_ARG, "cluster size %u > %u", cluster_k, spt::kClusterSlots);
+    if (branching == 1) return fail(nullptr, SPT_ERR_ARG, "tree branching 1");
+    const spt::AccelTables t = spt::build_accel(centers4, radii, n, cluster_k, spt::render_group_size(), branching);
+    const std::string bad = spt::validate_accel(t, centers4, radii, n);
+    if (!bad.empty()) return fail(nullptr, SPT_ERR_STATE, "traversal tables invalid: %s", bad.c_str());
+    if (out_nodes) *out_nodes = t.n_nodes;
+    return SPT_OK;
 }
 
 int spt_set_workspace(spt_ctx *ctx, uint64_t bytes)

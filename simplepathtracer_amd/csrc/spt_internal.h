@@ -31,15 +31,15 @@ __host__ __device__ inline uint32_t rows_owned(const RowMap &m)
 
 constexpr uint32_t kMaxGroup = 16;     // sphere-table padding granule (>= SPT_GROUP)
 constexpr uint32_t kClusterSlots = 8;  // slots per culling cluster (members <= 8, dummies pad)
+constexpr uint32_t kNoSlot = 0xFFFFFFFFu;  // AccelNode::slot of inner nodes
 
 // Hot-loop traversal tables (spt_accel.cpp).
 struct AccelView {
-    const float4 *slots;       // {cx, cy, cz, r*r} in traversal order (always groups, then clusters)
-    const uint32_t *orig;      // original sphere index per slot
-    const float4 *bounds;      // per cluster {Cb, K1}
-    const float4 *slots_eye;   // per slot {C - eye, |C - eye|^2} (primary rays)
-    const float4 *bounds_eye;  // per cluster {Cb - eye, |Cb - eye|^2}
-    uint32_t always_groups, clusters, cluster_k;
+    const float4 *slots;    // {cx, cy, cz, r*r} in traversal order (always groups, then clusters)
+    const uint32_t *orig;   // original sphere index per slot
+    const void *nodes;      // AccelNode[8][n_nodes + 1]: per-octant preorder layouts (spt_accel.h)
+    uint32_t always_groups, n_nodes;
+    uint32_t tree;  // 0: flat cluster list (every node a leaf), 1: tree with inner nodes
 };
 
 struct DeviceScene {

@@ -10,16 +10,11 @@
 // handed out by a wave-level ballot/mbcnt prefix over a block claimed from one
 // global counter, so lanes never wait for the slowest path of their wave.
 //
-// Lanes that start a sample cast their primary ray in a batched pass right at
-// refill time: all primary rays share the origin eyePos, so C - eye and
-// |C - eye|^2 of every sphere (and cluster bound) come precomputed with the same
-// fp32 operations (bit-identical values), the test drops from 18 to 10 VALU and
-// the refilled lanes -- adjacent pixels of one sample -- cull clusters well.
-// The main cast then carries secondary rays only.
-//
 // Sphere data is read with wave-uniform scalar loads (s_load) -- the sphere
-// index of the hot loop is the same for all lanes.  Clusters of small spheres
-// are skipped when no lane can pass any member's test (spt_accel.cpp).
+// index of the hot loop is the same for all lanes.  Small spheres sit in 8-slot
+// clusters under a tree of bounding spheres walked by the whole wave without a
+// stack (preorder + skip links); a subtree is skipped when no lane can pass any
+// member's test (spt_accel.cpp).
 //
 // fold_kernel: RenderSegment's `pixelColor += sample` in sample order followed by
 // `*= 1/g_samples` (SingleThreadPathTracer.hpp:121-134) or RenderSegmentTask's
@@ -39,10 +34,9 @@
 #define SPT_DIAG 0
 #endif
 
-// Primary-ray batch at refill time: number of refill rounds per iteration
-// (0 = primaries go through the main cast like any other ray).
-#ifndef SPT_PRIM_ROUNDS
-#define SPT_PRIM_ROUNDS 0
+// 1: flat cluster lists use the tree walk's three tests too (A/B switch)
+#ifndef SPT_FLAT_FULL
+#define SPT_FLAT_FULL 0
 #endif
 
 #pragma clang fp contract(off)
@@ -62,6 +56,7 @@ constexpr float kGlassToAir = 1.5f / 1.0f;
 // Tables as constant-address-space data: wave-uniform indices become scalar
 // (s_load) reads even though the kernel also stores to global memory.
 typedef __attribute__((address_space(4))) const float cfloat;
+typedef __attribute__((address_space(4))) const uint32_t cuint;
 
 __device__ __forceinline__ float4 ld_uniform(cfloat *p, uint32_t i)
 {
@@ -81,17 +76,15 @@ struct Hit {
     f3 p;                // its closest contact point
 };
 
-// One group of SPT_GROUP slots (Collision.hpp:87-109): RaySphereIntersection for
+// One group of G slots {C, r*r} (Collision.hpp:87-109): RaySphereIntersection for
 // all of them, then the rare closest-contact / distance update behind a single
-// branch.  EYE: the slots hold {C - eye, |C - eye|^2} (primary rays, o == eye),
-// else {C, r*r}; `rr` then comes from the regular table.  Slots are visited in
-// traversal order, so the winner is the lexicographic minimum of (distance,
-// original index): identical to the reference's strict-'>' scan in index order
-// (first index wins ties; NaN and FLT_MAX distances never win).
-template <bool EYE, int G>
-__device__ __forceinline__ void test_group(const float4 (&sp)[G], const float (&rr)[G],
-                                           const uint32_t *__restrict__ orig, uint32_t slot, const f3 &o, const f3 &d,
-                                           float dod, Hit &h)
+// branch.  Slots are visited in traversal order, so the winner is the
+// lexicographic minimum of (distance, original index): identical to the
+// reference's strict-'>' scan in index order (first index wins ties; NaN and
+// FLT_MAX distances never win).
+template <int G>
+__device__ __forceinline__ void test_group(const float4 (&sp)[G], const uint32_t *__restrict__ orig, uint32_t slot,
+                                           const f3 &o, const f3 &d, float dod, Hit &h)
 {
     float tcv[G], hv[G];
     bool pass[G];
@@ -99,18 +92,10 @@ __device__ __forceinline__ void test_group(const float4 (&sp)[G], const float (&
 #pragma unroll
     for (int k = 0; k < G; ++k) {
         // RaySphereIntersection, Collision.hpp:9-17
-        float tc, d2, r2;
-        if (EYE) {
-            tc = (sp[k].x * d.x + sp[k].y * d.y) + sp[k].z * d.z;
-            d2 = sp[k].w - tc * tc;
-            r2 = rr[k];
-        } else {
-            const float ocx = sp[k].x - o.x, ocy = sp[k].y - o.y, ocz = sp[k].z - o.z;
-            tc = (ocx * d.x + ocy * d.y) + ocz * d.z;
-            d2 = ((ocx * ocx + ocy * ocy) + ocz * ocz) - tc * tc;
-            r2 = sp[k].w;
-        }
-        const float hh = r2 - d2;
+        const float ocx = sp[k].x - o.x, ocy = sp[k].y - o.y, ocz = sp[k].z - o.z;
+        const float tc = (ocx * d.x + ocy * d.y) + ocz * d.z;
+        const float d2 = ((ocx * ocx + ocy * ocy) + ocz * ocz) - tc * tc;
+        const float hh = sp[k].w - d2;
         tcv[k] = tc;
         hv[k] = hh;
         pass[k] = tc > 1e-3f && hh > 1e-3f;
@@ -138,11 +123,31 @@ __device__ __forceinline__ void test_group(const float4 (&sp)[G], const float (&
     }
 }
 
+// Wave-diagnostic counters of the SPT_DIAG build.
+struct CastDiag {
+    unsigned long long nodes = 0, leaves = 0, pairs = 0, live = 0;
+};
+
+// Leaf test: the cluster's kClusterSlots slots, two s_load_dwordx16 off one base pointer.
+__device__ __forceinline__ void test_leaf(cfloat *slots, const uint32_t *__restrict__ orig, uint32_t leaf_slot,
+                                          const f3 &o, const f3 &d, float dod, Hit &h)
+{
+    cfloat *cs = slots + 4 * leaf_slot;
+    float4 m8[kClusterSlots];
+#pragma unroll
+    for (int k = 0; k < (int)kClusterSlots; ++k) m8[k] = ld_uniform(cs, k);
+    test_group<(int)kClusterSlots>(m8, orig, leaf_slot, o, d, dod, h);
+}
+
 // FindClosestIntersectionSphere for every lane of the wave (Collision.hpp:87-109).
-// `active`: lanes whose result matters (others never open a cluster).
-template <bool EYE>
+// `active`: lanes whose result matters (others never open a node).
+// TREE = false: the clusters form a flat list (small scenes) and a node is
+// entered when the ray's line may pass one of its members (the "line" test of
+// DESIGN.md §4.4).  TREE = true: preorder walk of the cluster tree in the layout
+// of the wave's majority direction octant with the line, front and near tests.
+template <bool TREE>
 __device__ __forceinline__ Hit find_closest(const AccelView &ac, uint32_t n, const f3 &o, const f3 &d, bool active,
-                                            unsigned long long &diag_clusters)
+                                            CastDiag &dg)
 {
     Hit h;
     h.idx = n;
@@ -150,61 +155,101 @@ __device__ __forceinline__ Hit find_closest(const AccelView &ac, uint32_t n, con
     h.best = FLT_MAX;
     h.p = o;
     const float dod = dot(o, d);
-    cfloat *slots = (cfloat *)(EYE ? ac.slots_eye : ac.slots);
-    cfloat *rrs = (cfloat *)ac.slots;
-    float4 g4[SPT_GROUP];
-    float rr[SPT_GROUP];
+    cfloat *slots = (cfloat *)ac.slots;
     // always-tested spheres (ground, large balls; every sphere when culling is off)
     for (uint32_t g = 0; g < ac.always_groups; ++g) {
+        float4 g4[SPT_GROUP];
 #pragma unroll
-        for (int k = 0; k < SPT_GROUP; ++k) {
-            g4[k] = ld_uniform(slots, g * SPT_GROUP + k);
-            rr[k] = EYE ? rrs[4 * (g * SPT_GROUP + k) + 3] : 0.f;
-        }
-        test_group<EYE, SPT_GROUP>(g4, rr, ac.orig, g * SPT_GROUP, o, d, dod, h);
+        for (int k = 0; k < SPT_GROUP; ++k) g4[k] = ld_uniform(slots, g * SPT_GROUP + k);
+        test_group<SPT_GROUP>(g4, ac.orig, g * SPT_GROUP, o, d, dod, h);
     }
-    // clusters: skipped when no lane can pass any member's test (spt_accel.cpp).
     // Lanes whose direction is not unit length within 1e-6 (the glass branch
     // reflects without renormalising) never cull.
     const float ddev = lensq(d) - 1.0f;
     const bool no_cull = active && !(ddev <= 1e-6f && ddev >= -1e-6f);
-    cfloat *bounds = (cfloat *)(EYE ? ac.bounds_eye : ac.bounds);
-    cfloat *k1s = (cfloat *)ac.bounds;
-    const uint32_t cbase = ac.always_groups * SPT_GROUP;
-    float4 bn = ld_uniform(bounds, 0);  // prefetched one cluster ahead (table is padded)
-    float k1n = k1s[3];
-    for (uint32_t c = 0; c < ac.clusters; ++c) {
-        const float4 b = bn;
-        const float k1 = k1n;
-        bn = ld_uniform(bounds, c + 1);
-        k1n = k1s[4 * (c + 1) + 3];
-        float d2b, occb;
-        if (EYE) {
-            const float tcb = (b.x * d.x + b.y * d.y) + b.z * d.z;
-            occb = b.w;
-            d2b = occb - tcb * tcb;
-        } else {
-            const f3 ocb = mk(b.x - o.x, b.y - o.y, b.z - o.z);
-            const float tcb = dot(ocb, d);
-            occb = lensq(ocb);
-            d2b = occb - tcb * tcb;
-        }
-        const bool might = no_cull || (active && d2b <= k1 + 1e-4f * occb);
-        const unsigned long long mm = __ballot(might);
-        diag_clusters += mm != 0ull;
-        if (mm != 0ull) {
-            // the cluster's kClusterSlots slots: two s_load_dwordx16 off one base pointer
-            const uint32_t s0 = cbase + c * kClusterSlots;
-            cfloat *cs = slots + 4 * s0;
-            float4 m8[kClusterSlots];
-            float r8[kClusterSlots];
+    const unsigned long long live_mask = __ballot(active);
+    cuint *nodes = (cuint *)ac.nodes;
+    if (!TREE) {
+#if !SPT_FLAT_FULL
+        // flat list: node i is leaf i; bound prefetched one node ahead (pad record)
+        uint32_t nb[6];
 #pragma unroll
-            for (int k = 0; k < (int)kClusterSlots; ++k) {
-                m8[k] = ld_uniform(cs, k);
-                r8[k] = EYE ? rrs[4 * (s0 + k) + 3] : 0.f;
+        for (int q = 0; q < 6; ++q) nb[q] = nodes[q];
+        for (uint32_t i = 0; i < ac.n_nodes; ++i) {
+            const float bx = __uint_as_float(nb[0]), by = __uint_as_float(nb[1]), bz = __uint_as_float(nb[2]);
+            const float k1 = __uint_as_float(nb[3]);
+            const uint32_t leaf_slot = nb[5];
+#pragma unroll
+            for (int q = 0; q < 6; ++q) nb[q] = nodes[8 * (i + 1) + q];
+            const f3 ocb = mk(bx - o.x, by - o.y, bz - o.z);
+            const float tcb = dot(ocb, d);
+            const float occb = lensq(ocb);
+            const float d2b = occb - tcb * tcb;
+            const bool might = no_cull || (active && d2b <= k1 + 1e-4f * occb);
+            const unsigned long long mm = __ballot(might);
+            if (SPT_DIAG) {
+                dg.nodes += 1;
+                dg.leaves += mm != 0ull ? 1 : 0;
+                dg.pairs += (unsigned long long)__popcll(mm);
+                dg.live += mm != 0ull ? (unsigned long long)__popcll(live_mask) : 0ull;
             }
-            test_group<EYE, (int)kClusterSlots>(m8, r8, ac.orig, s0, o, d, dod, h);
+            if (mm != 0ull) test_leaf(slots, ac.orig, leaf_slot, o, d, dod, h);
         }
+        return h;
+#endif
+    }
+    const float olen = __builtin_amdgcn_sqrtf(lensq(o));  // |o|, for the distance margin
+    if (TREE) {
+        // the layout of the wave's majority direction octant (siblings front to back)
+        const uint32_t nlive = (uint32_t)__popcll(live_mask);
+        const uint32_t oct = (2u * (uint32_t)__popcll(__ballot(active && d.x < 0.f)) > nlive ? 1u : 0u) |
+                             (2u * (uint32_t)__popcll(__ballot(active && d.y < 0.f)) > nlive ? 2u : 0u) |
+                             (2u * (uint32_t)__popcll(__ballot(active && d.z < 0.f)) > nlive ? 4u : 0u);
+        nodes += (size_t)8 * (ac.n_nodes + 1) * oct;
+    }
+    uint32_t i = 0;
+    uint32_t nb[7];
+#pragma unroll
+    for (int q = 0; q < 7; ++q) nb[q] = nodes[q];
+    while (i < ac.n_nodes) {
+        const float bx = __uint_as_float(nb[0]), by = __uint_as_float(nb[1]), bz = __uint_as_float(nb[2]);
+        const float k1 = __uint_as_float(nb[3]), rb = __uint_as_float(nb[6]);
+        const uint32_t skip = nb[4], leaf_slot = nb[5];
+        // speculative prefetch of the preorder successor
+#pragma unroll
+        for (int q = 0; q < 7; ++q) nb[q] = nodes[8 * (i + 1) + q];
+        // Three conservative tests; a lane may need the node only
+        // if all pass.  line: the ray's line passes within the bound; front: some
+        // member may lie in front (tc > 1e-3); near: some member's contact point
+        // may be closer than the lane's current winner (never equal: strict margin).
+        const f3 ocb = mk(bx - o.x, by - o.y, bz - o.z);
+        const float tcb = dot(ocb, d);
+        const float occb = lensq(ocb);
+        const float d2b = occb - tcb * tcb;
+        const float lb = __builtin_amdgcn_sqrtf(occb);
+        const float slack = 1e-4f * (lb + rb);
+        const float lc = ((lb - rb) - slack) - (2e-5f * olen + 1e-6f);
+        const bool line = d2b <= k1 + 1e-4f * occb;
+        const bool front = tcb >= -(rb + slack);
+        const bool near = !(lc > 0.f && lc * lc > h.best * 1.0001f);
+        const bool might = no_cull || (active && line && front && near);
+        const unsigned long long mm = __ballot(might);
+        const bool leaf = leaf_slot != kNoSlot;
+        if (SPT_DIAG) {
+            dg.nodes += 1;
+            dg.leaves += (mm != 0ull && leaf) ? 1 : 0;
+            if (leaf) {
+                dg.pairs += (unsigned long long)__popcll(mm);
+                dg.live += mm != 0ull ? (unsigned long long)__popcll(live_mask) : 0ull;
+            }
+        }
+        if (mm != 0ull && leaf) test_leaf(slots, ac.orig, leaf_slot, o, d, dod, h);
+        const uint32_t next = (mm != 0ull && !leaf) ? i + 1 : skip;
+        if (next != i + 1) {
+#pragma unroll
+            for (int q = 0; q < 7; ++q) nb[q] = nodes[8 * next + q];
+        }
+        i = next;
     }
     return h;
 }
@@ -336,7 +381,16 @@ __device__ __forceinline__ void shade_step(const RenderArgs &a, Path &ps, const 
 
 }  // namespace
 
-__global__ __launch_bounds__(kRenderBlock) void render_kernel(RenderArgs a)
+#ifndef SPT_WAVES_PER_EU
+#define SPT_WAVES_PER_EU 0
+#endif
+#if SPT_WAVES_PER_EU
+#define SPT_RENDER_ATTR __attribute__((amdgpu_waves_per_eu(SPT_WAVES_PER_EU, SPT_WAVES_PER_EU)))
+#else
+#define SPT_RENDER_ATTR
+#endif
+
+__global__ __launch_bounds__(kRenderBlock) SPT_RENDER_ATTR void render_kernel(RenderArgs a)
 {
     const uint32_t lane = __lane_id();
     const uint32_t n = a.scene.n;
@@ -351,7 +405,8 @@ __global__ __launch_bounds__(kRenderBlock) void render_kernel(RenderArgs a)
     uint32_t blk_cur = 0, blk_end = 0;
     bool exhausted = false;
     unsigned long long casts = 0, done = 0, dropped = 0;
-    unsigned long long d_iters = 0, d_clusters = 0, d_cyc_cast = 0, d_cyc_shade = 0, d_cyc_refill = 0, d_prim = 0;
+    unsigned long long d_iters = 0, d_cyc_cast = 0, d_cyc_shade = 0, d_cyc_refill = 0;
+    CastDiag dg;
 #if SPT_DIAG
     unsigned long long d_t0 = __builtin_amdgcn_s_memtime();
 #define SPT_STAMP(acc)                                              \
@@ -367,13 +422,9 @@ __global__ __launch_bounds__(kRenderBlock) void render_kernel(RenderArgs a)
 #endif
 
     for (;;) {
-        // ---- refill: hand out (pixel, sample) items to idle lanes (ballot + prefix),
-        // cast their primary rays in one eye-relative batch and shade the hits.
-        // Two rounds, so lanes whose primary ray went to the sky start again at once.
-#pragma unroll 1
-        for (int round = 0; round < (SPT_PRIM_ROUNDS > 0 ? SPT_PRIM_ROUNDS : 1); ++round) {
-            const unsigned long long need = __ballot(ps.phase == PH_IDLE);
-            if (need == 0ull || exhausted) break;
+        // ---- refill: hand out (pixel, sample) items to idle lanes (ballot + prefix)
+        const unsigned long long need = __ballot(ps.phase == PH_IDLE);
+        if (need != 0ull && !exhausted) {
             const uint32_t cnt = (uint32_t)__popcll(need);
             const uint32_t rank = lane_rank(need);
             const uint32_t avail = blk_end - blk_cur;
@@ -396,8 +447,7 @@ __global__ __launch_bounds__(kRenderBlock) void render_kernel(RenderArgs a)
                     blk_end = ne;
                 }
             }
-            const bool fresh = ps.phase == PH_IDLE && mine != 0xFFFFFFFFu;
-            if (fresh) {
+            if (ps.phase == PH_IDLE && mine != 0xFFFFFFFFu) {
                 // primary ray, SingleThreadPathTracer.hpp:123-130.  Items are ordered
                 // [sample][pixel]: a claim is a run of adjacent pixels of one sample.
                 ps.item = mine;
@@ -420,26 +470,19 @@ __global__ __launch_bounds__(kRenderBlock) void render_kernel(RenderArgs a)
                 ps.bounce = a.bounces;
                 ps.spec = 0;
             }
-            if (SPT_PRIM_ROUNDS == 0) break;
-            const unsigned long long fm = __ballot(fresh);
-            if (fm == 0ull) break;
-            SPT_STAMP(d_cyc_refill);
-            casts += (unsigned long long)__popcll(fm);
-            d_prim += 1;
-            const Hit h = find_closest<true>(a.scene.accel, n, eye, ps.d, fresh, d_clusters);
-            SPT_STAMP(d_cyc_cast);
-            if (fresh) shade_step(a, ps, h, done, dropped);
-            SPT_STAMP(d_cyc_shade);
         }
         const unsigned long long live = __ballot(ps.phase != PH_IDLE);
         if (live == 0ull) {
             if (exhausted) break;
             continue;
         }
+        SPT_STAMP(d_cyc_refill);
         casts += (unsigned long long)__popcll(live);
         ++d_iters;
-        // ---- secondary casts + one shading step ----
-        const Hit h = find_closest<false>(a.scene.accel, n, ps.o, ps.d, ps.phase != PH_IDLE, d_clusters);
+        // ---- one cast + one shading step ----
+        const bool act = ps.phase != PH_IDLE;
+        const Hit h = a.scene.accel.tree ? find_closest<true>(a.scene.accel, n, ps.o, ps.d, act, dg)
+                                         : find_closest<false>(a.scene.accel, n, ps.o, ps.d, act, dg);
         SPT_STAMP(d_cyc_cast);
         if (ps.phase != PH_IDLE) shade_step(a, ps, h, done, dropped);
         SPT_STAMP(d_cyc_shade);
@@ -452,19 +495,19 @@ __global__ __launch_bounds__(kRenderBlock) void render_kernel(RenderArgs a)
 #if SPT_DIAG
     if (lane == 0) {
         atomicAdd(&a.counters[4], d_iters);
-        atomicAdd(&a.counters[5], d_clusters);
-        atomicAdd(&a.counters[6], d_prim);
+        atomicAdd(&a.counters[5], dg.leaves);
+        atomicAdd(&a.counters[6], dg.nodes);
         atomicAdd(&a.counters[7], d_cyc_cast);
         atomicAdd(&a.counters[8], d_cyc_shade);
         atomicAdd(&a.counters[9], d_cyc_refill);
+        atomicAdd(&a.counters[10], dg.pairs);
+        atomicAdd(&a.counters[11], dg.live);
     }
 #endif
     (void)d_iters;
-    (void)d_clusters;
     (void)d_cyc_cast;
     (void)d_cyc_shade;
     (void)d_cyc_refill;
-    (void)d_prim;
 #undef SPT_STAMP
 }
 

@@ -83,6 +83,11 @@ class Context:
         """Culling cluster size (0 = brute force over every sphere); results identical."""
         self._check(_native.lib().spt_set_cluster_size(self._h, int(k)))
 
+    def set_cluster_tree(self, branching: int) -> None:
+        """Children per inner node of the cluster tree (0 = flat list,
+        _native.TREE_AUTO = default heuristic); results identical."""
+        self._check(_native.lib().spt_set_cluster_tree(self._h, int(branching)))
+
     def set_workspace(self, nbytes: int) -> None:
         self._check(_native.lib().spt_set_workspace(self._h, int(nbytes)))
 

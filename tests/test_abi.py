@@ -77,3 +77,54 @@ def test_cpp_dropin_shim_compiles_against_the_c_abi(native, tmp_path):
     (no HIP headers) in a translation unit shaped like the reference's."""
     import os
     assert os.path.exists(_build_shim_harness(tmp_path))
+
+
+def _accel_check(native, centers, radii, k, b):
+    P = ctypes.c_void_p
+    c = np.ascontiguousarray(centers, np.float32)
+    r = np.ascontiguousarray(radii, np.float32)
+    nodes = ctypes.c_uint32(0)
+    rc = native.lib().spt_accel_check(c.ctypes.data_as(P), r.ctypes.data_as(P), len(r), k, b, ctypes.byref(nodes))
+    return rc, nodes.value, native.lib().spt_last_error(None)
+
+
+@pytest.mark.parametrize("k,b", [(8, 0), (8, 2), (8, 4), (8, 16), (3, 4), (5, 0), (1, 2), (0, 4)])
+@pytest.mark.parametrize("scene", ["random", "stress2000", "stress10000"])
+def test_traversal_tables_are_valid(native, scene, k, b):
+    """The culling tree's exactness rests on host-built tables: every sphere in
+    exactly one slot, sound preorder/skip links in all 8 octant layouts, and every
+    node's bounding sphere containing all members below it (spt_accel.cpp)."""
+    import simplepathtracer_amd as spt
+    s = spt.generate_spheres(1) if scene == "random" else spt.generate_stress(2, int(scene[6:]))
+    rc, nodes, err = _accel_check(native, s.centers, s.radii, k, b)
+    assert rc == 0, err
+    if k == 0:
+        assert nodes == 0  # brute force: every sphere in the always-list
+    elif b == 0:
+        assert nodes == -(-(s.n - 4) // k)  # flat: one node per cluster (4 big spheres are "always")
+    else:
+        assert nodes > -(-(s.n - 4) // k)
+
+
+@pytest.mark.parametrize("case", ["empty", "tiny", "coincident", "nonfinite", "huge_spread"])
+def test_traversal_tables_edge_scenes(native, case):
+    rng = np.random.default_rng(7)
+    if case == "empty":
+        c, r = np.zeros((0, 4)), np.zeros(0)
+    elif case == "tiny":
+        c, r = rng.normal(size=(5, 4)), np.full(5, 0.3)
+    elif case == "coincident":  # every centre identical: degenerate Morton keys and Rb = r
+        c, r = np.ones((300, 4)), np.full(300, 0.2)
+    elif case == "nonfinite":  # non-finite spheres go to the always-list, never into a bound
+        c, r = rng.normal(size=(400, 4)) * 10, rng.uniform(0.1, 0.3, 400)
+        c[17, 1] = np.inf
+        r[33] = np.nan
+        c[90, 0] = np.nan
+    else:  # bounds spanning 1e-3 .. 1e5
+        c = np.concatenate([rng.normal(size=(200, 4)) * 1e-3, rng.normal(size=(200, 4)) * 1e5])
+        r = np.concatenate([np.full(200, 1e-4), np.full(200, 10.0)])
+    for k, b in ((8, 0), (8, 4), (2, 2)):
+        rc, _, err = _accel_check(native, c, r, k, b)
+        assert rc == 0, (case, k, b, err)
+    rc, _, _ = _accel_check(native, c, r, 9, 0)
+    assert rc == 1

@@ -12,7 +12,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 ap = argparse.ArgumentParser()
-ap.add_argument("libs", nargs="+", help="lib.so or lib.so:cluster_k")
+ap.add_argument("libs", nargs="+", help="lib.so[:cluster_k[:tree_branching]]")
 ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--config", default="c2")
 ap.add_argument("--mode", type=int, default=0)
@@ -27,11 +27,13 @@ view = spt.camera_basis()
 P = ctypes.c_void_p
 ctxs = []
 for name in args.libs:
-    libname, _, ck = name.partition(":")
-    if ck:
-        os.environ["SPT_CLUSTER_K"] = ck
-    else:
-        os.environ.pop("SPT_CLUSTER_K", None)
+    libname, _, rest = name.partition(":")
+    ck, _, tb = rest.partition(":")
+    for var, val in (("SPT_CLUSTER_K", ck), ("SPT_TREE_B", tb)):
+        if val:
+            os.environ[var] = val
+        else:
+            os.environ.pop(var, None)
     L = ctypes.CDLL(os.path.join(ROOT, "simplepathtracer_amd", "lib", libname))
     L.spt_ctx_create.argtypes = [ctypes.c_int, P]
     L.spt_set_scene.argtypes = [P, P, P, P, P, P, ctypes.c_uint32]

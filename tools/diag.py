@@ -7,9 +7,9 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import simplepathtracer_amd as spt  # noqa: E402
 
 cfg = sys.argv[1] if len(sys.argv) > 1 else "c2"
-W, H, spp, b = {"c2": (1200, 800, 100, 50), "c2s": (1200, 800, 8, 50)}[cfg]
+W, H, spp, b = {"c2": (1200, 800, 100, 50), "c2s": (1200, 800, 8, 50), "c5s": (1920, 1080, 4, 50)}[cfg]
 ctx = spt.Context(0)
-scene = spt.generate_spheres(1)
+scene = spt.generate_stress(1, 10000) if cfg.startswith("c5") else spt.generate_spheres(1)
 ctx.set_scene(scene)
 ctx.set_camera(spt.camera_basis(), spt.scene.DEFAULT_EYE, spt.INIT_COLOR)
 ctx.set_params(W, H, spp, b, 1)
@@ -17,10 +17,13 @@ ctx.render_segment(0, H, 0, W)
 ctx.reset_stats()
 ctx.render_segment(0, H, 0, W)
 st = ctx.stats()
-it, hb, lh, cc, cs, cr, cb = st["diag"][:7]
+it, leaves, nodes, cc, cs, cr, pairs, live = st["diag"][:8]
 print(f"casts={st['casts']} samples={st['samples']} wave_iters={it} live_lanes/iter={st['casts']/max(it,1):.2f}")
 k = int(os.environ.get("SPT_CLUSTER_K", "8"))
-print(f"clusters entered per pass={hb/max(it+lh,1):.2f} (cluster size {k}); primary passes/secondary pass={lh/max(it,1):.3f}")
+print(f"per wave cast: tree nodes tested={nodes/max(it,1):.2f} clusters entered={leaves/max(it,1):.2f} "
+      f"(cluster size {k}, tree {os.environ.get('SPT_TREE_B', 'auto')})")
 tot = max(cc + cs + cr, 1)
-print(f"cycle shares: cast {cc/tot:.3f} shade {cs/tot:.3f} (ball_vector {cb/tot:.3f}) refill+ballot {cr/tot:.3f}")
+print(f"cycle shares: cast {cc/tot:.3f} shade {cs/tot:.3f} refill+ballot {cr/tot:.3f}")
+print(f"(lane, cluster) pairs that may pass per cast={pairs/max(st['casts'],1):.2f}; "
+      f"lane efficiency of entered clusters={pairs/max(live,1):.3f}")
 print(f"render_ms={st['render_ms']:.3f}")

@@ -29,6 +29,45 @@ __host__ __device__ inline uint32_t rows_owned(const RowMap &m)
     return r;
 }
 
+// Pixel of the q-th item of one sample in a region of `rows` x `width` pixels
+// whose items run through 8x8 tiles (row-major tiles, row-major inside a tile;
+// ragged tiles at the right and bottom edges).  A wave's consecutive items then
+// cover a compact patch instead of a 64-pixel row strip, so its rays start close
+// together and cull together.  Bijective on [0, rows*width).
+__host__ __device__ inline void tile_pixel(uint32_t q, uint32_t width, uint32_t rows, uint32_t &lr, uint32_t &col)
+{
+    const uint32_t band = (q / width) >> 3;
+    const uint32_t h = rows - (band << 3) < 8u ? rows - (band << 3) : 8u;
+    const uint32_t qb = q - band * 8u * width;
+    const uint32_t ft = width >> 3, wr = width & 7u;
+    uint32_t row, c;
+    if (h == 8u) {
+        const uint32_t t = qb >> 6;
+        if (t < ft) {
+            row = (qb >> 3) & 7u;
+            c = (t << 3) | (qb & 7u);
+        } else {
+            const uint32_t e = qb - (ft << 6);
+            row = e / wr;
+            c = (ft << 3) + (e - row * wr);
+        }
+    } else {
+        const uint32_t th = h << 3;
+        const uint32_t t = qb / th;
+        if (t < ft) {
+            const uint32_t e = qb - t * th;
+            row = e >> 3;
+            c = (t << 3) | (e & 7u);
+        } else {
+            const uint32_t e = qb - ft * th;
+            row = e / wr;
+            c = (ft << 3) + (e - row * wr);
+        }
+    }
+    lr = (band << 3) + row;
+    col = c;
+}
+
 constexpr uint32_t kMaxGroup = 16;     // sphere-table padding granule (>= SPT_GROUP)
 constexpr uint32_t kClusterSlots = 8;  // slots per culling cluster (members <= 8, dummies pad)
 constexpr uint32_t kNoSlot = 0xFFFFFFFFu;  // AccelNode::slot of inner nodes

@@ -34,6 +34,11 @@
 #define SPT_DIAG 0
 #endif
 
+// 1: items run through 8x8 pixel tiles of each sample (tile_pixel), 0: row-major
+#ifndef SPT_TILE
+#define SPT_TILE 1
+#endif
+
 // 1: flat cluster lists use the tree walk's three tests too (A/B switch)
 #ifndef SPT_FLAT_FULL
 #define SPT_FLAT_FULL 0
@@ -395,6 +400,8 @@ __global__ __launch_bounds__(kRenderBlock) SPT_RENDER_ATTR void render_kernel(Re
     const uint32_t lane = __lane_id();
     const uint32_t n = a.scene.n;
     const f3 eye = mk(a.cam.eye[0], a.cam.eye[1], a.cam.eye[2]);
+    const uint32_t rows = a.npix / a.map.width;  // region rows (uniform)
+    (void)rows;
 
     Path ps;
     ps.phase = PH_IDLE;
@@ -449,13 +456,20 @@ __global__ __launch_bounds__(kRenderBlock) SPT_RENDER_ATTR void render_kernel(Re
             }
             if (ps.phase == PH_IDLE && mine != 0xFFFFFFFFu) {
                 // primary ray, SingleThreadPathTracer.hpp:123-130.  Items are ordered
-                // [sample][pixel]: a claim is a run of adjacent pixels of one sample.
-                ps.item = mine;
-                const uint32_t sl = ps.item / a.npix;
+                // [sample][8x8 tile][pixel]: a claim is a compact patch of one sample.
+                const uint32_t sl = mine / a.npix;
                 const uint32_t s = a.s0 + sl;
-                const uint32_t pl = ps.item - sl * a.npix;
+                const uint32_t pl = mine - sl * a.npix;
+#if SPT_TILE
+                uint32_t lr, cx;
+                tile_pixel(pl, a.map.width, rows, lr, cx);
+                ps.item = sl * a.npix + lr * a.map.width + cx;  // slot: [sample][row-major pixel]
+                const uint32_t x = a.map.x0 + cx;
+#else
+                ps.item = mine;
                 const uint32_t lr = pl / a.map.width;
                 const uint32_t x = a.map.x0 + (pl - lr * a.map.width);
+#endif
                 const uint32_t y = a.map.parts == 1u ? a.map.y0 + lr : row_of(a.map, lr);
                 ps.st = fmix64(a.seed_key ^ (((uint64_t)(y * a.width + x) << 32) | (uint64_t)s));
                 const float u = ((float)y + uniform(ps.st, -1.f, 1.f)) / (float)a.width;

@@ -128,3 +128,17 @@ def test_traversal_tables_edge_scenes(native, case):
         assert rc == 0, (case, k, b, err)
     rc, _, _ = _accel_check(native, c, r, 9, 0)
     assert rc == 1
+
+
+def test_tile_item_map_is_a_bijection(tmp_path):
+    """The kernel's [sample][8x8 tile][pixel] item order (spt::tile_pixel) covers
+    every pixel of any region exactly once; compiled for the host with hipcc."""
+    import os
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = tmp_path / "tile_check"
+    subprocess.run(["hipcc", "-O2", "-std=c++17", "-x", "hip", "--offload-arch=gfx950",
+                    "-I", os.path.join(root, "simplepathtracer_amd", "csrc"), "-I", os.path.join(root, "include"),
+                    os.path.join(root, "tests", "cpp", "tile_check.cpp"), "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0 and out.stdout.strip() == "ok", out.stdout

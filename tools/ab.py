@@ -12,7 +12,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 ap = argparse.ArgumentParser()
-ap.add_argument("libs", nargs="+", help="lib.so[:cluster_k[:tree_branching]]")
+ap.add_argument("libs", nargs="+", help="lib.so[:cluster_k[:tree_branching]][@VAR=VAL,...] (env at ctx creation)")
 ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--config", default="c2")
 ap.add_argument("--mode", type=int, default=0)
@@ -27,7 +27,11 @@ view = spt.camera_basis()
 P = ctypes.c_void_p
 ctxs = []
 for name in args.libs:
-    libname, _, rest = name.partition(":")
+    spec, _, envs = name.partition("@")
+    for kv in filter(None, envs.split(",")):
+        var, _, val = kv.partition("=")
+        os.environ[var] = val
+    libname, _, rest = spec.partition(":")
     ck, _, tb = rest.partition(":")
     for var, val in (("SPT_CLUSTER_K", ck), ("SPT_TREE_B", tb)):
         if val:
@@ -52,6 +56,8 @@ for name in args.libs:
     assert L.spt_set_camera(h, q(view), q(e), q(sk)) == 0
     assert L.spt_set_params(h, W, H, SPP, B, 1) == 0
     ctxs.append((name, L, h))
+    for kv in filter(None, envs.split(",")):
+        os.environ.pop(kv.partition("=")[0], None)
 frames = {name: torch.zeros((H * W, 4), dtype=torch.float32, device="cuda") for name, _, _ in ctxs}
 res = {name: [] for name, _, _ in ctxs}
 for r in range(args.rounds + 1):

@@ -38,18 +38,20 @@ struct spt_ctx {
     std::mutex mu;
     std::string err;
     int num_cu = 0;
-    uint32_t grid = 0, block = spt::kRenderBlock, claim = 128;
+    uint32_t grid = 0, block = spt::kRenderBlock, claim = 0;  // 0 = per launch (claim_size)
 
     // scene (Globals.hpp:31-37)
-    float4 *d_hit = nullptr, *d_shade = nullptr, *d_slots = nullptr;
+    float4 *d_shade = nullptr, *d_slots = nullptr;
     spt::AccelNode *d_nodes = nullptr;
     uint32_t *d_mat = nullptr, *d_orig = nullptr;
-    size_t hit_cap = 0, shade_cap = 0, mat_cap = 0, slots_cap = 0, orig_cap = 0, nodes_cap = 0;
+    size_t shade_cap = 0, mat_cap = 0, slots_cap = 0, orig_cap = 0, nodes_cap = 0;
     spt::AccelTables tables;
     uint32_t n = 0;
     bool scene_set = false;
     // host copy of the hit geometry, to rebuild the traversal tables
     std::vector<float> h_centers, h_radii;
+    std::vector<float4> h_shade;  // {r, g, b, fuzz} per sphere
+    std::vector<uint32_t> h_mat;
     uint32_t cluster_k = 8;                 // members per culling cluster; 0 = brute force
     uint32_t tree_branching = SPT_TREE_AUTO;  // children per inner node; 0 = flat cluster list
     spt::AccelView accel{};
@@ -170,6 +172,17 @@ uint64_t fmix64(uint64_t z)
     return z ^ (z >> 31);
 }
 
+// Items per claim from the global counter: whole 8x8 tiles, up to 4 of them (a
+// wave's live paths then stay within one compact patch), fewer when the launch
+// is small enough that claims in flight would unbalance the tail.
+uint32_t claim_size(const spt_ctx *ctx, uint64_t items)
+{
+    if (ctx->claim) return ctx->claim;
+    const uint64_t waves = (uint64_t)ctx->grid * (ctx->block / 64);
+    const uint64_t fair = items / std::max<uint64_t>(waves * 8, 1);
+    return (uint32_t)std::min<uint64_t>(256, std::max<uint64_t>(64, fair / 64 * 64));
+}
+
 // Render the rows of `map` and fold them into d_rgba (local pixel order) and/or
 // d_rgb8 (full frame).  keep_samples: leave the per-sample colours of a single
 // batch in d_samples (debug path).
@@ -196,7 +209,7 @@ int render_impl(spt_ctx *ctx, int mode, const spt::RowMap &map, float4 *d_rgba, 
     }
 
     spt::RenderArgs ra{};
-    ra.scene = spt::DeviceScene{ctx->d_hit, ctx->d_shade, ctx->d_mat, ctx->n, ctx->accel};
+    ra.scene = spt::DeviceScene{ctx->d_shade, ctx->d_mat, ctx->n, ctx->accel};
     ra.cam = ctx->cam;
     ra.width = ctx->W;
     ra.height = ctx->H;
@@ -205,7 +218,7 @@ int render_impl(spt_ctx *ctx, int mode, const spt::RowMap &map, float4 *d_rgba, 
     ra.seed_key = fmix64(ctx->seed);
     ra.map = map;
     ra.npix = npix;
-    ra.claim = ctx->claim;
+    ra.claim = claim_size(ctx, (uint64_t)npix * spp_batch);
     ra.samples = ctx->d_samples;
     ra.head = ctx->d_head;
     ra.counters = ctx->d_counters;
@@ -274,8 +287,18 @@ int rebuild_accel(spt_ctx *ctx)
                                           resolve_branching(ctx));
     const std::string bad = spt::validate_accel(t, ctx->h_centers.data(), ctx->h_radii.data(), ctx->n);
     if (!bad.empty()) return fail(ctx, SPT_ERR_STATE, "traversal tables invalid: %s", bad.c_str());
+    // shading tables in slot order: the kernel keeps the winner's slot, not its index
+    std::vector<float4> shade(t.slots.size(), make_float4(0.f, 0.f, 0.f, 0.f));
+    std::vector<uint32_t> mat(t.slots.size(), SPT_SKYBOX);
+    for (size_t j = 0; j < t.slots.size(); ++j)
+        if (t.orig[j] != 0xFFFFFFFFu) {
+            shade[j] = ctx->h_shade[t.orig[j]];
+            mat[j] = ctx->h_mat[t.orig[j]];
+        }
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     int rc = upload(ctx, &ctx->d_slots, &ctx->slots_cap, t.slots);
+    if (!rc) rc = upload(ctx, &ctx->d_shade, &ctx->shade_cap, shade);
+    if (!rc) rc = upload(ctx, &ctx->d_mat, &ctx->mat_cap, mat);
     if (!rc) rc = upload(ctx, &ctx->d_orig, &ctx->orig_cap, t.orig);
     if (!rc) rc = upload(ctx, &ctx->d_nodes, &ctx->nodes_cap, t.nodes);
     if (rc) return rc;
@@ -391,7 +414,7 @@ void spt_ctx_destroy(spt_ctx *ctx)
             (void)hipEventDestroy(p.a);
             (void)hipEventDestroy(p.b);
         }
-    void *bufs[] = {ctx->d_hit, ctx->d_shade, ctx->d_mat, ctx->d_slots, ctx->d_orig, ctx->d_nodes,
+    void *bufs[] = {ctx->d_shade, ctx->d_mat, ctx->d_slots, ctx->d_orig, ctx->d_nodes,
                     ctx->d_samples, ctx->d_acc,
                     ctx->d_head, ctx->d_counters, ctx->d_stage, ctx->d_frame8};
     for (void *b : bufs)
@@ -414,23 +437,19 @@ int spt_set_scene(spt_ctx *ctx, const float *centers4, const float *radii, const
     if (n > 0 && (!centers4 || !radii || !colors4 || !materials || !fuzz))
         return fail(ctx, SPT_ERR_ARG, "null scene array");
     HIP_TRY(ctx, hipSetDevice(ctx->device));
-    std::vector<float4> hit(std::max<uint32_t>(n, 1)), shade(std::max<uint32_t>(n, 1));
-    std::vector<uint32_t> mat(std::max<uint32_t>(n, 1));
+    std::vector<float4> shade(n);
+    std::vector<uint32_t> mat(n);
     for (uint32_t i = 0; i < n; ++i) {
-        const float r = radii[i];
-        hit[i] = make_float4(centers4[4 * i], centers4[4 * i + 1], centers4[4 * i + 2], r * r);
         shade[i] = make_float4(colors4[4 * i], colors4[4 * i + 1], colors4[4 * i + 2], fuzz[i]);
         mat[i] = materials[i];
     }
-    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-    int rc = upload(ctx, &ctx->d_hit, &ctx->hit_cap, hit);
-    if (!rc) rc = upload(ctx, &ctx->d_shade, &ctx->shade_cap, shade);
-    if (!rc) rc = upload(ctx, &ctx->d_mat, &ctx->mat_cap, mat);
-    if (rc) return rc;
+    ctx->h_shade = std::move(shade);
+    ctx->h_mat = std::move(mat);
     ctx->h_centers.assign(centers4, centers4 + 4 * (size_t)n);
     ctx->h_radii.assign(radii, radii + n);
     ctx->n = n;
-    if ((rc = rebuild_accel(ctx))) return rc;
+    int rc = rebuild_accel(ctx);
+    if (rc) return rc;
     ctx->scene_set = true;
     return SPT_OK;
 }

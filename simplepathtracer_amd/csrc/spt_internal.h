@@ -71,6 +71,7 @@ __host__ __device__ inline void tile_pixel(uint32_t q, uint32_t width, uint32_t 
 constexpr uint32_t kMaxGroup = 16;     // sphere-table padding granule (>= SPT_GROUP)
 constexpr uint32_t kClusterSlots = 8;  // slots per culling cluster (members <= 8, dummies pad)
 constexpr uint32_t kNoSlot = 0xFFFFFFFFu;  // AccelNode::slot of inner nodes
+constexpr uint32_t kMiss = 0xFFFFFFFFu;    // Hit::idx when no sphere was hit
 
 // Hot-loop traversal tables (spt_accel.cpp).
 struct AccelView {
@@ -82,9 +83,8 @@ struct AccelView {
 };
 
 struct DeviceScene {
-    const float4 *hit;      // {cx, cy, cz, r*r} in original order (shading)
-    const float4 *shade;    // {red, green, blue, fuzz}
-    const uint32_t *mat;    // material id
+    const float4 *shade;    // {red, green, blue, fuzz} per slot (hit geometry: accel.slots)
+    const uint32_t *mat;    // material id per slot
     uint32_t n;
     AccelView accel;
 };

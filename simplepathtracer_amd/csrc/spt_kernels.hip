@@ -75,8 +75,7 @@ __device__ __forceinline__ uint32_t lane_rank(unsigned long long mask)
 
 // Closest-hit state of one FindClosestIntersectionSphere call.
 struct Hit {
-    uint32_t idx;        // original sphere index, n = miss
-    uint32_t best_orig;  // tie-break key of the current winner
+    uint32_t idx;        // slot of the winner (traversal order), kMiss = none
     float best;          // its squared distance
     f3 p;                // its closest contact point
 };
@@ -115,11 +114,12 @@ __device__ __forceinline__ void test_group(const float4 (&sp)[G], const uint32_t
                 const f3 p = mk(o.x + d.x * t, o.y + d.y * t, o.z + d.z * t);
                 if (dod < dot(p, d)) {
                     const float ds = lensq(sub(o, p));
-                    const uint32_t oi = orig[slot + k];
-                    if (ds < h.best || (ds == h.best && oi < h.best_orig)) {
+                    bool better = ds < h.best;
+                    if (ds == h.best && h.idx != kMiss)  // exact tie (rare): first original index wins
+                        better = orig[slot + k] < orig[h.idx];
+                    if (better) {
                         h.best = ds;
-                        h.best_orig = oi;
-                        h.idx = oi;
+                        h.idx = slot + k;
                         h.p = p;
                     }
                 }
@@ -151,12 +151,11 @@ __device__ __forceinline__ void test_leaf(cfloat *slots, const uint32_t *__restr
 // DESIGN.md §4.4).  TREE = true: preorder walk of the cluster tree in the layout
 // of the wave's majority direction octant with the line, front and near tests.
 template <bool TREE>
-__device__ __forceinline__ Hit find_closest(const AccelView &ac, uint32_t n, const f3 &o, const f3 &d, bool active,
+__device__ __forceinline__ Hit find_closest(const AccelView &ac, const f3 &o, const f3 &d, bool active,
                                             CastDiag &dg)
 {
     Hit h;
-    h.idx = n;
-    h.best_orig = 0;
+    h.idx = kMiss;
     h.best = FLT_MAX;
     h.p = o;
     const float dod = dot(o, d);
@@ -272,8 +271,8 @@ struct Path {
 __device__ __forceinline__ void shade_step(const RenderArgs &a, Path &ps, const Hit &h, unsigned long long &done,
                                            unsigned long long &dropped)
 {
-    const uint32_t n = a.scene.n;
-    const float4 *__restrict__ hit = a.scene.hit;
+    // hit, shade and material tables are in slot order (spt_accel.cpp)
+    const float4 *__restrict__ hit = a.scene.accel.slots;
     const float4 *__restrict__ shade = a.scene.shade;
     const uint32_t *__restrict__ mat = a.scene.mat;
     const uint32_t idx = h.idx;
@@ -282,12 +281,12 @@ __device__ __forceinline__ void shade_step(const RenderArgs &a, Path &ps, const 
     f3 col = mk(0.f, 0.f, 0.f);
     const bool dl = ps.phase == PH_DLOOP;
     uint32_t m = SPT_SKYBOX_ID;
-    if (idx < n) m = mat[idx];
+    if (idx != kMiss) m = mat[idx];
     bool scatter, refr;
     if (dl) {
         // while (--bounceCount && sphereIndex < N), SingleThreadPathTracer.hpp:28
         --ps.bounce;
-        const bool end = ps.bounce == 0u || idx >= n;
+        const bool end = ps.bounce == 0u || idx == kMiss;
         if (end) {
             col = ps.c;
             fin = true;
@@ -398,7 +397,6 @@ __device__ __forceinline__ void shade_step(const RenderArgs &a, Path &ps, const 
 __global__ __launch_bounds__(kRenderBlock) SPT_RENDER_ATTR void render_kernel(RenderArgs a)
 {
     const uint32_t lane = __lane_id();
-    const uint32_t n = a.scene.n;
     const f3 eye = mk(a.cam.eye[0], a.cam.eye[1], a.cam.eye[2]);
     const uint32_t rows = a.npix / a.map.width;  // region rows (uniform)
     (void)rows;
@@ -409,7 +407,11 @@ __global__ __launch_bounds__(kRenderBlock) SPT_RENDER_ATTR void render_kernel(Re
     ps.st = 0;
     ps.o = ps.d = ps.c = mk(0.f, 0.f, 0.f);
 
+    // Items are handed out in claims of a.claim from one global counter; each wave
+    // keeps the next claim in flight (lane 0) so the atomic's latency is hidden.
     uint32_t blk_cur = 0, blk_end = 0;
+    uint32_t pend = 0;
+    if (lane == 0) pend = atomicAdd(a.head, a.claim);
     bool exhausted = false;
     unsigned long long casts = 0, done = 0, dropped = 0;
     unsigned long long d_iters = 0, d_cyc_cast = 0, d_cyc_shade = 0, d_cyc_refill = 0;
@@ -440,9 +442,9 @@ __global__ __launch_bounds__(kRenderBlock) SPT_RENDER_ATTR void render_kernel(Re
             if (avail >= cnt) {
                 blk_cur += cnt;
             } else {
-                uint32_t nb = 0;
-                if (lane == 0) nb = atomicAdd(a.head, a.claim);
-                nb = __builtin_amdgcn_readfirstlane(nb);
+                // switch to the claim in flight and put the next one in flight
+                const uint32_t nb = __builtin_amdgcn_readfirstlane(pend);
+                if (nb < a.n_items && lane == 0) pend = atomicAdd(a.head, a.claim);
                 if (nb >= a.n_items) {
                     exhausted = true;
                     blk_cur = blk_end = 0;
@@ -495,8 +497,8 @@ __global__ __launch_bounds__(kRenderBlock) SPT_RENDER_ATTR void render_kernel(Re
         ++d_iters;
         // ---- one cast + one shading step ----
         const bool act = ps.phase != PH_IDLE;
-        const Hit h = a.scene.accel.tree ? find_closest<true>(a.scene.accel, n, ps.o, ps.d, act, dg)
-                                         : find_closest<false>(a.scene.accel, n, ps.o, ps.d, act, dg);
+        const Hit h = a.scene.accel.tree ? find_closest<true>(a.scene.accel, ps.o, ps.d, act, dg)
+                                         : find_closest<false>(a.scene.accel, ps.o, ps.d, act, dg);
         SPT_STAMP(d_cyc_cast);
         if (ps.phase != PH_IDLE) shade_step(a, ps, h, done, dropped);
         SPT_STAMP(d_cyc_shade);

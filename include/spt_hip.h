@@ -183,8 +183,10 @@ SPT_API int spt_camera_basis(const float eye[4], const float look_at[4], const f
 /* ---- numerics self-test ------------------------------------------------------
  * Runs the device primitives the render path relies on over n inputs and
  * writes SPT_SELFTEST_COLS floats per input: a/b, sqrtf(a),
- * float(sqrt(double(a))), float(pow5(double(a))), uniform draw, u8 of a. */
-#define SPT_SELFTEST_COLS 8
+ * sqrt(double(a)) and pow5(double(a)) as two float words each, uniform(-1,1)
+ * of bits, u8 of a, Normalize({a, b, c}) (3 floats) and c/a, with c the float
+ * whose bit pattern is bits. */
+#define SPT_SELFTEST_COLS 12
 SPT_API int spt_selftest_numerics(spt_ctx *ctx, const float *a, const float *b, const uint32_t *bits, uint32_t n,
                           float *out);
 

@@ -35,15 +35,10 @@ __device__ __forceinline__ f3 neg(f3 a) { return f3{-a.x, -a.y, -a.z}; }
 __device__ __forceinline__ float dot(f3 a, f3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
 // Math.hpp:122-133 (mul + 2x hadd)
 __device__ __forceinline__ float lensq(f3 a) { return (a.x * a.x + a.y * a.y) + a.z * a.z; }
-// Math.hpp:140-154: v / sqrt(|v|^2), lane-wise IEEE division
-__device__ __forceinline__ f3 normalize(f3 a)
-{
-    float l = __builtin_sqrtf(lensq(a));
-    return f3{a.x / l, a.y / l, a.z / l};
-}
 // Correctly rounded sqrt for arguments known to be normal and positive (the
 // hit test only takes the root of r*r - d2 > 1e-3): v_sqrt_f32 (<= 1 ulp) plus
-// the residual correction hipcc emits for sqrtf, without its denormal scaling.
+// the residual correction hipcc emits for sqrtf, without its denormal scaling
+// (which applies below 2^-96 only) and its +-0/+inf pass-through.
 __device__ __forceinline__ float sqrt_pos_normal(float h)
 {
     float s = __builtin_amdgcn_sqrtf(h);
@@ -56,6 +51,61 @@ __device__ __forceinline__ float sqrt_pos_normal(float h)
     return s;
 }
 
+// IEEE f32 division without div_scale / div_fixup.  hipcc lowers `a / b` to
+//   div_scale(b), rcp, e = fma(-b, rc, 1), rc = fma(e, rc, rc), q = a * rc,
+//   r = fma(-b, q, a), q = fma(r, rc, q), r = fma(-b, q, a),
+//   div_fmas(r, rc, q), div_fixup.
+// For |a| in [2^-40, 2^40] and |b| in [2^-40, 2^42] (both normal, exponent gap
+// < 96, quotient normal, no overflow) div_scale returns its operand with VCC = 0,
+// div_fmas is then a plain fma and div_fixup returns the quotient unchanged
+// (CDNA ISA, V_DIV_SCALE/FMAS/FIXUP_F32), so the core below is bit-identical.
+// The reciprocal refinement depends on b only and is shared by equal divisors.
+struct Recip {
+    float b, rc;
+};
+__device__ __forceinline__ Recip recip(float b)
+{
+    float rc = __builtin_amdgcn_rcpf(b);
+    const float e = __builtin_fmaf(-b, rc, 1.0f);
+    rc = __builtin_fmaf(e, rc, rc);
+    return Recip{b, rc};
+}
+__device__ __forceinline__ float div_core(float a, Recip r)
+{
+    float q = a * r.rc;
+    float e = __builtin_fmaf(-r.b, q, a);
+    q = __builtin_fmaf(e, r.rc, q);
+    e = __builtin_fmaf(-r.b, q, a);
+    return __builtin_fmaf(e, r.rc, q);
+}
+__device__ __forceinline__ bool div_operand_ok(float x)
+{
+    const float ax = __builtin_fabsf(x);
+    return ax >= 0x1p-40f && ax <= 0x1p40f;  // false for 0, inf, NaN
+}
+// a / b (IEEE): the core when both operands are in range (b <= 2^40 here), the
+// full sequence on the lanes that are not.
+__device__ __forceinline__ float div_rn(float a, float b)
+{
+    float q = div_core(a, recip(b));
+    if (__builtin_expect(!(div_operand_ok(a) && div_operand_ok(b)), 0)) q = a / b;
+    return q;
+}
+
+// Math.hpp:140-154: v / sqrt(|v|^2), lane-wise IEEE division.  Components in
+// [2^-40, 2^40] give |v|^2 in [2^-80, 2^82) (unscaled sqrt path) and a divisor in
+// [2^-40, 2^41], inside div_core's range; other lanes take the full sequences.
+__device__ __forceinline__ f3 normalize(f3 a)
+{
+    const float L = lensq(a);
+    const Recip r = recip(sqrt_pos_normal(L));
+    f3 out = f3{div_core(a.x, r), div_core(a.y, r), div_core(a.z, r)};
+    if (__builtin_expect(!(div_operand_ok(a.x) && div_operand_ok(a.y) && div_operand_ok(a.z)), 0)) {
+        const float l = __builtin_sqrtf(L);
+        out = f3{a.x / l, a.y / l, a.z / l};
+    }
+    return out;
+}
 // Math.hpp:156-159: vec - normal * Dot(vec, normal) * 2.f
 __device__ __forceinline__ f3 reflect(f3 v, f3 n) { return sub(v, mul(mul(n, dot(v, n)), 2.0f)); }
 

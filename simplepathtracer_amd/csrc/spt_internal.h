@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "spt_hip.h"
+
 namespace spt {
 
 // Row map of a launch: rows y in [y0, y1) with ((y - y0) / strip) % parts == part.

@@ -232,7 +232,10 @@ __device__ __forceinline__ Hit find_closest(const AccelView &ac, const f3 &o, co
         const float d2b = occb - tcb * tcb;
         const float lb = __builtin_amdgcn_sqrtf(occb);
         const float slack = 1e-4f * (lb + rb);
-        const float lc = ((lb - rb) - slack) - (2e-5f * olen + 1e-6f);
+        // near: a member's computed contact distance t is at least
+        // (|Cb-o| - Rb) - 2.6e-3 (|Cb-o| + Rb) (rounding of hh under the sqrt and
+        // | |d| - 1 | <= 5e-7); 4e-3 keeps headroom
+        const float lc = ((lb - rb) - 4e-3f * (lb + rb)) - (2e-5f * olen + 1e-6f);
         const bool line = d2b <= k1 + 1e-4f * occb;
         const bool front = tcb >= -(rb + slack);
         const bool near = !(lc > 0.f && lc * lc > h.best * 1.0001f);
@@ -399,6 +402,8 @@ __global__ __launch_bounds__(kRenderBlock) SPT_RENDER_ATTR void render_kernel(Re
     const uint32_t lane = __lane_id();
     const f3 eye = mk(a.cam.eye[0], a.cam.eye[1], a.cam.eye[2]);
     const uint32_t rows = a.npix / a.map.width;  // region rows (uniform)
+    // shared reciprocals of the primary-ray divisors (div_core range: 1 <= W, H <= 2^32)
+    const Recip rw = recip((float)a.width), rh = recip((float)a.height);
     (void)rows;
 
     Path ps;
@@ -474,8 +479,13 @@ __global__ __launch_bounds__(kRenderBlock) SPT_RENDER_ATTR void render_kernel(Re
 #endif
                 const uint32_t y = a.map.parts == 1u ? a.map.y0 + lr : row_of(a.map, lr);
                 ps.st = fmix64(a.seed_key ^ (((uint64_t)(y * a.width + x) << 32) | (uint64_t)s));
-                const float u = ((float)y + uniform(ps.st, -1.f, 1.f)) / (float)a.width;
-                const float v = ((float)x + uniform(ps.st, -1.f, 1.f)) / (float)a.height;
+                const float un = (float)y + uniform(ps.st, -1.f, 1.f);
+                const float vn = (float)x + uniform(ps.st, -1.f, 1.f);
+                float u = div_core(un, rw), v = div_core(vn, rh);  // / g_width, / g_height
+                if (__builtin_expect(!(div_operand_ok(un) && div_operand_ok(vn)), 0)) {
+                    u = un / (float)a.width;
+                    v = vn / (float)a.height;
+                }
                 const float vx = -1.f + 2.f * v, vy = -1.f + 2.f * u;
                 const float *m = a.cam.view;
                 ps.d = normalize(mk((m[0] * vx + m[1] * vy) + (m[2] * 1.f + m[3] * 0.f),
@@ -587,9 +597,9 @@ __global__ void selftest_kernel(const float *a, const float *b, const uint32_t *
 {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    const float x = a[i], y = b[i];
-    float *o = out + (size_t)i * 8;
-    o[0] = x / y;
+    const float x = a[i], y = b[i], c = __uint_as_float(bits[i]);
+    float *o = out + (size_t)i * SPT_SELFTEST_COLS;
+    o[0] = div_rn(x, y);
     o[1] = __builtin_sqrtf(x);
     const double sq = __builtin_sqrt((double)x);
     const double p5 = pow5((double)x);
@@ -600,6 +610,11 @@ __global__ void selftest_kernel(const float *a, const float *b, const uint32_t *
     o[5] = __builtin_bit_cast(float, (uint32_t)(p5b >> 32));
     o[6] = canon_u32(bits[i]) * (1.f - (-1.f)) + (-1.f);
     o[7] = (float)f2u8(x);
+    const f3 nv = normalize(mk(x, y, c));  // c: any bit pattern (NaN, inf, denormal, huge)
+    o[8] = nv.x;
+    o[9] = nv.y;
+    o[10] = nv.z;
+    o[11] = div_rn(c, x);
 }
 
 hipError_t launch_render(const RenderArgs &a, uint32_t grid, uint32_t block, hipStream_t s)

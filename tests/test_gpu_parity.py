@@ -84,6 +84,23 @@ def test_device_numerics_match_host(ctx, oracle):
     want_u = np.array([oracle.lib().spo_uniform_u32(int(x), -1.0, 1.0) for x in u[:4096]], np.float32)
     assert_bitwise(out[:4096, 6], want_u, "uniform(-1,1)")
     assert np.array_equal(out[:, 7], np.trunc(np.where(a < 2**31, a, 0)).astype(np.int64).astype(np.uint8))
+    # Normalize (Math.hpp:140-154) and c / a through the shortened division core,
+    # c = any float bit pattern: NaN/inf/denormal/huge lanes take the full sequence
+    c = u.view(np.float32)
+    with np.errstate(all="ignore"):
+        L = (a * a + b * b) + c * c
+        l = np.sqrt(L)
+        want = np.stack([a / l, b / l, c / l], 1)
+        q = c / a
+    same_or_nan(out[:, 8:11], want, "Normalize")
+    same_or_nan(out[:, 11], q, "division over the full float range")
+
+
+def same_or_nan(got, want, what):
+    got, want = np.asarray(got, np.float32), np.asarray(want, np.float32)
+    nan = np.isnan(got) & np.isnan(want)
+    bad = (got.view(np.uint32) != want.view(np.uint32)) & ~nan
+    assert not bad.any(), f"{what}: {int(bad.sum())} mismatches, first {got[bad][:4]} vs {want[bad][:4]}"
 
 
 # ---------------------------------------------------------------- goldens

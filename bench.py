@@ -73,7 +73,7 @@ def main():
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--mode", default="segment", choices=["segment", "task"])
     ap.add_argument("--strip", type=int, default=8)
-    ap.add_argument("--cpu-spp", type=int, default=8, help="spp of the bounded CPU-baseline sample")
+    ap.add_argument("--cpu-spp", type=int, default=32, help="spp of the bounded CPU-baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dump", default="", help="write rank 0's final g_data bytes to this file")
@@ -157,6 +157,12 @@ def main():
         achieved = algo_tflop / (avg_ms / 1e3)
         samples_per_launch = st["samples"] / launches
         hbm_bytes = 16.0 * samples_per_launch  # per-sample colour slot written by the render kernel
+        traffic = None
+        tpath = os.path.join(ROOT, "profiles", "traffic.json")
+        if os.path.exists(tpath):
+            rec = json.load(open(tpath)).get(args.config, {}).get("render_kernel")
+            if rec and world == 1:
+                traffic = rec["fetch_bytes"] + rec["write_bytes"]
         out = {
             "metric": "Msamples/s (pixels×spp/s), RTIOW random-sphere scene, 1/2/4/8 MI355X",
             "value": round(value, 3),
@@ -175,7 +181,9 @@ def main():
                        "width": W, "height": H, "spp": spp, "bounces": bounces, "spheres": scene.n,
                        "parallelism": f"row-strips{args.strip}x{world}" if world > 1 else "1 GPU"},
             "roofline": {"bound": "valu", "achieved": round(achieved, 3), "peak": round(VALU_PEAK_TOPS, 2),
-                         "unit": "TFLOP/s", "frac": round(achieved / VALU_PEAK_TOPS, 4), "traffic": None,
+                         "unit": "TFLOP/s", "frac": round(achieved / VALU_PEAK_TOPS, 4), "traffic": traffic,
+                         "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE, profiles/traffic.json)",
+                         "algorithmic_bytes": hbm_bytes,
                          "kernel": "render_kernel", "avg_launch_ms": round(avg_ms, 4),
                          "rays_per_launch": rays_per_launch,
                          "flop_per_launch": FLOP_PER_TEST * scene.n * rays_per_launch},

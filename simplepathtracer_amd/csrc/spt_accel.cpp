@@ -13,18 +13,20 @@
 //    is stored in preorder with skip links, so the wave-uniform traversal needs no
 //    stack: enter a node (next record) if any lane may pass, else jump to `skip`.
 //
-// Cull condition, derived in DESIGN.md §4.4 (fp32 error analysis of both the
-// member test and the cluster test for a ray whose fp32 direction has
-// | |d|^2 - 1 | <= 1e-6; other lanes never cull): a member can pass only if the
-// node's computed value
-//     d2b = |Cb-o|^2 - ((Cb-o).d)^2  <=  K1 + K2 * |Cb-o|^2,
-// K1 = 1.15 Rb^2 + 1e-5, K2 = 1e-4  (each about 2x the derived worst case).
+// Cull conditions, derived in DESIGN.md §4.4 from an fp32 error analysis of the
+// member test and of the node test for a ray whose computed |d|^2 is within 1e-6
+// of 1 (other lanes never cull):
+//   line:  keep iff d2b = |Cb-o|^2 - ((Cb-o).d)^2 <= K1 + 1e-4 |Cb-o|^2,
+//          K1 = 1.15 Rb^2 + 1e-5 (rounded up);  derived need 1.0835 Rb^2 + 3.6e-5 |Cb-o|^2
+//   front: cull iff (Cb-o).d < -(Rb + 1e-4 (|Cb-o| + Rb))      (tree nodes)
+//   near:  cull iff Lc > 0 and Lc^2 > best (1 + 1e-4),
+//          Lc = |Cb-o| - Rb - 4e-3 (|Cb-o| + Rb) - 2e-5 |o| - 1e-6   (tree nodes)
+// They use only the containment of the members (Rb >= |Cm - Cb| + r_m), so they
+// hold for inner nodes as for clusters; nodes failing them for every lane of a
+// wave are skipped with their subtree.  Tests run in traversal order, so the
+// closest hit is selected by the lexicographic (distance, original index)
+// minimum, which equals the reference's strict-'>' first-index-wins scan.
 // Eight preorder layouts, one per direction octant, differ only in sibling order.
-// The derivation uses only the containment of the members, so it holds for inner
-// nodes as for clusters.  The kernel evaluates exactly that; nodes failing it for
-// every lane are skipped with their subtree.  Tests run in traversal order, so the closest hit is selected by the
-// lexicographic (distance, original index) minimum, which equals the
-// reference's strict-'>' first-index-wins scan.
 #include "spt_accel.h"
 #include "spt_internal.h"
 

@@ -34,6 +34,11 @@
 #define SPT_DIAG 0
 #endif
 
+// 1: the cube-minus-ball rejection loop runs cooperatively across the wave
+#ifndef SPT_COOP_BALL
+#define SPT_COOP_BALL 1
+#endif
+
 // 1: items run through 8x8 pixel tiles of each sample (tile_pixel), 0: row-major
 #ifndef SPT_TILE
 #define SPT_TILE 1
@@ -176,15 +181,16 @@ __device__ __forceinline__ Hit find_closest(const AccelView &ac, const f3 &o, co
     if (!TREE) {
 #if !SPT_FLAT_FULL
         // flat list: node i is leaf i; bound prefetched one node ahead (pad record)
-        uint32_t nb[6];
+        constexpr int kNb = 6;
+        uint32_t nb[kNb];
 #pragma unroll
-        for (int q = 0; q < 6; ++q) nb[q] = nodes[q];
+        for (int q = 0; q < kNb; ++q) nb[q] = nodes[q];
         for (uint32_t i = 0; i < ac.n_nodes; ++i) {
             const float bx = __uint_as_float(nb[0]), by = __uint_as_float(nb[1]), bz = __uint_as_float(nb[2]);
             const float k1 = __uint_as_float(nb[3]);
             const uint32_t leaf_slot = nb[5];
 #pragma unroll
-            for (int q = 0; q < 6; ++q) nb[q] = nodes[8 * (i + 1) + q];
+            for (int q = 0; q < kNb; ++q) nb[q] = nodes[8 * (i + 1) + q];
             const f3 ocb = mk(bx - o.x, by - o.y, bz - o.z);
             const float tcb = dot(ocb, d);
             const float occb = lensq(ocb);
@@ -268,11 +274,69 @@ struct Path {
     f3 o, d, c;
 };
 
+// GenerateUniformDistInsideSphereVector (Random.hpp:115-127) for every lane with
+// `need`, all 64 lanes cooperating.  The stream is counter-based (draw n of a lane
+// is mix(st0 + (n+1) gamma)), so trial j = draws 3j..3j+2 can be evaluated by any
+// lane.  Round 0: every lane runs its own trial 0.  Later rounds: each still
+// pending lane gets H helper lanes (H = the largest power of two <= 64 / pending,
+// at most 16) that evaluate its trials jb .. jb+H-1 at once; it takes the lowest
+// accepted one.  The result and the advanced state st0 + 3 (j* + 1) gamma equal
+// the sequential loop's.  Must be called in wave-uniform control flow.
+// `lds`: 64 words of wave-private LDS.
+__device__ __forceinline__ f3 coop_ball_vector(uint64_t &st, bool need, uint32_t *lds)
+{
+    const uint32_t lane = __lane_id();
+    const uint64_t st0 = st;
+    uint64_t t = st0;
+    f3 r;
+    r.x = uniform(t, -0.5f, 0.5f);
+    r.y = uniform(t, -0.5f, 0.5f);
+    r.z = uniform(t, -0.5f, 0.5f);
+    uint32_t jacc = 0;
+    unsigned long long pend = __ballot(need && lensq(r) < 0.25f);
+    uint32_t jb = 1;
+    const uint32_t s_lo = (uint32_t)st0, s_hi = (uint32_t)(st0 >> 32);
+    while (pend != 0ull) {
+        const uint32_t np = (uint32_t)__popcll(pend);
+        const uint32_t q64 = 64u / np;
+        uint32_t lg = 31u - (uint32_t)__builtin_clz(q64);
+        lg = lg > 4u ? 4u : lg;
+        const bool is_p = (pend >> lane) & 1ull;
+        const uint32_t rank = lane_rank(pend);
+        if (is_p) lds[rank] = lane;
+        const uint32_t pidx = lane >> lg, tt = lane & ((1u << lg) - 1u);
+        const bool valid = pidx < np;
+        const uint32_t src = lds[valid ? pidx : 0u];
+        const uint32_t h_lo = (uint32_t)__shfl((int)s_lo, (int)src), h_hi = (uint32_t)__shfl((int)s_hi, (int)src);
+        uint64_t b = (((uint64_t)h_hi << 32) | h_lo) + (uint64_t)(3u * (jb + tt)) * kGamma;
+        f3 c;
+        c.x = uniform(b, -0.5f, 0.5f);
+        c.y = uniform(b, -0.5f, 0.5f);
+        c.z = uniform(b, -0.5f, 0.5f);
+        const unsigned long long acc = __ballot(valid && !(lensq(c) < 0.25f));
+        const uint32_t seg = is_p ? (uint32_t)(acc >> (rank << lg)) & ((1u << (1u << lg)) - 1u) : 0u;
+        const bool found = seg != 0u;
+        const uint32_t tstar = found ? (uint32_t)__builtin_ctz(seg) : 0u;
+        const uint32_t from = found ? (rank << lg) + tstar : lane;
+        const float rx = __shfl(c.x, (int)from), ry = __shfl(c.y, (int)from), rz = __shfl(c.z, (int)from);
+        if (found) {
+            r = mk(rx, ry, rz);
+            jacc = jb + tstar;
+        }
+        pend = __ballot(is_p && !found);
+        jb += 1u << lg;
+    }
+    if (need) st = st0 + (uint64_t)(3u * (jacc + 1u)) * kGamma;
+    return r;
+}
+
 // One shading step after a cast: the material switch of TraceAndSampleColor
 // (SingleThreadPathTracer.hpp:94-112) in PH_TRACE, or one turn of the diffuse
 // bounce loop (21-37) in PH_DLOOP.  Finishing paths write their sample slot.
-__device__ __forceinline__ void shade_step(const RenderArgs &a, Path &ps, const Hit &h, unsigned long long &done,
-                                           unsigned long long &dropped)
+// Called by every lane of the wave (`act` = the lane holds a path), so the
+// cooperative cube-minus-ball sampler runs in uniform control flow.
+__device__ __forceinline__ void shade_step(const RenderArgs &a, Path &ps, const Hit &h, bool act,
+                                           unsigned long long &done, unsigned long long &dropped, uint32_t *lds)
 {
     // hit, shade and material tables are in slot order (spt_accel.cpp)
     const float4 *__restrict__ hit = a.scene.accel.slots;
@@ -284,9 +348,10 @@ __device__ __forceinline__ void shade_step(const RenderArgs &a, Path &ps, const 
     f3 col = mk(0.f, 0.f, 0.f);
     const bool dl = ps.phase == PH_DLOOP;
     uint32_t m = SPT_SKYBOX_ID;
-    if (idx != kMiss) m = mat[idx];
-    bool scatter, refr;
-    if (dl) {
+    if (act && idx != kMiss) m = mat[idx];
+    bool scatter = false, refr = false;
+    if (!act) {
+    } else if (dl) {
         // while (--bounceCount && sphereIndex < N), SingleThreadPathTracer.hpp:28
         --ps.bounce;
         const bool end = ps.bounce == 0u || idx == kMiss;
@@ -308,6 +373,11 @@ __device__ __forceinline__ void shade_step(const RenderArgs &a, Path &ps, const 
         }
     }
     bool spec_event = false;
+#if SPT_COOP_BALL
+    const f3 rv_coop = coop_ball_vector(ps.st, scatter, lds);
+#else
+    (void)lds;
+#endif
     if (scatter) {
         // contact point + normal + cube-minus-ball vector, shared by the diffuse
         // first hit (lines 23-26), the diffuse loop (30-33) and the mirror (41-43)
@@ -315,7 +385,11 @@ __device__ __forceinline__ void shade_step(const RenderArgs &a, Path &ps, const 
         const f3 C = mk(cs.x, cs.y, cs.z);
         ps.o = h.p;
         const f3 nrm = normalize(sub(ps.o, C));
+#if SPT_COOP_BALL
+        f3 rv = rv_coop;
+#else
         f3 rv = ball_vector(ps.st);
+#endif
         f3 base;
         if (dl) {
             ps.c = mul(ps.c, 0.5f);
@@ -406,6 +480,7 @@ __global__ __launch_bounds__(kRenderBlock) SPT_RENDER_ATTR void render_kernel(Re
     const Recip rw = recip((float)a.width), rh = recip((float)a.height);
     (void)rows;
 
+    __shared__ uint32_t s_lds[kRenderBlock];  // wave-private scratch of the cooperative sampler
     Path ps;
     ps.phase = PH_IDLE;
     ps.item = ps.bounce = ps.spec = 0;
@@ -510,7 +585,7 @@ __global__ __launch_bounds__(kRenderBlock) SPT_RENDER_ATTR void render_kernel(Re
         const Hit h = a.scene.accel.tree ? find_closest<true>(a.scene.accel, ps.o, ps.d, act, dg)
                                          : find_closest<false>(a.scene.accel, ps.o, ps.d, act, dg);
         SPT_STAMP(d_cyc_cast);
-        if (ps.phase != PH_IDLE) shade_step(a, ps, h, done, dropped);
+        shade_step(a, ps, h, act, done, dropped, s_lds + (threadIdx.x & ~63u));
         SPT_STAMP(d_cyc_shade);
     }
 

@@ -104,14 +104,16 @@ SPT_API int spt_set_camera(spt_ctx *ctx, const float view[16], const float eye[4
  * bounces == 0 is rejected: `while (--bounceCount && ...)` would never count
  * down (SingleThreadPathTracer.hpp:28). */
 SPT_API int spt_set_params(spt_ctx *ctx, uint32_t width, uint32_t height, uint32_t spp, uint32_t bounces, uint64_t seed);
-/* Hot-loop culling: small spheres are grouped into clusters of k <= 8 (default 8)
+/* Hot-loop culling: small spheres are grouped into clusters of k <= 8
+ * (SPT_CLUSTER_AUTO, the default: 4 for a flat cluster list, 8 for a tree)
  * whose conservative bounding test skips them exactly when no ray of a wave can
  * pass RaySphereIntersection for any member; k = 0 tests every sphere for every
  * ray (the reference's brute force).  Results are identical either way. */
+#define SPT_CLUSTER_AUTO 0xFFFFFFFFu
 SPT_API int spt_set_cluster_size(spt_ctx *ctx, uint32_t k);
 /* Clusters are the leaves of a tree of bounding spheres walked by the whole wave;
  * `branching` children per inner node, 0 = flat list of clusters, SPT_TREE_AUTO
- * (default) = flat up to 64 clusters, else 4.  Results are identical for any value. */
+ * (default) = flat while n / 8 <= 64, else 4.  Results are identical for any value. */
 #define SPT_TREE_AUTO 0xFFFFFFFFu
 SPT_API int spt_set_cluster_tree(spt_ctx *ctx, uint32_t branching);
 /* Host-only check (no device needed): build the traversal tables for a scene and

@@ -20,6 +20,7 @@ STATUS_NAMES = {0: "SPT_OK", 1: "SPT_ERR_ARG", 2: "SPT_ERR_STATE", 3: "SPT_ERR_H
                 5: "SPT_ERR_NODEVICE"}
 MODE_SEGMENT, MODE_TASK = 0, 1
 TREE_AUTO = 0xFFFFFFFF  # spt_set_cluster_tree default
+CLUSTER_AUTO = 0xFFFFFFFF  # spt_set_cluster_size default
 SELFTEST_COLS = 12
 
 

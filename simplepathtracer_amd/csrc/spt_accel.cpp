@@ -65,10 +65,11 @@ const float4 kDummy = make_float4(0.f, 0.f, 0.f, -INFINITY);  // r*r = -inf: nev
 }  // namespace
 
 AccelTables build_accel(const float *centers4, const float *radii, uint32_t n, uint32_t cluster_k, uint32_t group,
-                        uint32_t branching)
+                        uint32_t branching, uint32_t leaf_slots)
 {
     AccelTables t;
     t.group = group;
+    t.leaf_slots = leaf_slots;
     std::vector<uint32_t> always, small;
     if (cluster_k == 0 || n <= 32) {
         always.resize(n);
@@ -101,7 +102,7 @@ AccelTables build_accel(const float *centers4, const float *radii, uint32_t n, u
     const size_t cbase = t.slots.size();
 
     if (!small.empty()) {
-        const uint32_t k = std::min(cluster_k, kClusterSlots);  // members per cluster
+        const uint32_t k = std::min(cluster_k, leaf_slots);  // members per cluster
         // Morton order of the small spheres' centres
         double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
         for (uint32_t i : small)
@@ -122,11 +123,11 @@ AccelTables build_accel(const float *centers4, const float *radii, uint32_t n, u
         std::vector<uint32_t> sorted(keyed.size());
         for (size_t j = 0; j < keyed.size(); ++j) sorted[j] = keyed[j].second;
 
-        // leaves: k consecutive spheres each, kClusterSlots slots each
+        // leaves: k consecutive spheres each, leaf_slots slots each
         const uint32_t leaves = (uint32_t)((sorted.size() + k - 1) / k);
         for (uint32_t c = 0; c < leaves; ++c) {
             for (size_t j = (size_t)c * k; j < std::min(sorted.size(), (size_t)(c + 1) * k); ++j) push_slot(sorted[j]);
-            pad_to(kClusterSlots, cbase);
+            pad_to(leaf_slots, cbase);
         }
         t.leaves = leaves;
 
@@ -201,7 +202,7 @@ AccelTables build_accel(const float *centers4, const float *radii, uint32_t n, u
                 const size_t me = t.nodes.size();
                 t.nodes.push_back(bounds[lvl][j]);
                 if (lvl == 0) {
-                    t.nodes[me].slot = (uint32_t)(cbase + (size_t)sp.c0 * kClusterSlots);
+                    t.nodes[me].slot = (uint32_t)(cbase + (size_t)sp.c0 * leaf_slots);
                 } else {
                     t.nodes[me].slot = kNoSlot;
                     const size_t nb = levels[lvl - 1].size();
@@ -230,11 +231,16 @@ std::string validate_accel(const AccelTables &t, const float *centers4, const fl
 {
     char buf[256];
     auto bad = [&](const char *fmt, auto... a) {
-        std::snprintf(buf, sizeof buf, fmt, a...);
+        if constexpr (sizeof...(a) == 0)
+            std::snprintf(buf, sizeof buf, "%s", fmt);
+        else
+            std::snprintf(buf, sizeof buf, fmt, a...);
         return std::string(buf);
     };
     const size_t g = t.group, cbase = (size_t)t.always_groups * g;
     if (t.slots.size() != t.orig.size()) return bad("slots/orig size mismatch");
+    if (t.leaf_slots != kClusterSlots && !(t.leaf_slots == kFlatLeafSlots && t.n_nodes == t.leaves))
+        return bad("leaf width %u needs a flat list", t.leaf_slots);
     if (t.slots.size() < cbase + 2 * g) return bad("slot table lacks the prefetch pad");
     if (t.nodes.size() != 8 * ((size_t)t.n_nodes + 1)) return bad("node table is not 8 layouts of %u + 1", t.n_nodes);
     // every sphere exactly once
@@ -260,7 +266,7 @@ std::string validate_accel(const AccelTables &t, const float *centers4, const fl
                 return bad("layout %u node %u: skip %u breaks preorder", oct, i, nd.skip);
             if (leaf) {
                 ++leaves;
-                if (nd.slot < cbase || (nd.slot - cbase) % kClusterSlots || nd.slot + kClusterSlots > t.slots.size())
+                if (nd.slot < cbase || (nd.slot - cbase) % t.leaf_slots || nd.slot + t.leaf_slots > t.slots.size())
                     return bad("layout %u node %u: leaf slot %u out of range", oct, i, nd.slot);
             }
             // containment of every member below: |Cm - Cb| + r <= Rb and 1.15 Rb^2 + 1e-5 <= K1
@@ -268,7 +274,7 @@ std::string validate_accel(const AccelTables &t, const float *centers4, const fl
                 return bad("layout %u node %u: K1 below 1.15 Rb^2 + 1e-5", oct, i);
             for (uint32_t q = i; q < nd.skip; ++q) {
                 if (L[q].slot == kNoSlot) continue;
-                for (uint32_t k = 0; k < kClusterSlots; ++k) {
+                for (uint32_t k = 0; k < t.leaf_slots; ++k) {
                     const uint32_t o = t.orig[L[q].slot + k];
                     if (o == 0xFFFFFFFFu) continue;
                     double d2 = 0;

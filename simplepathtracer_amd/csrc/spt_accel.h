@@ -17,7 +17,7 @@ struct AccelNode {
     float cx, cy, cz;  // bounding-sphere centre Cb
     float k1;          // cull constant K1 = 1.15 Rb^2 + 1e-5 (rounded up)
     uint32_t skip;     // next node when this one is culled (or is a leaf)
-    uint32_t slot;     // leaf: first of its kClusterSlots slots; inner: kNoSlot
+    uint32_t slot;     // leaf: first of its leaf_slots slots; inner: kNoSlot
     float rb;          // bounding radius Rb (rounded up)
     uint32_t pad;
 };
@@ -32,12 +32,14 @@ struct AccelTables {
     uint32_t n_nodes = 0;           // tree nodes (without the pad)
     uint32_t leaves = 0;            // clusters
     uint32_t depth = 0;             // levels of the tree (1 = flat cluster list)
+    uint32_t leaf_slots = kClusterSlots;  // slots per leaf (members <= leaf_slots)
 };
 
 // cluster_k: members per cluster (0, or n <= 32: every sphere is "always" tested).
 // branching: children per inner node; 0 = flat list of clusters (no inner nodes).
+// leaf_slots: kFlatLeafSlots (flat lists only, cluster_k <= 4) or kClusterSlots.
 AccelTables build_accel(const float *centers4, const float *radii, uint32_t n, uint32_t cluster_k, uint32_t group,
-                        uint32_t branching);
+                        uint32_t branching, uint32_t leaf_slots);
 
 // Structural and containment checks of the tables the kernel relies on for
 // exactness and in-bounds loads; empty string = valid, else the first problem.

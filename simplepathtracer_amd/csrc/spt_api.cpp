@@ -52,7 +52,7 @@ struct spt_ctx {
     std::vector<float> h_centers, h_radii;
     std::vector<float4> h_shade;  // {r, g, b, fuzz} per sphere
     std::vector<uint32_t> h_mat;
-    uint32_t cluster_k = 8;                 // members per culling cluster; 0 = brute force
+    uint32_t cluster_k = SPT_CLUSTER_AUTO;  // members per culling cluster; 0 = brute force
     uint32_t tree_branching = SPT_TREE_AUTO;  // children per inner node; 0 = flat cluster list
     spt::AccelView accel{};
     // camera (Globals.hpp:21-29)
@@ -270,21 +270,30 @@ int upload(spt_ctx *ctx, T **p, size_t *cap, const std::vector<T> &v)
     return SPT_OK;
 }
 
-// Children per inner node of the cluster tree: flat list for small scenes (the
-// wave enters most clusters anyway), a 4-ary tree once the list gets long.
-uint32_t resolve_branching(const spt_ctx *ctx)
+// Traversal shape for the current scene: a flat list of 4-sphere clusters for
+// small scenes (the wave enters most clusters anyway, and 4-slot leaves measured
+// faster there), a 4-ary tree of 8-sphere clusters once that list gets long.
+struct Shape {
+    uint32_t k, branching, leaf_slots;
+};
+Shape resolve_shape(const spt_ctx *ctx)
 {
-    if (ctx->tree_branching != SPT_TREE_AUTO) return ctx->tree_branching;
-    const uint32_t k = std::max<uint32_t>(1, std::min(ctx->cluster_k, spt::kClusterSlots));
-    return ctx->n / k > 64 ? 4u : 0u;
+    const bool tree = ctx->tree_branching == SPT_TREE_AUTO ? ctx->n / spt::kClusterSlots > 64
+                                                           : ctx->tree_branching >= 2;
+    Shape sh;
+    sh.k = ctx->cluster_k != SPT_CLUSTER_AUTO ? ctx->cluster_k : tree ? spt::kClusterSlots : spt::kFlatLeafSlots;
+    sh.branching = tree ? (ctx->tree_branching == SPT_TREE_AUTO ? 4u : ctx->tree_branching) : 0u;
+    sh.leaf_slots = !tree && sh.k <= spt::kFlatLeafSlots ? spt::kFlatLeafSlots : spt::kClusterSlots;
+    return sh;
 }
 
 // Build and upload the hot-loop traversal tables (spt_accel.cpp) for the current scene.
 int rebuild_accel(spt_ctx *ctx)
 {
     const uint32_t g = spt::render_group_size();
-    spt::AccelTables t = spt::build_accel(ctx->h_centers.data(), ctx->h_radii.data(), ctx->n, ctx->cluster_k, g,
-                                          resolve_branching(ctx));
+    const Shape sh = resolve_shape(ctx);
+    spt::AccelTables t = spt::build_accel(ctx->h_centers.data(), ctx->h_radii.data(), ctx->n, sh.k, g, sh.branching,
+                                          sh.leaf_slots);
     const std::string bad = spt::validate_accel(t, ctx->h_centers.data(), ctx->h_radii.data(), ctx->n);
     if (!bad.empty()) return fail(ctx, SPT_ERR_STATE, "traversal tables invalid: %s", bad.c_str());
     // shading tables in slot order: the kernel keeps the winner's slot, not its index
@@ -303,7 +312,7 @@ int rebuild_accel(spt_ctx *ctx)
     if (!rc) rc = upload(ctx, &ctx->d_nodes, &ctx->nodes_cap, t.nodes);
     if (rc) return rc;
     ctx->accel = spt::AccelView{ctx->d_slots, ctx->d_orig, ctx->d_nodes, t.always_groups, t.n_nodes,
-                                t.n_nodes > t.leaves ? 1u : 0u};
+                                t.n_nodes > t.leaves ? 1u : 0u, t.leaf_slots};
     ctx->tables = std::move(t);
     return SPT_OK;
 }
@@ -493,7 +502,8 @@ int spt_set_cluster_size(spt_ctx *ctx, uint32_t k)
 {
     if (!ctx) return fail(nullptr, SPT_ERR_ARG, "null context");
     std::lock_guard<std::mutex> lk(ctx->mu);
-    if (k > spt::kClusterSlots) return fail(ctx, SPT_ERR_ARG, "cluster size %u > %u", k, spt::kClusterSlots);
+    if (k > spt::kClusterSlots && k != SPT_CLUSTER_AUTO)
+        return fail(ctx, SPT_ERR_ARG, "cluster size %u > %u", k, spt::kClusterSlots);
     ctx->cluster_k = k;
     if (!ctx->scene_set) return SPT_OK;
     HIP_TRY(ctx, hipSetDevice(ctx->device));
@@ -518,7 +528,9 @@ int spt_accel_check(const float *centers4, const float *radii, uint32_t n, uint3
     if (n > 0 && (!centers4 || !radii)) return fail(nullptr, SPT_ERR_ARG, "null scene array");
     if (cluster_k > spt::kClusterSlots) return fail(nullptr, SPT_ERR_ARG, "cluster size %u > %u", cluster_k, spt::kClusterSlots);
     if (branching == 1) return fail(nullptr, SPT_ERR_ARG, "tree branching 1");
-    const spt::AccelTables t = spt::build_accel(centers4, radii, n, cluster_k, spt::render_group_size(), branching);
+    const uint32_t k = cluster_k == 0 ? 0u : cluster_k;
+    const uint32_t leaf = branching == 0 && k <= spt::kFlatLeafSlots ? spt::kFlatLeafSlots : spt::kClusterSlots;
+    const spt::AccelTables t = spt::build_accel(centers4, radii, n, k, spt::render_group_size(), branching, leaf);
     const std::string bad = spt::validate_accel(t, centers4, radii, n);
     if (!bad.empty()) return fail(nullptr, SPT_ERR_STATE, "traversal tables invalid: %s", bad.c_str());
     if (out_nodes) *out_nodes = t.n_nodes;

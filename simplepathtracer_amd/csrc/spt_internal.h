@@ -71,7 +71,8 @@ __host__ __device__ inline void tile_pixel(uint32_t q, uint32_t width, uint32_t 
 }
 
 constexpr uint32_t kMaxGroup = 16;     // sphere-table padding granule (>= SPT_GROUP)
-constexpr uint32_t kClusterSlots = 8;  // slots per culling cluster (members <= 8, dummies pad)
+constexpr uint32_t kClusterSlots = 8;  // max members per cluster = slots of a tree leaf
+constexpr uint32_t kFlatLeafSlots = 4; // slots of a flat-list leaf holding <= 4 members
 constexpr uint32_t kNoSlot = 0xFFFFFFFFu;  // AccelNode::slot of inner nodes
 constexpr uint32_t kMiss = 0xFFFFFFFFu;    // Hit::idx when no sphere was hit
 
@@ -81,7 +82,8 @@ struct AccelView {
     const uint32_t *orig;   // original sphere index per slot
     const void *nodes;      // AccelNode[8][n_nodes + 1]: per-octant preorder layouts (spt_accel.h)
     uint32_t always_groups, n_nodes;
-    uint32_t tree;  // 0: flat cluster list (every node a leaf), 1: tree with inner nodes
+    uint32_t tree;        // 0: flat cluster list (every node a leaf), 1: tree with inner nodes
+    uint32_t leaf_slots;  // slots per leaf: kFlatLeafSlots or kClusterSlots
 };
 
 struct DeviceScene {

@@ -138,15 +138,17 @@ struct CastDiag {
     unsigned long long nodes = 0, leaves = 0, pairs = 0, live = 0;
 };
 
-// Leaf test: the cluster's kClusterSlots slots, two s_load_dwordx16 off one base pointer.
+// Leaf test: the cluster's S slots (S = 8: two s_load_dwordx16, S = 4: one) off one
+// base pointer.
+template <int S>
 __device__ __forceinline__ void test_leaf(cfloat *slots, const uint32_t *__restrict__ orig, uint32_t leaf_slot,
                                           const f3 &o, const f3 &d, float dod, Hit &h)
 {
     cfloat *cs = slots + 4 * leaf_slot;
-    float4 m8[kClusterSlots];
+    float4 ms[S];
 #pragma unroll
-    for (int k = 0; k < (int)kClusterSlots; ++k) m8[k] = ld_uniform(cs, k);
-    test_group<(int)kClusterSlots>(m8, orig, leaf_slot, o, d, dod, h);
+    for (int k = 0; k < S; ++k) ms[k] = ld_uniform(cs, k);
+    test_group<S>(ms, orig, leaf_slot, o, d, dod, h);
 }
 
 // FindClosestIntersectionSphere for every lane of the wave (Collision.hpp:87-109).
@@ -155,7 +157,7 @@ __device__ __forceinline__ void test_leaf(cfloat *slots, const uint32_t *__restr
 // entered when the ray's line may pass one of its members (the "line" test of
 // DESIGN.md §4.4).  TREE = true: preorder walk of the cluster tree in the layout
 // of the wave's majority direction octant with the line, front and near tests.
-template <bool TREE>
+template <bool TREE, int LEAF>
 __device__ __forceinline__ Hit find_closest(const AccelView &ac, const f3 &o, const f3 &d, bool active,
                                             CastDiag &dg)
 {
@@ -203,7 +205,7 @@ __device__ __forceinline__ Hit find_closest(const AccelView &ac, const f3 &o, co
                 dg.pairs += (unsigned long long)__popcll(mm);
                 dg.live += mm != 0ull ? (unsigned long long)__popcll(live_mask) : 0ull;
             }
-            if (mm != 0ull) test_leaf(slots, ac.orig, leaf_slot, o, d, dod, h);
+            if (mm != 0ull) test_leaf<LEAF>(slots, ac.orig, leaf_slot, o, d, dod, h);
         }
         return h;
 #endif
@@ -256,7 +258,7 @@ __device__ __forceinline__ Hit find_closest(const AccelView &ac, const f3 &o, co
                 dg.live += mm != 0ull ? (unsigned long long)__popcll(live_mask) : 0ull;
             }
         }
-        if (mm != 0ull && leaf) test_leaf(slots, ac.orig, leaf_slot, o, d, dod, h);
+        if (mm != 0ull && leaf) test_leaf<LEAF>(slots, ac.orig, leaf_slot, o, d, dod, h);
         const uint32_t next = (mm != 0ull && !leaf) ? i + 1 : skip;
         if (next != i + 1) {
 #pragma unroll
@@ -471,6 +473,9 @@ __device__ __forceinline__ void shade_step(const RenderArgs &a, Path &ps, const 
 #define SPT_RENDER_ATTR
 #endif
 
+// One kernel per traversal shape (flat list of 4- or 8-slot leaves, tree of
+// 8-slot leaves), each with its own register allocation; launch_render picks.
+template <bool TREE, int LEAF>
 __global__ __launch_bounds__(kRenderBlock) SPT_RENDER_ATTR void render_kernel(RenderArgs a)
 {
     const uint32_t lane = __lane_id();
@@ -582,8 +587,7 @@ __global__ __launch_bounds__(kRenderBlock) SPT_RENDER_ATTR void render_kernel(Re
         ++d_iters;
         // ---- one cast + one shading step ----
         const bool act = ps.phase != PH_IDLE;
-        const Hit h = a.scene.accel.tree ? find_closest<true>(a.scene.accel, ps.o, ps.d, act, dg)
-                                         : find_closest<false>(a.scene.accel, ps.o, ps.d, act, dg);
+        const Hit h = find_closest<TREE, LEAF>(a.scene.accel, ps.o, ps.d, act, dg);
         SPT_STAMP(d_cyc_cast);
         shade_step(a, ps, h, act, done, dropped, s_lds + (threadIdx.x & ~63u));
         SPT_STAMP(d_cyc_shade);
@@ -694,7 +698,12 @@ __global__ void selftest_kernel(const float *a, const float *b, const uint32_t *
 
 hipError_t launch_render(const RenderArgs &a, uint32_t grid, uint32_t block, hipStream_t s)
 {
-    hipLaunchKernelGGL(render_kernel, dim3(grid), dim3(block), 0, s, a);
+    if (a.scene.accel.tree)
+        hipLaunchKernelGGL((render_kernel<true, (int)kClusterSlots>), dim3(grid), dim3(block), 0, s, a);
+    else if (a.scene.accel.leaf_slots == kFlatLeafSlots)
+        hipLaunchKernelGGL((render_kernel<false, (int)kFlatLeafSlots>), dim3(grid), dim3(block), 0, s, a);
+    else
+        hipLaunchKernelGGL((render_kernel<false, (int)kClusterSlots>), dim3(grid), dim3(block), 0, s, a);
     return hipGetLastError();
 }
 
@@ -725,7 +734,15 @@ uint32_t render_group_size() { return SPT_GROUP; }
 
 hipError_t render_occupancy(uint32_t block, int *blocks_per_cu)
 {
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, render_kernel, (int)block, 0);
+    // the smallest occupancy of the three shapes sizes the persistent grid
+    int a = 0, b = 0, c = 0;
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, render_kernel<true, (int)kClusterSlots>, (int)block, 0);
+    if (e == hipSuccess)
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, render_kernel<false, (int)kFlatLeafSlots>, (int)block, 0);
+    if (e == hipSuccess)
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&c, render_kernel<false, (int)kClusterSlots>, (int)block, 0);
+    *blocks_per_cu = a < b ? (a < c ? a : c) : (b < c ? b : c);
+    return e;
 }
 
 }  // namespace spt

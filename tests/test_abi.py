@@ -88,7 +88,7 @@ def _accel_check(native, centers, radii, k, b):
     return rc, nodes.value, native.lib().spt_last_error(None)
 
 
-@pytest.mark.parametrize("k,b", [(8, 0), (8, 2), (8, 4), (8, 16), (3, 4), (5, 0), (1, 2), (0, 4)])
+@pytest.mark.parametrize("k,b", [(8, 0), (4, 0), (2, 0), (8, 2), (8, 4), (8, 16), (3, 4), (5, 0), (1, 2), (0, 4)])
 @pytest.mark.parametrize("scene", ["random", "stress2000", "stress10000"])
 def test_traversal_tables_are_valid(native, scene, k, b):
     """The culling tree's exactness rests on host-built tables: every sphere in

@@ -387,19 +387,20 @@ def test_bench_two_ranks_on_one_gpu_matches_one_rank(spt, tmp_path):
 def test_culling_is_exact(spt, ctx, golden_scenes, scene_name):
     """Cluster-tree culling (spt_accel.cpp) skips only spheres that cannot pass:
     frames and ray counts are bit-identical to brute force (cluster size 0) for
-    any cluster size and tree shape (flat list, binary, 4-ary, 16-ary)."""
+    any cluster size and tree shape (flat lists of 4- and 8-slot leaves, binary,
+    4-ary, 16-ary trees)."""
     if scene_name == "random":
         scene, W, H, spp, region = scene_from(spt, golden_scenes, "random"), 1200, 800, 16, (0, 800, 0, 1200)
     else:
         scene, W, H, spp, region = spt.generate_stress(5, 2000), 480, 270, 8, (0, 270, 0, 480)
     setup(ctx, scene, W, H, spp, 50)
     outs = []
-    for k, b in ((0, 0), (8, 0), (8, 2), (8, 4), (3, 16), (5, 4)):
+    for k, b in ((0, 0), (8, 0), (4, 0), (3, 0), (8, 2), (8, 4), (3, 16), (5, 4)):
         ctx.set_cluster_size(k)
         ctx.set_cluster_tree(b)
         ctx.reset_stats()
         outs.append(((k, b), ctx.render_segment(*region), ctx.stats()["casts"]))
-    ctx.set_cluster_size(8)
+    ctx.set_cluster_size(spt._native.CLUSTER_AUTO)
     ctx.set_cluster_tree(spt._native.TREE_AUTO)
     for kb, img, casts in outs[1:]:
         assert_bitwise(img, outs[0][1], f"cluster size / tree branching {kb} vs brute force")

@@ -19,7 +19,7 @@ ctx.render_segment(0, H, 0, W)
 st = ctx.stats()
 it, leaves, nodes, cc, cs, cr, pairs, live = st["diag"][:8]
 print(f"casts={st['casts']} samples={st['samples']} wave_iters={it} live_lanes/iter={st['casts']/max(it,1):.2f}")
-k = int(os.environ.get("SPT_CLUSTER_K", "8"))
+k = os.environ.get("SPT_CLUSTER_K", "auto")
 print(f"per wave cast: tree nodes tested={nodes/max(it,1):.2f} clusters entered={leaves/max(it,1):.2f} "
       f"(cluster size {k}, tree {os.environ.get('SPT_TREE_B', 'auto')})")
 tot = max(cc + cs + cr, 1)

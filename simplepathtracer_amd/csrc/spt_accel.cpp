@@ -191,6 +191,7 @@ AccelTables build_accel(const float *centers4, const float *radii, uint32_t n, u
             auto ordered = [&](uint32_t lvl, size_t q0, size_t q1) {
                 std::vector<size_t> ix;
                 for (size_t q = q0; q < q1; ++q) ix.push_back(q);
+                if (levels.size() == 1) return ix;  // flat list: slot order (the kernel relies on it)
                 std::stable_sort(ix.begin(), ix.end(), [&](size_t a, size_t b) {
                     const AccelNode &na = bounds[lvl][a], &nb = bounds[lvl][b];
                     return sx * na.cx + sy * na.cy + sz * na.cz < sx * nb.cx + sy * nb.cy + sz * nb.cz;
@@ -289,6 +290,9 @@ std::string validate_accel(const AccelTables &t, const float *centers4, const fl
             }
         }
         if (leaves != t.leaves) return bad("layout %u: %zu leaves, expected %u", oct, leaves, t.leaves);
+        if (t.n_nodes == t.leaves)  // flat list: node i is leaf i, in slot order
+            for (uint32_t i = 0; i < t.n_nodes; ++i)
+                if (L[i].slot != cbase + (size_t)i * t.leaf_slots) return bad("flat layout %u not in slot order", oct);
     }
     return std::string();
 }

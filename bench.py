@@ -156,7 +156,8 @@ def main():
         algo_tflop = FLOP_PER_TEST * scene.n * rays_per_launch / 1e12
         achieved = algo_tflop / (avg_ms / 1e3)
         samples_per_launch = st["samples"] / launches
-        hbm_bytes = 16.0 * samples_per_launch  # per-sample colour slot written by the render kernel
+        slot_bytes = 12.0 if args.mode == "segment" else 16.0  # per-sample slot: rgb (+ counted flag in task mode)
+        hbm_bytes = slot_bytes * samples_per_launch  # written by the render kernel
         traffic = None
         tpath = os.path.join(ROOT, "profiles", "traffic.json")
         if os.path.exists(tpath):

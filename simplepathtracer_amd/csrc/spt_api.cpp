@@ -65,7 +65,7 @@ struct spt_ctx {
 
     // workspace
     uint64_t ws_bytes = 4ull << 30;
-    float4 *d_samples = nullptr;
+    float *d_samples = nullptr;
     size_t samples_cap = 0;
     float4 *d_acc = nullptr;
     size_t acc_cap = 0;
@@ -194,14 +194,15 @@ int render_impl(spt_ctx *ctx, int mode, const spt::RowMap &map, float4 *d_rgba, 
     if (npix64 == 0) return SPT_OK;
     if (npix64 > 0x7FFFFFFFull) return fail(ctx, SPT_ERR_ARG, "region too large (%llu pixels)", (unsigned long long)npix64);
     const uint32_t npix = (uint32_t)npix64;
-    uint64_t budget = std::max<uint64_t>(ctx->ws_bytes / sizeof(float4), 1);
+    const uint32_t slot_floats = mode == SPT_MODE_SEGMENT ? 3u : 4u;  // task mode keeps the counted flag
+    uint64_t budget = std::max<uint64_t>(ctx->ws_bytes / (slot_floats * sizeof(float)), 1);
     budget = std::min<uint64_t>(budget, 0x7FFFFFFFull);
     uint64_t per = std::max<uint64_t>(1, budget / npix);
     const uint32_t spp_batch = (uint32_t)std::min<uint64_t>(ctx->spp, per);
     if (keep_samples && spp_batch != ctx->spp)
         return fail(ctx, SPT_ERR_ARG, "region * spp exceeds the workspace for spt_render_samples");
     const uint64_t items_max = (uint64_t)npix * spp_batch;
-    int rc = ensure(ctx, &ctx->d_samples, &ctx->samples_cap, items_max);
+    int rc = ensure(ctx, &ctx->d_samples, &ctx->samples_cap, items_max * slot_floats);
     if (rc) return rc;
     if (spp_batch < ctx->spp) {
         rc = ensure(ctx, &ctx->d_acc, &ctx->acc_cap, npix);
@@ -220,11 +221,13 @@ int render_impl(spt_ctx *ctx, int mode, const spt::RowMap &map, float4 *d_rgba, 
     ra.npix = npix;
     ra.claim = claim_size(ctx, (uint64_t)npix * spp_batch);
     ra.samples = ctx->d_samples;
+    ra.slot_floats = slot_floats;
     ra.head = ctx->d_head;
     ra.counters = ctx->d_counters;
 
     spt::FoldArgs fa{};
     fa.samples = ctx->d_samples;
+    fa.slot_floats = slot_floats;
     fa.acc = ctx->d_acc;
     fa.out_rgba = d_rgba;
     fa.out_rgb8 = d_rgb8;
@@ -625,12 +628,17 @@ int spt_render_samples(spt_ctx *ctx, int mode, uint32_t yB, uint32_t yE, uint32_
     spt::RowMap map{yB, yE, 1u, 1u, 0u, xB, xE - xB};
     if ((rc = render_impl(ctx, mode, map, nullptr, nullptr, ctx->stream, true))) return rc;
     const size_t npix = (size_t)(xE - xB) * (yE - yB);
-    std::vector<float4> buf(npix * ctx->spp);  // device order [sample][pixel]
-    HIP_TRY(ctx, hipMemcpyAsync(buf.data(), ctx->d_samples, buf.size() * sizeof(float4), hipMemcpyDeviceToHost,
+    const size_t sf = mode == SPT_MODE_SEGMENT ? 3 : 4;
+    std::vector<float> buf(npix * ctx->spp * sf);  // device order [sample][pixel], sf floats per slot
+    HIP_TRY(ctx, hipMemcpyAsync(buf.data(), ctx->d_samples, buf.size() * sizeof(float), hipMemcpyDeviceToHost,
                                 ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     for (size_t p = 0; p < npix; ++p)
-        for (size_t s = 0; s < ctx->spp; ++s) std::memcpy(out + 4 * (p * ctx->spp + s), &buf[s * npix + p], 16);
+        for (size_t s = 0; s < ctx->spp; ++s) {
+            float *o = out + 4 * (p * ctx->spp + s);
+            std::memcpy(o, &buf[(s * npix + p) * sf], sf * sizeof(float));
+            if (sf == 3) o[3] = 1.0f;  // segment mode: every sample counts
+        }
     return collect_timings(ctx);
 }
 

@@ -110,13 +110,15 @@ struct RenderArgs {
     uint32_t s0;         // first sample index of the batch
     uint32_t n_items;    // npix * spp_batch
     uint32_t claim;      // items per queue claim
-    float4 *samples;     // [n_items] per-sample colour, w = counted
+    float *samples;      // [n_items] per-sample colour: {r, g, b} (segment mode) or {r, g, b, counted} (task mode)
+    uint32_t slot_floats;  // 3 or 4
     uint32_t *head;      // queue head (zeroed before launch)
     unsigned long long *counters;  // [0] casts, [1] samples, [2] dropped
 };
 
 struct FoldArgs {
-    const float4 *samples;
+    const float *samples;  // slot_floats per slot, [sample][pixel]
+    uint32_t slot_floats;
     float4 *acc;         // persistent accumulator (w = sample count)
     float4 *out_rgba;    // nullable, local pixel order
     uint8_t *out_rgb8;   // nullable, full frame (g_data layout)

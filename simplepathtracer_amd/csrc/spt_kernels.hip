@@ -455,7 +455,15 @@ __device__ __forceinline__ void shade_step(const RenderArgs &a, Path &ps, const 
         }
     }
     if (fin) {
-        a.samples[ps.item] = make_float4(col.x, col.y, col.z, counted);
+        if (a.mode == 0u) {
+            // RenderSegment counts every sample: 12-byte slots
+            float *o3 = a.samples + (size_t)3 * ps.item;
+            o3[0] = col.x;
+            o3[1] = col.y;
+            o3[2] = col.z;
+        } else {
+            *(float4 *)(a.samples + (size_t)4 * ps.item) = make_float4(col.x, col.y, col.z, counted);
+        }
         ps.phase = PH_IDLE;
         ps.d = mk(0.f, 0.f, 0.f);
         ++done;
@@ -621,14 +629,26 @@ __global__ __launch_bounds__(256) void fold_kernel(FoldArgs a)
     const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= a.npix) return;
     float4 acc = a.first ? make_float4(0.f, 0.f, 0.f, 0.f) : a.acc[p];
-    const float4 *s = a.samples + p;
-    for (uint32_t k = 0; k < a.spp_batch; ++k) {
-        const float4 c = s[(size_t)k * a.npix];  // [sample][pixel]: coalesced across lanes
-        if (a.mode == 0 || c.w != 0.f) {
-            acc.x = acc.x + c.x;
-            acc.y = acc.y + c.y;
-            acc.z = acc.z + c.z;
+    if (a.mode == 0) {
+        // RenderSegment: 12-byte slots, every sample counts
+        const float *s = a.samples + (size_t)3 * p;
+        for (uint32_t k = 0; k < a.spp_batch; ++k) {
+            const float *c = s + (size_t)3 * k * a.npix;  // [sample][pixel]: coalesced across lanes
+            acc.x = acc.x + c[0];
+            acc.y = acc.y + c[1];
+            acc.z = acc.z + c[2];
             acc.w = acc.w + 1.f;
+        }
+    } else {
+        const float4 *s = (const float4 *)a.samples + p;
+        for (uint32_t k = 0; k < a.spp_batch; ++k) {
+            const float4 c = s[(size_t)k * a.npix];
+            if (c.w != 0.f) {
+                acc.x = acc.x + c.x;
+                acc.y = acc.y + c.y;
+                acc.z = acc.z + c.z;
+                acc.w = acc.w + 1.f;
+            }
         }
     }
     if (!a.last) {

@@ -21,8 +21,8 @@ for d in ("pmc1", "pmc2", "pmc3", "pmc4"):
     if not os.path.exists(p):
         continue
     for r in csv.DictReader(open(p)):
-        if r["Kernel_Name"].startswith("spt::"):
-            agg[(r["Kernel_Name"].split("(")[0], r["Counter_Name"])].append(float(r["Counter_Value"]))
+        if "spt::" in r["Kernel_Name"]:
+            agg[(r["Kernel_Name"].split("(")[0].replace("void ", ""), r["Counter_Name"])].append(float(r["Counter_Value"]))
 out += ["", "## PMC counters (average per dispatch, separate passes)\n", "| kernel | counter | value |", "|---|---|---|"]
 for (k, c), v in sorted(agg.items()):
     val = sum(v) / len(v)

@@ -120,8 +120,13 @@ __device__ __forceinline__ void test_group(const float4 (&sp)[G], const uint32_t
                 if (dod < dot(p, d)) {
                     const float ds = lensq(sub(o, p));
                     bool better = ds < h.best;
-                    if (ds == h.best && h.idx != kMiss)  // exact tie (rare): first original index wins
-                        better = orig[slot + k] < orig[h.idx];
+                    // exact tie (rare): the first original index wins.  Behind a
+                    // wave-uniform branch, so the index loads (and the vmcnt waits
+                    // they would drag into the hot loop) run only when some lane ties.
+                    const bool tie = ds == h.best && h.idx != kMiss;
+                    if (__builtin_expect(__ballot(tie) != 0ull, 0)) {
+                        if (tie) better = orig[slot + k] < orig[h.idx];
+                    }
                     if (better) {
                         h.best = ds;
                         h.idx = slot + k;
@@ -179,6 +184,9 @@ __device__ __forceinline__ Hit find_closest(const AccelView &ac, const f3 &o, co
     const float ddev = lensq(d) - 1.0f;
     const bool no_cull = active && !(ddev <= 1e-6f && ddev >= -1e-6f);
     const unsigned long long live_mask = __ballot(active);
+    // node masks are formed as (ballot(test) & live) | nocull: the ballot of a
+    // compare is the compare's own lane mask, with no VALU round trip
+    const unsigned long long nocull_mask = __ballot(no_cull);
     cuint *nodes = (cuint *)ac.nodes;
     if (!TREE) {
 #if !SPT_FLAT_FULL
@@ -197,8 +205,7 @@ __device__ __forceinline__ Hit find_closest(const AccelView &ac, const f3 &o, co
             const float tcb = dot(ocb, d);
             const float occb = lensq(ocb);
             const float d2b = occb - tcb * tcb;
-            const bool might = no_cull || (active && d2b <= k1 + 1e-4f * occb);
-            const unsigned long long mm = __ballot(might);
+            const unsigned long long mm = (__ballot(d2b <= k1 + 1e-4f * occb) & live_mask) | nocull_mask;
             if (SPT_DIAG) {
                 dg.nodes += 1;
                 dg.leaves += mm != 0ull ? 1 : 0;
@@ -247,8 +254,7 @@ __device__ __forceinline__ Hit find_closest(const AccelView &ac, const f3 &o, co
         const bool line = d2b <= k1 + 1e-4f * occb;
         const bool front = tcb >= -(rb + slack);
         const bool near = !(lc > 0.f && lc * lc > h.best * 1.0001f);
-        const bool might = no_cull || (active && line && front && near);
-        const unsigned long long mm = __ballot(might);
+        const unsigned long long mm = (__ballot(line && front && near) & live_mask) | nocull_mask;
         const bool leaf = leaf_slot != kNoSlot;
         if (SPT_DIAG) {
             dg.nodes += 1;

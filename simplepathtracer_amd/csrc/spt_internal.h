@@ -70,6 +70,48 @@ __host__ __device__ inline void tile_pixel(uint32_t q, uint32_t width, uint32_t 
     col = c;
 }
 
+// (sample, pixel) of the q-th item of a batch of S samples over a region of
+// `rows` x `width` pixels, items ordered [8-row band][8-column tile][sample]
+// [pixel in tile] (ragged tiles at the right and bottom edges).  A claim of
+// consecutive items then stays inside one 8x8 tile across several samples, so a
+// wave's rays start close together whatever the claim size.  Full tiles use
+// shifts; only edge tiles divide.  Bijective on [0, rows*width*S) (host test).
+__host__ __device__ inline void ts_item(uint32_t q, uint32_t width, uint32_t rows, uint32_t S, uint32_t &sl,
+                                        uint32_t &lr, uint32_t &col)
+{
+    // 8*width*S <= rows*width*S < 2^31 whenever rows >= 8; a single band otherwise
+    const uint32_t band = rows >= 8u ? q / (8u * width * S) : 0u;
+    const uint32_t h = rows - (band << 3) < 8u ? rows - (band << 3) : 8u;
+    const uint32_t qb = q - band * 8u * width * S;
+    const uint32_t ft = width >> 3, wr = width & 7u;
+    const uint32_t ti = h * 8u * S;  // items of a full-width tile of this band
+    uint32_t e, wt, c0;
+    if (h == 8u) {
+        const uint32_t t = qb / (64u * S);
+        if (t < ft) {
+            e = qb - t * 64u * S;
+            sl = e >> 6;
+            const uint32_t pix = e & 63u;
+            lr = (band << 3) + (pix >> 3);
+            col = (t << 3) + (pix & 7u);
+            return;
+        }
+        e = qb - ft * ti;
+        wt = wr;
+        c0 = ft << 3;
+    } else {
+        const uint32_t t = qb / ti;
+        wt = t < ft ? 8u : wr;
+        e = qb - (t < ft ? t : ft) * ti;
+        c0 = (t < ft ? t : ft) << 3;
+    }
+    sl = e / (h * wt);
+    const uint32_t pix = e - sl * h * wt;
+    const uint32_t row = pix / wt;
+    lr = (band << 3) + row;
+    col = c0 + (pix - row * wt);
+}
+
 constexpr uint32_t kMaxGroup = 16;     // sphere-table padding granule (>= SPT_GROUP)
 constexpr uint32_t kClusterSlots = 8;  // max members per cluster = slots of a tree leaf
 constexpr uint32_t kFlatLeafSlots = 4; // slots of a flat-list leaf holding <= 4 members

@@ -39,7 +39,11 @@
 #define SPT_COOP_BALL 1
 #endif
 
-// 1: items run through 8x8 pixel tiles of each sample (tile_pixel), 0: row-major
+// Item order of a batch: SPT_TS_ORDER 1 = [band][8x8 tile][sample][pixel] (ts_item);
+// else SPT_TILE 1 = [sample][8x8 tile][pixel] (tile_pixel), 0 = [sample][row-major pixel]
+#ifndef SPT_TS_ORDER
+#define SPT_TS_ORDER 1
+#endif
 #ifndef SPT_TILE
 #define SPT_TILE 1
 #endif
@@ -556,17 +560,25 @@ __global__ __launch_bounds__(kRenderBlock) SPT_RENDER_ATTR void render_kernel(Re
                 }
             }
             if (ps.phase == PH_IDLE && mine != 0xFFFFFFFFu) {
-                // primary ray, SingleThreadPathTracer.hpp:123-130.  Items are ordered
-                // [sample][8x8 tile][pixel]: a claim is a compact patch of one sample.
+                // primary ray, SingleThreadPathTracer.hpp:123-130.  A claim of
+                // consecutive items stays inside one 8x8 tile (ts_item).
+#if SPT_TS_ORDER
+                uint32_t sl, lr, cx;
+                ts_item(mine, a.map.width, rows, a.spp_batch, sl, lr, cx);
+                const uint32_t s = a.s0 + sl;
+                ps.item = sl * a.npix + lr * a.map.width + cx;  // slot: [sample][row-major pixel]
+                const uint32_t x = a.map.x0 + cx;
+#elif SPT_TILE
                 const uint32_t sl = mine / a.npix;
                 const uint32_t s = a.s0 + sl;
-                const uint32_t pl = mine - sl * a.npix;
-#if SPT_TILE
                 uint32_t lr, cx;
-                tile_pixel(pl, a.map.width, rows, lr, cx);
+                tile_pixel(mine - sl * a.npix, a.map.width, rows, lr, cx);
                 ps.item = sl * a.npix + lr * a.map.width + cx;  // slot: [sample][row-major pixel]
                 const uint32_t x = a.map.x0 + cx;
 #else
+                const uint32_t sl = mine / a.npix;
+                const uint32_t s = a.s0 + sl;
+                const uint32_t pl = mine - sl * a.npix;
                 ps.item = mine;
                 const uint32_t lr = pl / a.map.width;
                 const uint32_t x = a.map.x0 + (pl - lr * a.map.width);

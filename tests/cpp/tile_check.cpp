@@ -1,6 +1,7 @@
-// Host check of spt::tile_pixel (spt_internal.h): for every region shape in a
-// range, the item -> (row, col) map is a bijection onto the region, and full
-// 8x8 tiles are contiguous runs of 64 items.  Exit status 0 = pass.
+// Host check of the kernel's item orders (spt_internal.h): spt::tile_pixel
+// ([sample][tile][pixel]) and spt::ts_item ([band][tile][sample][pixel]) are
+// bijections onto the region (x samples) for every shape in a range plus the
+// config sizes, and full 8x8 tiles are contiguous runs of 64 items.  Exit 0 = pass.
 #include <cstdio>
 #include <vector>
 
@@ -39,6 +40,44 @@ int main()
             if (lr >= rows || col >= width || seen[(size_t)lr * width + col]++) {
                 std::printf("FAIL rows=%u width=%u q=%u\n", rows, width, q);
                 return 1;
+            }
+        }
+    }
+    // ts_item: [band][tile][sample][pixel] over rows x width x S is a bijection
+    for (uint32_t S = 1; S <= 5; S += 2)
+        for (uint32_t rows = 1; rows <= 27; ++rows)
+            for (uint32_t width = 1; width <= 35; ++width) {
+                std::vector<int> seen((size_t)rows * width * S, 0);
+                for (uint32_t q = 0; q < rows * width * S; ++q) {
+                    uint32_t sl, lr, col;
+                    spt::ts_item(q, width, rows, S, sl, lr, col);
+                    if (sl >= S || lr >= rows || col >= width || seen[((size_t)sl * rows + lr) * width + col]++) {
+                        std::printf("FAIL ts rows=%u width=%u S=%u q=%u -> (%u, %u, %u)\n", rows, width, S, q, sl, lr, col);
+                        return 1;
+                    }
+                    // full tiles: 64 consecutive items are the 64 pixels of one tile and sample
+                    if (rows % 8 == 0 && width % 8 == 0) {
+                        uint32_t s0, l0, c0;
+                        spt::ts_item(q & ~63u, width, rows, S, s0, l0, c0);
+                        if (s0 != sl || lr / 8 != l0 / 8 || col / 8 != c0 / 8) {
+                            std::printf("FAIL ts run rows=%u width=%u S=%u q=%u\n", rows, width, S, q);
+                            return 1;
+                        }
+                    }
+                }
+            }
+    {
+        const uint32_t shapes[][3] = {{800, 1200, 4}, {101, 1201, 3}, {1080, 1920, 2}, {7, 1200, 9}};
+        for (auto &sh : shapes) {
+            const uint32_t rows = sh[0], width = sh[1], S = sh[2];
+            std::vector<unsigned char> seen((size_t)rows * width * S, 0);
+            for (uint32_t q = 0; q < rows * width * S; ++q) {
+                uint32_t sl, lr, col;
+                spt::ts_item(q, width, rows, S, sl, lr, col);
+                if (sl >= S || lr >= rows || col >= width || seen[((size_t)sl * rows + lr) * width + col]++) {
+                    std::printf("FAIL ts rows=%u width=%u S=%u q=%u\n", rows, width, S, q);
+                    return 1;
+                }
             }
         }
     }

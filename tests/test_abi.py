@@ -130,9 +130,10 @@ def test_traversal_tables_edge_scenes(native, case):
     assert rc == 1
 
 
-def test_tile_item_map_is_a_bijection(tmp_path):
-    """The kernel's [sample][8x8 tile][pixel] item order (spt::tile_pixel) covers
-    every pixel of any region exactly once; compiled for the host with hipcc."""
+def test_item_orders_are_bijections(tmp_path):
+    """The kernel's item orders -- [band][8x8 tile][sample][pixel] (spt::ts_item,
+    the default) and [sample][8x8 tile][pixel] (spt::tile_pixel) -- cover every
+    (sample, pixel) of any region exactly once; compiled for the host with hipcc."""
     import os
     import subprocess
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))

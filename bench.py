@@ -72,7 +72,10 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--mode", default="segment", choices=["segment", "task"])
-    ap.add_argument("--strip", type=int, default=8)
+    ap.add_argument("--strip", type=int, default=0, help="rows per strip (0: largest of 8/4/2/1 splitting evenly)")
+    ap.add_argument("--streams", type=int, default=2,
+                    help="frames in flight on alternating HIP streams (the next frame fills the GPU while "
+                         "the previous one's last paths drain; each stream has its own workspace)")
     ap.add_argument("--cpu-spp", type=int, default=32, help="spp of the bounded CPU-baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -108,18 +111,28 @@ def main():
     ctx.set_camera(view, spt.scene.DEFAULT_EYE, spt.INIT_COLOR)
     ctx.set_params(W, H, spp, bounces, 1)
 
-    from simplepathtracer_amd.distributed import FrameSplit, render_frame
-    split = FrameSplit(W, H, world, args.strip)
-    stream = torch.cuda.current_stream(dev).cuda_stream
-    frame = torch.zeros((H * W, 4), dtype=torch.float32, device=dev) if rank == 0 else None
-    g_data = torch.zeros(W * H * 3, dtype=torch.uint8, device=dev) if rank == 0 else None
-    local_tile = gathered = None
-    if world > 1:
-        local_tile = torch.zeros((split.tile_pixels(), 4), dtype=torch.float32, device=dev)
-        gathered = torch.zeros((world * split.tile_pixels(), 4), dtype=torch.float32, device=dev)
+    from simplepathtracer_amd.distributed import FrameSplit, even_strip, render_frame
+    split = FrameSplit(W, H, world, args.strip or even_strip(H, world))
+    nst = max(1, args.streams)
+    streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(nst - 1)]
+    bufs = []
+    for _ in range(nst):  # per-stream frame buffers: frames in flight do not share outputs
+        b = {"frame": torch.zeros((H * W, 4), dtype=torch.float32, device=dev) if rank == 0 else None,
+             "g_data": torch.zeros(W * H * 3, dtype=torch.uint8, device=dev) if rank == 0 else None,
+             "local": None, "gathered": None}
+        if world > 1:
+            b["local"] = torch.zeros((split.tile_pixels(), 4), dtype=torch.float32, device=dev)
+            b["gathered"] = torch.zeros((world * split.tile_pixels(), 4), dtype=torch.float32, device=dev)
+        bufs.append(b)
+    counter = [0]
 
     def step():
-        render_frame(ctx, split, rank, mode, local_tile, gathered, frame, g_data, stream)
+        k = counter[0] % nst
+        counter[0] += 1
+        b = bufs[k]
+        with torch.cuda.stream(streams[k]):  # RCCL collectives follow the current stream
+            render_frame(ctx, split, rank, mode, b["local"], b["gathered"], b["frame"], b["g_data"],
+                         streams[k].cuda_stream)
 
     for _ in range(args.warmup):
         step()
@@ -180,7 +193,8 @@ def main():
             "config": {"workload": f"{args.config}: {scene_name} scene seed 1 (N={scene.n} spheres), {W}x{H}, "
                                    f"{spp} spp, depth {bounces}, {args.mode} mode",
                        "width": W, "height": H, "spp": spp, "bounces": bounces, "spheres": scene.n,
-                       "parallelism": f"row-strips{args.strip}x{world}" if world > 1 else "1 GPU"},
+                       "parallelism": f"row-strips{split.strip}x{world}" if world > 1 else "1 GPU",
+                       "frames_in_flight": nst},
             "roofline": {"bound": "valu", "achieved": round(achieved, 3), "peak": round(VALU_PEAK_TOPS, 2),
                          "unit": "TFLOP/s", "frac": round(achieved / VALU_PEAK_TOPS, 4), "traffic": traffic,
                          "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE, profiles/traffic.json)",
@@ -199,7 +213,8 @@ def main():
             out["cpu_baseline"] = cpu_baseline(scene, view, cw, ch, args.cpu_spp, bounces, args.cpu_threads)
         print(json.dumps(out), flush=True)
         if args.dump:
-            g_data.cpu().numpy().tofile(args.dump)
+            torch.cuda.synchronize(dev)
+            bufs[(counter[0] - 1) % nst]["g_data"].cpu().numpy().tofile(args.dump)
     ctx.close()
     if world > 1:
         dist.destroy_process_group()

@@ -146,7 +146,10 @@ SPT_API int spt_render_segment_task(spt_ctx *ctx, uint32_t yBegin, uint32_t yEnd
  *   owned rows, then x).  d_rgb8 (nullable): device full frame in g_data layout.
  * stream: a hipStream_t; NULL is HIP's default (null) stream, as for any HIP
  * call.  Launches are ordered on that stream only.  Returns after enqueueing;
- * pair with spt_synchronize or the caller's stream sync. */
+ * pair with spt_synchronize or the caller's stream sync.  Each distinct stream
+ * (up to 4 per context) gets its own workspace, so renders enqueued on different
+ * streams may be in flight together: the next frame's blocks then fill the GPU
+ * while the previous frame's last paths drain. */
 SPT_API int spt_render_rows_async(spt_ctx *ctx, int mode, uint32_t yBegin, uint32_t yEnd, uint32_t strip, uint32_t parts,
                           uint32_t part, uint32_t xBegin, uint32_t xEnd, void *d_rgba, void *d_rgb8, void *stream);
 /* Number of rows the (yBegin, yEnd, strip, parts, part) map owns. */

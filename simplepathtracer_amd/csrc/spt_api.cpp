@@ -32,6 +32,18 @@ struct EventPair {
 
 }  // namespace
 
+namespace {
+constexpr size_t kMaxWorkspaces = 4;
+struct Workspace {
+    hipStream_t stream = nullptr;  // key
+    float *d_samples = nullptr;    // per-sample slots of the current batch
+    size_t samples_cap = 0;
+    float4 *d_acc = nullptr;       // ordered partial sums when a frame is batched
+    size_t acc_cap = 0;
+    uint32_t *d_head = nullptr;    // claim counter
+};
+}  // namespace
+
 struct spt_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -65,11 +77,10 @@ struct spt_ctx {
 
     // workspace
     uint64_t ws_bytes = 4ull << 30;
-    float *d_samples = nullptr;
-    size_t samples_cap = 0;
-    float4 *d_acc = nullptr;
-    size_t acc_cap = 0;
-    uint32_t *d_head = nullptr;
+    // one workspace per stream, so renders on different streams can be in flight
+    // together (the next frame's blocks fill the GPU while the last paths of the
+    // previous one drain)
+    std::vector<Workspace> ws;
     unsigned long long *d_counters = nullptr;
     float4 *d_stage = nullptr;
     size_t stage_cap = 0;
@@ -183,6 +194,25 @@ uint32_t claim_size(const spt_ctx *ctx, uint64_t items)
     return (uint32_t)std::min<uint64_t>(256, std::max<uint64_t>(64, fair / 64 * 64));
 }
 
+// The workspace of stream s (created on first use, at most kMaxWorkspaces).
+Workspace *workspace_for(spt_ctx *ctx, hipStream_t s)
+{
+    for (Workspace &w : ctx->ws)
+        if (w.stream == s) return &w;
+    if (ctx->ws.size() >= kMaxWorkspaces) {
+        fail(ctx, SPT_ERR_STATE, "more than %zu streams in use on one context", kMaxWorkspaces);
+        return nullptr;
+    }
+    Workspace w;
+    w.stream = s;
+    if (hipMalloc((void **)&w.d_head, sizeof(uint32_t)) != hipSuccess) {
+        fail(ctx, SPT_ERR_NOMEM, "workspace allocation failed");
+        return nullptr;
+    }
+    ctx->ws.push_back(w);
+    return &ctx->ws.back();
+}
+
 // Render the rows of `map` and fold them into d_rgba (local pixel order) and/or
 // d_rgb8 (full frame).  keep_samples: leave the per-sample colours of a single
 // batch in d_samples (debug path).
@@ -202,10 +232,12 @@ int render_impl(spt_ctx *ctx, int mode, const spt::RowMap &map, float4 *d_rgba, 
     if (keep_samples && spp_batch != ctx->spp)
         return fail(ctx, SPT_ERR_ARG, "region * spp exceeds the workspace for spt_render_samples");
     const uint64_t items_max = (uint64_t)npix * spp_batch;
-    int rc = ensure(ctx, &ctx->d_samples, &ctx->samples_cap, items_max * slot_floats);
+    Workspace *w = workspace_for(ctx, s);
+    if (!w) return SPT_ERR_STATE;
+    int rc = ensure(ctx, &w->d_samples, &w->samples_cap, items_max * slot_floats);
     if (rc) return rc;
     if (spp_batch < ctx->spp) {
-        rc = ensure(ctx, &ctx->d_acc, &ctx->acc_cap, npix);
+        rc = ensure(ctx, &w->d_acc, &w->acc_cap, npix);
         if (rc) return rc;
     }
 
@@ -220,15 +252,15 @@ int render_impl(spt_ctx *ctx, int mode, const spt::RowMap &map, float4 *d_rgba, 
     ra.map = map;
     ra.npix = npix;
     ra.claim = claim_size(ctx, (uint64_t)npix * spp_batch);
-    ra.samples = ctx->d_samples;
+    ra.samples = w->d_samples;
     ra.slot_floats = slot_floats;
-    ra.head = ctx->d_head;
+    ra.head = w->d_head;
     ra.counters = ctx->d_counters;
 
     spt::FoldArgs fa{};
-    fa.samples = ctx->d_samples;
+    fa.samples = w->d_samples;
     fa.slot_floats = slot_floats;
-    fa.acc = ctx->d_acc;
+    fa.acc = w->d_acc;
     fa.out_rgba = d_rgba;
     fa.out_rgb8 = d_rgb8;
     fa.map = map;
@@ -243,7 +275,7 @@ int render_impl(spt_ctx *ctx, int mode, const spt::RowMap &map, float4 *d_rgba, 
         ra.spp_batch = b;
         ra.s0 = s0;
         ra.n_items = npix * b;
-        HIP_TRY(ctx, hipMemsetAsync(ctx->d_head, 0, sizeof(uint32_t), s));
+        HIP_TRY(ctx, hipMemsetAsync(w->d_head, 0, sizeof(uint32_t), s));
         EventPair ev = get_pair(ctx);
         HIP_TRY(ctx, hipEventRecord(ev.a, s));
         HIP_TRY(ctx, spt::launch_render(ra, ctx->grid, ctx->block, s));
@@ -406,8 +438,7 @@ int spt_ctx_create(int device, spt_ctx **out)
     if (const char *e = std::getenv("SPT_CLUSTER_K")) ctx->cluster_k = (uint32_t)std::max(0, std::atoi(e));
     if (const char *e = std::getenv("SPT_TREE_B")) ctx->tree_branching = (uint32_t)std::max(0, std::atoi(e));
     ctx->grid = (uint32_t)(per_cu * ctx->num_cu);
-    if (hipMalloc((void **)&ctx->d_head, sizeof(uint32_t)) != hipSuccess ||
-        hipMalloc((void **)&ctx->d_counters, 12 * sizeof(unsigned long long)) != hipSuccess ||
+    if (hipMalloc((void **)&ctx->d_counters, 12 * sizeof(unsigned long long)) != hipSuccess ||
         hipMemset(ctx->d_counters, 0, 12 * sizeof(unsigned long long)) != hipSuccess) {
         spt_ctx_destroy(ctx);
         return fail(nullptr, SPT_ERR_NOMEM, "workspace allocation failed");
@@ -426,11 +457,14 @@ void spt_ctx_destroy(spt_ctx *ctx)
             (void)hipEventDestroy(p.a);
             (void)hipEventDestroy(p.b);
         }
+    (void)hipDeviceSynchronize();  // async renders on caller streams
     void *bufs[] = {ctx->d_shade, ctx->d_mat, ctx->d_slots, ctx->d_orig, ctx->d_nodes,
-                    ctx->d_samples, ctx->d_acc,
-                    ctx->d_head, ctx->d_counters, ctx->d_stage, ctx->d_frame8};
+                    ctx->d_counters, ctx->d_stage, ctx->d_frame8};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
+    for (Workspace &w : ctx->ws)
+        for (void *b : {(void *)w.d_samples, (void *)w.d_acc, (void *)w.d_head})
+            if (b) (void)hipFree(b);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -630,7 +664,8 @@ int spt_render_samples(spt_ctx *ctx, int mode, uint32_t yB, uint32_t yE, uint32_
     const size_t npix = (size_t)(xE - xB) * (yE - yB);
     const size_t sf = mode == SPT_MODE_SEGMENT ? 3 : 4;
     std::vector<float> buf(npix * ctx->spp * sf);  // device order [sample][pixel], sf floats per slot
-    HIP_TRY(ctx, hipMemcpyAsync(buf.data(), ctx->d_samples, buf.size() * sizeof(float), hipMemcpyDeviceToHost,
+    HIP_TRY(ctx, hipMemcpyAsync(buf.data(), workspace_for(ctx, ctx->stream)->d_samples, buf.size() * sizeof(float),
+                                hipMemcpyDeviceToHost,
                                 ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     for (size_t p = 0; p < npix; ++p)

@@ -17,6 +17,15 @@ import numpy as np
 from .renderer import rows_count
 
 
+def even_strip(height: int, world: int) -> int:
+    """Rows per strip: the largest of 8, 4, 2, 1 that deals the frame's strips
+    evenly over the ranks (config 2 at 8 ranks: 200 strips of 4 rows), else 8."""
+    for s in (8, 4, 2, 1):
+        if height % s == 0 and (height // s) % world == 0:
+            return s
+    return 8
+
+
 @dataclass(frozen=True)
 class FrameSplit:
     width: int

@@ -5,9 +5,12 @@ One step = one frame of BASELINE.json config 2 (GenerateSpheres seed 1,
 1200x800, 100 spp, depth 50): every (pixel, sample) path traced by the gfx950
 megakernel, folded in sample order, written as float RGBA + RGB8 g_data.
 With N GPUs (torchrun, one process per GPU) the frame is split into interleaved
-8-row strips, rank r renders strips r, r+N, ...; the float tiles are gathered to
-rank 0 over RCCL (all_gather_into_tensor) and assembled there (strong scaling:
-the frame is fixed, per-GPU work shrinks with N).
+row strips (8 rows, or fewer so the strips deal evenly: 4 at N = 8), rank r renders
+strips r, r+N, ...; the float tiles are gathered to rank 0 over RCCL
+(all_gather_into_tensor) and assembled there (strong scaling: the frame is fixed,
+per-GPU work shrinks with N).  Consecutive frames alternate over two HIP streams
+(`--streams`), each with its own workspace and output buffers, so one frame's last
+paths drain while the next frame fills the GPU and its gather overlaps rendering.
 
 Prints ONE JSON line on rank 0 (see DESIGN.md §Measurement for every field).
 """

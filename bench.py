@@ -209,7 +209,9 @@ def main():
                              "peak": HBM_PEAK_GBS, "unit": "GB/s",
                              "frac": round(hbm_bytes / (avg_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 6)},
             "rays_per_sample": round(casts_all / max(samples_all, 1), 4),
-            "fold_ms_per_step": round(st["fold_ms"] / args.steps, 4),
+            # with frames in flight the fold runs beside the next frame's render and its
+            # own event span mostly measures waiting for CUs: reported for --streams 1 only
+            "fold_ms_per_step": round(st["fold_ms"] / args.steps, 4) if nst == 1 else None,
         }
         if world == 1 and not args.no_cpu_baseline:
             cw, ch = (W, H) if args.config != "c3" else (1920, 1080)

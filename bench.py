@@ -75,6 +75,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--mode", default="segment", choices=["segment", "task"])
+    ap.add_argument("--engine", default="megakernel", choices=["megakernel", "wavefront"],
+                    help="render loop: persistent megakernel, or the material-queue wavefront variant")
     ap.add_argument("--strip", type=int, default=0, help="rows per strip (0: largest of 8/4/2/1 splitting evenly)")
     ap.add_argument("--streams", type=int, default=2,
                     help="frames in flight on alternating HIP streams (the next frame fills the GPU while "
@@ -110,6 +112,8 @@ def main():
     view = spt.camera_basis()
     mode = spt.MODE_TASK if args.mode == "task" else spt.MODE_SEGMENT
     ctx = spt.Context(local)
+    if args.engine == "wavefront":
+        ctx.set_engine(spt._native.ENGINE_WAVEFRONT)
     ctx.set_scene(scene)
     ctx.set_camera(view, spt.scene.DEFAULT_EYE, spt.INIT_COLOR)
     ctx.set_params(W, H, spp, bounces, 1)
@@ -194,7 +198,7 @@ def main():
             "dtype": "f32",
             "data": "synthetic",
             "config": {"workload": f"{args.config}: {scene_name} scene seed 1 (N={scene.n} spheres), {W}x{H}, "
-                                   f"{spp} spp, depth {bounces}, {args.mode} mode",
+                                   f"{spp} spp, depth {bounces}, {args.mode} mode, {args.engine}",
                        "width": W, "height": H, "spp": spp, "bounces": bounces, "spheres": scene.n,
                        "parallelism": f"row-strips{split.strip}x{world}" if world > 1 else "1 GPU",
                        "frames_in_flight": nst},

@@ -122,6 +122,14 @@ SPT_API int spt_set_cluster_tree(spt_ctx *ctx, uint32_t branching);
  * member below it).  *out_nodes (nullable) = tree nodes per layout. */
 SPT_API int spt_accel_check(const float *centers4, const float *radii, uint32_t n, uint32_t cluster_k,
                             uint32_t branching, uint32_t *out_nodes);
+/* Engine of the render loop (results are bit-identical either way):
+ * SPT_ENGINE_MEGAKERNEL (default) -- one persistent kernel, per-lane state machines;
+ * SPT_ENGINE_WAVEFRONT -- RenderSegmentTask's material-queue design
+ *   (TaskBasedPathTracer.hpp:54-193) as separate kernels per pass: extend (cast +
+ *   category queues by ballot/prefix compaction) and one shading kernel per
+ *   category; the host reads the queue length back after each pass. */
+enum { SPT_ENGINE_MEGAKERNEL = 0, SPT_ENGINE_WAVEFRONT = 1 };
+SPT_API int spt_set_engine(spt_ctx *ctx, int engine);
 /* Upper bound of the per-sample workspace (default 4 GiB).  Larger frames are
  * rendered in sample batches folded in order. */
 SPT_API int spt_set_workspace(spt_ctx *ctx, uint64_t bytes);

@@ -21,6 +21,7 @@ STATUS_NAMES = {0: "SPT_OK", 1: "SPT_ERR_ARG", 2: "SPT_ERR_STATE", 3: "SPT_ERR_H
 MODE_SEGMENT, MODE_TASK = 0, 1
 TREE_AUTO = 0xFFFFFFFF  # spt_set_cluster_tree default
 CLUSTER_AUTO = 0xFFFFFFFF  # spt_set_cluster_size default
+ENGINE_MEGAKERNEL, ENGINE_WAVEFRONT = 0, 1
 SELFTEST_COLS = 12
 
 
@@ -84,6 +85,7 @@ def lib() -> ctypes.CDLL:
         "spt_set_workspace": ([P, u64], I),
         "spt_set_cluster_size": ([P, u32], I),
         "spt_set_cluster_tree": ([P, u32], I),
+        "spt_set_engine": ([P, I], I),
         "spt_accel_check": ([P, P, u32, u32, u32, P], I),
         "spt_render_segment": ([P, u32, u32, u32, u32, P, P], I),
         "spt_render_segment_task": ([P, u32, u32, u32, u32, P, P], I),

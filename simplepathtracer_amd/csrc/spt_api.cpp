@@ -41,6 +41,8 @@ struct Workspace {
     float4 *d_acc = nullptr;       // ordered partial sums when a frame is batched
     size_t acc_cap = 0;
     uint32_t *d_head = nullptr;    // claim counter
+    spt::WavefrontBuffers wf{};    // queues of the wavefront engine (allocated on first use)
+    uint32_t *h_count = nullptr;   // pinned host word: queue length read back per pass
 };
 }  // namespace
 
@@ -66,6 +68,8 @@ struct spt_ctx {
     std::vector<uint32_t> h_mat;
     uint32_t cluster_k = SPT_CLUSTER_AUTO;  // members per culling cluster; 0 = brute force
     uint32_t tree_branching = SPT_TREE_AUTO;  // children per inner node; 0 = flat cluster list
+    int engine = SPT_ENGINE_MEGAKERNEL;
+    uint32_t wf_cap = 1u << 22;  // rays per wavefront queue
     spt::AccelView accel{};
     // camera (Globals.hpp:21-29)
     spt::Camera cam{};
@@ -213,6 +217,38 @@ Workspace *workspace_for(spt_ctx *ctx, hipStream_t s)
     return &ctx->ws.back();
 }
 
+// Queues of the wavefront engine in workspace w, for `cap` rays.
+int ensure_wavefront(spt_ctx *ctx, Workspace *w, uint32_t cap)
+{
+    spt::WavefrontBuffers &b = w->wf;
+    if (b.cap >= cap && b.hit) return SPT_OK;
+    HIP_TRY(ctx, hipDeviceSynchronize());
+    void *old[] = {b.o[0], b.o[1], b.d[0], b.d[1], b.m[0], b.m[1], b.st[0], b.st[1], b.hit, b.cat_idx, b.counts,
+                   b.tag, b.bcount, b.boff, b.scan_tmp};
+    for (void *p : old)
+        if (p) (void)hipFree(p);
+    b = spt::WavefrontBuffers{};
+    bool ok = true;
+    for (int q = 0; q < 2; ++q) {
+        ok = ok && hipMalloc((void **)&b.o[q], (size_t)cap * sizeof(float4)) == hipSuccess;
+        ok = ok && hipMalloc((void **)&b.d[q], (size_t)cap * sizeof(float4)) == hipSuccess;
+        ok = ok && hipMalloc((void **)&b.m[q], (size_t)cap * sizeof(float4)) == hipSuccess;
+        ok = ok && hipMalloc((void **)&b.st[q], (size_t)cap * sizeof(uint2)) == hipSuccess;
+    }
+    ok = ok && hipMalloc((void **)&b.hit, (size_t)cap * sizeof(float4)) == hipSuccess;
+    ok = ok && hipMalloc((void **)&b.cat_idx, (size_t)cap * sizeof(uint32_t)) == hipSuccess;
+    ok = ok && hipMalloc((void **)&b.counts, (1 + spt::kWfCats) * sizeof(uint32_t)) == hipSuccess;
+    ok = ok && hipMalloc((void **)&b.tag, (size_t)cap) == hipSuccess;
+    ok = ok && hipMalloc((void **)&b.bcount, (size_t)(spt::kWfCats + 1) * (cap / 64 + 1) * sizeof(uint32_t)) == hipSuccess;
+    ok = ok && hipMalloc((void **)&b.boff, (size_t)(spt::kWfCats + 1) * (cap / 64 + 1) * sizeof(uint32_t)) == hipSuccess;
+    b.scan_bytes = std::max<size_t>(spt::wavefront_scan_bytes(cap), 16);
+    ok = ok && hipMalloc(&b.scan_tmp, b.scan_bytes) == hipSuccess;
+    if (!w->h_count) ok = ok && hipHostMalloc((void **)&w->h_count, sizeof(uint32_t)) == hipSuccess;
+    if (!ok) return fail(ctx, SPT_ERR_NOMEM, "wavefront queues for %u rays: allocation failed", cap);
+    b.cap = cap;
+    return SPT_OK;
+}
+
 // Render the rows of `map` and fold them into d_rgba (local pixel order) and/or
 // d_rgb8 (full frame).  keep_samples: leave the per-sample colours of a single
 // batch in d_samples (debug path).
@@ -275,11 +311,31 @@ int render_impl(spt_ctx *ctx, int mode, const spt::RowMap &map, float4 *d_rgba, 
         ra.spp_batch = b;
         ra.s0 = s0;
         ra.n_items = npix * b;
-        HIP_TRY(ctx, hipMemsetAsync(w->d_head, 0, sizeof(uint32_t), s));
         EventPair ev = get_pair(ctx);
-        HIP_TRY(ctx, hipEventRecord(ev.a, s));
-        HIP_TRY(ctx, spt::launch_render(ra, ctx->grid, ctx->block, s));
-        HIP_TRY(ctx, hipEventRecord(ev.b, s));
+        if (ctx->engine == SPT_ENGINE_WAVEFRONT) {
+            // queue passes until every item is issued and the queue has drained; the
+            // host reads the queue length back after each pass (4 bytes, pinned)
+            const uint32_t cap = (uint32_t)std::min<uint64_t>(ctx->wf_cap, std::max<uint32_t>(ra.n_items, 1024u));
+            if ((rc = ensure_wavefront(ctx, w, cap))) return rc;
+            HIP_TRY(ctx, hipEventRecord(ev.a, s));
+            uint32_t cur = 0, n_cur = 0, next_item = 0;
+            while (next_item < ra.n_items || n_cur > 0) {
+                const uint32_t gen = std::min(cap - n_cur, ra.n_items - next_item);
+                HIP_TRY(ctx, spt::launch_wavefront_pass(w->wf, ra, cur, n_cur, next_item, gen, s));
+                next_item += gen;
+                HIP_TRY(ctx, hipMemcpyAsync(w->h_count, w->wf.counts, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+                HIP_TRY(ctx, hipStreamSynchronize(s));
+                n_cur = *w->h_count;
+                cur ^= 1u;
+                if (n_cur > cap) return fail(ctx, SPT_ERR_STATE, "wavefront queue overflow (%u > %u)", n_cur, cap);
+            }
+            HIP_TRY(ctx, hipEventRecord(ev.b, s));
+        } else {
+            HIP_TRY(ctx, hipMemsetAsync(w->d_head, 0, sizeof(uint32_t), s));
+            HIP_TRY(ctx, hipEventRecord(ev.a, s));
+            HIP_TRY(ctx, spt::launch_render(ra, ctx->grid, ctx->block, s));
+            HIP_TRY(ctx, hipEventRecord(ev.b, s));
+        }
         ctx->pending_render.push_back(ev);
         ctx->launches++;
         if (keep_samples) continue;
@@ -437,6 +493,7 @@ int spt_ctx_create(int device, spt_ctx **out)
     if (const char *e = std::getenv("SPT_CLAIM")) ctx->claim = (uint32_t)std::max(1, std::atoi(e));
     if (const char *e = std::getenv("SPT_CLUSTER_K")) ctx->cluster_k = (uint32_t)std::max(0, std::atoi(e));
     if (const char *e = std::getenv("SPT_TREE_B")) ctx->tree_branching = (uint32_t)std::max(0, std::atoi(e));
+    if (const char *e = std::getenv("SPT_WF_CAP")) ctx->wf_cap = (uint32_t)std::max(1024, std::atoi(e));
     ctx->grid = (uint32_t)(per_cu * ctx->num_cu);
     if (hipMalloc((void **)&ctx->d_counters, 12 * sizeof(unsigned long long)) != hipSuccess ||
         hipMemset(ctx->d_counters, 0, 12 * sizeof(unsigned long long)) != hipSuccess) {
@@ -462,9 +519,15 @@ void spt_ctx_destroy(spt_ctx *ctx)
                     ctx->d_counters, ctx->d_stage, ctx->d_frame8};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
-    for (Workspace &w : ctx->ws)
-        for (void *b : {(void *)w.d_samples, (void *)w.d_acc, (void *)w.d_head})
+    for (Workspace &w : ctx->ws) {
+        const spt::WavefrontBuffers &q = w.wf;
+        for (void *b : {(void *)w.d_samples, (void *)w.d_acc, (void *)w.d_head, (void *)q.o[0], (void *)q.o[1],
+                        (void *)q.d[0], (void *)q.d[1], (void *)q.m[0], (void *)q.m[1], (void *)q.st[0],
+                        (void *)q.st[1], (void *)q.hit, (void *)q.cat_idx, (void *)q.counts, (void *)q.tag,
+                        (void *)q.bcount, (void *)q.boff, q.scan_tmp})
             if (b) (void)hipFree(b);
+        if (w.h_count) (void)hipHostFree(w.h_count);
+    }
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -571,6 +634,16 @@ int spt_accel_check(const float *centers4, const float *radii, uint32_t n, uint3
     const std::string bad = spt::validate_accel(t, centers4, radii, n);
     if (!bad.empty()) return fail(nullptr, SPT_ERR_STATE, "traversal tables invalid: %s", bad.c_str());
     if (out_nodes) *out_nodes = t.n_nodes;
+    return SPT_OK;
+}
+
+int spt_set_engine(spt_ctx *ctx, int engine)
+{
+    if (!ctx) return fail(nullptr, SPT_ERR_ARG, "null context");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    if (engine != SPT_ENGINE_MEGAKERNEL && engine != SPT_ENGINE_WAVEFRONT)
+        return fail(ctx, SPT_ERR_ARG, "unknown engine %d", engine);
+    ctx->engine = engine;
     return SPT_OK;
 }
 

@@ -170,6 +170,29 @@ struct FoldArgs {
 };
 
 hipError_t launch_render(const RenderArgs &a, uint32_t grid, uint32_t block, hipStream_t s);
+
+// Wavefront variant (spt_wavefront.hip): double-buffered ray queues of `cap`
+// rays, a hit record per ray, kWfCats category queues and their counters.
+constexpr uint32_t kWfCats = 5;  // sky/miss, diffuse first hit, mirror, glass, diffuse-loop step
+struct WavefrontBuffers {
+    float4 *o[2], *d[2], *m[2];
+    uint2 *st[2];
+    float4 *hit;
+    uint32_t *cat_idx;  // [cap] category-major list of ray indices
+    uint8_t *tag;       // [cap] category, then alive flag
+    uint32_t *bcount;   // [kWfCats + 1][cap / 64 + 1] per-wave counts
+    uint32_t *boff;     // their exclusive scan
+    uint32_t *counts;   // [0] next queue length
+    void *scan_tmp;     // hipCUB scan scratch
+    size_t scan_bytes;
+    uint32_t cap;
+};
+size_t wavefront_scan_bytes(uint32_t cap);
+// One pass: append gen_n new paths (items gen_base..) after the n_cur queued rays
+// of queue `cur`, cast them all, shade them category by category and compact the
+// survivors, in order, into queue cur^1; the new length is left in counts[0].
+hipError_t launch_wavefront_pass(const WavefrontBuffers &b, const RenderArgs &a, uint32_t cur, uint32_t n_cur,
+                                 uint32_t gen_base, uint32_t gen_n, hipStream_t s);
 hipError_t launch_fold(const FoldArgs &a, hipStream_t s);
 hipError_t launch_assemble(const float4 *tiles, uint32_t max_rows, RowMap base, uint32_t width, uint32_t height,
                            float4 *frame, uint8_t *rgb8, hipStream_t s);

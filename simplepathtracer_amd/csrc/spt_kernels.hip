@@ -21,466 +21,10 @@
 // count-weighted resolve (TaskBasedPathTracer.hpp:196-205), plus WritePixel.
 // Sums are formed in sample order, so results are bit-identical to the
 // sequential reference loop whatever order the paths finished in.
-#include "spt_device.h"
-#include "spt_internal.h"
-
-#include <float.h>
-
-#ifndef SPT_GROUP
-#define SPT_GROUP 4
-#endif
-
-#ifndef SPT_DIAG
-#define SPT_DIAG 0
-#endif
-
-// 1: the cube-minus-ball rejection loop runs cooperatively across the wave
-#ifndef SPT_COOP_BALL
-#define SPT_COOP_BALL 1
-#endif
-
-// Item order of a batch: SPT_TS_ORDER 1 = [band][8x8 tile][sample][pixel] (ts_item);
-// else SPT_TILE 1 = [sample][8x8 tile][pixel] (tile_pixel), 0 = [sample][row-major pixel]
-#ifndef SPT_TS_ORDER
-#define SPT_TS_ORDER 1
-#endif
-#ifndef SPT_TILE
-#define SPT_TILE 1
-#endif
-
-// 1: flat cluster lists use the tree walk's three tests too (A/B switch)
-#ifndef SPT_FLAT_FULL
-#define SPT_FLAT_FULL 0
-#endif
-
-#pragma clang fp contract(off)
+#include "spt_path.h"
 
 namespace spt {
 
-namespace {
-
-constexpr uint32_t PH_IDLE = 0, PH_TRACE = 1, PH_DLOOP = 2;
-
-// rSq of SampleColorRefractive (lines 58 and 75): float(pow(double(-0.2f), 2)).
-// The exact square of a float is representable in double, so pow returns it.
-constexpr float kRsq = (float)((double)((1.0f - 1.5f) / (1.0f + 1.5f)) * (double)((1.0f - 1.5f) / (1.0f + 1.5f)));
-constexpr float kAirToGlass = 1.0f / 1.5f;
-constexpr float kGlassToAir = 1.5f / 1.0f;
-
-// Tables as constant-address-space data: wave-uniform indices become scalar
-// (s_load) reads even though the kernel also stores to global memory.
-typedef __attribute__((address_space(4))) const float cfloat;
-typedef __attribute__((address_space(4))) const uint32_t cuint;
-
-__device__ __forceinline__ float4 ld_uniform(cfloat *p, uint32_t i)
-{
-    return make_float4(p[4 * i + 0], p[4 * i + 1], p[4 * i + 2], p[4 * i + 3]);
-}
-
-__device__ __forceinline__ uint32_t lane_rank(unsigned long long mask)
-{
-    return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
-}
-
-// Closest-hit state of one FindClosestIntersectionSphere call.
-struct Hit {
-    uint32_t idx;        // slot of the winner (traversal order), kMiss = none
-    float best;          // its squared distance
-    f3 p;                // its closest contact point
-};
-
-// One group of G slots {C, r*r} (Collision.hpp:87-109): RaySphereIntersection for
-// all of them, then the rare closest-contact / distance update behind a single
-// branch.  Slots are visited in traversal order, so the winner is the
-// lexicographic minimum of (distance, original index): identical to the
-// reference's strict-'>' scan in index order (first index wins ties; NaN and
-// FLT_MAX distances never win).
-template <int G>
-__device__ __forceinline__ void test_group(const float4 (&sp)[G], const uint32_t *__restrict__ orig, uint32_t slot,
-                                           const f3 &o, const f3 &d, float dod, Hit &h)
-{
-    float tcv[G], hv[G];
-    bool pass[G];
-    bool any = false;
-#pragma unroll
-    for (int k = 0; k < G; ++k) {
-        // RaySphereIntersection, Collision.hpp:9-17
-        const float ocx = sp[k].x - o.x, ocy = sp[k].y - o.y, ocz = sp[k].z - o.z;
-        const float tc = (ocx * d.x + ocy * d.y) + ocz * d.z;
-        const float d2 = ((ocx * ocx + ocy * ocy) + ocz * ocz) - tc * tc;
-        const float hh = sp[k].w - d2;
-        tcv[k] = tc;
-        hv[k] = hh;
-        pass[k] = tc > 1e-3f && hh > 1e-3f;
-        any = any || pass[k];
-    }
-    if (any) {
-#pragma unroll
-        for (int k = 0; k < G; ++k) {
-            if (pass[k]) {
-                // CalculateRaySphereClosestContactPoint, Collision.hpp:19-27,49-56
-                const float t = tcv[k] - sqrt_pos_normal(hv[k]);
-                const f3 p = mk(o.x + d.x * t, o.y + d.y * t, o.z + d.z * t);
-                if (dod < dot(p, d)) {
-                    const float ds = lensq(sub(o, p));
-                    bool better = ds < h.best;
-                    // exact tie (rare): the first original index wins.  Behind a
-                    // wave-uniform branch, so the index loads (and the vmcnt waits
-                    // they would drag into the hot loop) run only when some lane ties.
-                    const bool tie = ds == h.best && h.idx != kMiss;
-                    if (__builtin_expect(__ballot(tie) != 0ull, 0)) {
-                        if (tie) better = orig[slot + k] < orig[h.idx];
-                    }
-                    if (better) {
-                        h.best = ds;
-                        h.idx = slot + k;
-                        h.p = p;
-                    }
-                }
-            }
-        }
-    }
-}
-
-// Wave-diagnostic counters of the SPT_DIAG build.
-struct CastDiag {
-    unsigned long long nodes = 0, leaves = 0, pairs = 0, live = 0;
-};
-
-// Leaf test: the cluster's S slots (S = 8: two s_load_dwordx16, S = 4: one) off one
-// base pointer.
-template <int S>
-__device__ __forceinline__ void test_leaf(cfloat *slots, const uint32_t *__restrict__ orig, uint32_t leaf_slot,
-                                          const f3 &o, const f3 &d, float dod, Hit &h)
-{
-    cfloat *cs = slots + 4 * leaf_slot;
-    float4 ms[S];
-#pragma unroll
-    for (int k = 0; k < S; ++k) ms[k] = ld_uniform(cs, k);
-    test_group<S>(ms, orig, leaf_slot, o, d, dod, h);
-}
-
-// FindClosestIntersectionSphere for every lane of the wave (Collision.hpp:87-109).
-// `active`: lanes whose result matters (others never open a node).
-// TREE = false: the clusters form a flat list (small scenes) and a node is
-// entered when the ray's line may pass one of its members (the "line" test of
-// DESIGN.md §4.4).  TREE = true: preorder walk of the cluster tree in the layout
-// of the wave's majority direction octant with the line, front and near tests.
-template <bool TREE, int LEAF>
-__device__ __forceinline__ Hit find_closest(const AccelView &ac, const f3 &o, const f3 &d, bool active,
-                                            CastDiag &dg)
-{
-    Hit h;
-    h.idx = kMiss;
-    h.best = FLT_MAX;
-    h.p = o;
-    const float dod = dot(o, d);
-    cfloat *slots = (cfloat *)ac.slots;
-    // always-tested spheres (ground, large balls; every sphere when culling is off)
-    for (uint32_t g = 0; g < ac.always_groups; ++g) {
-        float4 g4[SPT_GROUP];
-#pragma unroll
-        for (int k = 0; k < SPT_GROUP; ++k) g4[k] = ld_uniform(slots, g * SPT_GROUP + k);
-        test_group<SPT_GROUP>(g4, ac.orig, g * SPT_GROUP, o, d, dod, h);
-    }
-    // Lanes whose direction is not unit length within 1e-6 (the glass branch
-    // reflects without renormalising) never cull.
-    const float ddev = lensq(d) - 1.0f;
-    const bool no_cull = active && !(ddev <= 1e-6f && ddev >= -1e-6f);
-    const unsigned long long live_mask = __ballot(active);
-    // node masks are formed as (ballot(test) & live) | nocull: the ballot of a
-    // compare is the compare's own lane mask, with no VALU round trip
-    const unsigned long long nocull_mask = __ballot(no_cull);
-    cuint *nodes = (cuint *)ac.nodes;
-    if (!TREE) {
-#if !SPT_FLAT_FULL
-        // flat list: node i is leaf i; bound prefetched one node ahead (pad record)
-        constexpr int kNb = 6;
-        uint32_t nb[kNb];
-#pragma unroll
-        for (int q = 0; q < kNb; ++q) nb[q] = nodes[q];
-        for (uint32_t i = 0; i < ac.n_nodes; ++i) {
-            const float bx = __uint_as_float(nb[0]), by = __uint_as_float(nb[1]), bz = __uint_as_float(nb[2]);
-            const float k1 = __uint_as_float(nb[3]);
-            const uint32_t leaf_slot = nb[5];
-#pragma unroll
-            for (int q = 0; q < kNb; ++q) nb[q] = nodes[8 * (i + 1) + q];
-            const f3 ocb = mk(bx - o.x, by - o.y, bz - o.z);
-            const float tcb = dot(ocb, d);
-            const float occb = lensq(ocb);
-            const float d2b = occb - tcb * tcb;
-            const unsigned long long mm = (__ballot(d2b <= k1 + 1e-4f * occb) & live_mask) | nocull_mask;
-            if (SPT_DIAG) {
-                dg.nodes += 1;
-                dg.leaves += mm != 0ull ? 1 : 0;
-                dg.pairs += (unsigned long long)__popcll(mm);
-                dg.live += mm != 0ull ? (unsigned long long)__popcll(live_mask) : 0ull;
-            }
-            if (mm != 0ull) test_leaf<LEAF>(slots, ac.orig, leaf_slot, o, d, dod, h);
-        }
-        return h;
-#endif
-    }
-    const float olen = __builtin_amdgcn_sqrtf(lensq(o));  // |o|, for the distance margin
-    if (TREE) {
-        // the layout of the wave's majority direction octant (siblings front to back)
-        const uint32_t nlive = (uint32_t)__popcll(live_mask);
-        const uint32_t oct = (2u * (uint32_t)__popcll(__ballot(active && d.x < 0.f)) > nlive ? 1u : 0u) |
-                             (2u * (uint32_t)__popcll(__ballot(active && d.y < 0.f)) > nlive ? 2u : 0u) |
-                             (2u * (uint32_t)__popcll(__ballot(active && d.z < 0.f)) > nlive ? 4u : 0u);
-        nodes += (size_t)8 * (ac.n_nodes + 1) * oct;
-    }
-    uint32_t i = 0;
-    uint32_t nb[7];
-#pragma unroll
-    for (int q = 0; q < 7; ++q) nb[q] = nodes[q];
-    while (i < ac.n_nodes) {
-        const float bx = __uint_as_float(nb[0]), by = __uint_as_float(nb[1]), bz = __uint_as_float(nb[2]);
-        const float k1 = __uint_as_float(nb[3]), rb = __uint_as_float(nb[6]);
-        const uint32_t skip = nb[4], leaf_slot = nb[5];
-        // speculative prefetch of the preorder successor
-#pragma unroll
-        for (int q = 0; q < 7; ++q) nb[q] = nodes[8 * (i + 1) + q];
-        // Three conservative tests; a lane may need the node only
-        // if all pass.  line: the ray's line passes within the bound; front: some
-        // member may lie in front (tc > 1e-3); near: some member's contact point
-        // may be closer than the lane's current winner (never equal: strict margin).
-        const f3 ocb = mk(bx - o.x, by - o.y, bz - o.z);
-        const float tcb = dot(ocb, d);
-        const float occb = lensq(ocb);
-        const float d2b = occb - tcb * tcb;
-        const float lb = __builtin_amdgcn_sqrtf(occb);
-        const float slack = 1e-4f * (lb + rb);
-        // near: a member's computed contact distance t is at least
-        // (|Cb-o| - Rb) - 2.6e-3 (|Cb-o| + Rb) (rounding of hh under the sqrt and
-        // | |d| - 1 | <= 5e-7); 4e-3 keeps headroom
-        const float lc = ((lb - rb) - 4e-3f * (lb + rb)) - (2e-5f * olen + 1e-6f);
-        const bool line = d2b <= k1 + 1e-4f * occb;
-        const bool front = tcb >= -(rb + slack);
-        const bool near = !(lc > 0.f && lc * lc > h.best * 1.0001f);
-        const unsigned long long mm = (__ballot(line && front && near) & live_mask) | nocull_mask;
-        const bool leaf = leaf_slot != kNoSlot;
-        if (SPT_DIAG) {
-            dg.nodes += 1;
-            dg.leaves += (mm != 0ull && leaf) ? 1 : 0;
-            if (leaf) {
-                dg.pairs += (unsigned long long)__popcll(mm);
-                dg.live += mm != 0ull ? (unsigned long long)__popcll(live_mask) : 0ull;
-            }
-        }
-        if (mm != 0ull && leaf) test_leaf<LEAF>(slots, ac.orig, leaf_slot, o, d, dod, h);
-        const uint32_t next = (mm != 0ull && !leaf) ? i + 1 : skip;
-        if (next != i + 1) {
-#pragma unroll
-            for (int q = 0; q < 7; ++q) nb[q] = nodes[8 * next + q];
-        }
-        i = next;
-    }
-    return h;
-}
-
-// Per-lane path state of the flattened recursion.
-struct Path {
-    uint32_t phase, item, bounce, spec;
-    uint64_t st;  // keyed splitmix stream of this (pixel, sample)
-    f3 o, d, c;
-};
-
-// GenerateUniformDistInsideSphereVector (Random.hpp:115-127) for every lane with
-// `need`, all 64 lanes cooperating.  The stream is counter-based (draw n of a lane
-// is mix(st0 + (n+1) gamma)), so trial j = draws 3j..3j+2 can be evaluated by any
-// lane.  Round 0: every lane runs its own trial 0.  Later rounds: each still
-// pending lane gets H helper lanes (H = the largest power of two <= 64 / pending,
-// at most 16) that evaluate its trials jb .. jb+H-1 at once; it takes the lowest
-// accepted one.  The result and the advanced state st0 + 3 (j* + 1) gamma equal
-// the sequential loop's.  Must be called in wave-uniform control flow.
-// `lds`: 64 words of wave-private LDS.
-__device__ __forceinline__ f3 coop_ball_vector(uint64_t &st, bool need, uint32_t *lds)
-{
-    const uint32_t lane = __lane_id();
-    const uint64_t st0 = st;
-    uint64_t t = st0;
-    f3 r;
-    r.x = uniform(t, -0.5f, 0.5f);
-    r.y = uniform(t, -0.5f, 0.5f);
-    r.z = uniform(t, -0.5f, 0.5f);
-    uint32_t jacc = 0;
-    unsigned long long pend = __ballot(need && lensq(r) < 0.25f);
-    uint32_t jb = 1;
-    const uint32_t s_lo = (uint32_t)st0, s_hi = (uint32_t)(st0 >> 32);
-    while (pend != 0ull) {
-        const uint32_t np = (uint32_t)__popcll(pend);
-        const uint32_t q64 = 64u / np;
-        uint32_t lg = 31u - (uint32_t)__builtin_clz(q64);
-        lg = lg > 4u ? 4u : lg;
-        const bool is_p = (pend >> lane) & 1ull;
-        const uint32_t rank = lane_rank(pend);
-        if (is_p) lds[rank] = lane;
-        const uint32_t pidx = lane >> lg, tt = lane & ((1u << lg) - 1u);
-        const bool valid = pidx < np;
-        const uint32_t src = lds[valid ? pidx : 0u];
-        const uint32_t h_lo = (uint32_t)__shfl((int)s_lo, (int)src), h_hi = (uint32_t)__shfl((int)s_hi, (int)src);
-        uint64_t b = (((uint64_t)h_hi << 32) | h_lo) + (uint64_t)(3u * (jb + tt)) * kGamma;
-        f3 c;
-        c.x = uniform(b, -0.5f, 0.5f);
-        c.y = uniform(b, -0.5f, 0.5f);
-        c.z = uniform(b, -0.5f, 0.5f);
-        const unsigned long long acc = __ballot(valid && !(lensq(c) < 0.25f));
-        const uint32_t seg = is_p ? (uint32_t)(acc >> (rank << lg)) & ((1u << (1u << lg)) - 1u) : 0u;
-        const bool found = seg != 0u;
-        const uint32_t tstar = found ? (uint32_t)__builtin_ctz(seg) : 0u;
-        const uint32_t from = found ? (rank << lg) + tstar : lane;
-        const float rx = __shfl(c.x, (int)from), ry = __shfl(c.y, (int)from), rz = __shfl(c.z, (int)from);
-        if (found) {
-            r = mk(rx, ry, rz);
-            jacc = jb + tstar;
-        }
-        pend = __ballot(is_p && !found);
-        jb += 1u << lg;
-    }
-    if (need) st = st0 + (uint64_t)(3u * (jacc + 1u)) * kGamma;
-    return r;
-}
-
-// One shading step after a cast: the material switch of TraceAndSampleColor
-// (SingleThreadPathTracer.hpp:94-112) in PH_TRACE, or one turn of the diffuse
-// bounce loop (21-37) in PH_DLOOP.  Finishing paths write their sample slot.
-// Called by every lane of the wave (`act` = the lane holds a path), so the
-// cooperative cube-minus-ball sampler runs in uniform control flow.
-__device__ __forceinline__ void shade_step(const RenderArgs &a, Path &ps, const Hit &h, bool act,
-                                           unsigned long long &done, unsigned long long &dropped, uint32_t *lds)
-{
-    // hit, shade and material tables are in slot order (spt_accel.cpp)
-    const float4 *__restrict__ hit = a.scene.accel.slots;
-    const float4 *__restrict__ shade = a.scene.shade;
-    const uint32_t *__restrict__ mat = a.scene.mat;
-    const uint32_t idx = h.idx;
-    bool fin = false;
-    float counted = 1.f;
-    f3 col = mk(0.f, 0.f, 0.f);
-    const bool dl = ps.phase == PH_DLOOP;
-    uint32_t m = SPT_SKYBOX_ID;
-    if (act && idx != kMiss) m = mat[idx];
-    bool scatter = false, refr = false;
-    if (!act) {
-    } else if (dl) {
-        // while (--bounceCount && sphereIndex < N), SingleThreadPathTracer.hpp:28
-        --ps.bounce;
-        const bool end = ps.bounce == 0u || idx == kMiss;
-        if (end) {
-            col = ps.c;
-            fin = true;
-        }
-        scatter = !end;
-        refr = false;
-    } else {
-        // TraceAndSampleColor material switch, SingleThreadPathTracer.hpp:98-111
-        scatter = m == SPT_DIFFUSE_ID || m == SPT_REFLECTIVE_ID;
-        refr = m == SPT_REFRACTIVE_ID;
-        if (!scatter && !refr) {
-            // SampleColorSkybox, lines 11-14
-            const float k = ps.d.y + 1.f;
-            col = mul(mk(a.cam.sky[0] * k, a.cam.sky[1] * k, a.cam.sky[2] * k), 0.5f);
-            fin = true;
-        }
-    }
-    bool spec_event = false;
-#if SPT_COOP_BALL
-    const f3 rv_coop = coop_ball_vector(ps.st, scatter, lds);
-#else
-    (void)lds;
-#endif
-    if (scatter) {
-        // contact point + normal + cube-minus-ball vector, shared by the diffuse
-        // first hit (lines 23-26), the diffuse loop (30-33) and the mirror (41-43)
-        const float4 cs = hit[idx];
-        const f3 C = mk(cs.x, cs.y, cs.z);
-        ps.o = h.p;
-        const f3 nrm = normalize(sub(ps.o, C));
-#if SPT_COOP_BALL
-        f3 rv = rv_coop;
-#else
-        f3 rv = ball_vector(ps.st);
-#endif
-        f3 base;
-        if (dl) {
-            ps.c = mul(ps.c, 0.5f);
-            base = add(ps.o, nrm);  // origin + normal (+ rv), line 32
-        } else if (m == SPT_DIFFUSE_ID) {
-            const float4 sh = shade[idx];
-            ps.c = mk(sh.x * 0.5f, sh.y * 0.5f, sh.z * 0.5f);
-            base = nrm;
-            ps.phase = PH_DLOOP;
-        } else {
-            base = reflect(ps.d, nrm);
-            rv = mul(rv, shade[idx].w);
-            spec_event = true;
-        }
-        ps.d = normalize(add(base, rv));
-    }
-    if (refr) {
-        // SampleColorRefractive, lines 48-92
-        const float4 cs = hit[idx];
-        const f3 C = mk(cs.x, cs.y, cs.z);
-        ps.o = h.p;
-        const f3 nrm = normalize(sub(ps.o, C));
-        const f3 d = ps.d;
-        const float cc = dot(neg(nrm), d);
-        f3 nd;
-        if (uniform(ps.st, 0.f, 1.f) < schlick(kRsq, cc)) {
-            nd = reflect(d, nrm);
-        } else if (no_tir(kAirToGlass, cc)) {
-            const f3 d2 = refract_dir(d, nrm, kAirToGlass, cc);
-            // CalculateRaySphereFarthestContactPoint, Collision.hpp:29-37,58-65
-            const f3 rs = sub(C, ps.o);
-            const float tc = dot(rs, d2);
-            const float dd = lensq(rs) - tc * tc;
-            const float t = tc + __builtin_sqrtf(cs.w - dd);
-            ps.o = mk(ps.o.x + d2.x * t, ps.o.y + d2.y * t, ps.o.z + d2.z * t);
-            const f3 n2 = neg(normalize(sub(ps.o, C)));
-            const float c2 = dot(neg(n2), d2);
-            if (uniform(ps.st, 0.f, 1.f) < schlick(kRsq, c2))
-                nd = reflect(d2, n2);
-            else if (no_tir(kGlassToAir, c2))
-                nd = refract_dir(d2, n2, kGlassToAir, c2);
-            else
-                nd = reflect(d2, n2);
-        } else {
-            nd = reflect(d, nrm);
-        }
-        ps.d = nd;
-        spec_event = true;
-    }
-    if (spec_event) {
-        ++ps.spec;
-        if (a.mode == 1u && ps.spec >= kTaskPasses) {
-            // RenderSegmentTask: this path would be processed in pass 10, which never runs
-            fin = true;
-            counted = 0.f;
-            col = mk(0.f, 0.f, 0.f);
-            ++dropped;
-        } else if (ps.spec > kSpecularCap) {
-            fin = true;
-            col = mk(0.f, 0.f, 0.f);
-        }
-    }
-    if (fin) {
-        if (a.mode == 0u) {
-            // RenderSegment counts every sample: 12-byte slots
-            float *o3 = a.samples + (size_t)3 * ps.item;
-            o3[0] = col.x;
-            o3[1] = col.y;
-            o3[2] = col.z;
-        } else {
-            *(float4 *)(a.samples + (size_t)4 * ps.item) = make_float4(col.x, col.y, col.z, counted);
-        }
-        ps.phase = PH_IDLE;
-        ps.d = mk(0.f, 0.f, 0.f);
-        ++done;
-    }
-}
-
-}  // namespace
 
 #ifndef SPT_WAVES_PER_EU
 #define SPT_WAVES_PER_EU 0
@@ -559,49 +103,7 @@ __global__ __launch_bounds__(kRenderBlock) SPT_RENDER_ATTR void render_kernel(Re
                     blk_end = ne;
                 }
             }
-            if (ps.phase == PH_IDLE && mine != 0xFFFFFFFFu) {
-                // primary ray, SingleThreadPathTracer.hpp:123-130.  A claim of
-                // consecutive items stays inside one 8x8 tile (ts_item).
-#if SPT_TS_ORDER
-                uint32_t sl, lr, cx;
-                ts_item(mine, a.map.width, rows, a.spp_batch, sl, lr, cx);
-                const uint32_t s = a.s0 + sl;
-                ps.item = sl * a.npix + lr * a.map.width + cx;  // slot: [sample][row-major pixel]
-                const uint32_t x = a.map.x0 + cx;
-#elif SPT_TILE
-                const uint32_t sl = mine / a.npix;
-                const uint32_t s = a.s0 + sl;
-                uint32_t lr, cx;
-                tile_pixel(mine - sl * a.npix, a.map.width, rows, lr, cx);
-                ps.item = sl * a.npix + lr * a.map.width + cx;  // slot: [sample][row-major pixel]
-                const uint32_t x = a.map.x0 + cx;
-#else
-                const uint32_t sl = mine / a.npix;
-                const uint32_t s = a.s0 + sl;
-                const uint32_t pl = mine - sl * a.npix;
-                ps.item = mine;
-                const uint32_t lr = pl / a.map.width;
-                const uint32_t x = a.map.x0 + (pl - lr * a.map.width);
-#endif
-                const uint32_t y = a.map.parts == 1u ? a.map.y0 + lr : row_of(a.map, lr);
-                ps.st = fmix64(a.seed_key ^ (((uint64_t)(y * a.width + x) << 32) | (uint64_t)s));
-                const float un = (float)y + uniform(ps.st, -1.f, 1.f);
-                const float vn = (float)x + uniform(ps.st, -1.f, 1.f);
-                float u = div_core(un, rw), v = div_core(vn, rh);  // / g_width, / g_height
-                if (__builtin_expect(!(div_operand_ok(un) && div_operand_ok(vn)), 0)) {
-                    u = un / (float)a.width;
-                    v = vn / (float)a.height;
-                }
-                const float vx = -1.f + 2.f * v, vy = -1.f + 2.f * u;
-                const float *m = a.cam.view;
-                ps.d = normalize(mk((m[0] * vx + m[1] * vy) + (m[2] * 1.f + m[3] * 0.f),
-                                    (m[4] * vx + m[5] * vy) + (m[6] * 1.f + m[7] * 0.f),
-                                    (m[8] * vx + m[9] * vy) + (m[10] * 1.f + m[11] * 0.f)));
-                ps.o = eye;
-                ps.phase = PH_TRACE;
-                ps.bounce = a.bounces;
-                ps.spec = 0;
-            }
+            if (ps.phase == PH_IDLE && mine != 0xFFFFFFFFu) start_path(a, mine, rows, rw, rh, eye, ps);
         }
         const unsigned long long live = __ballot(ps.phase != PH_IDLE);
         if (live == 0ull) {

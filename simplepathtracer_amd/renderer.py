@@ -88,6 +88,10 @@ class Context:
         _native.TREE_AUTO = default heuristic); results identical."""
         self._check(_native.lib().spt_set_cluster_tree(self._h, int(branching)))
 
+    def set_engine(self, engine: int) -> None:
+        """_native.ENGINE_MEGAKERNEL (default) or _native.ENGINE_WAVEFRONT; results identical."""
+        self._check(_native.lib().spt_set_engine(self._h, int(engine)))
+
     def set_workspace(self, nbytes: int) -> None:
         self._check(_native.lib().spt_set_workspace(self._h, int(nbytes)))
 

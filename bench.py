@@ -78,9 +78,11 @@ def main():
     ap.add_argument("--engine", default="megakernel", choices=["megakernel", "wavefront"],
                     help="render loop: persistent megakernel, or the material-queue wavefront variant")
     ap.add_argument("--strip", type=int, default=0, help="rows per strip (0: largest of 8/4/2/1 splitting evenly)")
-    ap.add_argument("--streams", type=int, default=2,
+    ap.add_argument("--streams", type=int, default=0,
                     help="frames in flight on alternating HIP streams (the next frame fills the GPU while "
-                         "the previous one's last paths drain; each stream has its own workspace)")
+                         "the previous one's last paths drain; each stream has its own workspace); 0 = auto: "
+                         "2 when a frame is one workspace batch, else 1 (long multi-batch frames gain nothing "
+                         "and would double the workspace)")
     ap.add_argument("--cpu-spp", type=int, default=32, help="spp of the bounded CPU-baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -120,7 +122,9 @@ def main():
 
     from simplepathtracer_amd.distributed import FrameSplit, even_strip, render_frame
     split = FrameSplit(W, H, world, args.strip or even_strip(H, world))
-    nst = max(1, args.streams)
+    slot_bytes = 12 if args.mode == "segment" else 16
+    one_batch = W * H * spp * slot_bytes <= (4 << 30)  # the context's default workspace
+    nst = args.streams if args.streams > 0 else (2 if one_batch else 1)
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(nst - 1)]
     bufs = []
     for _ in range(nst):  # per-stream frame buffers: frames in flight do not share outputs

@@ -174,6 +174,8 @@ AccelTables build_accel(const float *centers4, const float *radii, uint32_t n, u
             nd.cz = cbf[2];
             nd.rb = round_up(rb);
             nd.k1 = round_up(1.15 * (double)nd.rb * (double)nd.rb + 1e-5);
+            const double cb2 = (double)cbf[0] * cbf[0] + (double)cbf[1] * cbf[1] + (double)cbf[2] * cbf[2];
+            nd.cb2 = (float)cb2;
         };
         // Preorder emission, once per direction octant: siblings are ordered front to
         // back along the octant's diagonal, so a wave walking the layout of its
@@ -213,9 +215,15 @@ AccelTables build_accel(const float *centers4, const float *radii, uint32_t n, u
                 t.nodes[me].skip = (uint32_t)(t.nodes.size() - base);
             };
             for (size_t j : ordered(top, 0, levels[top].size())) emit(emit, top, j);
+            if (levels.size() == 1)  // flat list: the rb field carries K1' (expanded line test)
+                for (size_t q = base; q < t.nodes.size(); ++q) {
+                    const AccelNode &nd = t.nodes[q];
+                    const double cbb = (double)nd.cx * nd.cx + (double)nd.cy * nd.cy + (double)nd.cz * nd.cz;
+                    t.nodes[q].rb = round_up((double)nd.k1 + 4e-6 * cbb);
+                }
             if (oct == 0) t.n_nodes = (uint32_t)t.nodes.size();
             // pad node (the kernel prefetches one node past the layout)
-            t.nodes.push_back(AccelNode{0.f, 0.f, 0.f, -INFINITY, t.n_nodes + 1, kNoSlot, 0.f, 0});
+            t.nodes.push_back(AccelNode{0.f, 0.f, 0.f, -INFINITY, t.n_nodes + 1, kNoSlot, -INFINITY, 0.f});
         }
     }
     // the kernel prefetches one always-group past the list and one node past the tree
@@ -224,7 +232,7 @@ AccelTables build_accel(const float *centers4, const float *radii, uint32_t n, u
         t.orig.push_back(0xFFFFFFFFu);
     }
     if (t.nodes.empty())  // no tree: one pad record per octant layout (n_nodes = 0)
-        for (int oct = 0; oct < 8; ++oct) t.nodes.push_back(AccelNode{0.f, 0.f, 0.f, -INFINITY, 1, kNoSlot, 0.f, 0});
+        for (int oct = 0; oct < 8; ++oct) t.nodes.push_back(AccelNode{0.f, 0.f, 0.f, -INFINITY, 1, kNoSlot, -INFINITY, 0.f});
     return t;
 }
 
@@ -271,7 +279,13 @@ std::string validate_accel(const AccelTables &t, const float *centers4, const fl
                     return bad("layout %u node %u: leaf slot %u out of range", oct, i, nd.slot);
             }
             // containment of every member below: |Cm - Cb| + r <= Rb and 1.15 Rb^2 + 1e-5 <= K1
-            if (!((double)nd.k1 >= 1.15 * (double)nd.rb * (double)nd.rb + 1e-5))
+            // (flat lists: |Cm - Cb| + r <= sqrt((K1 - 1e-5) / 1.15) and K1' >= K1 + 4e-6 |Cb|^2)
+            const bool flat = t.n_nodes == t.leaves;
+            const double cbb = (double)nd.cx * nd.cx + (double)nd.cy * nd.cy + (double)nd.cz * nd.cz;
+            if (flat && !(std::fabs((double)nd.cb2 - cbb) <= 2e-7 * cbb && (double)nd.rb >= (double)nd.k1 + 4e-6 * cbb))
+                return bad("layout %u node %u: flat-list |Cb|^2 or K1' wrong", oct, i);
+            const double rbound = flat ? std::sqrt(std::max(0.0, ((double)nd.k1 - 1e-5) / 1.15)) : (double)nd.rb;
+            if (!flat && !((double)nd.k1 >= 1.15 * (double)nd.rb * (double)nd.rb + 1e-5))
                 return bad("layout %u node %u: K1 below 1.15 Rb^2 + 1e-5", oct, i);
             for (uint32_t q = i; q < nd.skip; ++q) {
                 if (L[q].slot == kNoSlot) continue;
@@ -284,7 +298,7 @@ std::string validate_accel(const AccelTables &t, const float *centers4, const fl
                         const double dd = (double)centers4[4 * o + c] - cb[c];
                         d2 += dd * dd;
                     }
-                    if (!(std::sqrt(d2) + std::fabs((double)radii[o]) <= (double)nd.rb))
+                    if (!(std::sqrt(d2) + std::fabs((double)radii[o]) <= rbound))
                         return bad("layout %u node %u: sphere %u not contained", oct, i, o);
                 }
             }

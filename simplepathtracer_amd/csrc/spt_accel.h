@@ -18,8 +18,9 @@ struct AccelNode {
     float k1;          // cull constant K1 = 1.15 Rb^2 + 1e-5 (rounded up)
     uint32_t skip;     // next node when this one is culled (or is a leaf)
     uint32_t slot;     // leaf: first of its leaf_slots slots; inner: kNoSlot
-    float rb;          // bounding radius Rb (rounded up)
-    uint32_t pad;
+    float rb;          // tree nodes: bounding radius Rb (rounded up);
+                       // flat lists: K1' = K1 + 4e-6 |Cb|^2 (rounded up), the expanded-form margin
+    float cb2;         // |Cb|^2 (flat lists' expanded line test)
 };
 
 struct AccelTables {

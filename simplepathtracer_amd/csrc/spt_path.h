@@ -177,22 +177,32 @@ __device__ __forceinline__ Hit find_closest(const AccelView &ac, const f3 &o, co
     cuint *nodes = (cuint *)ac.nodes;
     if (!TREE) {
 #if !SPT_FLAT_FULL
-        // flat list: node i is leaf i; bound prefetched one node ahead (pad record)
-        constexpr int kNb = 6;
+        // flat list: node i is leaf i; record prefetched one node ahead (pad record).
+        // The line test in expanded form, with FMAs (a conservative test need not
+        // follow the reference's operation order):
+        //   tcb  = Cb.d - o.d,   |Cb-o|^2 = |Cb|^2 - 2 Cb.o + |o|^2,   d2b = |Cb-o|^2 - tcb^2
+        // keep iff d2b <= K1 + 1e-4 |Cb-o|^2 + 4e-6 (|Cb|^2 + |o|^2): the absolute
+        // term covers the expansion's cancellation (<= 2.4e-6 (|Cb|^2 + |o|^2)).
+        // 13 VALU per node instead of 17.
+        const float oo = lensq(o);
+        const float eo = 4.1e-6f * oo;
+        constexpr int kNb = 8;
         uint32_t nb[kNb];
 #pragma unroll
         for (int q = 0; q < kNb; ++q) nb[q] = nodes[q];
         for (uint32_t i = 0; i < ac.n_nodes; ++i) {
             const float bx = __uint_as_float(nb[0]), by = __uint_as_float(nb[1]), bz = __uint_as_float(nb[2]);
-            const float k1 = __uint_as_float(nb[3]);
+            const float k1p = __uint_as_float(nb[6]), cb2 = __uint_as_float(nb[7]);  // K1' = K1 + 4e-6 |Cb|^2
             const uint32_t leaf_slot = nb[5];
 #pragma unroll
             for (int q = 0; q < kNb; ++q) nb[q] = nodes[8 * (i + 1) + q];
-            const f3 ocb = mk(bx - o.x, by - o.y, bz - o.z);
-            const float tcb = dot(ocb, d);
-            const float occb = lensq(ocb);
-            const float d2b = occb - tcb * tcb;
-            const unsigned long long mm = (__ballot(d2b <= k1 + 1e-4f * occb) & live_mask) | nocull_mask;
+            const float cbd = __builtin_fmaf(bx, d.x, __builtin_fmaf(by, d.y, bz * d.z));
+            const float cbo = __builtin_fmaf(bx, o.x, __builtin_fmaf(by, o.y, bz * o.z));
+            const float tcb = cbd - dod;
+            const float occb = __builtin_fmaf(-2.f, cbo, cb2) + oo;
+            const float d2b = __builtin_fmaf(-tcb, tcb, occb);
+            const float thr = __builtin_fmaf(1e-4f, occb, k1p) + eo;
+            const unsigned long long mm = (__ballot(d2b <= thr) & live_mask) | nocull_mask;
             if (SPT_DIAG) {
                 dg.nodes += 1;
                 dg.leaves += mm != 0ull ? 1 : 0;

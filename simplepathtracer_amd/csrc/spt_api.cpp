@@ -311,6 +311,8 @@ int render_impl(spt_ctx *ctx, int mode, const spt::RowMap &map, float4 *d_rgba, 
         ra.spp_batch = b;
         ra.s0 = s0;
         ra.n_items = npix * b;
+        ra.div_band = spt::make_fastdiv(rows >= 8 ? 8u * map.width * b : 1u);
+        ra.div_tile = spt::make_fastdiv(64u * b);
         EventPair ev = get_pair(ctx);
         if (ctx->engine == SPT_ENGINE_WAVEFRONT) {
             // queue passes until every item is issued and the queue has drained; the

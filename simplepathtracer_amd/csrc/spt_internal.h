@@ -70,24 +70,51 @@ __host__ __device__ inline void tile_pixel(uint32_t q, uint32_t width, uint32_t 
     col = c;
 }
 
+// Division of x < 2^31 by a divisor d >= 1 fixed for a launch (Granlund-Montgomery,
+// N = 31 bits): l = ceil(log2 d), m = floor(2^(31+l) / d) + 1 < 2^32, and
+// x / d == mulhi(x, m) >> (l - 1) for every x < 2^31; d == 1 passes x through.
+struct FastDiv {
+    uint32_t d, m, s;
+};
+inline FastDiv make_fastdiv(uint32_t d)
+{
+    FastDiv f{d, 0u, 0u};
+    if (d <= 1u) return f;
+    uint32_t l = 0;
+    while ((1ull << l) < d) ++l;
+    f.m = (uint32_t)(((1ull << (31 + l)) / d) + 1ull);
+    f.s = l - 1u;
+    return f;
+}
+__host__ __device__ inline uint32_t fast_div(uint32_t x, const FastDiv &f)
+{
+#ifdef __HIP_DEVICE_COMPILE__
+    const uint32_t hi = __umulhi(x, f.m);
+#else
+    const uint32_t hi = (uint32_t)(((uint64_t)x * f.m) >> 32);
+#endif
+    return f.d <= 1u ? x : hi >> f.s;
+}
+
 // (sample, pixel) of the q-th item of a batch of S samples over a region of
 // `rows` x `width` pixels, items ordered [8-row band][8-column tile][sample]
 // [pixel in tile] (ragged tiles at the right and bottom edges).  A claim of
 // consecutive items then stays inside one 8x8 tile across several samples, so a
 // wave's rays start close together whatever the claim size.  Full tiles use
 // shifts; only edge tiles divide.  Bijective on [0, rows*width*S) (host test).
-__host__ __device__ inline void ts_item(uint32_t q, uint32_t width, uint32_t rows, uint32_t S, uint32_t &sl,
-                                        uint32_t &lr, uint32_t &col)
+// div_band = FastDiv(8*width*S) (unused when rows < 8), div_tile = FastDiv(64*S).
+__host__ __device__ inline void ts_item(uint32_t q, uint32_t width, uint32_t rows, uint32_t S, const FastDiv &div_band,
+                                        const FastDiv &div_tile, uint32_t &sl, uint32_t &lr, uint32_t &col)
 {
     // 8*width*S <= rows*width*S < 2^31 whenever rows >= 8; a single band otherwise
-    const uint32_t band = rows >= 8u ? q / (8u * width * S) : 0u;
+    const uint32_t band = rows >= 8u ? fast_div(q, div_band) : 0u;
     const uint32_t h = rows - (band << 3) < 8u ? rows - (band << 3) : 8u;
     const uint32_t qb = q - band * 8u * width * S;
     const uint32_t ft = width >> 3, wr = width & 7u;
     const uint32_t ti = h * 8u * S;  // items of a full-width tile of this band
     uint32_t e, wt, c0;
     if (h == 8u) {
-        const uint32_t t = qb / (64u * S);
+        const uint32_t t = fast_div(qb, div_tile);
         if (t < ft) {
             e = qb - t * 64u * S;
             sl = e >> 6;
@@ -152,6 +179,7 @@ struct RenderArgs {
     uint32_t s0;         // first sample index of the batch
     uint32_t n_items;    // npix * spp_batch
     uint32_t claim;      // items per queue claim
+    FastDiv div_band, div_tile;  // ts_item divisors 8*width*spp_batch and 64*spp_batch
     float *samples;      // [n_items] per-sample colour: {r, g, b} (segment mode) or {r, g, b, counted} (task mode)
     uint32_t slot_floats;  // 3 or 4
     uint32_t *head;      // queue head (zeroed before launch)

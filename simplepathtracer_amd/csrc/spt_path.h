@@ -483,7 +483,7 @@ __device__ __forceinline__ void start_path(const RenderArgs &a, uint32_t mine, u
     // consecutive items stays inside one 8x8 tile (ts_item).
 #if SPT_TS_ORDER
     uint32_t sl, lr, cx;
-    ts_item(mine, a.map.width, rows, a.spp_batch, sl, lr, cx);
+    ts_item(mine, a.map.width, rows, a.spp_batch, a.div_band, a.div_tile, sl, lr, cx);
     const uint32_t s = a.s0 + sl;
     ps.item = sl * a.npix + lr * a.map.width + cx;  // slot: [sample][row-major pixel]
     const uint32_t x = a.map.x0 + cx;

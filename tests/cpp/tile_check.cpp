@@ -2,6 +2,7 @@
 // ([sample][tile][pixel]) and spt::ts_item ([band][tile][sample][pixel]) are
 // bijections onto the region (x samples) for every shape in a range plus the
 // config sizes, and full 8x8 tiles are contiguous runs of 64 items.  Exit 0 = pass.
+#include <algorithm>
 #include <cstdio>
 #include <vector>
 
@@ -47,10 +48,11 @@ int main()
     for (uint32_t S = 1; S <= 5; S += 2)
         for (uint32_t rows = 1; rows <= 27; ++rows)
             for (uint32_t width = 1; width <= 35; ++width) {
+                const spt::FastDiv fb = spt::make_fastdiv(rows >= 8 ? 8 * width * S : 1), ft = spt::make_fastdiv(64 * S);
                 std::vector<int> seen((size_t)rows * width * S, 0);
                 for (uint32_t q = 0; q < rows * width * S; ++q) {
                     uint32_t sl, lr, col;
-                    spt::ts_item(q, width, rows, S, sl, lr, col);
+                    spt::ts_item(q, width, rows, S, fb, ft, sl, lr, col);
                     if (sl >= S || lr >= rows || col >= width || seen[((size_t)sl * rows + lr) * width + col]++) {
                         std::printf("FAIL ts rows=%u width=%u S=%u q=%u -> (%u, %u, %u)\n", rows, width, S, q, sl, lr, col);
                         return 1;
@@ -58,7 +60,7 @@ int main()
                     // full tiles: 64 consecutive items are the 64 pixels of one tile and sample
                     if (rows % 8 == 0 && width % 8 == 0) {
                         uint32_t s0, l0, c0;
-                        spt::ts_item(q & ~63u, width, rows, S, s0, l0, c0);
+                        spt::ts_item(q & ~63u, width, rows, S, fb, ft, s0, l0, c0);
                         if (s0 != sl || lr / 8 != l0 / 8 || col / 8 != c0 / 8) {
                             std::printf("FAIL ts run rows=%u width=%u S=%u q=%u\n", rows, width, S, q);
                             return 1;
@@ -70,14 +72,40 @@ int main()
         const uint32_t shapes[][3] = {{800, 1200, 4}, {101, 1201, 3}, {1080, 1920, 2}, {7, 1200, 9}};
         for (auto &sh : shapes) {
             const uint32_t rows = sh[0], width = sh[1], S = sh[2];
+            const spt::FastDiv fb = spt::make_fastdiv(rows >= 8 ? 8 * width * S : 1), ft = spt::make_fastdiv(64 * S);
             std::vector<unsigned char> seen((size_t)rows * width * S, 0);
             for (uint32_t q = 0; q < rows * width * S; ++q) {
                 uint32_t sl, lr, col;
-                spt::ts_item(q, width, rows, S, sl, lr, col);
+                spt::ts_item(q, width, rows, S, fb, ft, sl, lr, col);
                 if (sl >= S || lr >= rows || col >= width || seen[((size_t)sl * rows + lr) * width + col]++) {
                     std::printf("FAIL ts rows=%u width=%u S=%u q=%u\n", rows, width, S, q);
                     return 1;
                 }
+            }
+        }
+    }
+    // FastDiv == plain division for x < 2^31 (edges, powers of two, random)
+    {
+        uint64_t z = 0x9E3779B97F4A7C15ull;
+        auto rnd = [&]() { z ^= z << 13; z ^= z >> 7; z ^= z << 17; return z; };
+        const uint32_t ds[] = {1, 2, 3, 5, 7, 63, 64, 65, 100, 640, 6400, 76800, 76801, 65536, 0x7FFFFFFF, 0x40000000, 12345677};
+        for (uint32_t d : ds) {
+            const spt::FastDiv f = spt::make_fastdiv(d);
+            for (uint32_t k = 0; k < 200000; ++k) {
+                uint32_t x = (uint32_t)(rnd() & 0x7FFFFFFF);
+                if (k < 64) x = k < 32 ? k : 0x7FFFFFFFu - (k - 32);
+                if (k >= 64 && k < 128) x = (uint32_t)std::min<uint64_t>(0x7FFFFFFFu, (uint64_t)d * (k - 64) + (k & 1 ? d - 1 : 0));
+                if (spt::fast_div(x, f) != x / d) {
+                    std::printf("FAIL fast_div %u / %u\n", x, d);
+                    return 1;
+                }
+            }
+        }
+        for (uint32_t k = 0; k < 2000000; ++k) {
+            const uint32_t d = (uint32_t)(rnd() % 0x7FFFFFFF) + 1, x = (uint32_t)(rnd() & 0x7FFFFFFF);
+            if (spt::fast_div(x, spt::make_fastdiv(d)) != x / d) {
+                std::printf("FAIL fast_div %u / %u\n", x, d);
+                return 1;
             }
         }
     }

@@ -177,8 +177,7 @@ __device__ __forceinline__ Hit find_closest(const AccelView &ac, const f3 &o, co
     cuint *nodes = (cuint *)ac.nodes;
     if (!TREE) {
 #if !SPT_FLAT_FULL
-        // flat list: node i is leaf i; record prefetched one node ahead (pad record).
-        // The line test in expanded form, with FMAs (a conservative test need not
+        // flat list: node i is leaf i.  The line test in expanded form, with FMAs (a conservative test need not
         // follow the reference's operation order):
         //   tcb  = Cb.d - o.d,   |Cb-o|^2 = |Cb|^2 - 2 Cb.o + |o|^2,   d2b = |Cb-o|^2 - tcb^2
         // keep iff d2b <= K1 + 1e-4 |Cb-o|^2 + 4e-6 (|Cb|^2 + |o|^2): the absolute
@@ -186,30 +185,39 @@ __device__ __forceinline__ Hit find_closest(const AccelView &ac, const f3 &o, co
         // 13 VALU per node instead of 17.
         const float oo = lensq(o);
         const float eo = 4.1e-6f * oo;
-        constexpr int kNb = 8;
-        uint32_t nb[kNb];
-#pragma unroll
-        for (int q = 0; q < kNb; ++q) nb[q] = nodes[q];
-        for (uint32_t i = 0; i < ac.n_nodes; ++i) {
-            const float bx = __uint_as_float(nb[0]), by = __uint_as_float(nb[1]), bz = __uint_as_float(nb[2]);
-            const float k1p = __uint_as_float(nb[6]), cb2 = __uint_as_float(nb[7]);  // K1' = K1 + 4e-6 |Cb|^2
-            const uint32_t leaf_slot = nb[5];
-#pragma unroll
-            for (int q = 0; q < kNb; ++q) nb[q] = nodes[8 * (i + 1) + q];
+        auto line_mask = [&](const uint32_t *r) {
+            const float bx = __uint_as_float(r[0]), by = __uint_as_float(r[1]), bz = __uint_as_float(r[2]);
+            const float k1p = __uint_as_float(r[6]), cb2 = __uint_as_float(r[7]);  // K1' = K1 + 4e-6 |Cb|^2
             const float cbd = __builtin_fmaf(bx, d.x, __builtin_fmaf(by, d.y, bz * d.z));
             const float cbo = __builtin_fmaf(bx, o.x, __builtin_fmaf(by, o.y, bz * o.z));
             const float tcb = cbd - dod;
             const float occb = __builtin_fmaf(-2.f, cbo, cb2) + oo;
             const float d2b = __builtin_fmaf(-tcb, tcb, occb);
             const float thr = __builtin_fmaf(1e-4f, occb, k1p) + eo;
-            const unsigned long long mm = (__ballot(d2b <= thr) & live_mask) | nocull_mask;
+            return (__ballot(d2b <= thr) & live_mask) | nocull_mask;
+        };
+        auto diag_node = [&](unsigned long long mm) {
             if (SPT_DIAG) {
                 dg.nodes += 1;
                 dg.leaves += mm != 0ull ? 1 : 0;
                 dg.pairs += (unsigned long long)__popcll(mm);
                 dg.live += mm != 0ull ? (unsigned long long)__popcll(live_mask) : 0ull;
             }
-            if (mm != 0ull) test_leaf<LEAF>(slots, ac.orig, leaf_slot, o, d, dod, h);
+        };
+        // flat list: node i is leaf i; record prefetched one node ahead (pad record).
+        uint32_t nb[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) nb[q] = nodes[q];
+        for (uint32_t i = 0; i < ac.n_nodes; ++i) {
+            uint32_t r[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                r[q] = nb[q];
+                nb[q] = nodes[8 * (i + 1) + q];
+            }
+            const unsigned long long mm = line_mask(r);
+            diag_node(mm);
+            if (mm != 0ull) test_leaf<LEAF>(slots, ac.orig, r[5], o, d, dod, h);
         }
         return h;
 #endif

@@ -32,11 +32,6 @@
 #define SPT_TILE 1
 #endif
 
-// 1: flat cluster lists use the tree walk's three tests too (A/B switch)
-#ifndef SPT_FLAT_FULL
-#define SPT_FLAT_FULL 0
-#endif
-
 #pragma clang fp contract(off)
 
 namespace spt {
@@ -176,9 +171,9 @@ __device__ __forceinline__ Hit find_closest(const AccelView &ac, const f3 &o, co
     const unsigned long long nocull_mask = __ballot(no_cull);
     cuint *nodes = (cuint *)ac.nodes;
     if (!TREE) {
-#if !SPT_FLAT_FULL
-        // flat list: node i is leaf i.  The line test in expanded form, with FMAs (a conservative test need not
-        // follow the reference's operation order):
+        // flat list: node i is leaf i.  The line test in expanded form, with FMAs
+        // (a conservative test need not follow the reference's operation order;
+        // DESIGN.md §4.4):
         //   tcb  = Cb.d - o.d,   |Cb-o|^2 = |Cb|^2 - 2 Cb.o + |o|^2,   d2b = |Cb-o|^2 - tcb^2
         // keep iff d2b <= K1 + 1e-4 |Cb-o|^2 + 4e-6 (|Cb|^2 + |o|^2): the absolute
         // term covers the expansion's cancellation (<= 2.4e-6 (|Cb|^2 + |o|^2)).
@@ -220,7 +215,6 @@ __device__ __forceinline__ Hit find_closest(const AccelView &ac, const f3 &o, co
             if (mm != 0ull) test_leaf<LEAF>(slots, ac.orig, r[5], o, d, dod, h);
         }
         return h;
-#endif
     }
     const float olen = __builtin_amdgcn_sqrtf(lensq(o));  // |o|, for the distance margin
     if (TREE) {

@@ -29,8 +29,13 @@ namespace spt {
 #ifndef SPT_WAVES_PER_EU
 #define SPT_WAVES_PER_EU 0
 #endif
+#ifndef SPT_NUM_SGPR
+#define SPT_NUM_SGPR 0
+#endif
 #if SPT_WAVES_PER_EU
 #define SPT_RENDER_ATTR __attribute__((amdgpu_waves_per_eu(SPT_WAVES_PER_EU, SPT_WAVES_PER_EU)))
+#elif SPT_NUM_SGPR
+#define SPT_RENDER_ATTR __attribute__((amdgpu_num_sgpr(SPT_NUM_SGPR)))
 #else
 #define SPT_RENDER_ATTR
 #endif

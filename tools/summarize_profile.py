@@ -9,7 +9,7 @@ import sys
 src, dst = sys.argv[1], sys.argv[2]
 out = [f"# rocprofv3 summary: {os.path.basename(src)}\n",
        "Command: `tools/profile.sh` = rocprofv3 --kernel-trace --stats and four separate --pmc passes over "
-       "`python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline` (config 2, 1x MI355X).\n",
+       "`python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --streams 1` (config 2, 1x MI355X, one frame in flight so per-kernel durations are not stretched by overlap).\n",
        "## Kernel trace (--kernel-trace --stats)\n", "| kernel | calls | avg ms | min ms | max ms | % |",
        "|---|---|---|---|---|---|"]
 for r in csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv"))):

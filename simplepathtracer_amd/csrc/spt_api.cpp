@@ -53,6 +53,7 @@ struct spt_ctx {
     std::string err;
     int num_cu = 0;
     uint32_t grid = 0, block = spt::kRenderBlock, claim = 0;  // 0 = per launch (claim_size)
+    uint32_t claims_per_wave = 2;                              // render_grid (config 1: 2 > 1, 4)
 
     // scene (Globals.hpp:31-37)
     float4 *d_shade = nullptr, *d_slots = nullptr;
@@ -198,6 +199,17 @@ uint32_t claim_size(const spt_ctx *ctx, uint64_t items)
     return (uint32_t)std::min<uint64_t>(256, std::max<uint64_t>(64, fair / 64 * 64));
 }
 
+// Blocks of one render launch: the occupancy-sized persistent grid, or fewer when
+// the launch has fewer claims than that grid has waves.  A wave without a claim
+// only starts, finds the counter exhausted and exits, and on config 1 (1250
+// claims, 8192 waves) those waves tripled the launch time.
+uint32_t render_grid(const spt_ctx *ctx, uint64_t items, uint32_t claim)
+{
+    const uint64_t claims = (items + claim - 1) / claim;
+    const uint64_t per_block = (uint64_t)(ctx->block / 64) * ctx->claims_per_wave;
+    return (uint32_t)std::min<uint64_t>(ctx->grid, std::max<uint64_t>(1, (claims + per_block - 1) / per_block));
+}
+
 // The workspace of stream s (created on first use, at most kMaxWorkspaces).
 Workspace *workspace_for(spt_ctx *ctx, hipStream_t s)
 {
@@ -335,7 +347,7 @@ int render_impl(spt_ctx *ctx, int mode, const spt::RowMap &map, float4 *d_rgba, 
         } else {
             HIP_TRY(ctx, hipMemsetAsync(w->d_head, 0, sizeof(uint32_t), s));
             HIP_TRY(ctx, hipEventRecord(ev.a, s));
-            HIP_TRY(ctx, spt::launch_render(ra, ctx->grid, ctx->block, s));
+            HIP_TRY(ctx, spt::launch_render(ra, render_grid(ctx, ra.n_items, ra.claim), ctx->block, s));
             HIP_TRY(ctx, hipEventRecord(ev.b, s));
         }
         ctx->pending_render.push_back(ev);
@@ -495,6 +507,7 @@ int spt_ctx_create(int device, spt_ctx **out)
     if (const char *e = std::getenv("SPT_CLAIM")) ctx->claim = (uint32_t)std::max(1, std::atoi(e));
     if (const char *e = std::getenv("SPT_CLUSTER_K")) ctx->cluster_k = (uint32_t)std::max(0, std::atoi(e));
     if (const char *e = std::getenv("SPT_TREE_B")) ctx->tree_branching = (uint32_t)std::max(0, std::atoi(e));
+    if (const char *e = std::getenv("SPT_CLAIMS_PER_WAVE")) ctx->claims_per_wave = (uint32_t)std::max(1, std::atoi(e));
     if (const char *e = std::getenv("SPT_WF_CAP")) ctx->wf_cap = (uint32_t)std::max(1024, std::atoi(e));
     ctx->grid = (uint32_t)(per_cu * ctx->num_cu);
     if (hipMalloc((void **)&ctx->d_counters, 12 * sizeof(unsigned long long)) != hipSuccess ||

@@ -29,8 +29,10 @@ namespace spt {
 #ifndef SPT_WAVES_PER_EU
 #define SPT_WAVES_PER_EU 0
 #endif
+// 80 SGPRs (with SPT_KERNARG_RELOAD) lets 8 waves per SIMD be resident instead of
+// 6 at the uncapped 106; 0 = no cap
 #ifndef SPT_NUM_SGPR
-#define SPT_NUM_SGPR 0
+#define SPT_NUM_SGPR 80
 #endif
 #if SPT_WAVES_PER_EU
 #define SPT_RENDER_ATTR __attribute__((amdgpu_waves_per_eu(SPT_WAVES_PER_EU, SPT_WAVES_PER_EU)))
@@ -51,6 +53,9 @@ __global__ __launch_bounds__(kRenderBlock) SPT_RENDER_ATTR void render_kernel(Re
     // shared reciprocals of the primary-ray divisors (div_core range: 1 <= W, H <= 2^32)
     const Recip rw = recip((float)a.width), rh = recip((float)a.height);
     (void)rows;
+    (void)rw;
+    (void)rh;
+    (void)eye;
 
     __shared__ uint32_t s_lds[kRenderBlock];  // wave-private scratch of the cooperative sampler
     Path ps;
@@ -108,7 +113,13 @@ __global__ __launch_bounds__(kRenderBlock) SPT_RENDER_ATTR void render_kernel(Re
                     blk_end = ne;
                 }
             }
-            if (ps.phase == PH_IDLE && mine != 0xFFFFFFFFu) start_path(a, mine, rows, rw, rh, eye, ps);
+            if (ps.phase == PH_IDLE && mine != 0xFFFFFFFFu) {
+#if SPT_KERNARG_RELOAD && defined(__HIP_DEVICE_COMPILE__)
+                start_path_kernarg(mine, rows, ps);
+#else
+                start_path(a, mine, rows, rw, rh, eye, ps);
+#endif
+            }
         }
         const unsigned long long live = __ballot(ps.phase != PH_IDLE);
         if (live == 0ull) {
@@ -126,10 +137,18 @@ __global__ __launch_bounds__(kRenderBlock) SPT_RENDER_ATTR void render_kernel(Re
         SPT_STAMP(d_cyc_shade);
     }
 
-    // per-lane done/dropped -> wave sums via atomics from every lane that has any
-    if (done) atomicAdd(&a.counters[1], done);
-    if (dropped) atomicAdd(&a.counters[2], dropped);
-    if (lane == 0) atomicAdd(&a.counters[0], casts);
+    // per-lane done/dropped -> wave sums (butterfly), one atomic per counter and wave
+    // (same-address atomics from every lane cost a launch ~10%; see render_grid)
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        done += __shfl_xor(done, o);
+        dropped += __shfl_xor(dropped, o);
+    }
+    if (lane == 0) {
+        if (casts) atomicAdd(&a.counters[0], casts);
+        if (done) atomicAdd(&a.counters[1], done);
+        if (dropped) atomicAdd(&a.counters[2], dropped);
+    }
 #if SPT_DIAG
     if (lane == 0) {
         atomicAdd(&a.counters[4], d_iters);

@@ -18,6 +18,13 @@
 #define SPT_DIAG 0
 #endif
 
+// 1: the megakernel's start_path reads its parameters from the kernarg segment
+// where used instead of holding them in SGPRs (with the 80-SGPR cap of
+// spt_kernels.hip: 8 resident waves per SIMD instead of 6)
+#ifndef SPT_KERNARG_RELOAD
+#define SPT_KERNARG_RELOAD 1
+#endif
+
 // 1: the cube-minus-ball rejection loop runs cooperatively across the wave
 #ifndef SPT_COOP_BALL
 #define SPT_COOP_BALL 1
@@ -478,6 +485,21 @@ __device__ __forceinline__ void shade_step(const RenderArgs &a, Path &ps, const 
 // Start the path of batch item `mine`: its (pixel, sample), keyed RNG stream and
 // primary ray (SingleThreadPathTracer.hpp:123-130).  rw, rh: shared reciprocals
 // of g_width, g_height (div_core); `rows` = rows of the region.
+#if defined(__HIP_DEVICE_COMPILE__)
+// The kernel's RenderArgs in the kernarg segment, behind an opaque zero offset: the
+// refill-only fields read through it are loaded (scalar cache) where they are used
+// instead of being hoisted into SGPRs for the kernel's lifetime.  Only valid in a
+// kernel whose first argument is a RenderArgs (render_kernel: start_path<true>).
+typedef __attribute__((address_space(4))) const RenderArgs kargs_t;
+__device__ __forceinline__ kargs_t *kernarg_args()
+{
+    uint32_t z;
+    asm volatile("s_mov_b32 %0, 0" : "=s"(z));
+    typedef __attribute__((address_space(4))) const char kchar;
+    return (kargs_t *)((kchar *)__builtin_amdgcn_kernarg_segment_ptr() + z);
+}
+#endif
+
 __device__ __forceinline__ void start_path(const RenderArgs &a, uint32_t mine, uint32_t rows, const Recip &rw,
                                            const Recip &rh, const f3 &eye, Path &ps)
 {
@@ -523,6 +545,30 @@ __device__ __forceinline__ void start_path(const RenderArgs &a, uint32_t mine, u
     ps.bounce = a.bounces;
     ps.spec = 0;
 }
+
+#if defined(__HIP_DEVICE_COMPILE__)
+// start_path with the refill parameters copied out of the kernarg segment at the
+// point of use (scalar loads); render_kernel only.
+__device__ __forceinline__ void start_path_kernarg(uint32_t mine, uint32_t rows, Path &ps)
+{
+    kargs_t &k = *kernarg_args();
+    RenderArgs a;
+    a.map = RowMap{k.map.y0, k.map.y1, k.map.strip, k.map.parts, k.map.part, k.map.x0, k.map.width};
+    a.width = k.width;
+    a.height = k.height;
+    a.bounces = k.bounces;
+    a.npix = k.npix;
+    a.spp_batch = k.spp_batch;
+    a.s0 = k.s0;
+    a.seed_key = k.seed_key;
+    a.div_band = FastDiv{k.div_band.d, k.div_band.m, k.div_band.s};
+    a.div_tile = FastDiv{k.div_tile.d, k.div_tile.m, k.div_tile.s};
+#pragma unroll
+    for (int q = 0; q < 12; ++q) a.cam.view[q] = k.cam.view[q];
+    start_path(a, mine, rows, recip((float)a.width), recip((float)a.height),
+               mk(k.cam.eye[0], k.cam.eye[1], k.cam.eye[2]), ps);
+}
+#endif
 
 }  // namespace
 }  // namespace spt

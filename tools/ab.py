@@ -21,8 +21,10 @@ torch.cuda.init()
 from simplepathtracer_amd import _native  # noqa: E402
 import simplepathtracer_amd as spt  # noqa: E402
 
-W, H, SPP, B = {"c2": (1200, 800, 100, 50), "c3s": (3840, 2160, 16, 50), "c5s": (1920, 1080, 4, 50)}[args.config]
-scene = spt.generate_stress(1, 10000) if args.config.startswith("c5") else spt.generate_spheres(1)
+W, H, SPP, B = {"c1": (200, 100, 4, 8), "c2": (1200, 800, 100, 50), "c3s": (3840, 2160, 16, 50),
+                "c5s": (1920, 1080, 4, 50)}[args.config]
+scene = (spt.generate_stress(1, 10000) if args.config.startswith("c5")
+         else spt.cornell3() if args.config == "c1" else spt.generate_spheres(1))
 view = spt.camera_basis()
 P = ctypes.c_void_p
 ctxs = []
@@ -38,7 +40,7 @@ for name in args.libs:
             os.environ[var] = val
         else:
             os.environ.pop(var, None)
-    L = ctypes.CDLL(os.path.join(ROOT, "simplepathtracer_amd", "lib", libname))
+    L = ctypes.CDLL(os.path.join(ROOT, "simplepathtracer_amd", "lib", os.path.basename(libname)))
     L.spt_ctx_create.argtypes = [ctypes.c_int, P]
     L.spt_set_scene.argtypes = [P, P, P, P, P, P, ctypes.c_uint32]
     L.spt_set_camera.argtypes = [P, P, P, P]

@@ -4,7 +4,7 @@
 set -o pipefail
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 TAG=${1:-prof}; shift || true
-ARGS=${@:-"--steps 3 --warmup 1 --no-cpu-baseline --streams 1"}
+ARGS=${@:-"--steps 12 --warmup 4 --no-cpu-baseline --streams 1"}
 OUT="$R/gpurun_out/$TAG"
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp

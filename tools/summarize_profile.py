@@ -7,14 +7,28 @@ import os
 import sys
 
 src, dst = sys.argv[1], sys.argv[2]
+timed = int(sys.argv[3]) if len(sys.argv) > 3 else 12  # bench --steps of the profiled run
 out = [f"# rocprofv3 summary: {os.path.basename(src)}\n",
        "Command: `tools/profile.sh` = rocprofv3 --kernel-trace --stats and four separate --pmc passes over "
-       "`python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --streams 1` (config 2, 1x MI355X, one frame in flight so per-kernel durations are not stretched by overlap).\n",
+       f"`python3 bench.py --steps {timed} --warmup 4 --no-cpu-baseline --streams 1` (config 2, 1x MI355X, one frame in flight so per-kernel durations are not stretched by overlap).\n",
        "## Kernel trace (--kernel-trace --stats)\n", "| kernel | calls | avg ms | min ms | max ms | % |",
        "|---|---|---|---|---|---|"]
 for r in csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv"))):
     out.append(f"| `{r['Name'][:60]}` | {r['Calls']} | {float(r['AverageNs'])/1e6:.4f} | "
                f"{float(r['MinNs'])/1e6:.4f} | {float(r['MaxNs'])/1e6:.4f} | {float(r['Percentage']):.2f} |")
+# the timed launches only (the last `timed` of each spt kernel): clocks ramp over the
+# warmup launches, and bench.py's HIP-event average covers the timed ones
+trace = os.path.join(src, "trace", "run_kernel_trace.csv")
+if os.path.exists(trace):
+    per = collections.defaultdict(list)
+    for r in csv.DictReader(open(trace)):
+        if "spt::" in r["Kernel_Name"]:
+            per[r["Kernel_Name"]].append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]) - int(r["Start_Timestamp"])))
+    out += ["", f"## Timed launches (last {timed} per kernel, from run_kernel_trace.csv)\n",
+            "| kernel | launches | avg ms | min ms | max ms |", "|---|---|---|---|---|"]
+    for k, v in sorted(per.items()):
+        d = [x[1] / 1e6 for x in sorted(v)][-timed:]
+        out.append(f"| `{k[:60]}` | {len(d)} | {sum(d)/len(d):.4f} | {min(d):.4f} | {max(d):.4f} |")
 agg = collections.defaultdict(list)
 for d in ("pmc1", "pmc2", "pmc3", "pmc4"):
     p = os.path.join(src, d, "run_counter_collection.csv")

@@ -215,11 +215,12 @@ AccelTables build_accel(const float *centers4, const float *radii, uint32_t n, u
                 t.nodes[me].skip = (uint32_t)(t.nodes.size() - base);
             };
             for (size_t j : ordered(top, 0, levels[top].size())) emit(emit, top, j);
-            if (levels.size() == 1)  // flat list: the rb field carries K1' (expanded line test)
+            if (levels.size() == 1)  // flat list: rb carries K1', cb2 the scaled |Cb|^2 (expanded line test)
                 for (size_t q = base; q < t.nodes.size(); ++q) {
                     const AccelNode &nd = t.nodes[q];
                     const double cbb = (double)nd.cx * nd.cx + (double)nd.cy * nd.cy + (double)nd.cz * nd.cz;
                     t.nodes[q].rb = round_up((double)nd.k1 + 4e-6 * cbb);
+                    t.nodes[q].cb2 = (float)(kFlatScale * cbb);
                 }
             if (oct == 0) t.n_nodes = (uint32_t)t.nodes.size();
             // pad node (the kernel prefetches one node past the layout)
@@ -279,10 +280,12 @@ std::string validate_accel(const AccelTables &t, const float *centers4, const fl
                     return bad("layout %u node %u: leaf slot %u out of range", oct, i, nd.slot);
             }
             // containment of every member below: |Cm - Cb| + r <= Rb and 1.15 Rb^2 + 1e-5 <= K1
-            // (flat lists: |Cm - Cb| + r <= sqrt((K1 - 1e-5) / 1.15) and K1' >= K1 + 4e-6 |Cb|^2)
+            // (flat lists: |Cm - Cb| + r <= sqrt((K1 - 1e-5) / 1.15), K1' >= K1 + 4e-6 |Cb|^2 and
+            // cb2 = kFlatScale |Cb|^2)
             const bool flat = t.n_nodes == t.leaves;
             const double cbb = (double)nd.cx * nd.cx + (double)nd.cy * nd.cy + (double)nd.cz * nd.cz;
-            if (flat && !(std::fabs((double)nd.cb2 - cbb) <= 2e-7 * cbb && (double)nd.rb >= (double)nd.k1 + 4e-6 * cbb))
+            if (flat && !(std::fabs((double)nd.cb2 - kFlatScale * cbb) <= 2e-7 * cbb &&
+                          (double)nd.rb >= (double)nd.k1 + 4e-6 * cbb))
                 return bad("layout %u node %u: flat-list |Cb|^2 or K1' wrong", oct, i);
             const double rbound = flat ? std::sqrt(std::max(0.0, ((double)nd.k1 - 1e-5) / 1.15)) : (double)nd.rb;
             if (!flat && !((double)nd.k1 >= 1.15 * (double)nd.rb * (double)nd.rb + 1e-5))

@@ -142,6 +142,10 @@ __host__ __device__ inline void ts_item(uint32_t q, uint32_t width, uint32_t row
 constexpr uint32_t kMaxGroup = 16;     // sphere-table padding granule (>= SPT_GROUP)
 constexpr uint32_t kClusterSlots = 8;  // max members per cluster = slots of a tree leaf
 constexpr uint32_t kFlatLeafSlots = 4; // slots of a flat-list leaf holding <= 4 members
+// Flat-list line test (spt_path.h find_closest): the 1e-4 |Cb-o|^2 margin is folded
+// in by scaling the expanded |Cb-o|^2 by kFlatScale = 1 - 1e-4; nodes store
+// kFlatScale |Cb|^2.
+constexpr double kFlatScale = 1.0 - 1e-4;
 constexpr uint32_t kNoSlot = 0xFFFFFFFFu;  // AccelNode::slot of inner nodes
 constexpr uint32_t kMiss = 0xFFFFFFFFu;    // Hit::idx when no sphere was hit
 

@@ -113,8 +113,19 @@ __device__ __forceinline__ void test_group(const float4 (&sp)[G], const uint32_t
                     // wave-uniform branch, so the index loads (and the vmcnt waits
                     // they would drag into the hot loop) run only when some lane ties.
                     const bool tie = ds == h.best && h.idx != kMiss;
-                    if (__builtin_expect(__ballot(tie) != 0ull, 0)) {
-                        if (tie) better = orig[slot + k] < orig[h.idx];
+                    unsigned long long tm = __ballot(tie);
+                    if (__builtin_expect(tm != 0ull, 0)) {
+                        // scalar loads only (one per distinct current winner): a
+                        // vector load here made every cast wait on vmcnt(0), i.e. on
+                        // the previous shading step's sample stores
+                        const uint32_t mo = ((cuint *)orig)[slot + k];
+                        while (tm != 0ull) {
+                            const uint32_t wi = __builtin_amdgcn_readlane(h.idx, (int)__builtin_ctzll(tm));
+                            const uint32_t wo = ((cuint *)orig)[wi];
+                            const bool same = tie && h.idx == wi;
+                            if (same) better = mo < wo;
+                            tm &= ~__ballot(same);
+                        }
                     }
                     if (better) {
                         h.best = ds;
@@ -180,23 +191,24 @@ __device__ __forceinline__ Hit find_closest(const AccelView &ac, const f3 &o, co
     if (!TREE) {
         // flat list: node i is leaf i.  The line test in expanded form, with FMAs
         // (a conservative test need not follow the reference's operation order;
-        // DESIGN.md §4.4):
-        //   tcb  = Cb.d - o.d,   |Cb-o|^2 = |Cb|^2 - 2 Cb.o + |o|^2,   d2b = |Cb-o|^2 - tcb^2
-        // keep iff d2b <= K1 + 1e-4 |Cb-o|^2 + 4e-6 (|Cb|^2 + |o|^2): the absolute
-        // term covers the expansion's cancellation (<= 2.4e-6 (|Cb|^2 + |o|^2)).
-        // 13 VALU per node instead of 17.
+        // DESIGN.md §4.4): keep iff
+        //   d2b <= K1 + 1e-4 |Cb-o|^2 + 4e-6 |Cb|^2 + 4.1e-6 |o|^2,   d2b = |Cb-o|^2 - tcb^2,
+        // evaluated as  c |Cb|^2 - 2c Cb.o + (c - 4.1e-6) |o|^2 - tcb^2 <= K1'  with
+        // c = kFlatScale = 1 - 1e-4, tcb = Cb.d - o.d and K1' = K1 + 4e-6 |Cb|^2
+        // (rounded up).  The absolute terms cover the expansion's rounding
+        // (<= 2.7e-6 (|Cb|^2 + |o|^2)).  Per node: 3 FMA (tcb), 3 FMA + 1 add (the
+        // scaled |Cb-o|^2), 1 FMA, 1 compare = 9 VALU.
         const float oo = lensq(o);
-        const float eo = 4.1e-6f * oo;
+        const float qo = (float)(kFlatScale - 4.1e-6) * oo;
+        const float m2c = (float)(-2.0 * kFlatScale);
+        const float osx = m2c * o.x, osy = m2c * o.y, osz = m2c * o.z;
         auto line_mask = [&](const uint32_t *r) {
             const float bx = __uint_as_float(r[0]), by = __uint_as_float(r[1]), bz = __uint_as_float(r[2]);
-            const float k1p = __uint_as_float(r[6]), cb2 = __uint_as_float(r[7]);  // K1' = K1 + 4e-6 |Cb|^2
-            const float cbd = __builtin_fmaf(bx, d.x, __builtin_fmaf(by, d.y, bz * d.z));
-            const float cbo = __builtin_fmaf(bx, o.x, __builtin_fmaf(by, o.y, bz * o.z));
-            const float tcb = cbd - dod;
-            const float occb = __builtin_fmaf(-2.f, cbo, cb2) + oo;
-            const float d2b = __builtin_fmaf(-tcb, tcb, occb);
-            const float thr = __builtin_fmaf(1e-4f, occb, k1p) + eo;
-            return (__ballot(d2b <= thr) & live_mask) | nocull_mask;
+            const float k1p = __uint_as_float(r[6]), cb2s = __uint_as_float(r[7]);  // K1', c |Cb|^2
+            const float tcb = __builtin_fmaf(bx, d.x, __builtin_fmaf(by, d.y, __builtin_fmaf(bz, d.z, -dod)));
+            const float w = __builtin_fmaf(bx, osx, __builtin_fmaf(by, osy, __builtin_fmaf(bz, osz, qo))) + cb2s;
+            const float x = __builtin_fmaf(-tcb, tcb, w);
+            return (__ballot(x <= k1p) & live_mask) | nocull_mask;
         };
         auto diag_node = [&](unsigned long long mm) {
             if (SPT_DIAG) {

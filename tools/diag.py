@@ -8,6 +8,8 @@ import simplepathtracer_amd as spt  # noqa: E402
 
 cfg = sys.argv[1] if len(sys.argv) > 1 else "c2"
 W, H, spp, b = {"c2": (1200, 800, 100, 50), "c2s": (1200, 800, 8, 50), "c5s": (1920, 1080, 4, 50)}[cfg]
+if len(sys.argv) > 2:  # bounces override (1: casts are almost all primary rays)
+    b = int(sys.argv[2])
 ctx = spt.Context(0)
 scene = spt.generate_stress(1, 10000) if cfg.startswith("c5") else spt.generate_spheres(1)
 ctx.set_scene(scene)

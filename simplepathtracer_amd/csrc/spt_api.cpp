@@ -309,6 +309,7 @@ int render_impl(spt_ctx *ctx, int mode, const spt::RowMap &map, float4 *d_rgba, 
     ra.mode = (uint32_t)mode;
     ra.seed_key = fmix64(ctx->seed);
     ra.map = map;
+    ra.div_strip = spt::make_fastdiv(std::max<uint32_t>(map.strip, 1u));
     ra.npix = npix;
     ra.claim = claim_size(ctx, (uint64_t)npix * spp_batch);
     ra.samples = w->d_samples;

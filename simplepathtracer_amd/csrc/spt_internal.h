@@ -96,6 +96,13 @@ __host__ __device__ inline uint32_t fast_div(uint32_t x, const FastDiv &f)
     return f.d <= 1u ? x : hi >> f.s;
 }
 
+// row_of with the strip division by multiply-shift (div_strip = FastDiv(m.strip))
+__host__ __device__ inline uint32_t row_of_fast(const RowMap &m, uint32_t lr, const FastDiv &div_strip)
+{
+    const uint32_t blk = fast_div(lr, div_strip);
+    return m.y0 + (blk * m.parts + m.part) * m.strip + (lr - blk * m.strip);
+}
+
 // (sample, pixel) of the q-th item of a batch of S samples over a region of
 // `rows` x `width` pixels, items ordered [8-row band][8-column tile][sample]
 // [pixel in tile] (ragged tiles at the right and bottom edges).  A claim of
@@ -184,6 +191,7 @@ struct RenderArgs {
     uint32_t n_items;    // npix * spp_batch
     uint32_t claim;      // items per queue claim
     FastDiv div_band, div_tile;  // ts_item divisors 8*width*spp_batch and 64*spp_batch
+    FastDiv div_strip;           // row_of_fast divisor map.strip
     float *samples;      // [n_items] per-sample colour: {r, g, b} (segment mode) or {r, g, b, counted} (task mode)
     uint32_t slot_floats;  // 3 or 4
     uint32_t *head;      // queue head (zeroed before launch)

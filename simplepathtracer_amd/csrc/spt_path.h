@@ -110,14 +110,12 @@ __device__ __forceinline__ void test_group(const float4 (&sp)[G], const uint32_t
                     const float ds = lensq(sub(o, p));
                     bool better = ds < h.best;
                     // exact tie (rare): the first original index wins.  Behind a
-                    // wave-uniform branch, so the index loads (and the vmcnt waits
-                    // they would drag into the hot loop) run only when some lane ties.
+                    // wave-uniform branch, with scalar loads only (one per distinct
+                    // current winner): a vector load here made every cast wait on
+                    // vmcnt(0), i.e. on the previous shading step's sample stores.
                     const bool tie = ds == h.best && h.idx != kMiss;
                     unsigned long long tm = __ballot(tie);
                     if (__builtin_expect(tm != 0ull, 0)) {
-                        // scalar loads only (one per distinct current winner): a
-                        // vector load here made every cast wait on vmcnt(0), i.e. on
-                        // the previous shading step's sample stores
                         const uint32_t mo = ((cuint *)orig)[slot + k];
                         while (tm != 0ull) {
                             const uint32_t wi = __builtin_amdgcn_readlane(h.idx, (int)__builtin_ctzll(tm));
@@ -538,7 +536,7 @@ __device__ __forceinline__ void start_path(const RenderArgs &a, uint32_t mine, u
     const uint32_t lr = pl / a.map.width;
     const uint32_t x = a.map.x0 + (pl - lr * a.map.width);
 #endif
-    const uint32_t y = a.map.parts == 1u ? a.map.y0 + lr : row_of(a.map, lr);
+    const uint32_t y = a.map.parts == 1u ? a.map.y0 + lr : row_of_fast(a.map, lr, a.div_strip);
     ps.st = fmix64(a.seed_key ^ (((uint64_t)(y * a.width + x) << 32) | (uint64_t)s));
     const float un = (float)y + uniform(ps.st, -1.f, 1.f);
     const float vn = (float)x + uniform(ps.st, -1.f, 1.f);
@@ -575,6 +573,7 @@ __device__ __forceinline__ void start_path_kernarg(uint32_t mine, uint32_t rows,
     a.seed_key = k.seed_key;
     a.div_band = FastDiv{k.div_band.d, k.div_band.m, k.div_band.s};
     a.div_tile = FastDiv{k.div_tile.d, k.div_tile.m, k.div_tile.s};
+    a.div_strip = FastDiv{k.div_strip.d, k.div_strip.m, k.div_strip.s};
 #pragma unroll
     for (int q = 0; q < 12; ++q) a.cam.view[q] = k.cam.view[q];
     start_path(a, mine, rows, recip((float)a.width), recip((float)a.height),

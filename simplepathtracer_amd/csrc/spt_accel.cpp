@@ -215,13 +215,20 @@ AccelTables build_accel(const float *centers4, const float *radii, uint32_t n, u
                 t.nodes[me].skip = (uint32_t)(t.nodes.size() - base);
             };
             for (size_t j : ordered(top, 0, levels[top].size())) emit(emit, top, j);
-            if (levels.size() == 1)  // flat list: rb carries K1', cb2 the scaled |Cb|^2 (expanded line test)
-                for (size_t q = base; q < t.nodes.size(); ++q) {
-                    const AccelNode &nd = t.nodes[q];
-                    const double cbb = (double)nd.cx * nd.cx + (double)nd.cy * nd.cy + (double)nd.cz * nd.cz;
-                    t.nodes[q].rb = round_up((double)nd.k1 + 4e-6 * cbb);
-                    t.nodes[q].cb2 = (float)(kFlatScale * cbb);
+            // expanded node tests (spt_path.h find_closest): flat lists
+            // keep K1' in rb and c |Cb|^2 in cb2; tree nodes F = Rb + 1e-4 (|Cb| + Rb)
+            // in rb and (c - kTreeNodeErr) |Cb|^2 in cb2
+            for (size_t q = base; q < t.nodes.size(); ++q) {
+                AccelNode &nd = t.nodes[q];
+                const double cbb = (double)nd.cx * nd.cx + (double)nd.cy * nd.cy + (double)nd.cz * nd.cz;
+                if (levels.size() == 1) {
+                    nd.rb = round_up((double)nd.k1 + 4e-6 * cbb);
+                    nd.cb2 = (float)(kFlatScale * cbb);
+                } else {
+                    nd.rb = round_up((double)nd.rb + 1e-4 * (std::sqrt(cbb) + (double)nd.rb));
+                    nd.cb2 = (float)((kFlatScale - kTreeNodeErr) * cbb);
                 }
+            }
             if (oct == 0) t.n_nodes = (uint32_t)t.nodes.size();
             // pad node (the kernel prefetches one node past the layout)
             t.nodes.push_back(AccelNode{0.f, 0.f, 0.f, -INFINITY, t.n_nodes + 1, kNoSlot, -INFINITY, 0.f});
@@ -279,17 +286,18 @@ std::string validate_accel(const AccelTables &t, const float *centers4, const fl
                 if (nd.slot < cbase || (nd.slot - cbase) % t.leaf_slots || nd.slot + t.leaf_slots > t.slots.size())
                     return bad("layout %u node %u: leaf slot %u out of range", oct, i, nd.slot);
             }
-            // containment of every member below: |Cm - Cb| + r <= Rb and 1.15 Rb^2 + 1e-5 <= K1
-            // (flat lists: |Cm - Cb| + r <= sqrt((K1 - 1e-5) / 1.15), K1' >= K1 + 4e-6 |Cb|^2 and
-            // cb2 = kFlatScale |Cb|^2)
+            // containment of every member below (Rb = max |Cm - Cb| + r over the members):
+            // flat lists: Rb <= sqrt((K1 - 1e-5) / 1.15), K1' >= K1 + 4e-6 |Cb|^2 and
+            // cb2 = c |Cb|^2; tree nodes: K1 >= 1.15 Rb^2 + 1e-5, F >= Rb + 1e-4 (|Cb| + Rb)
+            // and cb2 = (c - kTreeNodeErr) |Cb|^2
             const bool flat = t.n_nodes == t.leaves;
             const double cbb = (double)nd.cx * nd.cx + (double)nd.cy * nd.cy + (double)nd.cz * nd.cz;
             if (flat && !(std::fabs((double)nd.cb2 - kFlatScale * cbb) <= 2e-7 * cbb &&
                           (double)nd.rb >= (double)nd.k1 + 4e-6 * cbb))
                 return bad("layout %u node %u: flat-list |Cb|^2 or K1' wrong", oct, i);
-            const double rbound = flat ? std::sqrt(std::max(0.0, ((double)nd.k1 - 1e-5) / 1.15)) : (double)nd.rb;
-            if (!flat && !((double)nd.k1 >= 1.15 * (double)nd.rb * (double)nd.rb + 1e-5))
-                return bad("layout %u node %u: K1 below 1.15 Rb^2 + 1e-5", oct, i);
+            if (!flat && !(std::fabs((double)nd.cb2 - (kFlatScale - kTreeNodeErr) * cbb) <= 1e-7 * cbb))
+                return bad("layout %u node %u: tree-node scaled |Cb|^2 wrong", oct, i);
+            double rbm = 0;
             for (uint32_t q = i; q < nd.skip; ++q) {
                 if (L[q].slot == kNoSlot) continue;
                 for (uint32_t k = 0; k < t.leaf_slots; ++k) {
@@ -301,10 +309,13 @@ std::string validate_accel(const AccelTables &t, const float *centers4, const fl
                         const double dd = (double)centers4[4 * o + c] - cb[c];
                         d2 += dd * dd;
                     }
-                    if (!(std::sqrt(d2) + std::fabs((double)radii[o]) <= rbound))
-                        return bad("layout %u node %u: sphere %u not contained", oct, i, o);
+                    rbm = std::max(rbm, std::sqrt(d2) + std::fabs((double)radii[o]));
                 }
             }
+            const bool k1_ok = (double)nd.k1 >= 1.15 * rbm * rbm + 1e-5;
+            if (!k1_ok) return bad("layout %u node %u: a member lies outside the K1 bound", oct, i);
+            if (!flat && !((double)nd.rb >= rbm + 1e-4 * (std::sqrt(cbb) + rbm)))
+                return bad("layout %u node %u: a member lies outside the F bound", oct, i);
         }
         if (leaves != t.leaves) return bad("layout %u: %zu leaves, expected %u", oct, leaves, t.leaves);
         if (t.n_nodes == t.leaves)  // flat list: node i is leaf i, in slot order

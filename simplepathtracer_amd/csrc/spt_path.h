@@ -186,6 +186,12 @@ __device__ __forceinline__ Hit find_closest(const AccelView &ac, const f3 &o, co
     // compare is the compare's own lane mask, with no VALU round trip
     const unsigned long long nocull_mask = __ballot(no_cull);
     cuint *nodes = (cuint *)ac.nodes;
+    // per-lane terms of the expanded node tests (flat and tree):
+    // c |Cb-o|^2 - 4.1e-6 |o|^2 = c |Cb|^2 + (-2c o).Cb + (c - 4.1e-6) |o|^2, c = kFlatScale
+    const float oo = lensq(o);
+    const float qo = (float)(kFlatScale - 4.1e-6) * oo;
+    const float m2c = (float)(-2.0 * kFlatScale);
+    const float osx = m2c * o.x, osy = m2c * o.y, osz = m2c * o.z;
     if (!TREE) {
         // flat list: node i is leaf i.  The line test in expanded form, with FMAs
         // (a conservative test need not follow the reference's operation order;
@@ -196,10 +202,6 @@ __device__ __forceinline__ Hit find_closest(const AccelView &ac, const f3 &o, co
         // (rounded up).  The absolute terms cover the expansion's rounding
         // (<= 2.7e-6 (|Cb|^2 + |o|^2)).  Per node: 3 FMA (tcb), 3 FMA + 1 add (the
         // scaled |Cb-o|^2), 1 FMA, 1 compare = 9 VALU.
-        const float oo = lensq(o);
-        const float qo = (float)(kFlatScale - 4.1e-6) * oo;
-        const float m2c = (float)(-2.0 * kFlatScale);
-        const float osx = m2c * o.x, osy = m2c * o.y, osz = m2c * o.z;
         auto line_mask = [&](const uint32_t *r) {
             const float bx = __uint_as_float(r[0]), by = __uint_as_float(r[1]), bz = __uint_as_float(r[2]);
             const float k1p = __uint_as_float(r[6]), cb2s = __uint_as_float(r[7]);  // K1', c |Cb|^2
@@ -233,7 +235,7 @@ __device__ __forceinline__ Hit find_closest(const AccelView &ac, const f3 &o, co
         }
         return h;
     }
-    const float olen = __builtin_amdgcn_sqrtf(lensq(o));  // |o|, for the distance margin
+    const float olen = __builtin_amdgcn_sqrtf(oo);  // |o|, for the front and near margins
     if (TREE) {
         // the layout of the wave's majority direction octant (siblings front to back)
         const uint32_t nlive = (uint32_t)__popcll(live_mask);
@@ -242,34 +244,43 @@ __device__ __forceinline__ Hit find_closest(const AccelView &ac, const f3 &o, co
                              (2u * (uint32_t)__popcll(__ballot(active && d.z < 0.f)) > nlive ? 4u : 0u);
         nodes += (size_t)8 * (ac.n_nodes + 1) * oct;
     }
+    // Tree nodes {Cb, K1, skip, slot, F, c'|Cb|^2}: three conservative tests
+    // (DESIGN.md §4.4), without a square root per node; a lane may need the node
+    // only if all pass.  With tcb = Cb.d - o.d and
+    //   w = c' |Cb|^2 - 2c Cb.o + (c - 4.1e-6) |o|^2 <= c |Cb-o|^2   (c' = c - 3e-6),
+    //   line:  w - tcb^2 <= K1                (the ray's line passes within the bound)
+    //   front: tcb + 1e-4 |o| >= -F           (some member may lie in front, tc > 1e-3)
+    //   near:  w <= S^2,  S = (1.004 F + 2e-5 |o| + 1e-6 + sqrt(best (1 + 1e-4))) / 0.996
+    //          (some member's contact point may be closer than the lane's winner)
+    // with F >= Rb + 1e-4 (|Cb| + Rb).  15 VALU per node.
+    const float kq = (float)(1.0 / 0.996 * (1.0 + 1e-6));
+    const float c1004 = (float)(1.004 / 0.996 * (1.0 + 1e-6));
+    // near term of the lane's current winner, refreshed after every leaf test;
+    // inf while there is none (best = FLT_MAX: never culls)
+    auto near_term = [&](float best) {
+        return (__builtin_amdgcn_sqrtf(best * 1.0001f) * (1.0f + 0x1p-20f) + (2e-5f * olen + 1e-6f)) * kq;
+    };
+    float sbe = near_term(h.best);
     uint32_t i = 0;
-    uint32_t nb[7];
+    uint32_t nb[8];
 #pragma unroll
-    for (int q = 0; q < 7; ++q) nb[q] = nodes[q];
+    for (int q = 0; q < 8; ++q) nb[q] = nodes[q];
     while (i < ac.n_nodes) {
         const float bx = __uint_as_float(nb[0]), by = __uint_as_float(nb[1]), bz = __uint_as_float(nb[2]);
-        const float k1 = __uint_as_float(nb[3]), rb = __uint_as_float(nb[6]);
+        const float k1 = __uint_as_float(nb[3]), fr = __uint_as_float(nb[6]), cb2n = __uint_as_float(nb[7]);
         const uint32_t skip = nb[4], leaf_slot = nb[5];
         // speculative prefetch of the preorder successor
 #pragma unroll
-        for (int q = 0; q < 7; ++q) nb[q] = nodes[8 * (i + 1) + q];
-        // Three conservative tests; a lane may need the node only
-        // if all pass.  line: the ray's line passes within the bound; front: some
-        // member may lie in front (tc > 1e-3); near: some member's contact point
-        // may be closer than the lane's current winner (never equal: strict margin).
-        const f3 ocb = mk(bx - o.x, by - o.y, bz - o.z);
-        const float tcb = dot(ocb, d);
-        const float occb = lensq(ocb);
-        const float d2b = occb - tcb * tcb;
-        const float lb = __builtin_amdgcn_sqrtf(occb);
-        const float slack = 1e-4f * (lb + rb);
-        // near: a member's computed contact distance t is at least
-        // (|Cb-o| - Rb) - 2.6e-3 (|Cb-o| + Rb) (rounding of hh under the sqrt and
-        // | |d| - 1 | <= 5e-7); 4e-3 keeps headroom
-        const float lc = ((lb - rb) - 4e-3f * (lb + rb)) - (2e-5f * olen + 1e-6f);
-        const bool line = d2b <= k1 + 1e-4f * occb;
-        const bool front = tcb >= -(rb + slack);
-        const bool near = !(lc > 0.f && lc * lc > h.best * 1.0001f);
+        for (int q = 0; q < 8; ++q) nb[q] = nodes[8 * (i + 1) + q];
+        const float tcb = __builtin_fmaf(bx, d.x, __builtin_fmaf(by, d.y, __builtin_fmaf(bz, d.z, -dod)));
+        // Cb.o from o itself (not -2c o: two VGPRs fewer keep the kernel at 64)
+        const float cbo = __builtin_fmaf(bx, o.x, __builtin_fmaf(by, o.y, bz * o.z));
+        const float w = __builtin_fmaf(cbo, m2c, qo) + cb2n;
+        const float x = __builtin_fmaf(-tcb, tcb, w);
+        const float sn = __builtin_fmaf(fr, c1004, sbe);
+        const bool line = x <= k1;
+        const bool front = __builtin_fmaf(1e-4f, olen, tcb) >= -fr;
+        const bool near = !(w > sn * sn);
         const unsigned long long mm = (__ballot(line && front && near) & live_mask) | nocull_mask;
         const bool leaf = leaf_slot != kNoSlot;
         if (SPT_DIAG) {
@@ -280,11 +291,14 @@ __device__ __forceinline__ Hit find_closest(const AccelView &ac, const f3 &o, co
                 dg.live += mm != 0ull ? (unsigned long long)__popcll(live_mask) : 0ull;
             }
         }
-        if (mm != 0ull && leaf) test_leaf<LEAF>(slots, ac.orig, leaf_slot, o, d, dod, h);
+        if (mm != 0ull && leaf) {
+            test_leaf<LEAF>(slots, ac.orig, leaf_slot, o, d, dod, h);
+            sbe = near_term(h.best);
+        }
         const uint32_t next = (mm != 0ull && !leaf) ? i + 1 : skip;
         if (next != i + 1) {
 #pragma unroll
-            for (int q = 0; q < 7; ++q) nb[q] = nodes[8 * next + q];
+            for (int q = 0; q < 8; ++q) nb[q] = nodes[8 * next + q];
         }
         i = next;
     }

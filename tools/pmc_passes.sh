@@ -11,7 +11,7 @@ for group in "$@"; do
   i=$((i + 1))
   out="$R/gpurun_out/$TAG/pass$i"
   mkdir -p "$out"
-  SPT_LIB=$LIB timeout -k 10 300 rocprofv3 --pmc $group --output-format csv -d "$out" -o run -- python3 "$R/bench.py" --steps 2 --warmup 1 --no-cpu-baseline > "$out/log" 2>&1 || exit $?
+  SPT_LIB=$LIB timeout -k 10 300 rocprofv3 --pmc $group --output-format csv -d "$out" -o run -- python3 "$R/bench.py" --steps 2 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-} > "$out/log" 2>&1 || exit $?
 done
 python3 - "$R/gpurun_out/$TAG" <<'PY'
 import csv, glob, sys, collections

@@ -86,7 +86,6 @@ __device__ __forceinline__ void test_group(const float4 (&sp)[G], const uint32_t
 {
     float tcv[G], hv[G];
     bool pass[G];
-    bool any = false;
 #pragma unroll
     for (int k = 0; k < G; ++k) {
         // RaySphereIntersection, Collision.hpp:9-17
@@ -96,42 +95,43 @@ __device__ __forceinline__ void test_group(const float4 (&sp)[G], const uint32_t
         const float hh = sp[k].w - d2;
         tcv[k] = tc;
         hv[k] = hh;
-        pass[k] = tc > 1e-3f && hh > 1e-3f;
-        any = any || pass[k];
+        // tc > 1e-3 && hh > 1e-3 as one compare (VALU, not a scalar AND of two
+        // masks).  A NaN operand can make it true where the pair is false; such a
+        // lane's contact point is NaN and the dot test below rejects it.
+        pass[k] = __builtin_fminf(tc, hh) > 1e-3f;
     }
-    if (any) {
 #pragma unroll
-        for (int k = 0; k < G; ++k) {
-            if (pass[k]) {
-                // CalculateRaySphereClosestContactPoint, Collision.hpp:19-27,49-56
-                const float t = tcv[k] - sqrt_pos_normal(hv[k]);
-                const f3 p = mk(o.x + d.x * t, o.y + d.y * t, o.z + d.z * t);
-                if (dod < dot(p, d)) {
-                    const float ds = lensq(sub(o, p));
-                    bool better = ds < h.best;
-                    // exact tie (rare): the first original index wins.  Behind a
-                    // wave-uniform branch, with scalar loads only (one per distinct
-                    // current winner): a vector load here made every cast wait on
-                    // vmcnt(0), i.e. on the previous shading step's sample stores.
-                    const bool tie = ds == h.best && h.idx != kMiss;
-                    unsigned long long tm = __ballot(tie);
-                    if (__builtin_expect(tm != 0ull, 0)) {
-                        const uint32_t mo = ((cuint *)orig)[slot + k];
-                        while (tm != 0ull) {
-                            const uint32_t wi = __builtin_amdgcn_readlane(h.idx, (int)__builtin_ctzll(tm));
-                            const uint32_t wo = ((cuint *)orig)[wi];
-                            const bool same = tie && h.idx == wi;
-                            if (same) better = mo < wo;
-                            tm &= ~__ballot(same);
-                        }
-                    }
-                    if (better) {
-                        h.best = ds;
-                        h.idx = slot + k;
-                        h.p = p;
-                    }
+    for (int k = 0; k < G; ++k) {
+        // one wave-uniform branch per sphere and branch-free updates: the scalar
+        // unit is shared by the CU's four SIMDs
+        if (__ballot(pass[k]) != 0ull) {
+            // CalculateRaySphereClosestContactPoint, Collision.hpp:19-27,49-56
+            const float t = tcv[k] - sqrt_pos_normal(hv[k]);
+            const f3 p = mk(o.x + d.x * t, o.y + d.y * t, o.z + d.z * t);
+            const bool ok = pass[k] && dod < dot(p, d);
+            const float ds = lensq(sub(o, p));
+            bool better = ok && ds < h.best;
+            // exact tie (rare): the first original index wins.  Behind a
+            // wave-uniform branch, with scalar loads only (one per distinct
+            // current winner): a vector load here made every cast wait on
+            // vmcnt(0), i.e. on the previous shading step's sample stores.
+            const bool tie = ok && ds == h.best && h.idx != kMiss;
+            unsigned long long tm = __ballot(tie);
+            if (__builtin_expect(tm != 0ull, 0)) {
+                const uint32_t mo = ((cuint *)orig)[slot + k];
+                while (tm != 0ull) {
+                    const uint32_t wi = __builtin_amdgcn_readlane(h.idx, (int)__builtin_ctzll(tm));
+                    const uint32_t wo = ((cuint *)orig)[wi];
+                    const bool same = tie && h.idx == wi;
+                    if (same) better = mo < wo;
+                    tm &= ~__ballot(same);
                 }
             }
+            h.best = better ? ds : h.best;
+            h.idx = better ? slot + k : h.idx;
+            h.p.x = better ? p.x : h.p.x;
+            h.p.y = better ? p.y : h.p.y;
+            h.p.z = better ? p.z : h.p.z;
         }
     }
 }

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define SPT_ABI_VERSION 1
+#define SPT_ABI_VERSION 2
 
 /* Only the functions below are exported from libspt_hip.so (built with
  * -fvisibility=hidden), so several builds can be loaded side by side. */
@@ -72,10 +72,16 @@ typedef struct spt_stats {
     double last_render_ms; /* device time of the most recent render launch */
     uint32_t grid_blocks;  /* persistent grid of the render kernel */
     uint32_t block_threads;
-    uint64_t diag[8];      /* diagnostic build only (-DSPT_DIAG=1): wave iterations,
+    double render_busy_ms; /* length of the union of the render launches' intervals: with
+                              frames in flight on several streams launches overlap, and
+                              this is the device time during which some render launch ran */
+    uint64_t diag[12];     /* diagnostic build only (-DSPT_DIAG=1): wave iterations,
                               clusters entered, tree nodes tested, s_memtime cycles in
                               cast / shading / refill, (lane, cluster) pairs that may
-                              pass, live lanes of entered clusters */
+                              pass, live lanes of entered clusters, spheres tested per
+                              wave, their update branches taken (some lane passes),
+                              lanes passing in those branches, branches that
+                              improve some lane's winner */
 } spt_stats;
 
 SPT_API int spt_abi_version(void);

@@ -15,6 +15,7 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG_DIR, "lib", os.environ.get("SPT_LIB", "libspt_hip.so"))
 HEADER_PATH = os.path.join(os.path.dirname(PKG_DIR), "include", "spt_hip.h")
 
+ABI_VERSION = 2  # SPT_ABI_VERSION of include/spt_hip.h
 SPT_OK = 0
 STATUS_NAMES = {0: "SPT_OK", 1: "SPT_ERR_ARG", 2: "SPT_ERR_STATE", 3: "SPT_ERR_HIP", 4: "SPT_ERR_NOMEM",
                 5: "SPT_ERR_NODEVICE"}
@@ -42,7 +43,8 @@ class Stats(ctypes.Structure):
         ("last_render_ms", ctypes.c_double),
         ("grid_blocks", ctypes.c_uint32),
         ("block_threads", ctypes.c_uint32),
-        ("diag", ctypes.c_uint64 * 8),
+        ("render_busy_ms", ctypes.c_double),
+        ("diag", ctypes.c_uint64 * 12),
     ]
 
 
@@ -106,7 +108,7 @@ def lib() -> ctypes.CDLL:
         fn = getattr(L, name)
         fn.argtypes = args
         fn.restype = res
-    if L.spt_abi_version() != 1:
+    if L.spt_abi_version() != ABI_VERSION:
         raise ImportError("libspt_hip.so ABI version mismatch")
     _lib = L
     return L

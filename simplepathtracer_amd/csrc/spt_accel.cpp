@@ -60,6 +60,21 @@ float round_up(double x)
     return f;
 }
 
+float round_down(double x)
+{
+    float f = (float)x;
+    if ((double)f > x) f = std::nextafter(f, -INFINITY);
+    return f;
+}
+
+// K' of one cluster slot (AccelTables::kpre): c |C|^2 - r^2 (1 + 1e-6) - 4e-6 |C|^2,
+// rounded down, with r^2 the slot's float r*r
+float pretest_k(const float4 &s)
+{
+    const double cc = (double)s.x * s.x + (double)s.y * s.y + (double)s.z * s.z;
+    return round_down(kFlatScale * cc - (double)s.w * (1.0 + 1e-6) - 4e-6 * cc);
+}
+
 const float4 kDummy = make_float4(0.f, 0.f, 0.f, -INFINITY);  // r*r = -inf: never passes
 
 }  // namespace
@@ -241,6 +256,26 @@ AccelTables build_accel(const float *centers4, const float *radii, uint32_t n, u
     }
     if (t.nodes.empty())  // no tree: one pad record per octant layout (n_nodes = 0)
         for (int oct = 0; oct < 8; ++oct) t.nodes.push_back(AccelNode{0.f, 0.f, 0.f, -INFINITY, 1, kNoSlot, -INFINITY, 0.f});
+    // member pretest constants of the cluster slots (dummies: K' = +inf never passes)
+    t.kpre.assign(t.slots.size(), 0.f);
+    double cm = 0;
+    for (size_t j = cbase; j < t.slots.size(); ++j) {
+        if (t.orig[j] == 0xFFFFFFFFu) {
+            t.kpre[j] = INFINITY;
+            continue;
+        }
+        const float4 &q = t.slots[j];
+        t.kpre[j] = pretest_k(q);
+        cm = std::max(cm, std::sqrt((double)q.x * q.x + (double)q.y * q.y + (double)q.z * q.z) +
+                              std::sqrt((double)q.w));
+    }
+    t.pre_cm = round_up(cm * (1.0 + 1e-9));
+    if (!(cm <= 1e15)) {
+        // squares near the float range: the pretest passes every lane (K' = -inf)
+        t.pre_cm = INFINITY;
+        for (size_t j = cbase; j < t.slots.size(); ++j)
+            if (t.orig[j] != 0xFFFFFFFFu) t.kpre[j] = -INFINITY;
+    }
     return t;
 }
 
@@ -272,6 +307,22 @@ std::string validate_accel(const AccelTables &t, const float *centers4, const fl
     }
     for (uint32_t i = 0; i < n; ++i)
         if (!seen[i]) return bad("sphere %u missing from the slot table", i);
+    // member pretest constants (cluster slots)
+    if (t.kpre.size() != t.slots.size()) return bad("pretest table size mismatch");
+    for (size_t j = cbase; j < t.slots.size(); ++j) {
+        const float4 &q = t.slots[j];
+        if (t.orig[j] == 0xFFFFFFFFu) {
+            if (!(t.kpre[j] == INFINITY)) return bad("dummy slot %zu: pretest can pass", j);
+            continue;
+        }
+        if (t.pre_cm == INFINITY) {
+            if (!(t.kpre[j] == -INFINITY)) return bad("slot %zu: pretest not disabled", j);
+            continue;
+        }
+        if (!(t.kpre[j] == pretest_k(q))) return bad("slot %zu: pretest K' wrong", j);
+        const double cl = std::sqrt((double)q.x * q.x + (double)q.y * q.y + (double)q.z * q.z);
+        if (!((double)t.pre_cm >= cl + std::sqrt((double)q.w))) return bad("slot %zu: outside the pretest bound", j);
+    }
     for (uint32_t oct = 0; oct < 8; ++oct) {
         const AccelNode *L = t.nodes.data() + (size_t)oct * (t.n_nodes + 1);
         if (!(L[t.n_nodes].k1 == -INFINITY) || L[t.n_nodes].slot != kNoSlot) return bad("layout %u: bad pad", oct);

@@ -34,6 +34,12 @@ struct AccelTables {
     uint32_t leaves = 0;            // clusters
     uint32_t depth = 0;             // levels of the tree (1 = flat cluster list)
     uint32_t leaf_slots = kClusterSlots;  // slots per leaf (members <= leaf_slots)
+    // member pretest (spt_path.h test_group_pre): per slot
+    // K' = c |C|^2 - r^2 (1 + 1e-6) - 4e-6 |C|^2 rounded down (c = kFlatScale; +inf
+    // for dummies, 0 in the always-list), and pre_cm >= max |C| + r over the
+    // cluster members (rounded up)
+    std::vector<float> kpre;
+    float pre_cm = 0.f;
 };
 
 // cluster_k: members per cluster (0, or n <= 32: every sphere is "always" tested).

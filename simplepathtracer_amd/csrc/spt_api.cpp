@@ -60,7 +60,8 @@ struct spt_ctx {
     float4 *d_shade = nullptr, *d_slots = nullptr;
     spt::AccelNode *d_nodes = nullptr;
     uint32_t *d_mat = nullptr, *d_orig = nullptr;
-    size_t shade_cap = 0, mat_cap = 0, slots_cap = 0, orig_cap = 0, nodes_cap = 0;
+    float *d_kpre = nullptr;
+    size_t shade_cap = 0, mat_cap = 0, slots_cap = 0, orig_cap = 0, nodes_cap = 0, kpre_cap = 0;
     spt::AccelTables tables;
     uint32_t n = 0;
     bool scene_set = false;
@@ -96,6 +97,11 @@ struct spt_ctx {
     // timing
     std::vector<EventPair> pending_render, pending_fold, pool;
     double render_ms = 0, fold_ms = 0, last_render_ms = 0;
+    // render-launch intervals relative to ref_ev (recorded before the first launch
+    // after a stats reset), for the union of overlapping launches (render_busy_ms)
+    hipEvent_t ref_ev = nullptr;
+    bool ref_recorded = false;
+    std::vector<std::pair<double, double>> spans;
     uint64_t launches = 0;
 };
 
@@ -164,6 +170,9 @@ int collect_timings(spt_ctx *ctx)
             if (vec == &ctx->pending_render) {
                 ctx->render_ms += ms;
                 ctx->last_render_ms = ms;
+                float ta = 0.f;
+                HIP_TRY(ctx, hipEventElapsedTime(&ta, ctx->ref_ev, p.a));
+                ctx->spans.emplace_back((double)ta, (double)ta + ms);
             } else {
                 ctx->fold_ms += ms;
             }
@@ -172,6 +181,25 @@ int collect_timings(spt_ctx *ctx)
         vec->clear();
     }
     return SPT_OK;
+}
+
+// Length of the union of the recorded render-launch intervals.
+double busy_ms(const spt_ctx *ctx)
+{
+    std::vector<std::pair<double, double>> v = ctx->spans;
+    std::sort(v.begin(), v.end());
+    double total = 0, cs = 0, ce = -1e300;
+    for (const auto &iv : v) {
+        if (iv.first > ce) {
+            if (ce > cs) total += ce - cs;
+            cs = iv.first;
+            ce = iv.second;
+        } else {
+            ce = std::max(ce, iv.second);
+        }
+    }
+    if (ce > cs) total += ce - cs;
+    return total;
 }
 
 int check_ready(spt_ctx *ctx)
@@ -344,6 +372,10 @@ int render_impl(spt_ctx *ctx, int mode, const spt::RowMap &map, float4 *d_rgba, 
             const uint32_t cap = (uint32_t)std::min<uint64_t>(ctx->wf_cap, std::max<uint32_t>(ra.n_items, 1024u));
             if ((rc = ensure_wavefront(ctx, w, cap))) return rc;
             HIP_TRY(ctx, hipEventRecord(ev.a, s));
+            if (!ctx->ref_recorded) {
+                HIP_TRY(ctx, hipEventRecord(ctx->ref_ev, s));
+                ctx->ref_recorded = true;
+            }
             uint32_t cur = 0, n_cur = 0, next_item = 0;
             while (next_item < ra.n_items || n_cur > 0) {
                 const uint32_t gen = std::min(cap - n_cur, ra.n_items - next_item);
@@ -358,6 +390,10 @@ int render_impl(spt_ctx *ctx, int mode, const spt::RowMap &map, float4 *d_rgba, 
             HIP_TRY(ctx, hipEventRecord(ev.b, s));
         } else {
             HIP_TRY(ctx, hipMemsetAsync(w->d_head, 0, sizeof(uint32_t), s));
+            if (!ctx->ref_recorded) {
+                HIP_TRY(ctx, hipEventRecord(ctx->ref_ev, s));
+                ctx->ref_recorded = true;
+            }
             HIP_TRY(ctx, hipEventRecord(ev.a, s));
             HIP_TRY(ctx, spt::launch_render(ra, render_grid(ctx, ra.n_items, ra.claim), ctx->block, s));
             HIP_TRY(ctx, hipEventRecord(ev.b, s));
@@ -427,9 +463,10 @@ int rebuild_accel(spt_ctx *ctx)
     if (!rc) rc = upload(ctx, &ctx->d_mat, &ctx->mat_cap, mat);
     if (!rc) rc = upload(ctx, &ctx->d_orig, &ctx->orig_cap, t.orig);
     if (!rc) rc = upload(ctx, &ctx->d_nodes, &ctx->nodes_cap, t.nodes);
+    if (!rc) rc = upload(ctx, &ctx->d_kpre, &ctx->kpre_cap, t.kpre);
     if (rc) return rc;
     ctx->accel = spt::AccelView{ctx->d_slots, ctx->d_orig, ctx->d_nodes, t.always_groups, t.n_nodes,
-                                t.n_nodes > t.leaves ? 1u : 0u, t.leaf_slots};
+                                t.n_nodes > t.leaves ? 1u : 0u, t.leaf_slots, ctx->d_kpre, t.pre_cm};
     ctx->tables = std::move(t);
     return SPT_OK;
 }
@@ -523,8 +560,9 @@ int spt_ctx_create(int device, spt_ctx **out)
     if (const char *e = std::getenv("SPT_WF_CAP")) ctx->wf_cap = (uint32_t)std::max(1024, std::atoi(e));
     ctx->grid = (uint32_t)(per_cu * ctx->num_cu);
     ctx->grid_overlap = std::getenv("SPT_BLOCKS_PER_CU") || per_cu < 2 ? ctx->grid : (uint32_t)((per_cu - 1) * ctx->num_cu);
-    if (hipMalloc((void **)&ctx->d_counters, 12 * sizeof(unsigned long long)) != hipSuccess ||
-        hipMemset(ctx->d_counters, 0, 12 * sizeof(unsigned long long)) != hipSuccess) {
+    if (hipEventCreate(&ctx->ref_ev) != hipSuccess ||
+        hipMalloc((void **)&ctx->d_counters, 16 * sizeof(unsigned long long)) != hipSuccess ||
+        hipMemset(ctx->d_counters, 0, 16 * sizeof(unsigned long long)) != hipSuccess) {
         spt_ctx_destroy(ctx);
         return fail(nullptr, SPT_ERR_NOMEM, "workspace allocation failed");
     }
@@ -543,8 +581,9 @@ void spt_ctx_destroy(spt_ctx *ctx)
             (void)hipEventDestroy(p.b);
         }
     (void)hipDeviceSynchronize();  // async renders on caller streams
+    if (ctx->ref_ev) (void)hipEventDestroy(ctx->ref_ev);
     void *bufs[] = {ctx->d_shade, ctx->d_mat, ctx->d_slots, ctx->d_orig, ctx->d_nodes,
-                    ctx->d_counters, ctx->d_stage, ctx->d_frame8};
+                    ctx->d_kpre, ctx->d_counters, ctx->d_stage, ctx->d_frame8};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     for (Workspace &w : ctx->ws) {
@@ -785,16 +824,17 @@ int spt_get_stats(spt_ctx *ctx, spt_stats *out)
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     int rc = collect_timings(ctx);
     if (rc) return rc;
-    unsigned long long c[12] = {0};
+    unsigned long long c[16] = {0};
     HIP_TRY(ctx, hipMemcpy(c, ctx->d_counters, sizeof c, hipMemcpyDeviceToHost));
     out->casts = c[0];
     out->samples = c[1];
     out->dropped = c[2];
-    for (int i = 0; i < 8; ++i) out->diag[i] = c[4 + i];
+    for (int i = 0; i < 12; ++i) out->diag[i] = c[4 + i];
     out->launches = ctx->launches;
     out->render_ms = ctx->render_ms;
     out->fold_ms = ctx->fold_ms;
     out->last_render_ms = ctx->last_render_ms;
+    out->render_busy_ms = busy_ms(ctx);
     out->grid_blocks = ctx->grid;
     out->block_threads = ctx->block;
     return SPT_OK;
@@ -807,9 +847,11 @@ int spt_reset_stats(spt_ctx *ctx)
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     int rc = collect_timings(ctx);
     if (rc) return rc;
-    HIP_TRY(ctx, hipMemset(ctx->d_counters, 0, 12 * sizeof(unsigned long long)));
+    HIP_TRY(ctx, hipMemset(ctx->d_counters, 0, 16 * sizeof(unsigned long long)));
     ctx->render_ms = ctx->fold_ms = ctx->last_render_ms = 0;
     ctx->launches = 0;
+    ctx->spans.clear();
+    ctx->ref_recorded = false;
     return SPT_OK;
 }
 

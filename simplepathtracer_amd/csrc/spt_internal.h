@@ -167,6 +167,8 @@ struct AccelView {
     uint32_t always_groups, n_nodes;
     uint32_t tree;        // 0: flat cluster list (every node a leaf), 1: tree with inner nodes
     uint32_t leaf_slots;  // slots per leaf: kFlatLeafSlots or kClusterSlots
+    const float *kpre;    // member pretest constant K' per slot (spt_accel.h)
+    float pre_cm;         // >= max |C| + r over the cluster members
 };
 
 struct DeviceScene {

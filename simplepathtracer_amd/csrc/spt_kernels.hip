@@ -159,6 +159,10 @@ __global__ __launch_bounds__(kRenderBlock) SPT_RENDER_ATTR void render_kernel(Re
         atomicAdd(&a.counters[9], d_cyc_refill);
         atomicAdd(&a.counters[10], dg.pairs);
         atomicAdd(&a.counters[11], dg.live);
+        atomicAdd(&a.counters[12], dg.spheres);
+        atomicAdd(&a.counters[13], dg.branches);
+        atomicAdd(&a.counters[14], dg.passing);
+        atomicAdd(&a.counters[15], dg.improving);
     }
 #endif
     (void)d_iters;

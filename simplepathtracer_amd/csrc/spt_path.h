@@ -25,6 +25,12 @@
 #define SPT_KERNARG_RELOAD 1
 #endif
 
+// 1: flat-list cluster members are tested behind the conservative pretest of
+// test_group_pre (10 VALU per member instead of 18)
+#ifndef SPT_PRETEST
+#define SPT_PRETEST 1
+#endif
+
 // 1: the cube-minus-ball rejection loop runs cooperatively across the wave
 #ifndef SPT_COOP_BALL
 #define SPT_COOP_BALL 1
@@ -74,84 +80,165 @@ struct Hit {
     f3 p;                // its closest contact point
 };
 
-// One group of G slots {C, r*r} (Collision.hpp:87-109): RaySphereIntersection for
-// all of them, then the rare closest-contact / distance update behind a single
-// branch.  Slots are visited in traversal order, so the winner is the
-// lexicographic minimum of (distance, original index): identical to the
-// reference's strict-'>' scan in index order (first index wins ties; NaN and
-// FLT_MAX distances never win).
+// Wave-diagnostic counters of the SPT_DIAG build.
+struct CastDiag {
+    unsigned long long nodes = 0, leaves = 0, pairs = 0, live = 0;
+    unsigned long long spheres = 0, branches = 0, passing = 0, improving = 0;
+};
+
+// The closest-contact / distance update of one member (Collision.hpp:19-27,49-56,
+// 87-109) for the lanes that pass RaySphereIntersection (`pass`, with its tc and
+// hh); called in wave-uniform control flow when some lane passes.  Slots are
+// visited in traversal order, so the winner is the lexicographic minimum of
+// (distance, original index): identical to the reference's strict-'>' scan in
+// index order (first index wins ties; NaN and FLT_MAX distances never win).
+__device__ __forceinline__ void update_member(bool pass, float tc, float hh, const uint32_t *__restrict__ orig,
+                                              uint32_t s, const f3 &o, const f3 &d, float dod, Hit &h, CastDiag &dg)
+{
+    // CalculateRaySphereClosestContactPoint, Collision.hpp:19-27,49-56
+    const float t = tc - sqrt_pos_normal(hh);
+    const f3 p = mk(o.x + d.x * t, o.y + d.y * t, o.z + d.z * t);
+    const bool ok = pass && dod < dot(p, d);
+    const float ds = lensq(sub(o, p));
+    bool better = ok && ds < h.best;
+    // exact tie (rare): the first original index wins.  Behind a wave-uniform
+    // branch, with scalar loads only (one per distinct current winner): a vector
+    // load here made every cast wait on vmcnt(0), i.e. on the previous shading
+    // step's sample stores.
+    const bool tie = ok && ds == h.best && h.idx != kMiss;
+    unsigned long long tm = __ballot(tie);
+    if (__builtin_expect(tm != 0ull, 0)) {
+        const uint32_t mo = ((cuint *)orig)[s];
+        while (tm != 0ull) {
+            const uint32_t wi = __builtin_amdgcn_readlane(h.idx, (int)__builtin_ctzll(tm));
+            const uint32_t wo = ((cuint *)orig)[wi];
+            const bool same = tie && h.idx == wi;
+            if (same) better = mo < wo;
+            tm &= ~__ballot(same);
+        }
+    }
+    if (SPT_DIAG) dg.improving += __ballot(better) != 0ull ? 1 : 0;
+    h.best = better ? ds : h.best;
+    h.idx = better ? s : h.idx;
+    h.p.x = better ? p.x : h.p.x;
+    h.p.y = better ? p.y : h.p.y;
+    h.p.z = better ? p.z : h.p.z;
+}
+
+// RaySphereIntersection, Collision.hpp:9-17, in the reference's operation order:
+// tc and hh = r*r - d2; the lane passes iff tc > 1e-3 && hh > 1e-3.
+__device__ __forceinline__ bool ray_sphere(const float4 &sp, const f3 &o, const f3 &d, float &tc, float &hh)
+{
+    const float ocx = sp.x - o.x, ocy = sp.y - o.y, ocz = sp.z - o.z;
+    tc = (ocx * d.x + ocy * d.y) + ocz * d.z;
+    const float d2 = ((ocx * ocx + ocy * ocy) + ocz * ocz) - tc * tc;
+    hh = sp.w - d2;
+    // tc > 1e-3 && hh > 1e-3 as one compare (VALU, not a scalar AND of two masks).
+    // A NaN operand can make it true where the pair is false; such a lane's
+    // contact point is NaN and the dot test of update_member rejects it.
+    return __builtin_fminf(tc, hh) > 1e-3f;
+}
+
+// One group of G slots {C, r*r}: RaySphereIntersection for all of them, then the
+// rare update behind one wave-uniform branch per member (the scalar unit is
+// shared by the CU's four SIMDs).
 template <int G>
 __device__ __forceinline__ void test_group(const float4 (&sp)[G], const uint32_t *__restrict__ orig, uint32_t slot,
-                                           const f3 &o, const f3 &d, float dod, Hit &h)
+                                           const f3 &o, const f3 &d, float dod, Hit &h, CastDiag &dg)
 {
     float tcv[G], hv[G];
     bool pass[G];
 #pragma unroll
-    for (int k = 0; k < G; ++k) {
-        // RaySphereIntersection, Collision.hpp:9-17
-        const float ocx = sp[k].x - o.x, ocy = sp[k].y - o.y, ocz = sp[k].z - o.z;
-        const float tc = (ocx * d.x + ocy * d.y) + ocz * d.z;
-        const float d2 = ((ocx * ocx + ocy * ocy) + ocz * ocz) - tc * tc;
-        const float hh = sp[k].w - d2;
-        tcv[k] = tc;
-        hv[k] = hh;
-        // tc > 1e-3 && hh > 1e-3 as one compare (VALU, not a scalar AND of two
-        // masks).  A NaN operand can make it true where the pair is false; such a
-        // lane's contact point is NaN and the dot test below rejects it.
-        pass[k] = __builtin_fminf(tc, hh) > 1e-3f;
-    }
+    for (int k = 0; k < G; ++k) pass[k] = ray_sphere(sp[k], o, d, tcv[k], hv[k]);
 #pragma unroll
     for (int k = 0; k < G; ++k) {
-        // one wave-uniform branch per sphere and branch-free updates: the scalar
-        // unit is shared by the CU's four SIMDs
-        if (__ballot(pass[k]) != 0ull) {
-            // CalculateRaySphereClosestContactPoint, Collision.hpp:19-27,49-56
-            const float t = tcv[k] - sqrt_pos_normal(hv[k]);
-            const f3 p = mk(o.x + d.x * t, o.y + d.y * t, o.z + d.z * t);
-            const bool ok = pass[k] && dod < dot(p, d);
-            const float ds = lensq(sub(o, p));
-            bool better = ok && ds < h.best;
-            // exact tie (rare): the first original index wins.  Behind a
-            // wave-uniform branch, with scalar loads only (one per distinct
-            // current winner): a vector load here made every cast wait on
-            // vmcnt(0), i.e. on the previous shading step's sample stores.
-            const bool tie = ok && ds == h.best && h.idx != kMiss;
-            unsigned long long tm = __ballot(tie);
-            if (__builtin_expect(tm != 0ull, 0)) {
-                const uint32_t mo = ((cuint *)orig)[slot + k];
-                while (tm != 0ull) {
-                    const uint32_t wi = __builtin_amdgcn_readlane(h.idx, (int)__builtin_ctzll(tm));
-                    const uint32_t wo = ((cuint *)orig)[wi];
-                    const bool same = tie && h.idx == wi;
-                    if (same) better = mo < wo;
-                    tm &= ~__ballot(same);
-                }
-            }
-            h.best = better ? ds : h.best;
-            h.idx = better ? slot + k : h.idx;
-            h.p.x = better ? p.x : h.p.x;
-            h.p.y = better ? p.y : h.p.y;
-            h.p.z = better ? p.z : h.p.z;
+        if (SPT_DIAG) {
+            dg.spheres += 1;
+            dg.branches += __ballot(pass[k]) != 0ull ? 1 : 0;
+            dg.passing += (unsigned long long)__popcll(__ballot(pass[k]));
         }
+        if (__ballot(pass[k]) != 0ull) update_member(pass[k], tcv[k], hv[k], orig, slot + k, o, d, dod, h, dg);
     }
 }
 
-// Wave-diagnostic counters of the SPT_DIAG build.
-struct CastDiag {
-    unsigned long long nodes = 0, leaves = 0, pairs = 0, live = 0;
+// Per-lane terms of the member pretest (test_group_pre), formed once per cast.
+struct PreLane {
+    float osx, osy, osz;  // -2c o (c = kFlatScale, as the flat node test); o itself when !PRESCALED
+    float qoe;            // (c - 4.1e-6) |o|^2; +inf for inactive lanes, -inf for lanes that must not cull
+    float tinit;          // mt - o.d, mt = 2e-6 (pre_cm + |o|) + 1e-6; -inf inactive, +inf must not cull
 };
+
+// A group of cluster members behind a cheaper conservative pretest (10 VALU per
+// member instead of 18): with tcs = C.d - o.d + mt and
+//   w = c |C|^2 - r^2 (1 + 1e-6) - 4e-6 |C|^2 - 2c C.o + (c - 4.1e-6) |o|^2
+// (K' = the first three terms, stored per slot), a lane may pass the member only
+// if min(tcs, tcs^2 - w) > 1e-3 (every lane that passes the
+// reference test passes this one).  The exact test runs only behind the member's
+// wave-uniform branch.
+// PRESCALED = false (tree kernels, fewer live VGPRs): pl.os* hold o and the cross
+// term is formed as (C.o) * (-2c), one VALU more.
+template <int G, bool PRESCALED>
+__device__ __forceinline__ void test_group_pre(const float4 (&sp)[G], const float (&kp)[G],
+                                               const uint32_t *__restrict__ orig, uint32_t slot, const f3 &o,
+                                               const f3 &d, float dod, const PreLane &pl, Hit &h, CastDiag &dg)
+{
+    bool pre[G];
+#pragma unroll
+    for (int k = 0; k < G; ++k) {
+        const float tcs = __builtin_fmaf(sp[k].x, d.x, __builtin_fmaf(sp[k].y, d.y, __builtin_fmaf(sp[k].z, d.z, pl.tinit)));
+        float w;
+        if (PRESCALED) {
+            w = __builtin_fmaf(sp[k].x, pl.osx, __builtin_fmaf(sp[k].y, pl.osy, __builtin_fmaf(sp[k].z, pl.osz, pl.qoe))) +
+                kp[k];
+        } else {
+            const float co = __builtin_fmaf(sp[k].x, pl.osx, __builtin_fmaf(sp[k].y, pl.osy, sp[k].z * pl.osz));
+            w = __builtin_fmaf(co, (float)(-2.0 * kFlatScale), pl.qoe) + kp[k];
+        }
+        pre[k] = __builtin_fminf(tcs, __builtin_fmaf(tcs, tcs, -w)) > 1e-3f;
+    }
+#pragma unroll
+    for (int k = 0; k < G; ++k) {
+        if (SPT_DIAG) {
+            dg.spheres += 1;
+            dg.branches += __ballot(pre[k]) != 0ull ? 1 : 0;
+            dg.passing += (unsigned long long)__popcll(__ballot(pre[k]));
+        }
+        if (__ballot(pre[k]) != 0ull) {
+            float tc, hh;
+            const bool pass = ray_sphere(sp[k], o, d, tc, hh);
+            if (__ballot(pass) != 0ull) update_member(pass, tc, hh, orig, slot + k, o, d, dod, h, dg);
+        }
+    }
+}
 
 // Leaf test: the cluster's S slots (S = 8: two s_load_dwordx16, S = 4: one) off one
 // base pointer.
 template <int S>
 __device__ __forceinline__ void test_leaf(cfloat *slots, const uint32_t *__restrict__ orig, uint32_t leaf_slot,
-                                          const f3 &o, const f3 &d, float dod, Hit &h)
+                                          const f3 &o, const f3 &d, float dod, Hit &h, CastDiag &dg)
 {
     cfloat *cs = slots + 4 * leaf_slot;
     float4 ms[S];
 #pragma unroll
     for (int k = 0; k < S; ++k) ms[k] = ld_uniform(cs, k);
-    test_group<S>(ms, orig, leaf_slot, o, d, dod, h);
+    test_group<S>(ms, orig, leaf_slot, o, d, dod, h, dg);
+}
+
+// Leaf test behind the member pretest: the S slots plus their S pretest constants.
+template <int S, bool PRESCALED>
+__device__ __forceinline__ void test_leaf_pre(cfloat *slots, cfloat *kpre, const uint32_t *__restrict__ orig,
+                                              uint32_t leaf_slot, const f3 &o, const f3 &d, float dod,
+                                              const PreLane &pl, Hit &h, CastDiag &dg)
+{
+    cfloat *cs = slots + 4 * leaf_slot;
+    float4 ms[S];
+    float kp[S];
+#pragma unroll
+    for (int k = 0; k < S; ++k) ms[k] = ld_uniform(cs, k);
+    cfloat *kb = kpre + leaf_slot;  // one s_load_dwordx4 (S = 4) off a 64-bit base
+#pragma unroll
+    for (int k = 0; k < S; ++k) kp[k] = kb[k];
+    test_group_pre<S, PRESCALED>(ms, kp, orig, leaf_slot, o, d, dod, pl, h, dg);
 }
 
 // FindClosestIntersectionSphere for every lane of the wave (Collision.hpp:87-109).
@@ -175,7 +262,7 @@ __device__ __forceinline__ Hit find_closest(const AccelView &ac, const f3 &o, co
         float4 g4[SPT_GROUP];
 #pragma unroll
         for (int k = 0; k < SPT_GROUP; ++k) g4[k] = ld_uniform(slots, g * SPT_GROUP + k);
-        test_group<SPT_GROUP>(g4, ac.orig, g * SPT_GROUP, o, d, dod, h);
+        test_group<SPT_GROUP>(g4, ac.orig, g * SPT_GROUP, o, d, dod, h, dg);
     }
     // Lanes whose direction is not unit length within 1e-6 (the glass branch
     // reflects without renormalising) never cull.
@@ -218,6 +305,17 @@ __device__ __forceinline__ Hit find_closest(const AccelView &ac, const f3 &o, co
         // pass), so the ballot of the compare is the node mask: about 5 SALU per node
         // instead of 17.
         const float qoe = !active ? INFINITY : (no_cull ? -INFINITY : qo);
+#if SPT_PRETEST
+        // member pretest terms: the node test's -2c o and qoe, plus the tc slack
+        // mt = 2e-6 (pre_cm + |o|) + 1e-6 folded into -o.d
+        const float olen = __builtin_amdgcn_sqrtf(oo) * 1.000001f;
+        PreLane pl;
+        pl.osx = osx;
+        pl.osy = osy;
+        pl.osz = osz;
+        pl.qoe = qoe;
+        pl.tinit = !active ? -INFINITY : (no_cull ? INFINITY : __builtin_fmaf(2e-6f, ac.pre_cm + olen, 1e-6f) - dod);
+#endif
         auto node_x = [&](const uint32_t *r) {
             const float bx = __uint_as_float(r[0]), by = __uint_as_float(r[1]), bz = __uint_as_float(r[2]);
             const float cb2s = __uint_as_float(r[7]);  // c |Cb|^2
@@ -229,7 +327,11 @@ __device__ __forceinline__ Hit find_closest(const AccelView &ac, const f3 &o, co
         auto finish = [&](const uint32_t *r, float x) {
             const unsigned long long mm = __ballot(x <= __uint_as_float(r[6]));
             diag_node(mm);
-            if (mm != 0ull) test_leaf<LEAF>(slots, ac.orig, r[5], o, d, dod, h);
+#if SPT_PRETEST
+            if (mm != 0ull) test_leaf_pre<LEAF, true>(slots, (cfloat *)ac.kpre, ac.orig, r[5], o, d, dod, pl, h, dg);
+#else
+            if (mm != 0ull) test_leaf<LEAF>(slots, ac.orig, r[5], o, d, dod, h, dg);
+#endif
         };
         // The next record's load is issued only after this record's first use: a
         // scalar-load wait is lgkmcnt(0), so an earlier issue would be waited for here.
@@ -281,6 +383,14 @@ __device__ __forceinline__ Hit find_closest(const AccelView &ac, const f3 &o, co
         return (__builtin_amdgcn_sqrtf(best * 1.0001f) * (1.0f + 0x1p-20f) + (2e-5f * olen + 1e-6f)) * kq;
     };
     float sbe = near_term(h.best);
+#if SPT_PRETEST
+    PreLane pl;  // member pretest terms (see the flat list above), o unscaled
+    pl.osx = o.x;
+    pl.osy = o.y;
+    pl.osz = o.z;
+    pl.qoe = !active ? INFINITY : (no_cull ? -INFINITY : qo);
+    pl.tinit = !active ? -INFINITY : (no_cull ? INFINITY : __builtin_fmaf(2e-6f, ac.pre_cm + olen * 1.000001f, 1e-6f) - dod);
+#endif
     uint32_t i = 0;
     uint32_t nb[8];
 #pragma unroll
@@ -313,7 +423,11 @@ __device__ __forceinline__ Hit find_closest(const AccelView &ac, const f3 &o, co
             }
         }
         if (mm != 0ull && leaf) {
-            test_leaf<LEAF>(slots, ac.orig, leaf_slot, o, d, dod, h);
+#if SPT_PRETEST
+            test_leaf_pre<LEAF, false>(slots, (cfloat *)ac.kpre, ac.orig, leaf_slot, o, d, dod, pl, h, dg);
+#else
+            test_leaf<LEAF>(slots, ac.orig, leaf_slot, o, d, dod, h, dg);
+#endif
             sbe = near_term(h.best);
         }
         const uint32_t next = (mm != 0ull && !leaf) ? i + 1 : skip;

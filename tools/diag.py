@@ -28,4 +28,8 @@ tot = max(cc + cs + cr, 1)
 print(f"cycle shares: cast {cc/tot:.3f} shade {cs/tot:.3f} refill+ballot {cr/tot:.3f}")
 print(f"(lane, cluster) pairs that may pass per cast={pairs/max(st['casts'],1):.2f}; "
       f"lane efficiency of entered clusters={pairs/max(live,1):.3f}")
+sph, br, pas, imp = st["diag"][8:12]
+print(f"per wave cast: spheres tested={sph/max(it,1):.2f} update branches taken={br/max(it,1):.2f} "
+      f"({br/max(sph,1):.3f} of tested); lanes passing per taken branch={pas/max(br,1):.2f}; "
+      f"taken branches where some lane improves its winner={imp/max(br,1):.3f}")
 print(f"render_ms={st['render_ms']:.3f}")

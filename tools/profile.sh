@@ -4,7 +4,8 @@
 set -o pipefail
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 TAG=${1:-prof}; shift || true
-ARGS=${@:-"--steps 12 --warmup 4 --no-cpu-baseline --streams 1"}
+# default: the driver's own bench command (python bench.py, config 2, two frames in flight)
+ARGS=${@:-""}
 OUT="$R/gpurun_out/$TAG"
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp

@@ -409,3 +409,34 @@ def test_culling_is_exact(spt, ctx, golden_scenes, scene_name):
         ctx.set_cluster_size(9)  # clusters hold at most kClusterSlots = 8 members
     with pytest.raises(spt.SptError):
         ctx.set_cluster_tree(1)
+
+
+@pytest.mark.parametrize("shift,scale", [((3000.0, 0.0, -2000.0), 1.0), ((0.0, 0.0, 0.0), 1e-3),
+                                         ((-40.0, 7.0, 55.0), 30.0)])
+def test_culling_is_exact_far_and_scaled(spt, ctx, golden_scenes, shift, scale):
+    """The conservative node and member pretests carry margins that
+    grow with |C| + |o|; a scene translated far from the origin, shrunk to the scale
+    of the 1e-3 thresholds, or enlarged still renders bit-identically to brute force
+    (flat lists of 4-slot leaves and trees)."""
+    base = scene_from(spt, golden_scenes, "random")
+    c = np.array(base.centers, np.float32).copy()
+    c[:, :3] = (c[:, :3] * np.float32(scale) + np.float32(shift)).astype(np.float32)
+    scene = spt.Scene(c, (np.asarray(base.radii, np.float32) * np.float32(scale)).astype(np.float32),
+                      base.colors, base.materials, base.fuzz)
+    eye = [(e * scale + s) for e, s in zip(EYE[:3], shift)] + [0]
+    look = [(e * scale + s) for e, s in zip(LOOK[:3], shift)] + [0]
+    view = spt.camera_basis(eye, look, UP)
+    ctx.set_scene(scene)
+    ctx.set_camera(view, eye, SKY)
+    ctx.set_params(320, 200, 8, 50, 3)
+    outs = []
+    for k, b in ((0, 0), (spt._native.CLUSTER_AUTO, spt._native.TREE_AUTO), (8, 4)):
+        ctx.set_cluster_size(k)
+        ctx.set_cluster_tree(b)
+        ctx.reset_stats()
+        outs.append(((k, b), ctx.render_segment(0, 200, 0, 320), ctx.stats()["casts"]))
+    ctx.set_cluster_size(spt._native.CLUSTER_AUTO)
+    ctx.set_cluster_tree(spt._native.TREE_AUTO)
+    for kb, img, casts in outs[1:]:
+        assert_bitwise(img, outs[0][1], f"shift {shift} scale {scale}, culling {kb} vs brute force")
+        assert casts == outs[0][2]

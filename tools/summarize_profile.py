@@ -76,7 +76,7 @@ if tcfg:
         w = [sum(v) / len(v) for (k, c), v in agg.items() if short in k and c == "WRITE_SIZE"]
         if f and w:
             entry[kname] = {"fetch_bytes": int(2 * f[0] * 1024), "write_bytes": int(w[0] * 1024),
-                            "source": os.path.relpath(dst, os.path.join(os.path.dirname(tp)))}
+                            "source": os.path.relpath(os.path.abspath(dst), os.path.dirname(os.path.dirname(os.path.abspath(tp))))}
     doc[tcfg] = entry
     json.dump(doc, open(tp, "w"), indent=2)
 print("\n".join(out))

@@ -231,14 +231,16 @@ AccelTables build_accel(const float *centers4, const float *radii, uint32_t n, u
             };
             for (size_t j : ordered(top, 0, levels[top].size())) emit(emit, top, j);
             // expanded node tests (spt_path.h find_closest): flat lists
-            // keep K1' in rb and c |Cb|^2 in cb2; tree nodes F = Rb + 1e-4 (|Cb| + Rb)
+            // keep K1'' = K1' - c |Cb|^2 in rb and c |Cb|^2 in cb2; tree nodes F = Rb + 1e-4 (|Cb| + Rb)
             // in rb and (c - kTreeNodeErr) |Cb|^2 in cb2
             for (size_t q = base; q < t.nodes.size(); ++q) {
                 AccelNode &nd = t.nodes[q];
                 const double cbb = (double)nd.cx * nd.cx + (double)nd.cy * nd.cy + (double)nd.cz * nd.cz;
                 if (levels.size() == 1) {
-                    nd.rb = round_up((double)nd.k1 + 4e-6 * cbb);
+                    // K1'' = K1 + 4e-6 |Cb|^2 - c |Cb|^2: the kernel leaves c |Cb|^2 out of
+                    // the per-lane sum and compares against K1'' instead (one add fewer)
                     nd.cb2 = (float)(kFlatScale * cbb);
+                    nd.rb = round_up((double)nd.k1 + 4e-6 * cbb - (double)nd.cb2);
                 } else {
                     nd.rb = round_up((double)nd.rb + 1e-4 * (std::sqrt(cbb) + (double)nd.rb));
                     nd.cb2 = (float)((kFlatScale - kTreeNodeErr) * cbb);
@@ -270,6 +272,21 @@ AccelTables build_accel(const float *centers4, const float *radii, uint32_t n, u
                               std::sqrt((double)q.w));
     }
     t.pre_cm = round_up(cm * (1.0 + 1e-9));
+    // the always-list
+    double cma = 0;
+    bool fin = true;
+    for (size_t j = 0; j < cbase; ++j) {
+        if (t.orig[j] == 0xFFFFFFFFu) continue;
+        const float4 &q = t.slots[j];
+        fin = fin && std::isfinite(q.x) && std::isfinite(q.y) && std::isfinite(q.z) && std::isfinite(q.w);
+        if (fin)
+            cma = std::max(cma, std::sqrt((double)q.x * q.x + (double)q.y * q.y + (double)q.z * q.z) +
+                                    std::sqrt((double)q.w));
+    }
+    t.always_pre = fin && cma <= 1e15;
+    t.pre_cm_always = t.always_pre ? round_up(cma * (1.0 + 1e-9)) : INFINITY;
+    for (size_t j = 0; j < cbase; ++j)
+        t.kpre[j] = t.orig[j] == 0xFFFFFFFFu ? INFINITY : (t.always_pre ? pretest_k(t.slots[j]) : 0.f);
     if (!(cm <= 1e15)) {
         // squares near the float range: the pretest passes every lane (K' = -inf)
         t.pre_cm = INFINITY;
@@ -307,8 +324,22 @@ std::string validate_accel(const AccelTables &t, const float *centers4, const fl
     }
     for (uint32_t i = 0; i < n; ++i)
         if (!seen[i]) return bad("sphere %u missing from the slot table", i);
-    // member pretest constants (cluster slots)
+    // member pretest constants (cluster slots, and the always-list when it takes them)
     if (t.kpre.size() != t.slots.size()) return bad("pretest table size mismatch");
+    if (t.always_pre)
+        for (size_t j = 0; j < cbase; ++j) {
+            const float4 &q = t.slots[j];
+            if (t.orig[j] == 0xFFFFFFFFu) {
+                if (!(t.kpre[j] == INFINITY)) return bad("dummy always slot %zu: pretest can pass", j);
+                continue;
+            }
+            if (!(std::isfinite(q.x) && std::isfinite(q.y) && std::isfinite(q.z) && std::isfinite(q.w)))
+                return bad("always slot %zu: non-finite sphere behind the pretest", j);
+            if (!(t.kpre[j] == pretest_k(q))) return bad("always slot %zu: pretest K' wrong", j);
+            const double cl = std::sqrt((double)q.x * q.x + (double)q.y * q.y + (double)q.z * q.z);
+            if (!((double)t.pre_cm_always >= cl + std::sqrt((double)q.w)) || !(t.pre_cm_always <= 1.1e15f))
+                return bad("always slot %zu: outside the pretest bound", j);
+        }
     for (size_t j = cbase; j < t.slots.size(); ++j) {
         const float4 &q = t.slots[j];
         if (t.orig[j] == 0xFFFFFFFFu) {
@@ -338,13 +369,13 @@ std::string validate_accel(const AccelTables &t, const float *centers4, const fl
                     return bad("layout %u node %u: leaf slot %u out of range", oct, i, nd.slot);
             }
             // containment of every member below (Rb = max |Cm - Cb| + r over the members):
-            // flat lists: Rb <= sqrt((K1 - 1e-5) / 1.15), K1' >= K1 + 4e-6 |Cb|^2 and
+            // flat lists: Rb <= sqrt((K1 - 1e-5) / 1.15), K1'' >= K1 + 4e-6 |Cb|^2 - cb2 and
             // cb2 = c |Cb|^2; tree nodes: K1 >= 1.15 Rb^2 + 1e-5, F >= Rb + 1e-4 (|Cb| + Rb)
             // and cb2 = (c - kTreeNodeErr) |Cb|^2
             const bool flat = t.n_nodes == t.leaves;
             const double cbb = (double)nd.cx * nd.cx + (double)nd.cy * nd.cy + (double)nd.cz * nd.cz;
             if (flat && !(std::fabs((double)nd.cb2 - kFlatScale * cbb) <= 2e-7 * cbb &&
-                          (double)nd.rb >= (double)nd.k1 + 4e-6 * cbb))
+                          (double)nd.rb >= (double)nd.k1 + 4e-6 * cbb - (double)nd.cb2))
                 return bad("layout %u node %u: flat-list |Cb|^2 or K1' wrong", oct, i);
             if (!flat && !(std::fabs((double)nd.cb2 - (kFlatScale - kTreeNodeErr) * cbb) <= 1e-7 * cbb))
                 return bad("layout %u node %u: tree-node scaled |Cb|^2 wrong", oct, i);

@@ -19,7 +19,8 @@ struct AccelNode {
     uint32_t skip;     // next node when this one is culled (or is a leaf)
     uint32_t slot;     // leaf: first of its leaf_slots slots; inner: kNoSlot
     float rb;          // tree nodes: bounding radius Rb (rounded up);
-                       // flat lists: K1' = K1 + 4e-6 |Cb|^2 (rounded up), the expanded-form margin
+                       // flat lists: K1'' = K1 + 4e-6 |Cb|^2 - cb2 (rounded up), the expanded-form
+                       // margin less the node's c |Cb|^2 term
     float cb2;         // |Cb|^2 (flat lists' expanded line test)
 };
 
@@ -40,6 +41,11 @@ struct AccelTables {
     // cluster members (rounded up)
     std::vector<float> kpre;
     float pre_cm = 0.f;
+    // the always-list's pretest (every always sphere finite and Cm <= 1e15; else its
+    // spheres take the reference test directly): K' per always slot as above, +inf
+    // for its dummies, and its own bound
+    bool always_pre = false;
+    float pre_cm_always = 0.f;
 };
 
 // cluster_k: members per cluster (0, or n <= 32: every sphere is "always" tested).

@@ -466,7 +466,8 @@ int rebuild_accel(spt_ctx *ctx)
     if (!rc) rc = upload(ctx, &ctx->d_kpre, &ctx->kpre_cap, t.kpre);
     if (rc) return rc;
     ctx->accel = spt::AccelView{ctx->d_slots, ctx->d_orig, ctx->d_nodes, t.always_groups, t.n_nodes,
-                                t.n_nodes > t.leaves ? 1u : 0u, t.leaf_slots, ctx->d_kpre, t.pre_cm};
+                                t.n_nodes > t.leaves ? 1u : 0u, t.leaf_slots, ctx->d_kpre, t.pre_cm,
+                                t.pre_cm_always, t.always_pre ? 1u : 0u};
     ctx->tables = std::move(t);
     return SPT_OK;
 }

@@ -169,6 +169,8 @@ struct AccelView {
     uint32_t leaf_slots;  // slots per leaf: kFlatLeafSlots or kClusterSlots
     const float *kpre;    // member pretest constant K' per slot (spt_accel.h)
     float pre_cm;         // >= max |C| + r over the cluster members
+    float pre_cm_always;  // >= max |C| + r over the always-tested spheres
+    uint32_t always_pre;  // 1: the always-list takes the pretest (all finite, bounded)
 };
 
 struct DeviceScene {

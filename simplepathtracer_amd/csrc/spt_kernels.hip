@@ -29,10 +29,11 @@ namespace spt {
 #ifndef SPT_WAVES_PER_EU
 #define SPT_WAVES_PER_EU 0
 #endif
-// 80 SGPRs (with SPT_KERNARG_RELOAD) lets 8 waves per SIMD be resident instead of
-// 6 at the uncapped 106; 0 = no cap
+// SGPR cap of the render kernels (with SPT_KERNARG_RELOAD); 0 = no cap.  80 lets 8
+// waves per SIMD be resident, 81-96 seven, the uncapped 106 six; since the member
+// pretest 96 (7 waves, fewer SGPR spills) measures faster than 80
 #ifndef SPT_NUM_SGPR
-#define SPT_NUM_SGPR 80
+#define SPT_NUM_SGPR 96
 #endif
 #if SPT_WAVES_PER_EU
 #define SPT_RENDER_ATTR __attribute__((amdgpu_waves_per_eu(SPT_WAVES_PER_EU, SPT_WAVES_PER_EU)))
@@ -310,6 +311,14 @@ hipError_t render_occupancy(uint32_t block, int *blocks_per_cu)
     if (e == hipSuccess)
         e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&c, render_kernel<false, (int)kClusterSlots>, (int)block, 0);
     *blocks_per_cu = a < b ? (a < c ? a : c) : (b < c ? b : c);
+    // the occupancy API reports one block per CU too many at 81-96 and 97-112 SGPRs
+    // (MI355X_MICROARCH.md, Correctness boundaries): waves per SIMD are bounded by
+    // 800 / (ceil(sgpr / 16) * 16 + 16) SGPRs; 256-thread blocks = 1 wave per SIMD
+    if (SPT_NUM_SGPR > 0) {
+        // .sgpr_count = the cap minus the 2 VCC registers
+        const int cap = 800 / (((SPT_NUM_SGPR - 2 + 15) / 16) * 16 + 16);
+        if (*blocks_per_cu > cap) *blocks_per_cu = cap;
+    }
     return e;
 }
 

@@ -19,8 +19,8 @@
 #endif
 
 // 1: the megakernel's start_path reads its parameters from the kernarg segment
-// where used instead of holding them in SGPRs (with the 80-SGPR cap of
-// spt_kernels.hip: 8 resident waves per SIMD instead of 6)
+// where used instead of holding them in SGPRs (with the SGPR cap of
+// spt_kernels.hip: 7-8 resident waves per SIMD instead of 6)
 #ifndef SPT_KERNARG_RELOAD
 #define SPT_KERNARG_RELOAD 1
 #endif
@@ -29,6 +29,25 @@
 // test_group_pre (10 VALU per member instead of 18)
 #ifndef SPT_PRETEST
 #define SPT_PRETEST 1
+#endif
+
+// 1: the always-tested spheres behind the pretest too (finite scenes; measured 2.4%
+// slower on config 2: the ground passes for about half the rays, so its pretest
+// mostly adds the exact retest)
+#ifndef SPT_ALWAYS_PRE
+#define SPT_ALWAYS_PRE 0
+#endif
+// 1: leaf tables addressed by 32-bit byte offsets (SGPR-offset scalar loads)
+#ifndef SPT_LEAF_BYTEOFF
+#define SPT_LEAF_BYTEOFF 1
+#endif
+// 1: the tie mask of update_member as the AND of compare ballots (no VGPR round trip)
+#ifndef SPT_TIE_MASKS
+#define SPT_TIE_MASKS 1
+#endif
+// 1: flat node records loaded as one s_load_dwordx8 each
+#ifndef SPT_NODE_X8
+#define SPT_NODE_X8 1
 #endif
 
 // 1: the cube-minus-ball rejection loop runs cooperatively across the wave
@@ -98,7 +117,8 @@ __device__ __forceinline__ void update_member(bool pass, float tc, float hh, con
     // CalculateRaySphereClosestContactPoint, Collision.hpp:19-27,49-56
     const float t = tc - sqrt_pos_normal(hh);
     const f3 p = mk(o.x + d.x * t, o.y + d.y * t, o.z + d.z * t);
-    const bool ok = pass && dod < dot(p, d);
+    const bool front = dod < dot(p, d);
+    const bool ok = pass && front;
     const float ds = lensq(sub(o, p));
     bool better = ok && ds < h.best;
     // exact tie (rare): the first original index wins.  Behind a wave-uniform
@@ -106,7 +126,13 @@ __device__ __forceinline__ void update_member(bool pass, float tc, float hh, con
     // load here made every cast wait on vmcnt(0), i.e. on the previous shading
     // step's sample stores.
     const bool tie = ok && ds == h.best && h.idx != kMiss;
+#if SPT_TIE_MASKS
+    // the ballot of a compare is its own lane mask; a ballot of the combined bool
+    // would go through a VGPR (v_cndmask + v_cmp) first
+    unsigned long long tm = __ballot(pass) & __ballot(front) & __ballot(ds == h.best) & __ballot(h.idx != kMiss);
+#else
     unsigned long long tm = __ballot(tie);
+#endif
     if (__builtin_expect(tm != 0ull, 0)) {
         const uint32_t mo = ((cuint *)orig)[s];
         while (tm != 0ull) {
@@ -230,12 +256,20 @@ __device__ __forceinline__ void test_leaf_pre(cfloat *slots, cfloat *kpre, const
                                               uint32_t leaf_slot, const f3 &o, const f3 &d, float dod,
                                               const PreLane &pl, Hit &h, CastDiag &dg)
 {
+    // 32-bit byte offsets off the table bases: the loads take them as SGPR offsets
+    // (no 64-bit address arithmetic on the scalar unit)
+#if SPT_LEAF_BYTEOFF
+    typedef __attribute__((address_space(4))) const char cchar;
+    cfloat *cs = (cfloat *)((cchar *)slots + (leaf_slot << 4));
+    cfloat *kb = (cfloat *)((cchar *)kpre + (leaf_slot << 2));
+#else
     cfloat *cs = slots + 4 * leaf_slot;
+    cfloat *kb = kpre + leaf_slot;
+#endif
     float4 ms[S];
     float kp[S];
 #pragma unroll
     for (int k = 0; k < S; ++k) ms[k] = ld_uniform(cs, k);
-    cfloat *kb = kpre + leaf_slot;  // one s_load_dwordx4 (S = 4) off a 64-bit base
 #pragma unroll
     for (int k = 0; k < S; ++k) kp[k] = kb[k];
     test_group_pre<S, PRESCALED>(ms, kp, orig, leaf_slot, o, d, dod, pl, h, dg);
@@ -257,38 +291,56 @@ __device__ __forceinline__ Hit find_closest(const AccelView &ac, const f3 &o, co
     h.p = o;
     const float dod = dot(o, d);
     cfloat *slots = (cfloat *)ac.slots;
-    // always-tested spheres (ground, large balls; every sphere when culling is off)
-    for (uint32_t g = 0; g < ac.always_groups; ++g) {
-        float4 g4[SPT_GROUP];
-#pragma unroll
-        for (int k = 0; k < SPT_GROUP; ++k) g4[k] = ld_uniform(slots, g * SPT_GROUP + k);
-        test_group<SPT_GROUP>(g4, ac.orig, g * SPT_GROUP, o, d, dod, h, dg);
-    }
     // Lanes whose direction is not unit length within 1e-6 (the glass branch
     // reflects without renormalising) never cull.
     const float ddev = lensq(d) - 1.0f;
     const bool no_cull = active && !(ddev <= 1e-6f && ddev >= -1e-6f);
-    const unsigned long long live_mask = __ballot(active);
-    // node masks are formed as (ballot(test) & live) | nocull: the ballot of a
-    // compare is the compare's own lane mask, with no VALU round trip
-    const unsigned long long nocull_mask = __ballot(no_cull);
-    cuint *nodes = (cuint *)ac.nodes;
     // per-lane terms of the expanded node tests (flat and tree):
     // c |Cb-o|^2 - 4.1e-6 |o|^2 = c |Cb|^2 + (-2c o).Cb + (c - 4.1e-6) |o|^2, c = kFlatScale
     const float oo = lensq(o);
     const float qo = (float)(kFlatScale - 4.1e-6) * oo;
     const float m2c = (float)(-2.0 * kFlatScale);
     const float osx = m2c * o.x, osy = m2c * o.y, osz = m2c * o.z;
+    // always-tested spheres (ground, large balls; every sphere when culling is off)
+#if SPT_PRETEST && SPT_ALWAYS_PRE
+    if (ac.always_pre) {
+        // behind the member pretest with the always-list's own bound Cm
+        PreLane pa;
+        pa.osx = osx;
+        pa.osy = osy;
+        pa.osz = osz;
+        pa.qoe = !active ? INFINITY : (no_cull ? -INFINITY : qo);
+        pa.tinit = !active ? -INFINITY
+                           : (no_cull ? INFINITY
+                                      : __builtin_fmaf(2e-6f, ac.pre_cm_always + __builtin_amdgcn_sqrtf(oo) * 1.000001f,
+                                                       1e-6f) - dod);
+        for (uint32_t g = 0; g < ac.always_groups; ++g)
+            test_leaf_pre<SPT_GROUP, true>(slots, (cfloat *)ac.kpre, ac.orig, g * SPT_GROUP, o, d, dod, pa, h, dg);
+    } else
+#endif
+    {
+        for (uint32_t g = 0; g < ac.always_groups; ++g) {
+            float4 g4[SPT_GROUP];
+#pragma unroll
+            for (int k = 0; k < SPT_GROUP; ++k) g4[k] = ld_uniform(slots, g * SPT_GROUP + k);
+            test_group<SPT_GROUP>(g4, ac.orig, g * SPT_GROUP, o, d, dod, h, dg);
+        }
+    }
+    const unsigned long long live_mask = __ballot(active);
+    // node masks are formed as (ballot(test) & live) | nocull: the ballot of a
+    // compare is the compare's own lane mask, with no VALU round trip
+    const unsigned long long nocull_mask = __ballot(no_cull);
+    cuint *nodes = (cuint *)ac.nodes;
     if (!TREE) {
         // flat list: node i is leaf i.  The line test in expanded form, with FMAs
         // (a conservative test need not follow the reference's operation order;
         // DESIGN.md §4.4): keep iff
         //   d2b <= K1 + 1e-4 |Cb-o|^2 + 4e-6 |Cb|^2 + 4.1e-6 |o|^2,   d2b = |Cb-o|^2 - tcb^2,
-        // evaluated as  c |Cb|^2 - 2c Cb.o + (c - 4.1e-6) |o|^2 - tcb^2 <= K1'  with
-        // c = kFlatScale = 1 - 1e-4, tcb = Cb.d - o.d and K1' = K1 + 4e-6 |Cb|^2
+        // evaluated as  -2c Cb.o + (c - 4.1e-6) |o|^2 - tcb^2 <= K1''  with
+        // c = kFlatScale = 1 - 1e-4, tcb = Cb.d - o.d and K1'' = K1 + 4e-6 |Cb|^2 - c |Cb|^2
         // (rounded up).  The absolute terms cover the expansion's rounding
-        // (<= 2.7e-6 (|Cb|^2 + |o|^2)).  Per node: 3 FMA (tcb), 3 FMA + 1 add (the
-        // scaled |Cb-o|^2), 1 FMA, 1 compare = 9 VALU.
+        // (<= 2.7e-6 (|Cb|^2 + |o|^2)).  Per node: 3 FMA (tcb), 3 FMA (the scaled
+        // |Cb-o|^2 less c |Cb|^2), 1 FMA, 1 compare = 8 VALU.
         auto diag_node = [&](unsigned long long mm) {
             if (SPT_DIAG) {
                 dg.nodes += 1;
@@ -316,14 +368,15 @@ __device__ __forceinline__ Hit find_closest(const AccelView &ac, const f3 &o, co
         pl.qoe = qoe;
         pl.tinit = !active ? -INFINITY : (no_cull ? INFINITY : __builtin_fmaf(2e-6f, ac.pre_cm + olen, 1e-6f) - dod);
 #endif
+        // c |Cb|^2 is left out of the sum: the node's threshold is K1'' = K1' - c |Cb|^2
+        // (one rounding fewer)
         auto node_x = [&](const uint32_t *r) {
             const float bx = __uint_as_float(r[0]), by = __uint_as_float(r[1]), bz = __uint_as_float(r[2]);
-            const float cb2s = __uint_as_float(r[7]);  // c |Cb|^2
             const float tcb = __builtin_fmaf(bx, d.x, __builtin_fmaf(by, d.y, __builtin_fmaf(bz, d.z, -dod)));
-            const float w = __builtin_fmaf(bx, osx, __builtin_fmaf(by, osy, __builtin_fmaf(bz, osz, qoe))) + cb2s;
+            const float w = __builtin_fmaf(bx, osx, __builtin_fmaf(by, osy, __builtin_fmaf(bz, osz, qoe)));
             return __builtin_fmaf(-tcb, tcb, w);
         };
-        // the node's mask (vs K1') and leaf test; `x` from node_x(r)
+        // the node's mask (vs K1'') and leaf test; `x` from node_x(r)
         auto finish = [&](const uint32_t *r, float x) {
             const unsigned long long mm = __ballot(x <= __uint_as_float(r[6]));
             diag_node(mm);
@@ -337,19 +390,33 @@ __device__ __forceinline__ Hit find_closest(const AccelView &ac, const f3 &o, co
         // scalar-load wait is lgkmcnt(0), so an earlier issue would be waited for here.
         cuint *p = nodes;
         uint32_t ra[8], rb[8];
+#if SPT_NODE_X8
+        // the whole record in one s_load_dwordx8 (the compiler would load only the six
+        // dwords the flat test uses, as four loads); the empty asm keeps all eight
+        typedef uint32_t u32x8 __attribute__((ext_vector_type(8)));
+        typedef __attribute__((address_space(4))) const u32x8 cu32x8;
+        auto load_rec = [&](cuint *q, uint32_t(&r)[8]) {
+            u32x8 v = *(cu32x8 *)q;
+            asm volatile("" : "+s"(v));
 #pragma unroll
-        for (int q = 0; q < 8; ++q) ra[q] = p[q];
+            for (int i = 0; i < 8; ++i) r[i] = v[i];
+        };
+#else
+        auto load_rec = [&](cuint *q, uint32_t(&r)[8]) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) r[i] = q[i];
+        };
+#endif
+        load_rec(p, ra);
         uint32_t left = ac.n_nodes;
         while (left >= 2u) {
             const float xa = node_x(ra);
             __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int q = 0; q < 8; ++q) rb[q] = p[8 + q];
+            load_rec(p + 8, rb);
             finish(ra, xa);
             const float xb = node_x(rb);
             __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int q = 0; q < 8; ++q) ra[q] = p[16 + q];
+            load_rec(p + 16, ra);
             finish(rb, xb);
             p += 16;
             left -= 2u;

@@ -26,6 +26,12 @@
 namespace spt {
 
 
+#ifndef SPT_DUP_START
+#define SPT_DUP_START 0
+#endif
+#ifndef SPT_DUP_CAST
+#define SPT_DUP_CAST 0
+#endif
 #ifndef SPT_WAVES_PER_EU
 #define SPT_WAVES_PER_EU 0
 #endif
@@ -38,7 +44,10 @@ namespace spt {
 #if SPT_WAVES_PER_EU
 #define SPT_RENDER_ATTR __attribute__((amdgpu_waves_per_eu(SPT_WAVES_PER_EU, SPT_WAVES_PER_EU)))
 #elif SPT_NUM_SGPR
-#define SPT_RENDER_ATTR __attribute__((amdgpu_num_sgpr(SPT_NUM_SGPR)))
+// the SGPR cap's wave count also bounds the VGPRs (7 waves: 72) so that registers
+// never become the tighter limit
+#define SPT_CAP_WAVES (800 / (((SPT_NUM_SGPR - 2 + 15) / 16) * 16 + 16) > 8 ? 8 : 800 / (((SPT_NUM_SGPR - 2 + 15) / 16) * 16 + 16))
+#define SPT_RENDER_ATTR __attribute__((amdgpu_num_sgpr(SPT_NUM_SGPR), amdgpu_waves_per_eu(SPT_CAP_WAVES)))
 #else
 #define SPT_RENDER_ATTR
 #endif
@@ -71,6 +80,7 @@ __global__ __launch_bounds__(kRenderBlock) SPT_RENDER_ATTR void render_kernel(Re
     uint32_t pend = 0;
     if (lane == 0) pend = atomicAdd(a.head, a.claim);
     bool exhausted = false;
+    uint32_t glass_wait = 0;  // iterations since a lane parked at glass (wave-uniform)
     unsigned long long casts = 0, done = 0, dropped = 0;
     unsigned long long d_iters = 0, d_cyc_cast = 0, d_cyc_shade = 0, d_cyc_refill = 0;
     CastDiag dg;
@@ -117,24 +127,57 @@ __global__ __launch_bounds__(kRenderBlock) SPT_RENDER_ATTR void render_kernel(Re
             if (ps.phase == PH_IDLE && mine != 0xFFFFFFFFu) {
 #if SPT_KERNARG_RELOAD && defined(__HIP_DEVICE_COMPILE__)
                 start_path_kernarg(mine, rows, ps);
+#if SPT_DUP_START
+                {
+                    Path p2 = ps;  // timing experiment only: a second, discarded refill
+                    uint32_t m2 = mine;
+                    asm volatile("" : "+v"(m2));
+                    start_path_kernarg(m2, rows, p2);
+                    asm volatile("" ::"v"(p2.d.x), "v"(p2.d.y), "v"(p2.d.z), "v"((uint32_t)p2.st));
+                }
+#endif
 #else
                 start_path(a, mine, rows, rw, rh, eye, ps);
 #endif
             }
         }
-        const unsigned long long live = __ballot(ps.phase != PH_IDLE);
+#if SPT_GLASS_PARK
+        // ---- parked glass hits: refracted together once enough wait, one waited
+        // long enough, or nothing else is left to cast
+        {
+            const unsigned long long parked = __ballot(ps.phase == PH_GLASS);
+            if (parked != 0ull) {
+                ++glass_wait;
+                const unsigned long long castable = __ballot(ps.phase == PH_TRACE || ps.phase == PH_DLOOP);
+                if (__popcll(parked) >= SPT_GLASS_BATCH || glass_wait >= SPT_GLASS_WAIT || castable == 0ull) {
+                    glass_step(a, ps, ps.phase == PH_GLASS, done, dropped);
+                    glass_wait = 0;
+                }
+            }
+        }
+#endif
+        const unsigned long long live = __ballot(ps.phase == PH_TRACE || ps.phase == PH_DLOOP);
         if (live == 0ull) {
-            if (exhausted) break;
+            if (exhausted && __ballot(ps.phase != PH_IDLE) == 0ull) break;
             continue;
         }
         SPT_STAMP(d_cyc_refill);
         casts += (unsigned long long)__popcll(live);
         ++d_iters;
         // ---- one cast + one shading step ----
-        const bool act = ps.phase != PH_IDLE;
+        const bool act = ps.phase == PH_TRACE || ps.phase == PH_DLOOP;
         const Hit h = find_closest<TREE, LEAF>(a.scene.accel, ps.o, ps.d, act, dg);
+#if SPT_DUP_CAST
+        {
+            // timing experiment only: a second, discarded cast (its marginal cost)
+            f3 o2 = ps.o;
+            asm volatile("" : "+v"(o2.x));
+            const Hit h2 = find_closest<TREE, LEAF>(a.scene.accel, o2, ps.d, act, dg);
+            asm volatile("" ::"v"(h2.idx), "v"(h2.best), "v"(h2.p.x));
+        }
+#endif
         SPT_STAMP(d_cyc_cast);
-        shade_step(a, ps, h, act, done, dropped, s_lds + (threadIdx.x & ~63u));
+        shade_step<true>(a, ps, h, act, done, dropped, s_lds + (threadIdx.x & ~63u));
         SPT_STAMP(d_cyc_shade);
     }
 

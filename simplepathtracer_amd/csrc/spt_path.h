@@ -50,6 +50,30 @@
 #define SPT_NODE_X8 1
 #endif
 
+#ifndef SPT_DUP_BALL
+#define SPT_DUP_BALL 0
+#endif
+
+// 1: a leaf's member pretests all run before its first branch
+#ifndef SPT_PRE_ILP
+#define SPT_PRE_ILP 1
+#endif
+
+// 1: the megakernel parks glass hits and refracts them in batches: the refraction
+// step (double-precision Schlick / Snell, two normalizes) otherwise runs in ~92% of
+// wave-iterations for ~4% of the lanes.  Measured neutral on config 2 (off)
+#ifndef SPT_GLASS_PARK
+#define SPT_GLASS_PARK 0
+#endif
+// glass_step runs once SPT_GLASS_BATCH lanes are parked, or SPT_GLASS_WAIT
+// iterations after the first one parked, or when no lane is left to cast
+#ifndef SPT_GLASS_BATCH
+#define SPT_GLASS_BATCH 6
+#endif
+#ifndef SPT_GLASS_WAIT
+#define SPT_GLASS_WAIT 4
+#endif
+
 // 1: the cube-minus-ball rejection loop runs cooperatively across the wave
 #ifndef SPT_COOP_BALL
 #define SPT_COOP_BALL 1
@@ -70,6 +94,9 @@ namespace spt {
 namespace {
 
 constexpr uint32_t PH_IDLE = 0, PH_TRACE = 1, PH_DLOOP = 2;
+// megakernel only: a path that hit glass waits here, its contact point in o and the
+// glass slot in gidx, until the wave runs the refraction step for a batch of them
+constexpr uint32_t PH_GLASS = 3;
 
 // rSq of SampleColorRefractive (lines 58 and 75): float(pow(double(-0.2f), 2)).
 // The exact square of a float is representable in double, so pow returns it.
@@ -222,6 +249,21 @@ __device__ __forceinline__ void test_group_pre(const float4 (&sp)[G], const floa
         }
         pre[k] = __builtin_fminf(tcs, __builtin_fmaf(tcs, tcs, -w)) > 1e-3f;
     }
+#if SPT_PRE_ILP
+    // all G pretests before the first branch (independent chains in flight
+    // together), and one branch past the group when no lane passes any member
+    unsigned long long pm[G], any = 0ull;
+#pragma unroll
+    for (int k = 0; k < G; ++k) {
+        pm[k] = __ballot(pre[k]);
+        any |= pm[k];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if (any == 0ull) {
+        if (SPT_DIAG) dg.spheres += G;
+        return;
+    }
+#endif
 #pragma unroll
     for (int k = 0; k < G; ++k) {
         if (SPT_DIAG) {
@@ -229,7 +271,11 @@ __device__ __forceinline__ void test_group_pre(const float4 (&sp)[G], const floa
             dg.branches += __ballot(pre[k]) != 0ull ? 1 : 0;
             dg.passing += (unsigned long long)__popcll(__ballot(pre[k]));
         }
+#if SPT_PRE_ILP
+        if (pm[k] != 0ull) {
+#else
         if (__ballot(pre[k]) != 0ull) {
+#endif
             float tc, hh;
             const bool pass = ray_sphere(sp[k], o, d, tc, hh);
             if (__ballot(pass) != 0ull) update_member(pass, tc, hh, orig, slot + k, o, d, dod, h, dg);
@@ -510,6 +556,7 @@ __device__ __forceinline__ Hit find_closest(const AccelView &ac, const f3 &o, co
 // Per-lane path state of the flattened recursion.
 struct Path {
     uint32_t phase, item, bounce, spec;
+    uint32_t gidx;  // PH_GLASS: slot of the glass sphere hit
     uint64_t st;  // keyed splitmix stream of this (pixel, sample)
     f3 o, d, c;
 };
@@ -570,11 +617,81 @@ __device__ __forceinline__ f3 coop_ball_vector(uint64_t &st, bool need, uint32_t
     return r;
 }
 
+// SampleColorRefractive (SingleThreadPathTracer.hpp:48-92) for a lane whose ray hit
+// the glass slot idx at the contact point ps.o: new ps.o (exit point) and ps.d.
+__device__ __forceinline__ void refract_event(const RenderArgs &a, Path &ps, uint32_t idx)
+{
+    const float4 cs = a.scene.accel.slots[idx];
+    const f3 C = mk(cs.x, cs.y, cs.z);
+    const f3 nrm = normalize(sub(ps.o, C));
+    const f3 d = ps.d;
+    const float cc = dot(neg(nrm), d);
+    f3 nd;
+    if (uniform(ps.st, 0.f, 1.f) < schlick(kRsq, cc)) {
+        nd = reflect(d, nrm);
+    } else if (no_tir(kAirToGlass, cc)) {
+        const f3 d2 = refract_dir(d, nrm, kAirToGlass, cc);
+        // CalculateRaySphereFarthestContactPoint, Collision.hpp:29-37,58-65
+        const f3 rs = sub(C, ps.o);
+        const float tc = dot(rs, d2);
+        const float dd = lensq(rs) - tc * tc;
+        const float t = tc + __builtin_sqrtf(cs.w - dd);
+        ps.o = mk(ps.o.x + d2.x * t, ps.o.y + d2.y * t, ps.o.z + d2.z * t);
+        const f3 n2 = neg(normalize(sub(ps.o, C)));
+        const float c2 = dot(neg(n2), d2);
+        if (uniform(ps.st, 0.f, 1.f) < schlick(kRsq, c2))
+            nd = reflect(d2, n2);
+        else if (no_tir(kGlassToAir, c2))
+            nd = refract_dir(d2, n2, kGlassToAir, c2);
+        else
+            nd = reflect(d2, n2);
+    } else {
+        nd = reflect(d, nrm);
+    }
+    ps.d = nd;
+}
+
+// The tail of a shading step: the specular-event cap (RenderSegmentTask's pass limit,
+// the safety cap) and, for finishing paths, the sample slot write.
+__device__ __forceinline__ void finish_step(const RenderArgs &a, Path &ps, bool fin, bool spec_event, float counted,
+                                            f3 col, unsigned long long &done, unsigned long long &dropped)
+{
+    if (spec_event) {
+        ++ps.spec;
+        if (a.mode == 1u && ps.spec >= kTaskPasses) {
+            // RenderSegmentTask: this path would be processed in pass 10, which never runs
+            fin = true;
+            counted = 0.f;
+            col = mk(0.f, 0.f, 0.f);
+            ++dropped;
+        } else if (ps.spec > kSpecularCap) {
+            fin = true;
+            col = mk(0.f, 0.f, 0.f);
+        }
+    }
+    if (fin) {
+        if (a.mode == 0u) {
+            // RenderSegment counts every sample: 12-byte slots
+            float *o3 = a.samples + (size_t)3 * ps.item;
+            o3[0] = col.x;
+            o3[1] = col.y;
+            o3[2] = col.z;
+        } else {
+            *(float4 *)(a.samples + (size_t)4 * ps.item) = make_float4(col.x, col.y, col.z, counted);
+        }
+        ps.phase = PH_IDLE;
+        ps.d = mk(0.f, 0.f, 0.f);
+        ++done;
+    }
+}
+
 // One shading step after a cast: the material switch of TraceAndSampleColor
 // (SingleThreadPathTracer.hpp:94-112) in PH_TRACE, or one turn of the diffuse
 // bounce loop (21-37) in PH_DLOOP.  Finishing paths write their sample slot.
 // Called by every lane of the wave (`act` = the lane holds a path), so the
 // cooperative cube-minus-ball sampler runs in uniform control flow.
+// PARK (megakernel): glass hits are parked for glass_step instead of shaded here.
+template <bool PARK>
 __device__ __forceinline__ void shade_step(const RenderArgs &a, Path &ps, const Hit &h, bool act,
                                            unsigned long long &done, unsigned long long &dropped, uint32_t *lds)
 {
@@ -615,6 +732,14 @@ __device__ __forceinline__ void shade_step(const RenderArgs &a, Path &ps, const 
     bool spec_event = false;
 #if SPT_COOP_BALL
     const f3 rv_coop = coop_ball_vector(ps.st, scatter, lds);
+#if SPT_DUP_BALL
+    {
+        uint64_t st2 = ps.st;  // timing experiment only: a second, discarded sampler run
+        asm volatile("" : "+v"(st2));
+        const f3 r2 = coop_ball_vector(st2, scatter, lds);
+        asm volatile("" ::"v"(r2.x), "v"(r2.y), "v"(r2.z));
+    }
+#endif
 #else
     (void)lds;
 #endif
@@ -646,66 +771,34 @@ __device__ __forceinline__ void shade_step(const RenderArgs &a, Path &ps, const 
         }
         ps.d = normalize(add(base, rv));
     }
-    if (refr) {
-        // SampleColorRefractive, lines 48-92
-        const float4 cs = hit[idx];
-        const f3 C = mk(cs.x, cs.y, cs.z);
+#if SPT_GLASS_PARK
+    if (PARK && refr) {
+        // park: the refraction runs later, for a batch of the wave's glass hits
+        // (glass_step); the path's arithmetic is unchanged
         ps.o = h.p;
-        const f3 nrm = normalize(sub(ps.o, C));
-        const f3 d = ps.d;
-        const float cc = dot(neg(nrm), d);
-        f3 nd;
-        if (uniform(ps.st, 0.f, 1.f) < schlick(kRsq, cc)) {
-            nd = reflect(d, nrm);
-        } else if (no_tir(kAirToGlass, cc)) {
-            const f3 d2 = refract_dir(d, nrm, kAirToGlass, cc);
-            // CalculateRaySphereFarthestContactPoint, Collision.hpp:29-37,58-65
-            const f3 rs = sub(C, ps.o);
-            const float tc = dot(rs, d2);
-            const float dd = lensq(rs) - tc * tc;
-            const float t = tc + __builtin_sqrtf(cs.w - dd);
-            ps.o = mk(ps.o.x + d2.x * t, ps.o.y + d2.y * t, ps.o.z + d2.z * t);
-            const f3 n2 = neg(normalize(sub(ps.o, C)));
-            const float c2 = dot(neg(n2), d2);
-            if (uniform(ps.st, 0.f, 1.f) < schlick(kRsq, c2))
-                nd = reflect(d2, n2);
-            else if (no_tir(kGlassToAir, c2))
-                nd = refract_dir(d2, n2, kGlassToAir, c2);
-            else
-                nd = reflect(d2, n2);
-        } else {
-            nd = reflect(d, nrm);
-        }
-        ps.d = nd;
+        ps.gidx = idx;
+        ps.phase = PH_GLASS;
+        refr = false;
+    }
+#endif
+    if (refr) {
+        ps.o = h.p;
+        refract_event(a, ps, idx);
         spec_event = true;
     }
-    if (spec_event) {
-        ++ps.spec;
-        if (a.mode == 1u && ps.spec >= kTaskPasses) {
-            // RenderSegmentTask: this path would be processed in pass 10, which never runs
-            fin = true;
-            counted = 0.f;
-            col = mk(0.f, 0.f, 0.f);
-            ++dropped;
-        } else if (ps.spec > kSpecularCap) {
-            fin = true;
-            col = mk(0.f, 0.f, 0.f);
-        }
+    finish_step(a, ps, fin, spec_event, counted, col, done, dropped);
+}
+
+// The wave's parked glass hits (PH_GLASS lanes; `go` = this lane is one), shaded
+// together: SampleColorRefractive then the specular-event bookkeeping of shade_step.
+__device__ __forceinline__ void glass_step(const RenderArgs &a, Path &ps, bool go, unsigned long long &done,
+                                           unsigned long long &dropped)
+{
+    if (go) {
+        refract_event(a, ps, ps.gidx);
+        ps.phase = PH_TRACE;
     }
-    if (fin) {
-        if (a.mode == 0u) {
-            // RenderSegment counts every sample: 12-byte slots
-            float *o3 = a.samples + (size_t)3 * ps.item;
-            o3[0] = col.x;
-            o3[1] = col.y;
-            o3[2] = col.z;
-        } else {
-            *(float4 *)(a.samples + (size_t)4 * ps.item) = make_float4(col.x, col.y, col.z, counted);
-        }
-        ps.phase = PH_IDLE;
-        ps.d = mk(0.f, 0.f, 0.f);
-        ++done;
-    }
+    finish_step(a, ps, false, go, 1.f, mk(0.f, 0.f, 0.f), done, dropped);
 }
 
 // Start the path of batch item `mine`: its (pixel, sample), keyed RNG stream and

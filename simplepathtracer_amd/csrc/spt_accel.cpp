@@ -258,6 +258,15 @@ AccelTables build_accel(const float *centers4, const float *radii, uint32_t n, u
     }
     if (t.nodes.empty())  // no tree: one pad record per octant layout (n_nodes = 0)
         for (int oct = 0; oct < 8; ++oct) t.nodes.push_back(AccelNode{0.f, 0.f, 0.f, -INFINITY, 1, kNoSlot, -INFINITY, 0.f});
+    // compact flat records (kernel SPT_FLAT4)
+    if (t.n_nodes == t.leaves) {
+        for (uint32_t i = 0; i < t.n_nodes; ++i) {
+            const AccelNode &nd = t.nodes[i];
+            t.flat4.push_back(make_float4(nd.cx, nd.cy, nd.cz, nd.rb));
+        }
+        while (t.flat4.size() % 4) t.flat4.push_back(make_float4(0.f, 0.f, 0.f, NAN));
+        for (int k = 0; k < 4; ++k) t.flat4.push_back(make_float4(0.f, 0.f, 0.f, NAN));
+    }
     // member pretest constants of the cluster slots (dummies: K' = +inf never passes)
     t.kpre.assign(t.slots.size(), 0.f);
     double cm = 0;
@@ -324,7 +333,20 @@ std::string validate_accel(const AccelTables &t, const float *centers4, const fl
     }
     for (uint32_t i = 0; i < n; ++i)
         if (!seen[i]) return bad("sphere %u missing from the slot table", i);
-    // member pretest constants (cluster slots, and the always-list when it takes them)
+    // compact flat records: layout 0's {Cb, K1''} in order, NaN padding
+    if (t.n_nodes == t.leaves) {
+        if (t.flat4.size() != ((size_t)t.n_nodes + 3) / 4 * 4 + 4) return bad("flat4 table size wrong");
+        for (size_t i = 0; i < t.flat4.size(); ++i) {
+            const float4 &f = t.flat4[i];
+            if (i < t.n_nodes) {
+                const AccelNode &nd = t.nodes[i];
+                if (!(f.x == nd.cx && f.y == nd.cy && f.z == nd.cz && f.w == nd.rb)) return bad("flat4 record %zu", i);
+            } else if (!std::isnan(f.w)) {
+                return bad("flat4 pad %zu can pass", i);
+            }
+        }
+    }
+        // member pretest constants (cluster slots, and the always-list when it takes them)
     if (t.kpre.size() != t.slots.size()) return bad("pretest table size mismatch");
     if (t.always_pre)
         for (size_t j = 0; j < cbase; ++j) {

@@ -46,6 +46,10 @@ struct AccelTables {
     // for its dummies, and its own bound
     bool always_pre = false;
     float pre_cm_always = 0.f;
+    // flat lists: compact node records {Cb, K1''} of layout 0 in slot order, padded
+    // with NaN-threshold records to a multiple of 4 plus 4 (the kernel reads one
+    // chunk of 4 ahead); empty for trees
+    std::vector<float4> flat4;
 };
 
 // cluster_k: members per cluster (0, or n <= 32: every sphere is "always" tested).

@@ -50,6 +50,19 @@
 #define SPT_NODE_X8 1
 #endif
 
+// 1: flat lists walk compact 16-byte node records four per scalar load
+#ifndef SPT_FLAT4
+#define SPT_FLAT4 0
+#endif
+#ifndef SPT_FLAT_CHUNK
+#define SPT_FLAT_CHUNK 4
+#endif
+#ifndef SPT_DUP_LEAF
+#define SPT_DUP_LEAF 0
+#endif
+#ifndef SPT_DUP_ALWAYS
+#define SPT_DUP_ALWAYS 0
+#endif
 #ifndef SPT_DUP_BALL
 #define SPT_DUP_BALL 0
 #endif
@@ -370,6 +383,14 @@ __device__ __forceinline__ Hit find_closest(const AccelView &ac, const f3 &o, co
 #pragma unroll
             for (int k = 0; k < SPT_GROUP; ++k) g4[k] = ld_uniform(slots, g * SPT_GROUP + k);
             test_group<SPT_GROUP>(g4, ac.orig, g * SPT_GROUP, o, d, dod, h, dg);
+#if SPT_DUP_ALWAYS
+            {  // timing experiment only: the always-list tested again
+                Hit h2 = h;
+                asm volatile("" : "+v"(h2.best));
+                test_group<SPT_GROUP>(g4, ac.orig, g * SPT_GROUP, o, d, dod, h2, dg);
+                asm volatile("" ::"v"(h2.idx), "v"(h2.best), "v"(h2.p.x));
+            }
+#endif
         }
     }
     const unsigned long long live_mask = __ballot(active);
@@ -428,10 +449,69 @@ __device__ __forceinline__ Hit find_closest(const AccelView &ac, const f3 &o, co
             diag_node(mm);
 #if SPT_PRETEST
             if (mm != 0ull) test_leaf_pre<LEAF, true>(slots, (cfloat *)ac.kpre, ac.orig, r[5], o, d, dod, pl, h, dg);
+#if SPT_DUP_LEAF
+            if (mm != 0ull) {  // timing experiment only: each entered leaf tested again
+                Hit h2 = h;
+                asm volatile("" : "+v"(h2.best));
+                test_leaf_pre<LEAF, true>(slots, (cfloat *)ac.kpre, ac.orig, r[5], o, d, dod, pl, h2, dg);
+                asm volatile("" ::"v"(h2.idx), "v"(h2.best), "v"(h2.p.x));
+            }
+#endif
 #else
             if (mm != 0ull) test_leaf<LEAF>(slots, ac.orig, r[5], o, d, dod, h, dg);
 #endif
         };
+#if SPT_FLAT4 && SPT_PRETEST
+        // Compact flat records {Cb, K1''} (16 B, slot order: node i's leaf is slot
+        // cbase + i * LEAF), four per s_load_dwordx16.  Each chunk's four tests are
+        // independent chains, and the next chunk's load is in flight while this
+        // chunk's leaves are tested (a scalar-load wait is lgkmcnt(0), so the load is
+        // issued after the chunk's records are used).  The table is padded to whole
+        // chunks plus one with NaN thresholds, which no lane passes.
+        {
+            constexpr int CH = SPT_FLAT_CHUNK;  // records per scalar load: 2 (x8) or 4 (x16)
+            typedef uint32_t u32x16 __attribute__((ext_vector_type(4 * CH)));
+            typedef __attribute__((address_space(4))) const u32x16 cu32x16;
+            cuint *fq = (cuint *)ac.flat4;
+            const uint32_t nch = (ac.n_nodes + (uint32_t)CH - 1u) / (uint32_t)CH;
+            u32x16 ca = *(cu32x16 *)fq;
+            asm volatile("" : "+s"(ca));
+            uint32_t leaf = ac.flat_base;
+            auto chunk = [&](const u32x16 &c, cuint *nextp, u32x16 &nx) {
+                float xs[CH];
+#pragma unroll
+                for (int k = 0; k < CH; ++k) {
+                    const float bx = __uint_as_float(c[4 * k]), by = __uint_as_float(c[4 * k + 1]);
+                    const float bz = __uint_as_float(c[4 * k + 2]);
+                    const float tcb = __builtin_fmaf(bx, d.x, __builtin_fmaf(by, d.y, __builtin_fmaf(bz, d.z, -dod)));
+                    const float w = __builtin_fmaf(bx, osx, __builtin_fmaf(by, osy, __builtin_fmaf(bz, osz, qoe)));
+                    xs[k] = __builtin_fmaf(-tcb, tcb, w);
+                }
+                unsigned long long mm[CH];
+#pragma unroll
+                for (int k = 0; k < CH; ++k) mm[k] = __ballot(xs[k] <= __uint_as_float(c[4 * k + 3]));
+                __builtin_amdgcn_sched_barrier(0);
+                nx = *(cu32x16 *)nextp;
+                asm volatile("" : "+s"(nx));
+#pragma unroll
+                for (int k = 0; k < CH; ++k) {
+                    diag_node(mm[k]);
+                    if (mm[k] != 0ull)
+                        test_leaf_pre<LEAF, true>(slots, (cfloat *)ac.kpre, ac.orig, leaf + (uint32_t)k * LEAF, o, d,
+                                                  dod, pl, h, dg);
+                }
+                leaf += (uint32_t)CH * LEAF;
+            };
+            uint32_t c = 0;
+            u32x16 cb;
+            for (; c + 2u <= nch; c += 2u) {
+                chunk(ca, fq + 4u * CH * (c + 1u), cb);
+                chunk(cb, fq + 4u * CH * (c + 2u), ca);
+            }
+            if (c < nch) chunk(ca, fq + 4u * CH * (c + 1u), cb);
+            return h;
+        }
+#endif
         // The next record's load is issued only after this record's first use: a
         // scalar-load wait is lgkmcnt(0), so an earlier issue would be waited for here.
         cuint *p = nodes;

@@ -31,6 +31,11 @@
 #define SPT_PRETEST 1
 #endif
 
+// 1: tree leaves (config 5) behind the member pretest too (measured 10% slower on
+// config 5: the tree's walk, not its member tests, bounds it)
+#ifndef SPT_PRETEST_TREE
+#define SPT_PRETEST_TREE 0
+#endif
 // 1: the always-tested spheres behind the pretest too (finite scenes; measured 2.4%
 // slower on config 2: the ground passes for about half the rays, so its pretest
 // mostly adds the exact retest)
@@ -576,7 +581,7 @@ __device__ __forceinline__ Hit find_closest(const AccelView &ac, const f3 &o, co
         return (__builtin_amdgcn_sqrtf(best * 1.0001f) * (1.0f + 0x1p-20f) + (2e-5f * olen + 1e-6f)) * kq;
     };
     float sbe = near_term(h.best);
-#if SPT_PRETEST
+#if SPT_PRETEST && SPT_PRETEST_TREE
     PreLane pl;  // member pretest terms (see the flat list above), o unscaled
     pl.osx = o.x;
     pl.osy = o.y;
@@ -616,7 +621,7 @@ __device__ __forceinline__ Hit find_closest(const AccelView &ac, const f3 &o, co
             }
         }
         if (mm != 0ull && leaf) {
-#if SPT_PRETEST
+#if SPT_PRETEST && SPT_PRETEST_TREE
             test_leaf_pre<LEAF, false>(slots, (cfloat *)ac.kpre, ac.orig, leaf_slot, o, d, dod, pl, h, dg);
 #else
             test_leaf<LEAF>(slots, ac.orig, leaf_slot, o, d, dod, h, dg);

@@ -22,6 +22,7 @@ from simplepathtracer_amd import _native  # noqa: E402
 import simplepathtracer_amd as spt  # noqa: E402
 
 W, H, SPP, B = {"c1": (200, 100, 4, 8), "c2": (1200, 800, 100, 50), "c3s": (3840, 2160, 16, 50),
+                "c5": (1920, 1080, 256, 50),
                 "c5s": (1920, 1080, 4, 50)}[args.config]
 scene = (spt.generate_stress(1, 10000) if args.config.startswith("c5")
          else spt.cornell3() if args.config == "c1" else spt.generate_spheres(1))

@@ -203,9 +203,9 @@ SPT_API int spt_camera_basis(const float eye[4], const float look_at[4], const f
  * Runs the device primitives the render path relies on over n inputs and
  * writes SPT_SELFTEST_COLS floats per input: a/b, sqrtf(a),
  * sqrt(double(a)) and pow5(double(a)) as two float words each, uniform(-1,1)
- * of bits, u8 of a, Normalize({a, b, c}) (3 floats) and c/a, with c the float
- * whose bit pattern is bits. */
-#define SPT_SELFTEST_COLS 12
+ * of bits, u8 of a, Normalize({a, b, c}) (3 floats), c/a, uniform(-0.5,0.5) and
+ * uniform(0,1) of bits, with c the float whose bit pattern is bits. */
+#define SPT_SELFTEST_COLS 14
 SPT_API int spt_selftest_numerics(spt_ctx *ctx, const float *a, const float *b, const uint32_t *bits, uint32_t n,
                           float *out);
 

@@ -23,7 +23,7 @@ MODE_SEGMENT, MODE_TASK = 0, 1
 TREE_AUTO = 0xFFFFFFFF  # spt_set_cluster_tree default
 CLUSTER_AUTO = 0xFFFFFFFF  # spt_set_cluster_size default
 ENGINE_MEGAKERNEL, ENGINE_WAVEFRONT = 0, 1
-SELFTEST_COLS = 12
+SELFTEST_COLS = 14
 
 
 class SptError(RuntimeError):

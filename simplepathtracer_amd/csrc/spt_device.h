@@ -137,7 +137,16 @@ __device__ __forceinline__ float canon_u32(uint32_t bits)
     float u = (float)bits * 2.3283064365386963e-10f;  // * 2^-32, exact
     return u >= 1.0f ? 0x1.fffffep-1f : u;  // nextafterf(1, 0)
 }
-__device__ __forceinline__ float uniform(uint64_t &st, float a, float b) { return canon_u32(next_u32(st)) * (b - a) + a; }
+// uniform(a, b) from the raw draw.  Every call site has a power-of-two width b - a (1
+// or 2), so canon * (b - a) is exact and the reference's two roundings (the product
+// is exact, the add rounds once) are one FMA: fl(canon * w + a) == fma(f, 2^-32 w, a)
+// with f = float(bits).  The clamp moves onto f: f == 2^32 exactly when canon == 1.
+__device__ __forceinline__ float uniform_bits(uint32_t bits, float a, float b)
+{
+    const float f = __builtin_fminf((float)bits, 0x1.fffffep+31f);
+    return __builtin_fmaf(f, 0x1p-32f * (b - a), a);
+}
+__device__ __forceinline__ float uniform(uint64_t &st, float a, float b) { return uniform_bits(next_u32(st), a, b); }
 
 // Random.hpp:115-127 (== 129-141): x, y, z ~ U(-0.5,0.5) while Length < 0.5.
 // sqrt_rn is monotone and sqrt_rn(0.25) == 0.5, sqrt_rn(prev(0.25)) < 0.5, so

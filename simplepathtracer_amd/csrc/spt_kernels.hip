@@ -299,13 +299,15 @@ __global__ void selftest_kernel(const float *a, const float *b, const uint32_t *
     o[3] = __builtin_bit_cast(float, (uint32_t)(sqb >> 32));
     o[4] = __builtin_bit_cast(float, (uint32_t)p5b);
     o[5] = __builtin_bit_cast(float, (uint32_t)(p5b >> 32));
-    o[6] = canon_u32(bits[i]) * (1.f - (-1.f)) + (-1.f);
+    o[6] = uniform_bits(bits[i], -1.f, 1.f);
     o[7] = (float)f2u8(x);
     const f3 nv = normalize(mk(x, y, c));  // c: any bit pattern (NaN, inf, denormal, huge)
     o[8] = nv.x;
     o[9] = nv.y;
     o[10] = nv.z;
     o[11] = div_rn(c, x);
+    o[12] = uniform_bits(bits[i], -0.5f, 0.5f);
+    o[13] = uniform_bits(bits[i], 0.f, 1.f);
 }
 
 hipError_t launch_render(const RenderArgs &a, uint32_t grid, uint32_t block, hipStream_t s)

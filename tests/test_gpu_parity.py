@@ -83,6 +83,9 @@ def test_device_numerics_match_host(ctx, oracle):
         assert p5[i] == float(Fraction(float(a[i])) ** 5), (a[i], p5[i])
     want_u = np.array([oracle.lib().spo_uniform_u32(int(x), -1.0, 1.0) for x in u[:4096]], np.float32)
     assert_bitwise(out[:4096, 6], want_u, "uniform(-1,1)")
+    for col, lo, hi in ((12, -0.5, 0.5), (13, 0.0, 1.0)):
+        want_u = np.array([oracle.lib().spo_uniform_u32(int(x), lo, hi) for x in u[:4096]], np.float32)
+        assert_bitwise(out[:4096, col], want_u, f"uniform({lo},{hi})")
     assert np.array_equal(out[:, 7], np.trunc(np.where(a < 2**31, a, 0)).astype(np.int64).astype(np.uint8))
     # Normalize (Math.hpp:140-154) and c / a through the shortened division core,
     # c = any float bit pattern: NaN/inf/denormal/huge lanes take the full sequence

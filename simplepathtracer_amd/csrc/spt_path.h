@@ -62,6 +62,9 @@
 #ifndef SPT_FLAT_CHUNK
 #define SPT_FLAT_CHUNK 4
 #endif
+#ifndef SPT_REVERSE_ITEMS
+#define SPT_REVERSE_ITEMS 0
+#endif
 #ifndef SPT_DUP_LEAF
 #define SPT_DUP_LEAF 0
 #endif
@@ -911,6 +914,10 @@ __device__ __forceinline__ void start_path(const RenderArgs &a, uint32_t mine, u
     // consecutive items stays inside one 8x8 tile (ts_item).
 #if SPT_TS_ORDER
     uint32_t sl, lr, cx;
+#if SPT_REVERSE_ITEMS
+    // items handed out from the end of the batch (the last rows first)
+    mine = a.n_items - 1u - mine;
+#endif
     ts_item(mine, a.map.width, rows, a.spp_batch, a.div_band, a.div_tile, sl, lr, cx);
     const uint32_t s = a.s0 + sl;
     ps.item = sl * a.npix + lr * a.map.width + cx;  // slot: [sample][row-major pixel]
@@ -962,6 +969,7 @@ __device__ __forceinline__ void start_path_kernarg(uint32_t mine, uint32_t rows,
     a.height = k.height;
     a.bounces = k.bounces;
     a.npix = k.npix;
+    a.n_items = k.n_items;
     a.spp_batch = k.spp_batch;
     a.s0 = k.s0;
     a.seed_key = k.seed_key;

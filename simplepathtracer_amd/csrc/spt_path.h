@@ -65,6 +65,10 @@
 #ifndef SPT_REVERSE_ITEMS
 #define SPT_REVERSE_ITEMS 0
 #endif
+// trials per lane in the cube-minus-ball sampler's first round (1 or 2)
+#ifndef SPT_BALL_T0
+#define SPT_BALL_T0 1
+#endif
 #ifndef SPT_DUP_LEAF
 #define SPT_DUP_LEAF 0
 #endif
@@ -668,8 +672,27 @@ __device__ __forceinline__ f3 coop_ball_vector(uint64_t &st, bool need, uint32_t
     r.y = uniform(t, -0.5f, 0.5f);
     r.z = uniform(t, -0.5f, 0.5f);
     uint32_t jacc = 0;
+#if SPT_BALL_T0 >= 2
+    // round 0 evaluates each lane's trials 0 and 1 (fewer cooperative rounds: each
+    // round is a chain of ballots, LDS and cross-lane moves)
+    bool rej = lensq(r) < 0.25f;
+    {
+        f3 r1;
+        r1.x = uniform(t, -0.5f, 0.5f);
+        r1.y = uniform(t, -0.5f, 0.5f);
+        r1.z = uniform(t, -0.5f, 0.5f);
+        if (rej && !(lensq(r1) < 0.25f)) {
+            r = r1;
+            jacc = 1;
+            rej = false;
+        }
+    }
+    unsigned long long pend = __ballot(need && rej);
+    uint32_t jb = 2;
+#else
     unsigned long long pend = __ballot(need && lensq(r) < 0.25f);
     uint32_t jb = 1;
+#endif
     const uint32_t s_lo = (uint32_t)st0, s_hi = (uint32_t)(st0 >> 32);
     while (pend != 0ull) {
         const uint32_t np = (uint32_t)__popcll(pend);

@@ -258,15 +258,6 @@ AccelTables build_accel(const float *centers4, const float *radii, uint32_t n, u
     }
     if (t.nodes.empty())  // no tree: one pad record per octant layout (n_nodes = 0)
         for (int oct = 0; oct < 8; ++oct) t.nodes.push_back(AccelNode{0.f, 0.f, 0.f, -INFINITY, 1, kNoSlot, -INFINITY, 0.f});
-    // compact flat records (kernel SPT_FLAT4)
-    if (t.n_nodes == t.leaves) {
-        for (uint32_t i = 0; i < t.n_nodes; ++i) {
-            const AccelNode &nd = t.nodes[i];
-            t.flat4.push_back(make_float4(nd.cx, nd.cy, nd.cz, nd.rb));
-        }
-        while (t.flat4.size() % 4) t.flat4.push_back(make_float4(0.f, 0.f, 0.f, NAN));
-        for (int k = 0; k < 4; ++k) t.flat4.push_back(make_float4(0.f, 0.f, 0.f, NAN));
-    }
     // member pretest constants of the cluster slots (dummies: K' = +inf never passes)
     t.kpre.assign(t.slots.size(), 0.f);
     double cm = 0;
@@ -281,21 +272,6 @@ AccelTables build_accel(const float *centers4, const float *radii, uint32_t n, u
                               std::sqrt((double)q.w));
     }
     t.pre_cm = round_up(cm * (1.0 + 1e-9));
-    // the always-list
-    double cma = 0;
-    bool fin = true;
-    for (size_t j = 0; j < cbase; ++j) {
-        if (t.orig[j] == 0xFFFFFFFFu) continue;
-        const float4 &q = t.slots[j];
-        fin = fin && std::isfinite(q.x) && std::isfinite(q.y) && std::isfinite(q.z) && std::isfinite(q.w);
-        if (fin)
-            cma = std::max(cma, std::sqrt((double)q.x * q.x + (double)q.y * q.y + (double)q.z * q.z) +
-                                    std::sqrt((double)q.w));
-    }
-    t.always_pre = fin && cma <= 1e15;
-    t.pre_cm_always = t.always_pre ? round_up(cma * (1.0 + 1e-9)) : INFINITY;
-    for (size_t j = 0; j < cbase; ++j)
-        t.kpre[j] = t.orig[j] == 0xFFFFFFFFu ? INFINITY : (t.always_pre ? pretest_k(t.slots[j]) : 0.f);
     if (!(cm <= 1e15)) {
         // squares near the float range: the pretest passes every lane (K' = -inf)
         t.pre_cm = INFINITY;
@@ -333,35 +309,8 @@ std::string validate_accel(const AccelTables &t, const float *centers4, const fl
     }
     for (uint32_t i = 0; i < n; ++i)
         if (!seen[i]) return bad("sphere %u missing from the slot table", i);
-    // compact flat records: layout 0's {Cb, K1''} in order, NaN padding
-    if (t.n_nodes == t.leaves) {
-        if (t.flat4.size() != ((size_t)t.n_nodes + 3) / 4 * 4 + 4) return bad("flat4 table size wrong");
-        for (size_t i = 0; i < t.flat4.size(); ++i) {
-            const float4 &f = t.flat4[i];
-            if (i < t.n_nodes) {
-                const AccelNode &nd = t.nodes[i];
-                if (!(f.x == nd.cx && f.y == nd.cy && f.z == nd.cz && f.w == nd.rb)) return bad("flat4 record %zu", i);
-            } else if (!std::isnan(f.w)) {
-                return bad("flat4 pad %zu can pass", i);
-            }
-        }
-    }
-        // member pretest constants (cluster slots, and the always-list when it takes them)
+    // member pretest constants (cluster slots)
     if (t.kpre.size() != t.slots.size()) return bad("pretest table size mismatch");
-    if (t.always_pre)
-        for (size_t j = 0; j < cbase; ++j) {
-            const float4 &q = t.slots[j];
-            if (t.orig[j] == 0xFFFFFFFFu) {
-                if (!(t.kpre[j] == INFINITY)) return bad("dummy always slot %zu: pretest can pass", j);
-                continue;
-            }
-            if (!(std::isfinite(q.x) && std::isfinite(q.y) && std::isfinite(q.z) && std::isfinite(q.w)))
-                return bad("always slot %zu: non-finite sphere behind the pretest", j);
-            if (!(t.kpre[j] == pretest_k(q))) return bad("always slot %zu: pretest K' wrong", j);
-            const double cl = std::sqrt((double)q.x * q.x + (double)q.y * q.y + (double)q.z * q.z);
-            if (!((double)t.pre_cm_always >= cl + std::sqrt((double)q.w)) || !(t.pre_cm_always <= 1.1e15f))
-                return bad("always slot %zu: outside the pretest bound", j);
-        }
     for (size_t j = cbase; j < t.slots.size(); ++j) {
         const float4 &q = t.slots[j];
         if (t.orig[j] == 0xFFFFFFFFu) {

@@ -41,15 +41,6 @@ struct AccelTables {
     // cluster members (rounded up)
     std::vector<float> kpre;
     float pre_cm = 0.f;
-    // the always-list's pretest (every always sphere finite and Cm <= 1e15; else its
-    // spheres take the reference test directly): K' per always slot as above, +inf
-    // for its dummies, and its own bound
-    bool always_pre = false;
-    float pre_cm_always = 0.f;
-    // flat lists: compact node records {Cb, K1''} of layout 0 in slot order, padded
-    // with NaN-threshold records to a multiple of 4 plus 4 (the kernel reads one
-    // chunk of 4 ahead); empty for trees
-    std::vector<float4> flat4;
 };
 
 // cluster_k: members per cluster (0, or n <= 32: every sphere is "always" tested).

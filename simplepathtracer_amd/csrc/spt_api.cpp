@@ -61,8 +61,7 @@ struct spt_ctx {
     spt::AccelNode *d_nodes = nullptr;
     uint32_t *d_mat = nullptr, *d_orig = nullptr;
     float *d_kpre = nullptr;
-    float4 *d_flat4 = nullptr;
-    size_t shade_cap = 0, mat_cap = 0, slots_cap = 0, orig_cap = 0, nodes_cap = 0, kpre_cap = 0, flat4_cap = 0;
+    size_t shade_cap = 0, mat_cap = 0, slots_cap = 0, orig_cap = 0, nodes_cap = 0, kpre_cap = 0;
     spt::AccelTables tables;
     uint32_t n = 0;
     bool scene_set = false;
@@ -465,12 +464,9 @@ int rebuild_accel(spt_ctx *ctx)
     if (!rc) rc = upload(ctx, &ctx->d_orig, &ctx->orig_cap, t.orig);
     if (!rc) rc = upload(ctx, &ctx->d_nodes, &ctx->nodes_cap, t.nodes);
     if (!rc) rc = upload(ctx, &ctx->d_kpre, &ctx->kpre_cap, t.kpre);
-    if (!rc && !t.flat4.empty()) rc = upload(ctx, &ctx->d_flat4, &ctx->flat4_cap, t.flat4);
     if (rc) return rc;
     ctx->accel = spt::AccelView{ctx->d_slots, ctx->d_orig, ctx->d_nodes, t.always_groups, t.n_nodes,
-                                t.n_nodes > t.leaves ? 1u : 0u, t.leaf_slots, ctx->d_kpre, t.pre_cm,
-                                t.pre_cm_always, t.always_pre ? 1u : 0u, ctx->d_flat4,
-                                (uint32_t)((size_t)t.always_groups * t.group)};
+                                t.n_nodes > t.leaves ? 1u : 0u, t.leaf_slots, ctx->d_kpre, t.pre_cm};
     ctx->tables = std::move(t);
     return SPT_OK;
 }
@@ -587,7 +583,7 @@ void spt_ctx_destroy(spt_ctx *ctx)
     (void)hipDeviceSynchronize();  // async renders on caller streams
     if (ctx->ref_ev) (void)hipEventDestroy(ctx->ref_ev);
     void *bufs[] = {ctx->d_shade, ctx->d_mat, ctx->d_slots, ctx->d_orig, ctx->d_nodes,
-                    ctx->d_kpre, ctx->d_flat4, ctx->d_counters, ctx->d_stage, ctx->d_frame8};
+                    ctx->d_kpre, ctx->d_counters, ctx->d_stage, ctx->d_frame8};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     for (Workspace &w : ctx->ws) {

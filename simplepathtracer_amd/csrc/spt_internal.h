@@ -169,10 +169,6 @@ struct AccelView {
     uint32_t leaf_slots;  // slots per leaf: kFlatLeafSlots or kClusterSlots
     const float *kpre;    // member pretest constant K' per slot (spt_accel.h)
     float pre_cm;         // >= max |C| + r over the cluster members
-    float pre_cm_always;  // >= max |C| + r over the always-tested spheres
-    uint32_t always_pre;  // 1: the always-list takes the pretest (all finite, bounded)
-    const float4 *flat4;  // flat lists: {Cb, K1''} per node in slot order, NaN-padded
-    uint32_t flat_base;   // flat lists: slot of node 0's leaf (after the always-list)
 };
 
 struct DeviceScene {

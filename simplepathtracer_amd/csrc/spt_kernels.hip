@@ -80,7 +80,6 @@ __global__ __launch_bounds__(kRenderBlock) SPT_RENDER_ATTR void render_kernel(Re
     uint32_t pend = 0;
     if (lane == 0) pend = atomicAdd(a.head, a.claim);
     bool exhausted = false;
-    uint32_t glass_wait = 0;  // iterations since a lane parked at glass (wave-uniform)
     unsigned long long casts = 0, done = 0, dropped = 0;
     unsigned long long d_iters = 0, d_cyc_cast = 0, d_cyc_shade = 0, d_cyc_refill = 0;
     CastDiag dg;
@@ -141,31 +140,16 @@ __global__ __launch_bounds__(kRenderBlock) SPT_RENDER_ATTR void render_kernel(Re
 #endif
             }
         }
-#if SPT_GLASS_PARK
-        // ---- parked glass hits: refracted together once enough wait, one waited
-        // long enough, or nothing else is left to cast
-        {
-            const unsigned long long parked = __ballot(ps.phase == PH_GLASS);
-            if (parked != 0ull) {
-                ++glass_wait;
-                const unsigned long long castable = __ballot(ps.phase == PH_TRACE || ps.phase == PH_DLOOP);
-                if (__popcll(parked) >= SPT_GLASS_BATCH || glass_wait >= SPT_GLASS_WAIT || castable == 0ull) {
-                    glass_step(a, ps, ps.phase == PH_GLASS, done, dropped);
-                    glass_wait = 0;
-                }
-            }
-        }
-#endif
-        const unsigned long long live = __ballot(ps.phase == PH_TRACE || ps.phase == PH_DLOOP);
+        const unsigned long long live = __ballot(ps.phase != PH_IDLE);
         if (live == 0ull) {
-            if (exhausted && __ballot(ps.phase != PH_IDLE) == 0ull) break;
+            if (exhausted) break;
             continue;
         }
         SPT_STAMP(d_cyc_refill);
         casts += (unsigned long long)__popcll(live);
         ++d_iters;
         // ---- one cast + one shading step ----
-        const bool act = ps.phase == PH_TRACE || ps.phase == PH_DLOOP;
+        const bool act = ps.phase != PH_IDLE;
         const Hit h = find_closest<TREE, LEAF>(a.scene.accel, ps.o, ps.d, act, dg);
 #if SPT_DUP_CAST
         {
@@ -177,7 +161,7 @@ __global__ __launch_bounds__(kRenderBlock) SPT_RENDER_ATTR void render_kernel(Re
         }
 #endif
         SPT_STAMP(d_cyc_cast);
-        shade_step<true>(a, ps, h, act, done, dropped, s_lds + (threadIdx.x & ~63u));
+        shade_step(a, ps, h, act, done, dropped, s_lds + (threadIdx.x & ~63u));
         SPT_STAMP(d_cyc_shade);
     }
 

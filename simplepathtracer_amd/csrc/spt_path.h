@@ -36,12 +36,6 @@
 #ifndef SPT_PRETEST_TREE
 #define SPT_PRETEST_TREE 0
 #endif
-// 1: the always-tested spheres behind the pretest too (finite scenes; measured 2.4%
-// slower on config 2: the ground passes for about half the rays, so its pretest
-// mostly adds the exact retest)
-#ifndef SPT_ALWAYS_PRE
-#define SPT_ALWAYS_PRE 0
-#endif
 // 1: leaf tables addressed by 32-bit byte offsets (SGPR-offset scalar loads)
 #ifndef SPT_LEAF_BYTEOFF
 #define SPT_LEAF_BYTEOFF 1
@@ -55,20 +49,8 @@
 #define SPT_NODE_X8 1
 #endif
 
-// 1: flat lists walk compact 16-byte node records four per scalar load
-#ifndef SPT_FLAT4
-#define SPT_FLAT4 0
-#endif
-#ifndef SPT_FLAT_CHUNK
-#define SPT_FLAT_CHUNK 4
-#endif
-#ifndef SPT_REVERSE_ITEMS
-#define SPT_REVERSE_ITEMS 0
-#endif
-// trials per lane in the cube-minus-ball sampler's first round (1 or 2)
-#ifndef SPT_BALL_T0
-#define SPT_BALL_T0 1
-#endif
+// timing experiments only: a second, discarded evaluation of
+// one part of the path, whose cost is the part's marginal cost
 #ifndef SPT_DUP_LEAF
 #define SPT_DUP_LEAF 0
 #endif
@@ -84,20 +66,6 @@
 #define SPT_PRE_ILP 1
 #endif
 
-// 1: the megakernel parks glass hits and refracts them in batches: the refraction
-// step (double-precision Schlick / Snell, two normalizes) otherwise runs in ~92% of
-// wave-iterations for ~4% of the lanes.  Measured neutral on config 2 (off)
-#ifndef SPT_GLASS_PARK
-#define SPT_GLASS_PARK 0
-#endif
-// glass_step runs once SPT_GLASS_BATCH lanes are parked, or SPT_GLASS_WAIT
-// iterations after the first one parked, or when no lane is left to cast
-#ifndef SPT_GLASS_BATCH
-#define SPT_GLASS_BATCH 6
-#endif
-#ifndef SPT_GLASS_WAIT
-#define SPT_GLASS_WAIT 4
-#endif
 
 // 1: the cube-minus-ball rejection loop runs cooperatively across the wave
 #ifndef SPT_COOP_BALL
@@ -119,9 +87,6 @@ namespace spt {
 namespace {
 
 constexpr uint32_t PH_IDLE = 0, PH_TRACE = 1, PH_DLOOP = 2;
-// megakernel only: a path that hit glass waits here, its contact point in o and the
-// glass slot in gidx, until the wave runs the refraction step for a batch of them
-constexpr uint32_t PH_GLASS = 3;
 
 // rSq of SampleColorRefractive (lines 58 and 75): float(pow(double(-0.2f), 2)).
 // The exact square of a float is representable in double, so pow returns it.
@@ -373,22 +338,6 @@ __device__ __forceinline__ Hit find_closest(const AccelView &ac, const f3 &o, co
     const float m2c = (float)(-2.0 * kFlatScale);
     const float osx = m2c * o.x, osy = m2c * o.y, osz = m2c * o.z;
     // always-tested spheres (ground, large balls; every sphere when culling is off)
-#if SPT_PRETEST && SPT_ALWAYS_PRE
-    if (ac.always_pre) {
-        // behind the member pretest with the always-list's own bound Cm
-        PreLane pa;
-        pa.osx = osx;
-        pa.osy = osy;
-        pa.osz = osz;
-        pa.qoe = !active ? INFINITY : (no_cull ? -INFINITY : qo);
-        pa.tinit = !active ? -INFINITY
-                           : (no_cull ? INFINITY
-                                      : __builtin_fmaf(2e-6f, ac.pre_cm_always + __builtin_amdgcn_sqrtf(oo) * 1.000001f,
-                                                       1e-6f) - dod);
-        for (uint32_t g = 0; g < ac.always_groups; ++g)
-            test_leaf_pre<SPT_GROUP, true>(slots, (cfloat *)ac.kpre, ac.orig, g * SPT_GROUP, o, d, dod, pa, h, dg);
-    } else
-#endif
     {
         for (uint32_t g = 0; g < ac.always_groups; ++g) {
             float4 g4[SPT_GROUP];
@@ -473,57 +422,6 @@ __device__ __forceinline__ Hit find_closest(const AccelView &ac, const f3 &o, co
             if (mm != 0ull) test_leaf<LEAF>(slots, ac.orig, r[5], o, d, dod, h, dg);
 #endif
         };
-#if SPT_FLAT4 && SPT_PRETEST
-        // Compact flat records {Cb, K1''} (16 B, slot order: node i's leaf is slot
-        // cbase + i * LEAF), four per s_load_dwordx16.  Each chunk's four tests are
-        // independent chains, and the next chunk's load is in flight while this
-        // chunk's leaves are tested (a scalar-load wait is lgkmcnt(0), so the load is
-        // issued after the chunk's records are used).  The table is padded to whole
-        // chunks plus one with NaN thresholds, which no lane passes.
-        {
-            constexpr int CH = SPT_FLAT_CHUNK;  // records per scalar load: 2 (x8) or 4 (x16)
-            typedef uint32_t u32x16 __attribute__((ext_vector_type(4 * CH)));
-            typedef __attribute__((address_space(4))) const u32x16 cu32x16;
-            cuint *fq = (cuint *)ac.flat4;
-            const uint32_t nch = (ac.n_nodes + (uint32_t)CH - 1u) / (uint32_t)CH;
-            u32x16 ca = *(cu32x16 *)fq;
-            asm volatile("" : "+s"(ca));
-            uint32_t leaf = ac.flat_base;
-            auto chunk = [&](const u32x16 &c, cuint *nextp, u32x16 &nx) {
-                float xs[CH];
-#pragma unroll
-                for (int k = 0; k < CH; ++k) {
-                    const float bx = __uint_as_float(c[4 * k]), by = __uint_as_float(c[4 * k + 1]);
-                    const float bz = __uint_as_float(c[4 * k + 2]);
-                    const float tcb = __builtin_fmaf(bx, d.x, __builtin_fmaf(by, d.y, __builtin_fmaf(bz, d.z, -dod)));
-                    const float w = __builtin_fmaf(bx, osx, __builtin_fmaf(by, osy, __builtin_fmaf(bz, osz, qoe)));
-                    xs[k] = __builtin_fmaf(-tcb, tcb, w);
-                }
-                unsigned long long mm[CH];
-#pragma unroll
-                for (int k = 0; k < CH; ++k) mm[k] = __ballot(xs[k] <= __uint_as_float(c[4 * k + 3]));
-                __builtin_amdgcn_sched_barrier(0);
-                nx = *(cu32x16 *)nextp;
-                asm volatile("" : "+s"(nx));
-#pragma unroll
-                for (int k = 0; k < CH; ++k) {
-                    diag_node(mm[k]);
-                    if (mm[k] != 0ull)
-                        test_leaf_pre<LEAF, true>(slots, (cfloat *)ac.kpre, ac.orig, leaf + (uint32_t)k * LEAF, o, d,
-                                                  dod, pl, h, dg);
-                }
-                leaf += (uint32_t)CH * LEAF;
-            };
-            uint32_t c = 0;
-            u32x16 cb;
-            for (; c + 2u <= nch; c += 2u) {
-                chunk(ca, fq + 4u * CH * (c + 1u), cb);
-                chunk(cb, fq + 4u * CH * (c + 2u), ca);
-            }
-            if (c < nch) chunk(ca, fq + 4u * CH * (c + 1u), cb);
-            return h;
-        }
-#endif
         // The next record's load is issued only after this record's first use: a
         // scalar-load wait is lgkmcnt(0), so an earlier issue would be waited for here.
         cuint *p = nodes;
@@ -648,7 +546,6 @@ __device__ __forceinline__ Hit find_closest(const AccelView &ac, const f3 &o, co
 // Per-lane path state of the flattened recursion.
 struct Path {
     uint32_t phase, item, bounce, spec;
-    uint32_t gidx;  // PH_GLASS: slot of the glass sphere hit
     uint64_t st;  // keyed splitmix stream of this (pixel, sample)
     f3 o, d, c;
 };
@@ -672,27 +569,8 @@ __device__ __forceinline__ f3 coop_ball_vector(uint64_t &st, bool need, uint32_t
     r.y = uniform(t, -0.5f, 0.5f);
     r.z = uniform(t, -0.5f, 0.5f);
     uint32_t jacc = 0;
-#if SPT_BALL_T0 >= 2
-    // round 0 evaluates each lane's trials 0 and 1 (fewer cooperative rounds: each
-    // round is a chain of ballots, LDS and cross-lane moves)
-    bool rej = lensq(r) < 0.25f;
-    {
-        f3 r1;
-        r1.x = uniform(t, -0.5f, 0.5f);
-        r1.y = uniform(t, -0.5f, 0.5f);
-        r1.z = uniform(t, -0.5f, 0.5f);
-        if (rej && !(lensq(r1) < 0.25f)) {
-            r = r1;
-            jacc = 1;
-            rej = false;
-        }
-    }
-    unsigned long long pend = __ballot(need && rej);
-    uint32_t jb = 2;
-#else
     unsigned long long pend = __ballot(need && lensq(r) < 0.25f);
     uint32_t jb = 1;
-#endif
     const uint32_t s_lo = (uint32_t)st0, s_hi = (uint32_t)(st0 >> 32);
     while (pend != 0ull) {
         const uint32_t np = (uint32_t)__popcll(pend);
@@ -801,8 +679,6 @@ __device__ __forceinline__ void finish_step(const RenderArgs &a, Path &ps, bool 
 // bounce loop (21-37) in PH_DLOOP.  Finishing paths write their sample slot.
 // Called by every lane of the wave (`act` = the lane holds a path), so the
 // cooperative cube-minus-ball sampler runs in uniform control flow.
-// PARK (megakernel): glass hits are parked for glass_step instead of shaded here.
-template <bool PARK>
 __device__ __forceinline__ void shade_step(const RenderArgs &a, Path &ps, const Hit &h, bool act,
                                            unsigned long long &done, unsigned long long &dropped, uint32_t *lds)
 {
@@ -882,16 +758,6 @@ __device__ __forceinline__ void shade_step(const RenderArgs &a, Path &ps, const 
         }
         ps.d = normalize(add(base, rv));
     }
-#if SPT_GLASS_PARK
-    if (PARK && refr) {
-        // park: the refraction runs later, for a batch of the wave's glass hits
-        // (glass_step); the path's arithmetic is unchanged
-        ps.o = h.p;
-        ps.gidx = idx;
-        ps.phase = PH_GLASS;
-        refr = false;
-    }
-#endif
     if (refr) {
         ps.o = h.p;
         refract_event(a, ps, idx);
@@ -900,17 +766,6 @@ __device__ __forceinline__ void shade_step(const RenderArgs &a, Path &ps, const 
     finish_step(a, ps, fin, spec_event, counted, col, done, dropped);
 }
 
-// The wave's parked glass hits (PH_GLASS lanes; `go` = this lane is one), shaded
-// together: SampleColorRefractive then the specular-event bookkeeping of shade_step.
-__device__ __forceinline__ void glass_step(const RenderArgs &a, Path &ps, bool go, unsigned long long &done,
-                                           unsigned long long &dropped)
-{
-    if (go) {
-        refract_event(a, ps, ps.gidx);
-        ps.phase = PH_TRACE;
-    }
-    finish_step(a, ps, false, go, 1.f, mk(0.f, 0.f, 0.f), done, dropped);
-}
 
 // Start the path of batch item `mine`: its (pixel, sample), keyed RNG stream and
 // primary ray (SingleThreadPathTracer.hpp:123-130).  rw, rh: shared reciprocals
@@ -937,10 +792,6 @@ __device__ __forceinline__ void start_path(const RenderArgs &a, uint32_t mine, u
     // consecutive items stays inside one 8x8 tile (ts_item).
 #if SPT_TS_ORDER
     uint32_t sl, lr, cx;
-#if SPT_REVERSE_ITEMS
-    // items handed out from the end of the batch (the last rows first)
-    mine = a.n_items - 1u - mine;
-#endif
     ts_item(mine, a.map.width, rows, a.spp_batch, a.div_band, a.div_tile, sl, lr, cx);
     const uint32_t s = a.s0 + sl;
     ps.item = sl * a.npix + lr * a.map.width + cx;  // slot: [sample][row-major pixel]

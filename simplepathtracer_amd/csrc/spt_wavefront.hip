@@ -160,7 +160,7 @@ __global__ __launch_bounds__(256) void wf_shade(WfArgs w, uint32_t cat, uint32_t
     h.best = 0.f;
     h.p = mk(h4.x, h4.y, h4.z);
     unsigned long long done = 0, dropped = 0;
-    shade_step<false>(w.ra, ps, h, act, done, dropped, s_lds + (threadIdx.x & ~63u));
+    shade_step(w.ra, ps, h, act, done, dropped, s_lds + (threadIdx.x & ~63u));
     if (act) {
         const bool alive = ps.phase != PH_IDLE;
         if (alive) store_ray(w.cur, i, ps);  // in place; compacted in queue order below

@@ -199,6 +199,12 @@ SPT_API int spt_scene_generate_stress(uint32_t seed, uint32_t n, float *centers4
 /* Transpose(CreateCameraBasisMatrix(eye, lookAt, up)), Math.hpp:198-231. */
 SPT_API int spt_camera_basis(const float eye[4], const float look_at[4], const float up[4], float view_out[16]);
 
+/* io::SaveImage (IOHelpers.hpp:24-27) without stb: writes g_data (width x height,
+ * comp = g_stride = 3 bytes per pixel, row 0 first) as the 24-bit BMP that
+ * stbi_write_bmp(path, width, height, 3, g_data) writes: 54-byte header, rows
+ * from the last to the first, BGR, each row zero-padded to 4 bytes. */
+SPT_API int spt_save_bmp(const char *path, uint32_t width, uint32_t height, uint32_t comp, const uint8_t *data);
+
 /* ---- numerics self-test ------------------------------------------------------
  * Runs the device primitives the render path relies on over n inputs and
  * writes SPT_SELFTEST_COLS floats per input: a/b, sqrtf(a),

@@ -8,7 +8,9 @@
 
 #include <cmath>
 #include <cstdint>
+#include <cstdio>
 #include <cstdlib>
+#include <vector>
 
 #pragma clang fp contract(off)
 
@@ -183,6 +185,43 @@ extern "C" int spt_scene_generate_stress(uint32_t seed, uint32_t n, float *cente
     }
     fuzz[2] = 0.01f;
     return SPT_OK;
+}
+
+// stbi_write_bmp's 24-bit layout (stb_image_write.h stbi_write_bmp_core for comp 3:
+// file header "BM", size, 0, 0, 54; BITMAPINFOHEADER 40, w, h, 1 plane, 24 bpp, six
+// zero words; pixels bottom-up, BGR, rows padded to 4 bytes), IOHelpers.hpp:24-27.
+extern "C" int spt_save_bmp(const char *path, uint32_t width, uint32_t height, uint32_t comp, const uint8_t *data)
+{
+    if (!path || (!data && width && height) || comp != 3 || width > 0x7FFFFFFFu / 4 || height > 0x7FFFFFFFu)
+        return SPT_ERR_ARG;
+    const uint32_t pad = (0u - width * 3u) & 3u, row = width * 3u + pad;
+    if ((uint64_t)row * height > 0xFFFFFFFFull - 54) return SPT_ERR_ARG;
+    std::vector<uint8_t> out(54 + (size_t)row * height, 0);
+    auto put4 = [&](size_t at, uint32_t v) {
+        for (int k = 0; k < 4; ++k) out[at + k] = (uint8_t)(v >> (8 * k));
+    };
+    out[0] = 'B';
+    out[1] = 'M';
+    put4(2, (uint32_t)(54 + (uint64_t)row * height));
+    put4(10, 54);
+    put4(14, 40);
+    put4(18, width);
+    put4(22, height);
+    out[26] = 1;   // planes
+    out[28] = 24;  // bits per pixel
+    for (uint32_t r = 0; r < height; ++r) {
+        const uint8_t *src = data + (size_t)(height - 1 - r) * width * 3;
+        uint8_t *dst = out.data() + 54 + (size_t)r * row;
+        for (uint32_t x = 0; x < width; ++x) {
+            dst[3 * x + 0] = src[3 * x + 2];
+            dst[3 * x + 1] = src[3 * x + 1];
+            dst[3 * x + 2] = src[3 * x + 0];
+        }
+    }
+    FILE *f = std::fopen(path, "wb");
+    if (!f) return SPT_ERR_ARG;
+    const bool ok = std::fwrite(out.data(), 1, out.size(), f) == out.size();
+    return (std::fclose(f) == 0 && ok) ? SPT_OK : SPT_ERR_ARG;
 }
 
 extern "C" int spt_camera_basis(const float eye[4], const float look_at[4], const float up[4], float view_out[16])

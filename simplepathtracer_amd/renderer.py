@@ -181,6 +181,16 @@ class Globals:
         self.ctx.set_params(self.g_width, self.g_height, self.g_samples, self.g_bounces, self.seed)
 
 
+def SaveImage(g: Globals, directory: str = ".") -> str:
+    """io::SaveImage (IOHelpers.hpp:24-27): g_data as a 24-bit BMP named
+    output{g_samples}s{g_bounces}b.bmp, in stbi_write_bmp's layout; returns the path."""
+    import os
+    path = os.path.join(directory, f"output{g.g_samples}s{g.g_bounces}b.bmp")
+    data = np.ascontiguousarray(g.g_data, np.uint8)
+    _native.check(_native.lib().spt_save_bmp(path.encode(), g.g_width, g.g_height, g.g_stride, _p(data)))
+    return path
+
+
 def RenderSegment(segment: RenderSegmentData, g: Globals) -> np.ndarray:
     """SingleThreadPathTracer.hpp:114-137: render the rectangle into g.g_data.
     Returns the float pixel colours (region-local, the value io::WritePixel gets)."""

@@ -143,3 +143,25 @@ def test_item_orders_are_bijections(tmp_path):
                     os.path.join(root, "tests", "cpp", "tile_check.cpp"), "-o", str(exe)], check=True)
     out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
     assert out.returncode == 0 and out.stdout.strip() == "ok", out.stdout
+
+
+@pytest.mark.parametrize("w,h", [(4, 3), (5, 2), (1, 1), (7, 6)])
+def test_save_bmp_matches_stb_layout(native, tmp_path, w, h):
+    """io::SaveImage (IOHelpers.hpp:24-27) calls stbi_write_bmp(path, w, h, 3, g_data);
+    stb is an absent submodule, so the expected file is built here from stb's published
+    24-bit layout (stbi_write_bmp_core): 54-byte header, rows last-to-first, BGR,
+    rows zero-padded to 4 bytes (parity unpinned against stb itself)."""
+    import struct
+    rng = np.random.default_rng(w * 10 + h)
+    data = rng.integers(0, 256, w * h * 3, dtype=np.uint8)
+    path = tmp_path / "out.bmp"
+    P = ctypes.c_void_p
+    assert native.lib().spt_save_bmp(str(path).encode(), w, h, 3, data.ctypes.data_as(P)) == 0
+    pad = (-w * 3) & 3
+    rows = [data[(h - 1 - r) * w * 3:(h - r) * w * 3].reshape(w, 3)[:, ::-1].tobytes() + b"\0" * pad
+            for r in range(h)]
+    body = b"".join(rows)
+    header = b"BM" + struct.pack("<IHHI", 54 + len(body), 0, 0, 54) + \
+        struct.pack("<IiiHHIIiiII", 40, w, h, 1, 24, 0, 0, 0, 0, 0, 0)
+    assert path.read_bytes() == header + body
+    assert native.lib().spt_save_bmp(str(path).encode(), w, h, 4, data.ctypes.data_as(P)) != 0

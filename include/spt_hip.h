@@ -149,6 +149,17 @@ SPT_API int spt_set_workspace(spt_ctx *ctx, uint64_t bytes);
  *   io::WritePixel does (IOHelpers.hpp:17-22), other bytes untouched. */
 SPT_API int spt_render_segment(spt_ctx *ctx, uint32_t yBegin, uint32_t yEnd, uint32_t xBegin, uint32_t xEnd,
                        float *rgba_out, uint8_t *g_data);
+/* Progressive RenderSegment / RenderSegmentTask (the preview of RenderImageParallelMain,
+ * Renderer.hpp:257-302): the region is rendered in passes of pass_spp samples; after
+ * each pass rgba_out / g_data (either nullable) hold the render at the samples done so
+ * far -- bit-identical to a render with g_samples = samples_done, since samples are
+ * keyed per (pixel, sample) -- and cb(user, samples_done) runs on the calling thread
+ * (nullable; a nonzero return stops the render there).  The last pass is the full
+ * render.  cb must not call into the same context. */
+typedef int (*spt_progress_fn)(void *user, uint32_t samples_done);
+SPT_API int spt_render_progressive(spt_ctx *ctx, int mode, uint32_t yBegin, uint32_t yEnd, uint32_t xBegin,
+                                   uint32_t xEnd, uint32_t pass_spp, float *rgba_out, uint8_t *g_data,
+                                   spt_progress_fn cb, void *user);
 SPT_API int spt_render_segment_task(spt_ctx *ctx, uint32_t yBegin, uint32_t yEnd, uint32_t xBegin, uint32_t xEnd,
                             float *rgba_out, uint8_t *g_data);
 

@@ -103,6 +103,7 @@ def lib() -> ctypes.CDLL:
         "spt_scene_generate_stress": ([u32, u32, P, P, P, P, P], I),
         "spt_camera_basis": ([P, P, P, P], I),
         "spt_save_bmp": ([ctypes.c_char_p, u32, u32, u32, P], I),
+        "spt_render_progressive": ([P, I, u32, u32, u32, u32, u32, P, P, P, P], I),
         "spt_selftest_numerics": ([P, P, P, P, u32, P], I),
     }
     for name, (args, res) in sig.items():

@@ -17,6 +17,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <mutex>
 #include <string>
 #include <utility>
@@ -303,8 +304,15 @@ int ensure_wavefront(spt_ctx *ctx, Workspace *w, uint32_t cap)
 // Render the rows of `map` and fold them into d_rgba (local pixel order) and/or
 // d_rgb8 (full frame).  keep_samples: leave the per-sample colours of a single
 // batch in d_samples (debug path).
+// Progressive rendering: batches of at most pass_spp samples, outputs written after
+// every batch and after_pass(samples done) called (nonzero return: stop early).
+struct Progress {
+    uint32_t pass_spp;
+    std::function<int(uint32_t)> after_pass;
+};
+
 int render_impl(spt_ctx *ctx, int mode, const spt::RowMap &map, float4 *d_rgba, uint8_t *d_rgb8, hipStream_t s,
-                bool keep_samples)
+                bool keep_samples, const Progress *pg = nullptr)
 {
     const uint32_t rows = spt::rows_owned(map);
     const uint64_t npix64 = (uint64_t)rows * map.width;
@@ -315,7 +323,8 @@ int render_impl(spt_ctx *ctx, int mode, const spt::RowMap &map, float4 *d_rgba, 
     uint64_t budget = std::max<uint64_t>(ctx->ws_bytes / (slot_floats * sizeof(float)), 1);
     budget = std::min<uint64_t>(budget, 0x7FFFFFFFull);
     uint64_t per = std::max<uint64_t>(1, budget / npix);
-    const uint32_t spp_batch = (uint32_t)std::min<uint64_t>(ctx->spp, per);
+    uint32_t spp_batch = (uint32_t)std::min<uint64_t>(ctx->spp, per);
+    if (pg) spp_batch = std::min(spp_batch, std::max(pg->pass_spp, 1u));
     if (keep_samples && spp_batch != ctx->spp)
         return fail(ctx, SPT_ERR_ARG, "region * spp exceeds the workspace for spt_render_samples");
     const uint64_t items_max = (uint64_t)npix * spp_batch;
@@ -357,6 +366,7 @@ int render_impl(spt_ctx *ctx, int mode, const spt::RowMap &map, float4 *d_rgba, 
     fa.npix = npix;
     fa.spp_total = ctx->spp;
     fa.mode = mode;
+    fa.preview = pg ? 1 : 0;
 
     for (uint32_t s0 = 0; s0 < ctx->spp; s0 += spp_batch) {
         const uint32_t b = std::min(spp_batch, ctx->spp - s0);
@@ -404,11 +414,17 @@ int render_impl(spt_ctx *ctx, int mode, const spt::RowMap &map, float4 *d_rgba, 
         fa.spp_batch = b;
         fa.first = s0 == 0;
         fa.last = s0 + b >= ctx->spp;
+        fa.s_done = s0 + b;
         EventPair ef = get_pair(ctx);
         HIP_TRY(ctx, hipEventRecord(ef.a, s));
         HIP_TRY(ctx, spt::launch_fold(fa, s));
         HIP_TRY(ctx, hipEventRecord(ef.b, s));
         ctx->pending_fold.push_back(ef);
+        if (pg && pg->after_pass) {
+            const int r = pg->after_pass(s0 + b);
+            if (r < 0) return r;
+            if (r > 0) break;  // the caller stopped the render
+        }
     }
     if (ctx->pending_render.size() > 256) return collect_timings(ctx);
     return SPT_OK;
@@ -478,9 +494,10 @@ int check_region(spt_ctx *ctx, uint32_t yB, uint32_t yE, uint32_t xB, uint32_t x
     return SPT_OK;
 }
 
-// RenderSegment / RenderSegmentTask with host outputs.
+// RenderSegment / RenderSegmentTask with host outputs; with pass_spp > 0 progressively,
+// copying the outputs back and calling cb after every pass.
 int render_segment_host(spt_ctx *ctx, int mode, uint32_t yB, uint32_t yE, uint32_t xB, uint32_t xE, float *rgba,
-                        uint8_t *g_data)
+                        uint8_t *g_data, uint32_t pass_spp = 0, spt_progress_fn cb = nullptr, void *user = nullptr)
 {
     if (!ctx) return fail(nullptr, SPT_ERR_ARG, "null context");
     std::lock_guard<std::mutex> lk(ctx->mu);
@@ -498,16 +515,31 @@ int render_segment_host(spt_ctx *ctx, int mode, uint32_t yB, uint32_t yE, uint32
         d8 = ctx->d_frame8;
     }
     spt::RowMap map{yB, yE, 1u, 1u, 0u, xB, w};
-    if ((rc = render_impl(ctx, mode, map, ctx->d_stage, d8, ctx->stream, false))) return rc;
-    if (rgba) HIP_TRY(ctx, hipMemcpyAsync(rgba, ctx->d_stage, npix * sizeof(float4), hipMemcpyDeviceToHost, ctx->stream));
-    if (g_data) {
-        // rows y in [yB, yE) live at g_data rows H-1-y: one contiguous band, xB.. per row
-        const size_t pitch = (size_t)ctx->W * 3;
-        const size_t off = (size_t)(ctx->H - yE) * pitch + (size_t)xB * 3;
-        HIP_TRY(ctx, hipMemcpy2DAsync(g_data + off, pitch, ctx->d_frame8 + off, pitch, (size_t)w * 3, h,
-                                      hipMemcpyDeviceToHost, ctx->stream));
+    auto copy_out = [&]() -> int {
+        if (rgba)
+            HIP_TRY(ctx, hipMemcpyAsync(rgba, ctx->d_stage, npix * sizeof(float4), hipMemcpyDeviceToHost, ctx->stream));
+        if (g_data) {
+            // rows y in [yB, yE) live at g_data rows H-1-y: one contiguous band, xB.. per row
+            const size_t pitch = (size_t)ctx->W * 3;
+            const size_t off = (size_t)(ctx->H - yE) * pitch + (size_t)xB * 3;
+            HIP_TRY(ctx, hipMemcpy2DAsync(g_data + off, pitch, ctx->d_frame8 + off, pitch, (size_t)w * 3, h,
+                                          hipMemcpyDeviceToHost, ctx->stream));
+        }
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        return SPT_OK;
+    };
+    if (pass_spp == 0) {
+        if ((rc = render_impl(ctx, mode, map, ctx->d_stage, d8, ctx->stream, false))) return rc;
+    } else {
+        Progress pg{pass_spp, [&](uint32_t done) -> int {
+                        const int r = copy_out();
+                        if (r) return -r;
+                        return cb ? (cb(user, done) != 0 ? 1 : 0) : 0;
+                    }};
+        rc = render_impl(ctx, mode, map, ctx->d_stage, d8, ctx->stream, false, &pg);
+        if (rc) return rc < 0 ? -rc : rc;
     }
-    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    if ((rc = copy_out())) return rc;
     return collect_timings(ctx);
 }
 
@@ -732,6 +764,14 @@ int spt_render_segment_task(spt_ctx *ctx, uint32_t yB, uint32_t yE, uint32_t xB,
                             uint8_t *g_data)
 {
     return render_segment_host(ctx, SPT_MODE_TASK, yB, yE, xB, xE, rgba, g_data);
+}
+
+int spt_render_progressive(spt_ctx *ctx, int mode, uint32_t yB, uint32_t yE, uint32_t xB, uint32_t xE,
+                           uint32_t pass_spp, float *rgba, uint8_t *g_data, spt_progress_fn cb, void *user)
+{
+    if (mode != SPT_MODE_SEGMENT && mode != SPT_MODE_TASK) return fail(ctx, SPT_ERR_ARG, "bad mode %d", mode);
+    if (pass_spp == 0) return fail(ctx, SPT_ERR_ARG, "pass_spp must be >= 1");
+    return render_segment_host(ctx, mode, yB, yE, xB, xE, rgba, g_data, pass_spp, cb, user);
 }
 
 int spt_rows_count(uint32_t yB, uint32_t yE, uint32_t strip, uint32_t parts, uint32_t part, uint32_t *rows)

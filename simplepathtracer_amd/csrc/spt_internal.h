@@ -211,7 +211,9 @@ struct FoldArgs {
     uint8_t *out_rgb8;   // nullable, full frame (g_data layout)
     RowMap map;
     uint32_t width, height, npix, spp_batch, spp_total;
+    uint32_t s_done;     // samples folded after this batch (s0 + spp_batch)
     int first, last, mode;
+    int preview;         // write the outputs after every batch (progressive rendering)
 };
 
 hipError_t launch_render(const RenderArgs &a, uint32_t grid, uint32_t block, hipStream_t s);

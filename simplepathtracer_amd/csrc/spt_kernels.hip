@@ -229,10 +229,12 @@ __global__ __launch_bounds__(256) void fold_kernel(FoldArgs a)
     }
     if (!a.last) {
         a.acc[p] = acc;
-        return;
+        if (!a.preview) return;
     }
-    // RenderSegment: *= (1.f / g_samples) (line 133); RenderSegmentTask: *= 1.f / samples[i] (line 198)
-    const float scale = a.mode == 0 ? 1.f / (float)a.spp_total : 1.f / acc.w;
+    // RenderSegment: *= (1.f / g_samples) (line 133); RenderSegmentTask: *= 1.f / samples[i]
+    // (line 198).  s_done == g_samples after the last batch; a progressive preview after
+    // s_done samples is the render at g_samples = s_done, bit for bit (keyed samples).
+    const float scale = a.mode == 0 ? 1.f / (float)a.s_done : 1.f / acc.w;
     const float r = acc.x * scale, g = acc.y * scale, b = acc.z * scale;
     if (a.out_rgba) a.out_rgba[p] = make_float4(r, g, b, 0.f);
     if (a.out_rgb8) {

@@ -28,6 +28,9 @@ def _p(a: np.ndarray):
     return a.ctypes.data_as(ctypes.c_void_p)
 
 
+_PROGRESS_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_uint32)
+
+
 @dataclass
 class RenderSegmentData:
     """Definitions.hpp:15-21."""
@@ -104,6 +107,32 @@ class Context:
             assert g_data.dtype == np.uint8 and g_data.flags.c_contiguous
             gp = _p(g_data)
         self._check(fn(self._h, yB, yE, xB, xE, _p(rgba), gp))
+        return rgba
+
+    def render_progressive(self, yB, yE, xB, xE, pass_spp: int, g_data=None, callback=None, task=False):
+        """Progressive render in passes of pass_spp samples.  After each pass the returned
+        float4 array (and g_data, if given) hold the render at the samples done so far
+        (bit-identical to a render with that many samples) and callback(samples_done)
+        runs; a truthy return stops the render."""
+        rgba = np.zeros((max(yE - yB, 0) * max(xE - xB, 0), 4), np.float32)
+        gp = None
+        if g_data is not None:
+            assert g_data.dtype == np.uint8 and g_data.flags.c_contiguous
+            gp = _p(g_data)
+        errors = []
+
+        def tramp(_user, done):
+            try:
+                return 1 if (callback is not None and callback(int(done))) else 0
+            except BaseException as e:  # stop the render, re-raise below
+                errors.append(e)
+                return 1
+
+        cb = _PROGRESS_FN(tramp)
+        self._check(_native.lib().spt_render_progressive(self._h, int(task), yB, yE, xB, xE, pass_spp, _p(rgba), gp,
+                                                         ctypes.cast(cb, ctypes.c_void_p), None))
+        if errors:
+            raise errors[0]
         return rgba
 
     def render_samples(self, yB, yE, xB, xE, spp: int, task=False) -> np.ndarray:

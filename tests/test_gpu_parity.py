@@ -443,3 +443,39 @@ def test_culling_is_exact_far_and_scaled(spt, ctx, golden_scenes, shift, scale):
     for kb, img, casts in outs[1:]:
         assert_bitwise(img, outs[0][1], f"shift {shift} scale {scale}, culling {kb} vs brute force")
         assert casts == outs[0][2]
+
+
+@pytest.mark.parametrize("task", [False, True])
+def test_progressive_passes_equal_lower_spp_renders(spt, ctx, golden_scenes, task):
+    """spt_render_progressive (the preview of RenderImageParallelMain): after every pass
+    the outputs are the render at the samples done so far, bit for bit, and the last
+    pass is the full render; a callback can stop it early."""
+    scene, W, H = scene_from(spt, golden_scenes, "random"), 160, 96
+    region = (10, 70, 20, 140)
+    seen = []
+    setup(ctx, scene, W, H, 20, 50)
+    g = np.zeros(W * H * 3, np.uint8)
+    snaps = {}
+
+    def cb(done):
+        seen.append(done)
+        snaps[done] = g.copy()
+
+    full = ctx.render_progressive(*region, 7, g, cb, task=task)
+    assert seen == [7, 14, 20]
+    for m in (7, 14):
+        setup(ctx, scene, W, H, m, 50)
+        gm = np.zeros_like(g)
+        ref = ctx.render_segment(*region, gm, task=task)
+        assert np.array_equal(snaps[m], gm), f"preview after {m} samples"
+        _ = ref
+    setup(ctx, scene, W, H, 20, 50)
+    g2 = np.zeros_like(g)
+    assert_bitwise(full, ctx.render_segment(*region, g2, task=task), "final pass vs one-shot render")
+    assert np.array_equal(g, g2)
+    stopped = []
+    part = ctx.render_progressive(*region, 5, None, lambda d: stopped.append(d) or d >= 10, task=task)
+    assert stopped == [5, 10]
+    setup(ctx, scene, W, H, 10, 50)
+    assert_bitwise(part, ctx.render_segment(*region, task=task), "stopped after 10 samples")
+    setup(ctx, scene, W, H, 20, 50)

@@ -7,7 +7,7 @@ import os
 import sys
 
 src, dst = sys.argv[1], sys.argv[2]
-timed = int(sys.argv[3]) if len(sys.argv) > 3 else 10  # bench --steps of the profiled run
+timed = int(sys.argv[3]) if len(sys.argv) > 3 else 20  # bench --steps of the profiled run
 cmd = sys.argv[4] if len(sys.argv) > 4 else "(default arguments)"
 out = [f"# rocprofv3 summary: {os.path.basename(src)}\n",
        "Command: `tools/profile.sh` = rocprofv3 --kernel-trace --stats and four separate --pmc passes over "

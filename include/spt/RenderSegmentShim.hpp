@@ -93,6 +93,10 @@ inline void sync_globals()
     check(ctx, spt_set_camera(ctx, view, eye, sky), "spt_set_camera");
     check(ctx, spt_set_params(ctx, g_width, g_height, g_samples, g_bounces, seed), "spt_set_params");
     last.swap(key);
+    // page-lock g_data once (best effort): the per-call copy-back becomes a direct DMA
+    static const void *pinned = nullptr;
+    if (g_data && pinned != g_data && spt_pin_host(ctx, g_data, (size_t)g_width * g_height * 3) == SPT_OK)
+        pinned = g_data;
 }
 
 }  // namespace spt_shim

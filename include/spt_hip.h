@@ -156,6 +156,12 @@ SPT_API int spt_render_segment(spt_ctx *ctx, uint32_t yBegin, uint32_t yEnd, uin
  * keyed per (pixel, sample) -- and cb(user, samples_done) runs on the calling thread
  * (nullable; a nonzero return stops the render there).  The last pass is the full
  * render.  cb must not call into the same context. */
+/* Page-lock a caller-owned host buffer -- typically g_data (Globals.hpp:19, malloc'd)
+ * -- so the per-call device-to-host copy of the render is a direct DMA and the GL
+ * thread's UpdateTexture (Renderer.hpp:157-164) reads the same pinned bytes.
+ * Idempotent per pointer; spt_unpin_host releases it (spt_ctx_destroy releases all). */
+SPT_API int spt_pin_host(spt_ctx *ctx, void *ptr, size_t bytes);
+SPT_API int spt_unpin_host(spt_ctx *ctx, void *ptr);
 typedef int (*spt_progress_fn)(void *user, uint32_t samples_done);
 SPT_API int spt_render_progressive(spt_ctx *ctx, int mode, uint32_t yBegin, uint32_t yEnd, uint32_t xBegin,
                                    uint32_t xEnd, uint32_t pass_spp, float *rgba_out, uint8_t *g_data,

@@ -104,6 +104,8 @@ def lib() -> ctypes.CDLL:
         "spt_camera_basis": ([P, P, P, P], I),
         "spt_save_bmp": ([ctypes.c_char_p, u32, u32, u32, P], I),
         "spt_render_progressive": ([P, I, u32, u32, u32, u32, u32, P, P, P, P], I),
+        "spt_pin_host": ([P, P, ctypes.c_size_t], I),
+        "spt_unpin_host": ([P, P], I),
         "spt_selftest_numerics": ([P, P, P, P, u32, P], I),
     }
     for name, (args, res) in sig.items():

@@ -95,6 +95,8 @@ struct spt_ctx {
     uint8_t *d_frame8 = nullptr;
     size_t frame8_cap = 0;
 
+    std::vector<void *> pinned;  // host buffers registered by spt_pin_host
+
     // timing
     std::vector<EventPair> pending_render, pending_fold, pool;
     double render_ms = 0, fold_ms = 0, last_render_ms = 0;
@@ -613,6 +615,7 @@ void spt_ctx_destroy(spt_ctx *ctx)
             (void)hipEventDestroy(p.b);
         }
     (void)hipDeviceSynchronize();  // async renders on caller streams
+    for (void *p : ctx->pinned) (void)hipHostUnregister(p);
     if (ctx->ref_ev) (void)hipEventDestroy(ctx->ref_ev);
     void *bufs[] = {ctx->d_shade, ctx->d_mat, ctx->d_slots, ctx->d_orig, ctx->d_nodes,
                     ctx->d_kpre, ctx->d_counters, ctx->d_stage, ctx->d_frame8};
@@ -764,6 +767,31 @@ int spt_render_segment_task(spt_ctx *ctx, uint32_t yB, uint32_t yE, uint32_t xB,
                             uint8_t *g_data)
 {
     return render_segment_host(ctx, SPT_MODE_TASK, yB, yE, xB, xE, rgba, g_data);
+}
+
+int spt_pin_host(spt_ctx *ctx, void *ptr, size_t bytes)
+{
+    if (!ctx) return fail(nullptr, SPT_ERR_ARG, "null context");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    if (!ptr || bytes == 0) return fail(ctx, SPT_ERR_ARG, "null or empty host buffer");
+    if (std::find(ctx->pinned.begin(), ctx->pinned.end(), ptr) != ctx->pinned.end()) return SPT_OK;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    HIP_TRY(ctx, hipHostRegister(ptr, bytes, hipHostRegisterDefault));
+    ctx->pinned.push_back(ptr);
+    return SPT_OK;
+}
+
+int spt_unpin_host(spt_ctx *ctx, void *ptr)
+{
+    if (!ctx) return fail(nullptr, SPT_ERR_ARG, "null context");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    auto it = std::find(ctx->pinned.begin(), ctx->pinned.end(), ptr);
+    if (it == ctx->pinned.end()) return fail(ctx, SPT_ERR_ARG, "buffer %p was not pinned", ptr);
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    HIP_TRY(ctx, hipHostUnregister(ptr));
+    ctx->pinned.erase(it);
+    return SPT_OK;
 }
 
 int spt_render_progressive(spt_ctx *ctx, int mode, uint32_t yB, uint32_t yE, uint32_t xB, uint32_t xE,

@@ -109,6 +109,14 @@ class Context:
         self._check(fn(self._h, yB, yE, xB, xE, _p(rgba), gp))
         return rgba
 
+    def pin_host(self, arr: np.ndarray) -> None:
+        """Page-lock a host array (e.g. g_data) for direct device-to-host copies."""
+        assert arr.flags.c_contiguous
+        self._check(_native.lib().spt_pin_host(self._h, _p(arr), arr.nbytes))
+
+    def unpin_host(self, arr: np.ndarray) -> None:
+        self._check(_native.lib().spt_unpin_host(self._h, _p(arr)))
+
     def render_progressive(self, yB, yE, xB, xE, pass_spp: int, g_data=None, callback=None, task=False):
         """Progressive render in passes of pass_spp samples.  After each pass the returned
         float4 array (and g_data, if given) hold the render at the samples done so far

@@ -479,3 +479,20 @@ def test_progressive_passes_equal_lower_spp_renders(spt, ctx, golden_scenes, tas
     setup(ctx, scene, W, H, 10, 50)
     assert_bitwise(part, ctx.render_segment(*region, task=task), "stopped after 10 samples")
     setup(ctx, scene, W, H, 20, 50)
+
+
+def test_pinned_gdata_renders_the_same(spt, ctx, golden_scenes):
+    """spt_pin_host page-locks the caller's g_data (the per-frame UpdateTexture source,
+    Renderer.hpp:157-164); renders into it are unchanged."""
+    setup(ctx, scene_from(spt, golden_scenes, "random"), 120, 80, 6, 50)
+    g_plain = np.zeros(120 * 80 * 3, np.uint8)
+    a = ctx.render_segment(0, 80, 0, 120, g_plain)
+    g_pin = np.zeros_like(g_plain)
+    ctx.pin_host(g_pin)
+    ctx.pin_host(g_pin)  # idempotent
+    b = ctx.render_segment(0, 80, 0, 120, g_pin)
+    ctx.unpin_host(g_pin)
+    assert_bitwise(a, b, "pinned vs pageable")
+    assert np.array_equal(g_plain, g_pin)
+    with pytest.raises(spt.SptError):
+        ctx.unpin_host(g_pin)

@@ -496,3 +496,40 @@ def test_pinned_gdata_renders_the_same(spt, ctx, golden_scenes):
     assert np.array_equal(g_plain, g_pin)
     with pytest.raises(spt.SptError):
         ctx.unpin_host(g_pin)
+
+
+def test_config5_scene_region_vs_oracle(spt, ctx, oracle):
+    """BASELINE config 5's 10 000-sphere scene (cluster tree with line / front / near
+    culling): a 48x24 region of the 1920x1080 frame at 8 spp,
+    depth 50, every pixel bit-exact against the oracle's brute-force uint32 scan
+    (parity unpinned against the reference itself, which hangs past 255 spheres)."""
+    s = spt.generate_stress(1, 10000)
+    setup(ctx, s, 1920, 1080, 8, 50)
+    region = (600, 624, 900, 948)
+    got = ctx.render_segment(*region)
+    osc = oracle.OracleScene(s.centers, s.radii, s.colors, s.materials, s.fuzz)
+    fr = oracle.make_frame(spt.camera_basis(EYE, LOOK, UP), EYE, SKY, 1920, 1080, 8, 50, 1)
+    want, _ = oracle.render_segment(osc, fr, *region)
+    assert_bitwise(got[:, :3], want[:, :3], "config-5 scene region")
+
+
+def test_config3_full_frame_batches_vs_oracle(spt, ctx, oracle, golden_scenes):
+    """BASELINE config 3 at full size (3840x2160, 1024 spp, depth 50): 24 sample batches
+    of the workspace folded in order; sampled pixels bit-exact against the oracle and
+    the RGB8 bytes of those pixels equal WritePixel of the oracle's colour."""
+    setup(ctx, scene_from(spt, golden_scenes, "random"), 3840, 2160, 1024, 50)
+    ctx.reset_stats()
+    g = np.zeros(3840 * 2160 * 3, np.uint8)
+    a = ctx.render_segment(0, 2160, 0, 3840, g)
+    st = ctx.stats()
+    assert st["samples"] == 3840 * 2160 * 1024 and st["launches"] > 1
+    sc = oscene_from(oracle, golden_scenes, "random")
+    fr = oracle.make_frame(golden_scenes["view"], EYE, SKY, 3840, 2160, 1024, 50, 1)
+    rng = np.random.default_rng(7)
+    for _ in range(6):
+        x, y = int(rng.integers(0, 3840)), int(rng.integers(0, 2160))
+        gw = np.zeros(3840 * 2160 * 3, np.uint8)
+        want, _ = oracle.render_segment(sc, fr, y, y + 1, x, x + 1, rgb8=gw)
+        assert_bitwise(a[y * 3840 + x, :3], want[0, :3], f"pixel {(x, y)}")
+        i = 3 * ((2160 - 1 - y) * 3840 + x)
+        assert np.array_equal(g[i:i + 3], gw[i:i + 3])

@@ -61,6 +61,12 @@
 #define SPT_DUP_BALL 0
 #endif
 
+// 1: tree walks use the layout of the wave's majority direction octant (0: layout 0
+// for every wave: one eighth of the node table in the scalar cache)
+#ifndef SPT_TREE_OCTANTS
+#define SPT_TREE_OCTANTS 1
+#endif
+
 // 1: a leaf's member pretests all run before its first branch
 #ifndef SPT_PRE_ILP
 #define SPT_PRE_ILP 1
@@ -467,7 +473,11 @@ __device__ __forceinline__ Hit find_closest(const AccelView &ac, const f3 &o, co
         const uint32_t oct = (2u * (uint32_t)__popcll(__ballot(active && d.x < 0.f)) > nlive ? 1u : 0u) |
                              (2u * (uint32_t)__popcll(__ballot(active && d.y < 0.f)) > nlive ? 2u : 0u) |
                              (2u * (uint32_t)__popcll(__ballot(active && d.z < 0.f)) > nlive ? 4u : 0u);
+#if SPT_TREE_OCTANTS
         nodes += (size_t)8 * (ac.n_nodes + 1) * oct;
+#else
+        (void)oct;
+#endif
     }
     // Tree nodes {Cb, K1, skip, slot, F, c'|Cb|^2}: three conservative tests
     // (DESIGN.md §4.4), without a square root per node; a lane may need the node

@@ -52,10 +52,26 @@ namespace spt {
 #define SPT_RENDER_ATTR
 #endif
 
+// LDS tree variant (SPT_LDS_TREE): blocks of kLdsBlock threads copy node layout 0
+// into LDS once and walk it with broadcast LDS reads; two blocks per CU.
+#ifndef SPT_LDS_TREE
+#define SPT_LDS_TREE 1
+#endif
+#ifndef SPT_LDS_BLOCK
+#define SPT_LDS_BLOCK 1024
+#endif
+constexpr uint32_t kLdsBlock = SPT_LDS_BLOCK;
+// 32-byte node records (pad included) per block: 2432 = 76 KiB, with the sampler's
+// 4 KiB exactly half of the CU's 160 KiB
+#ifndef SPT_LDS_NODES
+#define SPT_LDS_NODES 2432
+#endif
+constexpr uint32_t kLdsNodeRecords = SPT_LDS_NODES;
+
 // One kernel per traversal shape (flat list of 4- or 8-slot leaves, tree of
 // 8-slot leaves), each with its own register allocation; launch_render picks.
-template <bool TREE, int LEAF>
-__global__ __launch_bounds__(kRenderBlock) SPT_RENDER_ATTR void render_kernel(RenderArgs a)
+template <bool TREE, int LEAF, bool LDSN, uint32_t BLOCK>
+__device__ __forceinline__ void render_body(const RenderArgs &a)
 {
     const uint32_t lane = __lane_id();
     const f3 eye = mk(a.cam.eye[0], a.cam.eye[1], a.cam.eye[2]);
@@ -67,7 +83,15 @@ __global__ __launch_bounds__(kRenderBlock) SPT_RENDER_ATTR void render_kernel(Re
     (void)rh;
     (void)eye;
 
-    __shared__ uint32_t s_lds[kRenderBlock];  // wave-private scratch of the cooperative sampler
+    __shared__ uint32_t s_lds[BLOCK];  // wave-private scratch of the cooperative sampler
+    __shared__ uint4 s_nodes[LDSN ? 2 * kLdsNodeRecords : 1];
+    if (LDSN) {
+        // the host launches this variant only when n_nodes + 1 <= kLdsNodeRecords
+        const uint4 *src = (const uint4 *)a.scene.accel.nodes;
+        const uint32_t n4 = 2u * (a.scene.accel.n_nodes + 1u);
+        for (uint32_t k = threadIdx.x; k < n4; k += BLOCK) s_nodes[k] = src[k];
+        __syncthreads();
+    }
     Path ps;
     ps.phase = PH_IDLE;
     ps.item = ps.bounce = ps.spec = 0;
@@ -150,7 +174,7 @@ __global__ __launch_bounds__(kRenderBlock) SPT_RENDER_ATTR void render_kernel(Re
         ++d_iters;
         // ---- one cast + one shading step ----
         const bool act = ps.phase != PH_IDLE;
-        const Hit h = find_closest<TREE, LEAF>(a.scene.accel, ps.o, ps.d, act, dg);
+        const Hit h = find_closest<TREE, LEAF, LDSN>(a.scene.accel, ps.o, ps.d, act, dg, (const uint32_t *)s_nodes);
 #if SPT_DUP_CAST
         {
             // timing experiment only: a second, discarded cast (its marginal cost)
@@ -199,6 +223,24 @@ __global__ __launch_bounds__(kRenderBlock) SPT_RENDER_ATTR void render_kernel(Re
     (void)d_cyc_refill;
 #undef SPT_STAMP
 }
+
+template <bool TREE, int LEAF>
+__global__ __launch_bounds__(kRenderBlock) SPT_RENDER_ATTR void render_kernel(RenderArgs a)
+{
+    render_body<TREE, LEAF, false, kRenderBlock>(a);
+}
+
+#if SPT_LDS_TREE
+// its own register budget: 1024-thread blocks, two per CU, need 8 waves per SIMD
+#ifndef SPT_LDS_NUM_SGPR
+#define SPT_LDS_NUM_SGPR 80
+#endif
+__global__ __launch_bounds__(kLdsBlock)
+    __attribute__((amdgpu_num_sgpr(SPT_LDS_NUM_SGPR), amdgpu_waves_per_eu(2 * kLdsBlock / 256))) void render_kernel_lds(RenderArgs a)
+{
+    render_body<true, (int)kClusterSlots, true, kLdsBlock>(a);
+}
+#endif
 
 __global__ __launch_bounds__(256) void fold_kernel(FoldArgs a)
 {
@@ -296,8 +338,43 @@ __global__ void selftest_kernel(const float *a, const float *b, const uint32_t *
     o[13] = uniform_bits(bits[i], 0.f, 1.f);
 }
 
+#if SPT_LDS_TREE
+// Blocks per CU of the LDS tree variant and CUs of the device (queried once).
+static void lds_tree_shape(int *per_cu, int *num_cu)
+{
+    static int pc = -1, nc = 0;
+    if (pc < 0) {
+        int dev = 0, b = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&nc, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, render_kernel_lds, (int)kLdsBlock, 0) != hipSuccess)
+            b = 0;
+        pc = b;
+    }
+    *per_cu = pc;
+    *num_cu = nc;
+}
+#endif
+
 hipError_t launch_render(const RenderArgs &a, uint32_t grid, uint32_t block, hipStream_t s)
 {
+#if SPT_LDS_TREE
+    if (a.scene.accel.tree && a.scene.accel.n_nodes + 1u <= kLdsNodeRecords) {
+        // all resident blocks, or fewer when the launch has under 2 claims per wave
+        // (render_grid's rule; a frame in flight on another stream only queues)
+        int per_cu = 0, num_cu = 0;
+        lds_tree_shape(&per_cu, &num_cu);
+        if (per_cu > 0) {
+            (void)grid;
+            (void)block;
+            const uint64_t claims = ((uint64_t)a.n_items + a.claim - 1) / a.claim;
+            const uint64_t per_block = 2 * (kLdsBlock / 64);
+            uint64_t g = (claims + per_block - 1) / per_block;
+            g = g < (uint64_t)per_cu * num_cu ? g : (uint64_t)per_cu * num_cu;
+            hipLaunchKernelGGL(render_kernel_lds, dim3((uint32_t)g), dim3(kLdsBlock), 0, s, a);
+            return hipGetLastError();
+        }
+    }
+#endif
     if (a.scene.accel.tree)
         hipLaunchKernelGGL((render_kernel<true, (int)kClusterSlots>), dim3(grid), dim3(block), 0, s, a);
     else if (a.scene.accel.leaf_slots == kFlatLeafSlots)

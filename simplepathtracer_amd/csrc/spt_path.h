@@ -323,9 +323,11 @@ __device__ __forceinline__ void test_leaf_pre(cfloat *slots, cfloat *kpre, const
 // entered when the ray's line may pass one of its members (the "line" test of
 // DESIGN.md §4.4).  TREE = true: preorder walk of the cluster tree in the layout
 // of the wave's majority direction octant with the line, front and near tests.
-template <bool TREE, int LEAF>
+// LDSN (tree only): the node records are read from the block's LDS copy of layout 0
+// (`lnodes`, render_kernel's prologue) instead of scalar loads of the octant layouts.
+template <bool TREE, int LEAF, bool LDSN = false>
 __device__ __forceinline__ Hit find_closest(const AccelView &ac, const f3 &o, const f3 &d, bool active,
-                                            CastDiag &dg)
+                                            CastDiag &dg, const uint32_t *lnodes = nullptr)
 {
     Hit h;
     h.idx = kMiss;
@@ -474,7 +476,7 @@ __device__ __forceinline__ Hit find_closest(const AccelView &ac, const f3 &o, co
                              (2u * (uint32_t)__popcll(__ballot(active && d.y < 0.f)) > nlive ? 2u : 0u) |
                              (2u * (uint32_t)__popcll(__ballot(active && d.z < 0.f)) > nlive ? 4u : 0u);
 #if SPT_TREE_OCTANTS
-        nodes += (size_t)8 * (ac.n_nodes + 1) * oct;
+        if (!LDSN) nodes += (size_t)8 * (ac.n_nodes + 1) * oct;
 #else
         (void)oct;
 #endif
@@ -504,18 +506,21 @@ __device__ __forceinline__ Hit find_closest(const AccelView &ac, const f3 &o, co
     pl.qoe = !active ? INFINITY : (no_cull ? -INFINITY : qo);
     pl.tinit = !active ? -INFINITY : (no_cull ? INFINITY : __builtin_fmaf(2e-6f, ac.pre_cm + olen * 1.000001f, 1e-6f) - dod);
 #endif
+    // node record q of node j: a scalar load, or a broadcast LDS read
+    auto ldn = [&](uint32_t j, int q) -> uint32_t { return LDSN ? lnodes[8 * j + q] : nodes[8 * j + q]; };
     uint32_t i = 0;
     uint32_t nb[8];
 #pragma unroll
-    for (int q = 0; q < 8; ++q) nb[q] = nodes[q];
+    for (int q = 0; q < 8; ++q) nb[q] = ldn(0, q);
     while (i < ac.n_nodes) {
         const float bx = __uint_as_float(nb[0]), by = __uint_as_float(nb[1]), bz = __uint_as_float(nb[2]);
         const float k1 = __uint_as_float(nb[3]), fr = __uint_as_float(nb[6]), cb2n = __uint_as_float(nb[7]);
-        const uint32_t skip = nb[4], leaf_slot = nb[5];
+        const uint32_t skip = LDSN ? __builtin_amdgcn_readfirstlane(nb[4]) : nb[4];
+        const uint32_t leaf_slot = LDSN ? __builtin_amdgcn_readfirstlane(nb[5]) : nb[5];
         // speculative prefetch of the preorder successor (prefetching the skip
         // target as well measured 4% slower on config 5)
 #pragma unroll
-        for (int q = 0; q < 8; ++q) nb[q] = nodes[8 * (i + 1) + q];
+        for (int q = 0; q < 8; ++q) nb[q] = ldn(i + 1, q);
         const float tcb = __builtin_fmaf(bx, d.x, __builtin_fmaf(by, d.y, __builtin_fmaf(bz, d.z, -dod)));
         // Cb.o from o itself (not -2c o: two VGPRs fewer keep the kernel at 64)
         const float cbo = __builtin_fmaf(bx, o.x, __builtin_fmaf(by, o.y, bz * o.z));
@@ -546,7 +551,7 @@ __device__ __forceinline__ Hit find_closest(const AccelView &ac, const f3 &o, co
         const uint32_t next = (mm != 0ull && !leaf) ? i + 1 : skip;
         if (next != i + 1) {
 #pragma unroll
-            for (int q = 0; q < 8; ++q) nb[q] = nodes[8 * next + q];
+            for (int q = 0; q < 8; ++q) nb[q] = ldn(next, q);
         }
         i = next;
     }

@@ -513,6 +513,32 @@ def test_config5_scene_region_vs_oracle(spt, ctx, oracle):
     assert_bitwise(got[:, :3], want[:, :3], "config-5 scene region")
 
 
+@pytest.mark.parametrize("n", [10000, 20000])
+def test_tree_kernels_lds_and_scalar_vs_oracle(spt, ctx, oracle, n):
+    """Both tree kernels: up to 2431 nodes the walk reads layout 0 from the block's LDS
+    copy (render_kernel_lds); a 20 000-sphere scene has more nodes and
+    takes the scalar-load kernel over the 8 octant layouts.  A 16x8 region at 4 spp,
+    bit-exact against the oracle's brute-force scan, and the same ray count."""
+    import ctypes
+    s = spt.generate_stress(3, n)
+    c = np.ascontiguousarray(s.centers, np.float32)
+    r = np.ascontiguousarray(s.radii, np.float32)
+    nodes = ctypes.c_uint32(0)
+    P = ctypes.c_void_p
+    assert spt.lib().spt_accel_check(c.ctypes.data_as(P), r.ctypes.data_as(P), len(r), 8, 4,
+                                            ctypes.byref(nodes)) == 0
+    assert (nodes.value + 1 <= 2432) == (n == 10000), nodes.value
+    setup(ctx, s, 1920, 1080, 4, 50)
+    region = (500, 508, 944, 960)
+    ctx.reset_stats()
+    got = ctx.render_segment(*region)
+    osc = oracle.OracleScene(s.centers, s.radii, s.colors, s.materials, s.fuzz)
+    fr = oracle.make_frame(spt.camera_basis(EYE, LOOK, UP), EYE, SKY, 1920, 1080, 4, 50, 1)
+    want, casts = oracle.render_segment(osc, fr, *region)
+    assert_bitwise(got[:, :3], want[:, :3], f"{n}-sphere region")
+    assert ctx.stats()["casts"] == casts
+
+
 def test_config3_full_frame_batches_vs_oracle(spt, ctx, oracle, golden_scenes):
     """BASELINE config 3 at full size (3840x2160, 1024 spp, depth 50): 24 sample batches
     of the workspace folded in order; sampled pixels bit-exact against the oracle and

@@ -67,6 +67,15 @@
 #define SPT_TREE_OCTANTS 1
 #endif
 
+// 1: tree node masks as the AND of the three compare ballots
+#ifndef SPT_TREE_BALLOTS
+#define SPT_TREE_BALLOTS 1
+#endif
+// 1: the LDS tree walk issues the successor's reads before the node's tests
+#ifndef SPT_LDS_EARLY
+#define SPT_LDS_EARLY 1
+#endif
+
 // 1: a leaf's member pretests all run before its first branch
 #ifndef SPT_PRE_ILP
 #define SPT_PRE_ILP 1
@@ -521,6 +530,10 @@ __device__ __forceinline__ Hit find_closest(const AccelView &ac, const f3 &o, co
         // target as well measured 4% slower on config 5)
 #pragma unroll
         for (int q = 0; q < 8; ++q) nb[q] = ldn(i + 1, q);
+#if SPT_LDS_EARLY
+        // LDS walk: keep the successor's ds_reads ahead of this node's tests
+        if (LDSN) __builtin_amdgcn_sched_barrier(0);
+#endif
         const float tcb = __builtin_fmaf(bx, d.x, __builtin_fmaf(by, d.y, __builtin_fmaf(bz, d.z, -dod)));
         // Cb.o from o itself (not -2c o: two VGPRs fewer keep the kernel at 64)
         const float cbo = __builtin_fmaf(bx, o.x, __builtin_fmaf(by, o.y, bz * o.z));
@@ -530,7 +543,12 @@ __device__ __forceinline__ Hit find_closest(const AccelView &ac, const f3 &o, co
         const bool line = x <= k1;
         const bool front = __builtin_fmaf(1e-4f, olen, tcb) >= -fr;
         const bool near = !(w > sn * sn);
+#if SPT_TREE_BALLOTS
+        // the AND of the three compare ballots: each is the compare's own lane mask
+        const unsigned long long mm = (__ballot(line) & __ballot(front) & __ballot(near) & live_mask) | nocull_mask;
+#else
         const unsigned long long mm = (__ballot(line && front && near) & live_mask) | nocull_mask;
+#endif
         const bool leaf = leaf_slot != kNoSlot;
         if (SPT_DIAG) {
             dg.nodes += 1;

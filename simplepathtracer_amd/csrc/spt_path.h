@@ -526,6 +526,11 @@ __device__ __forceinline__ Hit find_closest(const AccelView &ac, const f3 &o, co
         const float k1 = __uint_as_float(nb[3]), fr = __uint_as_float(nb[6]), cb2n = __uint_as_float(nb[7]);
         const uint32_t skip = LDSN ? __builtin_amdgcn_readfirstlane(nb[4]) : nb[4];
         const uint32_t leaf_slot = LDSN ? __builtin_amdgcn_readfirstlane(nb[5]) : nb[5];
+#if SPT_LDS_EARLY
+        // LDS walk: this node's scalars before the successor's reads are issued (a
+        // readfirstlane after them would wait for them: LDS waits are lgkmcnt(0))
+        if (LDSN) asm volatile("" ::"s"(skip), "s"(leaf_slot));
+#endif
         // speculative prefetch of the preorder successor (prefetching the skip
         // target as well measured 4% slower on config 5)
 #pragma unroll

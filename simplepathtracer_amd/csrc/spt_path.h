@@ -76,6 +76,11 @@
 #define SPT_LDS_EARLY 1
 #endif
 
+// 1: the LDS tree walk also prefetches each node's skip target
+#ifndef SPT_LDS_SKIPPF
+#define SPT_LDS_SKIPPF 0
+#endif
+
 // 1: a leaf's member pretests all run before its first branch
 #ifndef SPT_PRE_ILP
 #define SPT_PRE_ILP 1
@@ -535,6 +540,14 @@ __device__ __forceinline__ Hit find_closest(const AccelView &ac, const f3 &o, co
         // target as well measured 4% slower on config 5)
 #pragma unroll
         for (int q = 0; q < 8; ++q) nb[q] = ldn(i + 1, q);
+#if SPT_LDS_SKIPPF
+        // LDS walk: the skip target's record as well (a leaf's skip is i + 1)
+        uint32_t ns[8];
+        if (LDSN) {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) ns[q] = ldn(skip, q);
+        }
+#endif
 #if SPT_LDS_EARLY
         // LDS walk: keep the successor's ds_reads ahead of this node's tests
         if (LDSN) __builtin_amdgcn_sched_barrier(0);
@@ -573,8 +586,16 @@ __device__ __forceinline__ Hit find_closest(const AccelView &ac, const f3 &o, co
         }
         const uint32_t next = (mm != 0ull && !leaf) ? i + 1 : skip;
         if (next != i + 1) {
+#if SPT_LDS_SKIPPF
+            if (LDSN) {
 #pragma unroll
-            for (int q = 0; q < 8; ++q) nb[q] = ldn(next, q);
+                for (int q = 0; q < 8; ++q) nb[q] = ns[q];
+            } else
+#endif
+            {
+#pragma unroll
+                for (int q = 0; q < 8; ++q) nb[q] = ldn(next, q);
+            }
         }
         i = next;
     }

@@ -123,7 +123,7 @@ def main():
     from simplepathtracer_amd.distributed import FrameSplit, even_strip, render_frame
     split = FrameSplit(W, H, world, args.strip or even_strip(H, world))
     slot_bytes = 12 if args.mode == "segment" else 16
-    one_batch = W * H * spp * slot_bytes <= (4 << 30)  # the context's default workspace
+    one_batch = W * H * spp * slot_bytes <= (16 << 30)  # the context's default workspace
     nst = args.streams if args.streams > 0 else (2 if one_batch else 1)
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(nst - 1)]
     bufs = []

@@ -136,7 +136,7 @@ SPT_API int spt_accel_check(const float *centers4, const float *radii, uint32_t 
  *   category; the host reads the queue length back after each pass. */
 enum { SPT_ENGINE_MEGAKERNEL = 0, SPT_ENGINE_WAVEFRONT = 1 };
 SPT_API int spt_set_engine(spt_ctx *ctx, int engine);
-/* Upper bound of the per-sample workspace (default 4 GiB).  Larger frames are
+/* Upper bound of the per-sample workspace (default 16 GiB).  Larger frames are
  * rendered in sample batches folded in order. */
 SPT_API int spt_set_workspace(spt_ctx *ctx, uint64_t bytes);
 

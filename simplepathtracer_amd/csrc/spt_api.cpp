@@ -84,7 +84,7 @@ struct spt_ctx {
     bool params_set = false;
 
     // workspace
-    uint64_t ws_bytes = 4ull << 30;
+    uint64_t ws_bytes = 16ull << 30;  // of 288 GB HBM: config 5 in one launch, config 3 in 6
     // one workspace per stream, so renders on different streams can be in flight
     // together (the next frame's blocks fill the GPU while the last paths of the
     // previous one drain)

@@ -540,7 +540,7 @@ def test_tree_kernels_lds_and_scalar_vs_oracle(spt, ctx, oracle, n):
 
 
 def test_config3_full_frame_batches_vs_oracle(spt, ctx, oracle, golden_scenes):
-    """BASELINE config 3 at full size (3840x2160, 1024 spp, depth 50): 24 sample batches
+    """BASELINE config 3 at full size (3840x2160, 1024 spp, depth 50): 6 sample batches
     of the workspace folded in order; sampled pixels bit-exact against the oracle and
     the RGB8 bytes of those pixels equal WritePixel of the oracle's colour."""
     setup(ctx, scene_from(spt, golden_scenes, "random"), 3840, 2160, 1024, 50)

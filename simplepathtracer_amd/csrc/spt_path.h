@@ -76,6 +76,10 @@
 #define SPT_LDS_EARLY 1
 #endif
 
+// 1: flat node records pinned to SGPRs only when the walk reaches them
+#ifndef SPT_FLAT_LATE_PIN
+#define SPT_FLAT_LATE_PIN 0
+#endif
 // 1: the LDS tree walk also prefetches each node's skip target
 #ifndef SPT_LDS_SKIPPF
 #define SPT_LDS_SKIPPF 0
@@ -465,6 +469,36 @@ __device__ __forceinline__ Hit find_closest(const AccelView &ac, const f3 &o, co
             for (int i = 0; i < 8; ++i) r[i] = q[i];
         };
 #endif
+#if SPT_NODE_X8 && SPT_FLAT_LATE_PIN
+        // the record's register pin (which waits for its load) after the previous
+        // node's branch instead of right at the load's issue
+        typedef uint32_t u32x8b __attribute__((ext_vector_type(8)));
+        typedef __attribute__((address_space(4))) const u32x8b cu32x8b;
+        auto pin = [&](u32x8b &v, uint32_t(&r)[8]) {
+            asm volatile("" : "+s"(v));
+#pragma unroll
+            for (int i = 0; i < 8; ++i) r[i] = v[i];
+        };
+        u32x8b va = *(cu32x8b *)p, vb;
+        pin(va, ra);
+        uint32_t left = ac.n_nodes;
+        while (left >= 2u) {
+            const float xa = node_x(ra);
+            __builtin_amdgcn_sched_barrier(0);
+            vb = *(cu32x8b *)(p + 8);
+            __builtin_amdgcn_sched_barrier(0);
+            finish(ra, xa);
+            pin(vb, rb);
+            const float xb = node_x(rb);
+            __builtin_amdgcn_sched_barrier(0);
+            va = *(cu32x8b *)(p + 16);
+            __builtin_amdgcn_sched_barrier(0);
+            finish(rb, xb);
+            pin(va, ra);
+            p += 16;
+            left -= 2u;
+        }
+#else
         load_rec(p, ra);
         uint32_t left = ac.n_nodes;
         while (left >= 2u) {
@@ -479,6 +513,7 @@ __device__ __forceinline__ Hit find_closest(const AccelView &ac, const f3 &o, co
             p += 16;
             left -= 2u;
         }
+#endif
         if (left != 0u) finish(ra, node_x(ra));
         return h;
     }

@@ -339,19 +339,25 @@ __global__ void selftest_kernel(const float *a, const float *b, const uint32_t *
 }
 
 #if SPT_LDS_TREE
-// Blocks per CU of the LDS tree variant and CUs of the device (queried once).
+// Blocks per CU of the LDS tree variant and CUs of the device, queried once per
+// process (a thread-safe local static: RenderJob threads launch concurrently; every
+// device of the node is an MI355X).  per_cu = 0 disables the variant.
 static void lds_tree_shape(int *per_cu, int *num_cu)
 {
-    static int pc = -1, nc = 0;
-    if (pc < 0) {
-        int dev = 0, b = 0;
-        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&nc, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, render_kernel_lds, (int)kLdsBlock, 0) != hipSuccess)
-            b = 0;
-        pc = b;
-    }
-    *per_cu = pc;
-    *num_cu = nc;
+    struct Shape {
+        int pc = 0, nc = 0;
+    };
+    static const Shape shape = [] {
+        Shape r;
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&r.nc, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&r.pc, render_kernel_lds, (int)kLdsBlock, 0) != hipSuccess)
+            r.pc = 0;
+        return r;
+    }();
+    *per_cu = shape.pc;
+    *num_cu = shape.nc;
 }
 #endif
 

@@ -304,16 +304,25 @@ static v4 sample_reflective(tctx *t, v4 d, v4 o, uint32_t bounce, uint32_t idx)
     return trace(t, d, o, bounce);
 }
 
-/* SingleThreadPathTracer.hpp:48-92.  pow()/sqrt() on float arguments resolve to
- * ::pow(double,double) / ::sqrt(double) under libstdc++, so
- * Schlick and the Snell scalar are evaluated in double and narrowed. */
+/* SingleThreadPathTracer.hpp:48-92.  pow()/sqrt() on float arguments bind to
+ * std::pow(float,float) / std::sqrt(float) in the reference's translation unit:
+ * IOHelpers.hpp:5-9 includes the stb implementations, whose <math.h>/<stdlib.h>
+ * are libstdc++'s `using std::pow; using std::sqrt; using std::abs;` wrappers,
+ * before Renderer.hpp:6-8 includes the tracers and the scene generator
+ * (oracle/probe_overloads.cpp).  So Schlick, the total-internal-reflection test
+ * and the Snell scalar are all float: glibc's powf (called here, as the
+ * reference's __builtin_powf does) and the correctly rounded sqrtf. */
 static inline float schlick_of(float rsq, float c)
 {
-    return (float)((double)rsq + (double)(1.f - rsq) * pow((double)(1.f - c), 5.0));
+    return rsq + (1.f - rsq) * powf(1.f - c, 5.f);
+}
+static inline int no_tir(float r, float c)
+{
+    return r * sqrtf(1.f - c * c) < 1.f;
 }
 static inline v4 refract_dir(v4 d, v4 n, float r, float c)
 {
-    float k = (float)((double)(r * c) - sqrt((double)(1.f - r * r * (1.f - c * c))));
+    float k = r * c - sqrtf(1.f - r * r * (1.f - c * c));
     return vnorm(vadd(vmul(d, r), vmul(n, k)));
 }
 
@@ -328,23 +337,23 @@ static v4 sample_refractive(tctx *t, v4 d, v4 o, uint32_t bounce, uint32_t idx)
     v4 n = contact_normal(o, c0);
     float c = vdot(vneg(n), d);
     float r = nAir / nGlass;
-    float rsq = (float)pow((double)((nAir - nGlass) / (nAir + nGlass)), 2.0);
+    float rsq = powf((nAir - nGlass) / (nAir + nGlass), 2.f);
     float schlick = schlick_of(rsq, c);
     v4 nd;
 
     if (spo_uniform(&t->st, 0.f, 1.f) < schlick) {
         nd = vreflect(d, n);
-    } else if ((double)r * sqrt((double)(1.f - c * c)) < 1.0) {
+    } else if (no_tir(r, c)) {
         d = refract_dir(d, n, r, c);
         o = farthest_contact(c0, rad, o, d);
         n = vneg(contact_normal(o, c0));
         c = vdot(vneg(n), d);
         r = nGlass / nAir;
-        rsq = (float)pow((double)((nGlass - nAir) / (nGlass + nAir)), 2.0);
+        rsq = powf((nGlass - nAir) / (nGlass + nAir), 2.f);
         schlick = schlick_of(rsq, c);
         if (spo_uniform(&t->st, 0.f, 1.f) < schlick)
             nd = vreflect(d, n);
-        else if ((double)r * sqrt((double)(1.f - c * c)) < 1.0)
+        else if (no_tir(r, c))
             nd = refract_dir(d, n, r, c);
         else
             nd = vreflect(d, n);
@@ -543,21 +552,21 @@ uint64_t spo_render_segment_task(const spo_scene *sc, const spo_frame *fr, uint3
                 v4 n = contact_normal(tk->origin, c0);
                 float c = vdot(vneg(n), tk->direction);
                 float r = nAir / nGlass;
-                float rsq = (float)pow((double)((nAir - nGlass) / (nAir + nGlass)), 2.0);
+                float rsq = powf((nAir - nGlass) / (nAir + nGlass), 2.f);
                 float schlick = schlick_of(rsq, c);
                 if (spo_uniform(&tk->st, 0.f, 1.f) < schlick) {
                     tk->direction = vreflect(tk->direction, n);
-                } else if ((double)r * sqrt((double)(1.f - c * c)) < 1.0) {
+                } else if (no_tir(r, c)) {
                     tk->direction = refract_dir(tk->direction, n, r, c);
                     tk->origin = farthest_contact(c0, rad, tk->origin, tk->direction);
                     n = vneg(contact_normal(tk->origin, c0));
                     c = vdot(vneg(n), tk->direction);
                     r = nGlass / nAir;
-                    rsq = (float)pow((double)((nGlass - nAir) / (nGlass + nAir)), 2.0);
+                    rsq = powf((nGlass - nAir) / (nGlass + nAir), 2.f);
                     schlick = schlick_of(rsq, c);
                     if (spo_uniform(&tk->st, 0.f, 1.f) < schlick)
                         tk->direction = vreflect(tk->direction, n);
-                    else if ((double)r * sqrt((double)(1.f - c * c)) < 1.0)
+                    else if (no_tir(r, c))
                         tk->direction = refract_dir(tk->direction, n, r, c);
                     else
                         tk->direction = vreflect(tk->direction, n);
@@ -679,8 +688,8 @@ static void put_sphere(float *centers, float *radii, float *colors, uint8_t *mat
     materials[i] = m;
 }
 
-/* SceneGenerators.hpp:6-66 GenerateSpheres.  `abs(z)` (line 34) resolves to
- * ::abs(int) under libstdc++ (the float argument is truncated).  Draws that feed
+/* SceneGenerators.hpp:6-66 GenerateSpheres.  `abs(z)` (line 34) binds to
+ * std::abs(float) (the stb headers' <stdlib.h>, see schlick_of), i.e. fabsf.  Draws that feed
  * the dead g_attenuations (lines 56-59) are consumed to keep the stream. */
 uint32_t spo_generate_spheres(uint32_t seed, uint32_t cap, float *centers, float *radii, float *colors,
                               uint8_t *materials, float *fuzz)
@@ -696,7 +705,7 @@ uint32_t spo_generate_spheres(uint32_t seed, uint32_t cap, float *centers, float
     const float minR = 0.3f, maxR = 0.5f;
     v4 s1 = ld4(centers + 4), s2 = ld4(centers + 8), s3 = ld4(centers + 12);
     for (float z = 0; z < 20; z += 1.25f) {
-        const float bound = (float)abs((int)z) * 0.85f;
+        const float bound = fabsf(z) * 0.85f;
         for (float x = -5 - bound; x < 6 + bound; x += 1.25f) {
             if (spo_uniform(&st, 0, 1.f) > 0.5f) {
                 float r = spo_uniform(&st, minR, maxR);

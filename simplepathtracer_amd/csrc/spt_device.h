@@ -13,6 +13,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "spt_powf.h"
+
 #pragma clang fp contract(off)
 
 namespace spt {
@@ -164,39 +166,27 @@ __device__ __forceinline__ f3 ball_vector(uint64_t &st)
 }
 
 // ---------------------------------------------------------------------------
-// Refraction helpers (SingleThreadPathTracer.hpp:48-92).  Under libstdc++ the
-// float arguments of pow()/sqrt() promote to ::pow(double,double) and
-// ::sqrt(double); the GPU evaluates x^5 exactly as a double-double and rounds
-// once (glibc pow is accurate to ~2^-68 relative; the result is then narrowed
-// to float, so the two agree except on measure-zero ties).
+// Refraction helpers (SingleThreadPathTracer.hpp:48-92).  In the reference's
+// translation unit pow(float, float) and sqrt(float) bind to the float overloads
+// (the stb implementations included by IOHelpers.hpp:5-9 bring libstdc++'s
+// <math.h> wrapper; oracle/probe_overloads.cpp), so everything here is float:
+// glibc's powf restated bit for bit (spt_powf.h, exhaustively pinned) and the
+// correctly rounded sqrtf.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ double pow5(double x)
-{
-    double x2 = x * x;                         // exact: x has a 24-bit significand
-    double x4 = x2 * x2;
-    double x4l = __builtin_fma(x2, x2, -x4);   // exact low part of x2^2
-    double p = x4 * x;
-    double pl = __builtin_fma(x4, x, -p);      // exact low part of x4*x
-    return p + (pl + x4l * x);
-}
+__device__ __forceinline__ float pow5f(float x) { return spt_glibc_powf(x, 5.f); }
 
-__device__ __forceinline__ float schlick(float rsq, float c)
-{
-    return (float)((double)rsq + (double)(1.f - rsq) * pow5((double)(1.f - c)));
-}
+// rSq + (1 - rSq) * pow(1 - c, 5)  (lines 58-59, 75-76)
+__device__ __forceinline__ float schlick(float rsq, float c) { return rsq + (1.f - rsq) * pow5f(1.f - c); }
 
 // direction * r + n * (r*c - sqrt(1 - r*r*(1 - c*c)))  (lines 68, 84)
+__device__ __forceinline__ float refract_k(float r, float c) { return r * c - __builtin_sqrtf(1.f - r * r * (1.f - c * c)); }
 __device__ __forceinline__ f3 refract_dir(f3 d, f3 n, float r, float c)
 {
-    float k = (float)((double)(r * c) - __builtin_sqrt((double)(1.f - r * r * (1.f - c * c))));
-    return normalize(add(mul(d, r), mul(n, k)));
+    return normalize(add(mul(d, r), mul(n, refract_k(r, c))));
 }
 
-// r * sqrt(1 - c*c) < 1, evaluated in double (lines 66, 82)
-__device__ __forceinline__ bool no_tir(float r, float c)
-{
-    return (double)r * __builtin_sqrt((double)(1.f - c * c)) < 1.0;
-}
+// r * sqrt(1 - c*c) < 1  (lines 66, 82)
+__device__ __forceinline__ bool no_tir(float r, float c) { return r * __builtin_sqrtf(1.f - c * c) < 1.f; }
 
 // IOHelpers.hpp:17-22 + x86 cvttss2si semantics of static_cast<uint8_t>(float)
 __device__ __forceinline__ uint8_t f2u8(float v)

@@ -320,13 +320,10 @@ __global__ void selftest_kernel(const float *a, const float *b, const uint32_t *
     float *o = out + (size_t)i * SPT_SELFTEST_COLS;
     o[0] = div_rn(x, y);
     o[1] = __builtin_sqrtf(x);
-    const double sq = __builtin_sqrt((double)x);
-    const double p5 = pow5((double)x);
-    const uint64_t sqb = __builtin_bit_cast(uint64_t, sq), p5b = __builtin_bit_cast(uint64_t, p5);
-    o[2] = __builtin_bit_cast(float, (uint32_t)sqb);
-    o[3] = __builtin_bit_cast(float, (uint32_t)(sqb >> 32));
-    o[4] = __builtin_bit_cast(float, (uint32_t)p5b);
-    o[5] = __builtin_bit_cast(float, (uint32_t)(p5b >> 32));
+    o[2] = pow5f(x);                    // glibc powf(x, 5.f) restated
+    o[3] = pow5f(c);                    // ... over any bit pattern
+    o[4] = spt_glibc_powf(x, 2.f);      // the rSq form, powf(x, 2.f)
+    o[5] = no_tir(kAirToGlass, x) ? refract_k(kAirToGlass, x) : -1e30f;
     o[6] = uniform_bits(bits[i], -1.f, 1.f);
     o[7] = (float)f2u8(x);
     const f3 nv = normalize(mk(x, y, c));  // c: any bit pattern (NaN, inf, denormal, huge)

@@ -112,9 +112,11 @@ namespace {
 
 constexpr uint32_t PH_IDLE = 0, PH_TRACE = 1, PH_DLOOP = 2;
 
-// rSq of SampleColorRefractive (lines 58 and 75): float(pow(double(-0.2f), 2)).
-// The exact square of a float is representable in double, so pow returns it.
-constexpr float kRsq = (float)((double)((1.0f - 1.5f) / (1.0f + 1.5f)) * (double)((1.0f - 1.5f) / (1.0f + 1.5f)));
+// rSq of SampleColorRefractive (lines 58 and 75): powf(-0.2f, 2.f) = powf(0.2f, 2.f)
+// = 0x1.47ae16p-5, the correctly rounded square (glibc's powf agrees:
+// tests/cpp/kat_powf.cpp; selftest column 4 checks spt_glibc_powf on the device).
+constexpr float kRsq = ((1.0f - 1.5f) / (1.0f + 1.5f)) * ((1.0f - 1.5f) / (1.0f + 1.5f));
+static_assert(kRsq == 0x1.47ae16p-5f, "rSq");
 constexpr float kAirToGlass = 1.0f / 1.5f;
 constexpr float kGlassToAir = 1.5f / 1.0f;
 

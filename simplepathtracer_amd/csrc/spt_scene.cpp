@@ -93,9 +93,10 @@ extern "C" int spt_scene_generate_random(uint32_t seed, uint32_t capacity, float
     o.put(n++, v3(-7, 3, 14), 3, v3(223, 55, 132), SPT_DIFFUSE);
     const float minR = 0.3f, maxR = 0.5f;
     const V s1 = o.center(1), s2 = o.center(2), s3 = o.center(3);
-    // SceneGenerators.hpp:32-53.  abs(z) binds ::abs(int) under libstdc++.
+    // SceneGenerators.hpp:32-53.  abs(z) binds std::abs(float) in the reference's TU
+    // (oracle/probe_overloads.cpp).
     for (float z = 0; z < 20; z += 1.25f) {
-        const float bound = (float)std::abs((int)z) * 0.85f;
+        const float bound = std::fabs(z) * 0.85f;
         for (float x = -5 - bound; x < 6 + bound; x += 1.25f) {
             if (rng.uniform(0, 1.f) > 0.5f) {
                 const float r = rng.uniform(minR, maxR);

@@ -76,11 +76,29 @@ def test_device_numerics_match_host(ctx, oracle):
     out = ctx.selftest_numerics(a, b, u)
     assert_bitwise(out[:, 0], a / b, "fp32 division")
     assert_bitwise(out[:, 1], np.sqrt(a), "fp32 sqrt")
-    sq = out[:, 2:4].copy().view(np.float64).ravel()
-    assert np.array_equal(sq, np.sqrt(a.astype(np.float64))), "fp64 sqrt"
-    p5 = out[:, 4:6].copy().view(np.float64).ravel()
-    for i in range(0, n, 97):
-        assert p5[i] == float(Fraction(float(a[i])) ** 5), (a[i], p5[i])
+    # SampleColorRefractive's float powf / sqrtf (spt_powf.h restates glibc's powf)
+    libm = ctypes.CDLL("libm.so.6")
+    libm.powf.restype = ctypes.c_float
+    libm.powf.argtypes = [ctypes.c_float, ctypes.c_float]
+    c_any = u.view(np.float32)
+    hard = [float.fromhex(h) for h in ("0x1.003bap-24", "0x1.14708ep-1", "0x1.ef5ee8p-1", "0x1.14708ep+0")]
+    for i in list(range(0, n, 7)) + [n - 8 + k for k in range(8)]:
+        assert out[i, 2] == np.float32(libm.powf(float(a[i]), 5.0)), ("powf(x,5)", a[i])
+        want = np.float32(libm.powf(float(c_any[i]), 5.0))
+        assert out[i, 3].view(np.uint32) == want.view(np.uint32) or (np.isnan(out[i, 3]) and np.isnan(want)), \
+            ("powf(any,5)", c_any[i])
+        assert out[i, 4] == np.float32(libm.powf(float(a[i]), 2.0)), ("powf(x,2)", a[i])
+    ha = np.float32(hard + [-0.2, 0.2] + [0] * (len(a) - len(hard) - 2))[: len(a)]
+    oh = ctx.selftest_numerics(ha, b, u)
+    for i in range(len(hard) + 2):
+        assert oh[i, 2] == np.float32(libm.powf(float(ha[i]), 5.0)), ("hard powf", ha[i])
+        assert oh[i, 4] == np.float32(libm.powf(float(ha[i]), 2.0))
+    # r * sqrt(1 - c*c) < 1 and the Snell scalar r*c - sqrt(1 - r*r*(1 - c*c)), float
+    r = np.float32(1.0) / np.float32(1.5)
+    with np.errstate(all="ignore"):
+        tir_ok = r * np.sqrt(np.float32(1) - a * a) < np.float32(1)
+        k = r * a - np.sqrt(np.float32(1) - r * r * (np.float32(1) - a * a))
+    same_or_nan(out[:, 5], np.where(tir_ok, k, np.float32(-1e30)), "refraction scalar")
     want_u = np.array([oracle.lib().spo_uniform_u32(int(x), -1.0, 1.0) for x in u[:4096]], np.float32)
     assert_bitwise(out[:4096, 6], want_u, "uniform(-1,1)")
     for col, lo, hi in ((12, -0.5, 0.5), (13, 0.0, 1.0)):

@@ -17,8 +17,8 @@ run() {  # name timeout cmd...
 }
 for s in $STEPS; do
   case $s in
-    tests) run gpu_tests 900 python -m pytest tests -m gpu -x -q ;;
-    alltests) run gpu_tests 900 python -m pytest tests -m gpu -q ;;
+    tests) run gpu_tests 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ;;
+    alltests) run gpu_tests 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py ;;
     *) run custom 900 bash -c "$s" ;;

@@ -150,20 +150,9 @@ __device__ __forceinline__ float uniform_bits(uint32_t bits, float a, float b)
 }
 __device__ __forceinline__ float uniform(uint64_t &st, float a, float b) { return uniform_bits(next_u32(st), a, b); }
 
-// Random.hpp:115-127 (== 129-141): x, y, z ~ U(-0.5,0.5) while Length < 0.5.
-// sqrt_rn is monotone and sqrt_rn(0.25) == 0.5, sqrt_rn(prev(0.25)) < 0.5, so
-// `sqrtf(L) < 0.5f` <=> `L < 0.25f` (checked exhaustively in tests).
-__device__ __forceinline__ f3 ball_vector(uint64_t &st)
-{
-    f3 r;
-    do {
-        float x = uniform(st, -0.5f, 0.5f);
-        float y = uniform(st, -0.5f, 0.5f);
-        float z = uniform(st, -0.5f, 0.5f);
-        r = mk(x, y, z);
-    } while (lensq(r) < 0.25f);
-    return r;
-}
+// Random.hpp:115-127 (== 129-141), x, y, z ~ U(-0.5,0.5) while Length < 0.5, is
+// coop_ball_vector (spt_path.h).  sqrt_rn is monotone and sqrt_rn(0.25) == 0.5,
+// sqrt_rn(prev(0.25)) < 0.5, so `sqrtf(L) < 0.5f` <=> `L < 0.25f` (checked in tests).
 
 // ---------------------------------------------------------------------------
 // Refraction helpers (SingleThreadPathTracer.hpp:48-92).  In the reference's

@@ -26,12 +26,6 @@
 namespace spt {
 
 
-#ifndef SPT_DUP_START
-#define SPT_DUP_START 0
-#endif
-#ifndef SPT_DUP_CAST
-#define SPT_DUP_CAST 0
-#endif
 #ifndef SPT_WAVES_PER_EU
 #define SPT_WAVES_PER_EU 0
 #endif
@@ -54,9 +48,6 @@ namespace spt {
 
 // LDS tree variant (SPT_LDS_TREE): blocks of kLdsBlock threads copy node layout 0
 // into LDS once and walk it with broadcast LDS reads; two blocks per CU.
-#ifndef SPT_LDS_TREE
-#define SPT_LDS_TREE 1
-#endif
 #ifndef SPT_LDS_BLOCK
 #define SPT_LDS_BLOCK 1024
 #endif
@@ -148,17 +139,8 @@ __device__ __forceinline__ void render_body(const RenderArgs &a)
                 }
             }
             if (ps.phase == PH_IDLE && mine != 0xFFFFFFFFu) {
-#if SPT_KERNARG_RELOAD && defined(__HIP_DEVICE_COMPILE__)
+#if defined(__HIP_DEVICE_COMPILE__)
                 start_path_kernarg(mine, rows, ps);
-#if SPT_DUP_START
-                {
-                    Path p2 = ps;  // timing experiment only: a second, discarded refill
-                    uint32_t m2 = mine;
-                    asm volatile("" : "+v"(m2));
-                    start_path_kernarg(m2, rows, p2);
-                    asm volatile("" ::"v"(p2.d.x), "v"(p2.d.y), "v"(p2.d.z), "v"((uint32_t)p2.st));
-                }
-#endif
 #else
                 start_path(a, mine, rows, rw, rh, eye, ps);
 #endif
@@ -175,15 +157,6 @@ __device__ __forceinline__ void render_body(const RenderArgs &a)
         // ---- one cast + one shading step ----
         const bool act = ps.phase != PH_IDLE;
         const Hit h = find_closest<TREE, LEAF, LDSN>(a.scene.accel, ps.o, ps.d, act, dg, (const uint32_t *)s_nodes);
-#if SPT_DUP_CAST
-        {
-            // timing experiment only: a second, discarded cast (its marginal cost)
-            f3 o2 = ps.o;
-            asm volatile("" : "+v"(o2.x));
-            const Hit h2 = find_closest<TREE, LEAF>(a.scene.accel, o2, ps.d, act, dg);
-            asm volatile("" ::"v"(h2.idx), "v"(h2.best), "v"(h2.p.x));
-        }
-#endif
         SPT_STAMP(d_cyc_cast);
         shade_step(a, ps, h, act, done, dropped, s_lds + (threadIdx.x & ~63u));
         SPT_STAMP(d_cyc_shade);
@@ -230,7 +203,6 @@ __global__ __launch_bounds__(kRenderBlock) SPT_RENDER_ATTR void render_kernel(Re
     render_body<TREE, LEAF, false, kRenderBlock>(a);
 }
 
-#if SPT_LDS_TREE
 // its own register budget: 1024-thread blocks, two per CU, need 8 waves per SIMD
 #ifndef SPT_LDS_NUM_SGPR
 #define SPT_LDS_NUM_SGPR 80
@@ -240,7 +212,6 @@ __global__ __launch_bounds__(kLdsBlock)
 {
     render_body<true, (int)kClusterSlots, true, kLdsBlock>(a);
 }
-#endif
 
 __global__ __launch_bounds__(256) void fold_kernel(FoldArgs a)
 {
@@ -335,7 +306,6 @@ __global__ void selftest_kernel(const float *a, const float *b, const uint32_t *
     o[13] = uniform_bits(bits[i], 0.f, 1.f);
 }
 
-#if SPT_LDS_TREE
 // Blocks per CU of the LDS tree variant and CUs of the device, queried once per
 // process (a thread-safe local static: RenderJob threads launch concurrently; every
 // device of the node is an MI355X).  per_cu = 0 disables the variant.
@@ -356,11 +326,9 @@ static void lds_tree_shape(int *per_cu, int *num_cu)
     *per_cu = shape.pc;
     *num_cu = shape.nc;
 }
-#endif
 
 hipError_t launch_render(const RenderArgs &a, uint32_t grid, uint32_t block, hipStream_t s)
 {
-#if SPT_LDS_TREE
     if (a.scene.accel.tree && a.scene.accel.n_nodes + 1u <= kLdsNodeRecords) {
         // all resident blocks, or fewer when the launch has under 2 claims per wave
         // (render_grid's rule; a frame in flight on another stream only queues)
@@ -377,7 +345,6 @@ hipError_t launch_render(const RenderArgs &a, uint32_t grid, uint32_t block, hip
             return hipGetLastError();
         }
     }
-#endif
     if (a.scene.accel.tree)
         hipLaunchKernelGGL((render_kernel<true, (int)kClusterSlots>), dim3(grid), dim3(block), 0, s, a);
     else if (a.scene.accel.leaf_slots == kFlatLeafSlots)

@@ -21,89 +21,35 @@
 // 1: the megakernel's start_path reads its parameters from the kernarg segment
 // where used instead of holding them in SGPRs (with the SGPR cap of
 // spt_kernels.hip: 7-8 resident waves per SIMD instead of 6)
-#ifndef SPT_KERNARG_RELOAD
-#define SPT_KERNARG_RELOAD 1
-#endif
 
 // 1: flat-list cluster members are tested behind the conservative pretest of
 // test_group_pre (10 VALU per member instead of 18)
-#ifndef SPT_PRETEST
-#define SPT_PRETEST 1
-#endif
 
 // 1: tree leaves (config 5) behind the member pretest too (measured 10% slower on
 // config 5: the tree's walk, not its member tests, bounds it)
-#ifndef SPT_PRETEST_TREE
-#define SPT_PRETEST_TREE 0
-#endif
 // 1: leaf tables addressed by 32-bit byte offsets (SGPR-offset scalar loads)
-#ifndef SPT_LEAF_BYTEOFF
-#define SPT_LEAF_BYTEOFF 1
-#endif
 // 1: the tie mask of update_member as the AND of compare ballots (no VGPR round trip)
-#ifndef SPT_TIE_MASKS
-#define SPT_TIE_MASKS 1
-#endif
 // 1: flat node records loaded as one s_load_dwordx8 each
-#ifndef SPT_NODE_X8
-#define SPT_NODE_X8 1
-#endif
 
 // timing experiments only: a second, discarded evaluation of
 // one part of the path, whose cost is the part's marginal cost
-#ifndef SPT_DUP_LEAF
-#define SPT_DUP_LEAF 0
-#endif
-#ifndef SPT_DUP_ALWAYS
-#define SPT_DUP_ALWAYS 0
-#endif
-#ifndef SPT_DUP_BALL
-#define SPT_DUP_BALL 0
-#endif
 
 // 1: tree walks use the layout of the wave's majority direction octant (0: layout 0
 // for every wave: one eighth of the node table in the scalar cache)
-#ifndef SPT_TREE_OCTANTS
-#define SPT_TREE_OCTANTS 1
-#endif
 
 // 1: tree node masks as the AND of the three compare ballots
-#ifndef SPT_TREE_BALLOTS
-#define SPT_TREE_BALLOTS 1
-#endif
 // 1: the LDS tree walk issues the successor's reads before the node's tests
-#ifndef SPT_LDS_EARLY
-#define SPT_LDS_EARLY 1
-#endif
 
 // 1: flat node records pinned to SGPRs only when the walk reaches them
-#ifndef SPT_FLAT_LATE_PIN
-#define SPT_FLAT_LATE_PIN 0
-#endif
 // 1: the LDS tree walk also prefetches each node's skip target
-#ifndef SPT_LDS_SKIPPF
-#define SPT_LDS_SKIPPF 0
-#endif
 
 // 1: a leaf's member pretests all run before its first branch
-#ifndef SPT_PRE_ILP
-#define SPT_PRE_ILP 1
-#endif
 
 
 // 1: the cube-minus-ball rejection loop runs cooperatively across the wave
-#ifndef SPT_COOP_BALL
-#define SPT_COOP_BALL 1
-#endif
 
 // Item order of a batch: SPT_TS_ORDER 1 = [band][8x8 tile][sample][pixel] (ts_item);
 // else SPT_TILE 1 = [sample][8x8 tile][pixel] (tile_pixel), 0 = [sample][row-major pixel]
-#ifndef SPT_TS_ORDER
-#define SPT_TS_ORDER 1
-#endif
-#ifndef SPT_TILE
-#define SPT_TILE 1
-#endif
 
 #pragma clang fp contract(off)
 
@@ -169,13 +115,9 @@ __device__ __forceinline__ void update_member(bool pass, float tc, float hh, con
     // load here made every cast wait on vmcnt(0), i.e. on the previous shading
     // step's sample stores.
     const bool tie = ok && ds == h.best && h.idx != kMiss;
-#if SPT_TIE_MASKS
     // the ballot of a compare is its own lane mask; a ballot of the combined bool
     // would go through a VGPR (v_cndmask + v_cmp) first
     unsigned long long tm = __ballot(pass) & __ballot(front) & __ballot(ds == h.best) & __ballot(h.idx != kMiss);
-#else
-    unsigned long long tm = __ballot(tie);
-#endif
     if (__builtin_expect(tm != 0ull, 0)) {
         const uint32_t mo = ((cuint *)orig)[s];
         while (tm != 0ull) {
@@ -232,7 +174,7 @@ __device__ __forceinline__ void test_group(const float4 (&sp)[G], const uint32_t
 
 // Per-lane terms of the member pretest (test_group_pre), formed once per cast.
 struct PreLane {
-    float osx, osy, osz;  // -2c o (c = kFlatScale, as the flat node test); o itself when !PRESCALED
+    float osx, osy, osz;  // -2c o (c = kFlatScale, as the flat node test)
     float qoe;            // (c - 4.1e-6) |o|^2; +inf for inactive lanes, -inf for lanes that must not cull
     float tinit;          // mt - o.d, mt = 2e-6 (pre_cm + |o|) + 1e-6; -inf inactive, +inf must not cull
 };
@@ -243,10 +185,9 @@ struct PreLane {
 // (K' = the first three terms, stored per slot), a lane may pass the member only
 // if min(tcs, tcs^2 - w) > 1e-3 (every lane that passes the
 // reference test passes this one).  The exact test runs only behind the member's
-// wave-uniform branch.
-// PRESCALED = false (tree kernels, fewer live VGPRs): pl.os* hold o and the cross
-// term is formed as (C.o) * (-2c), one VALU more.
-template <int G, bool PRESCALED>
+// wave-uniform branch.  Flat lists only: on tree leaves (config 5) it measured 10%
+// slower -- the tree walk, not the member tests, bounds that kernel.
+template <int G>
 __device__ __forceinline__ void test_group_pre(const float4 (&sp)[G], const float (&kp)[G],
                                                const uint32_t *__restrict__ orig, uint32_t slot, const f3 &o,
                                                const f3 &d, float dod, const PreLane &pl, Hit &h, CastDiag &dg)
@@ -255,17 +196,10 @@ __device__ __forceinline__ void test_group_pre(const float4 (&sp)[G], const floa
 #pragma unroll
     for (int k = 0; k < G; ++k) {
         const float tcs = __builtin_fmaf(sp[k].x, d.x, __builtin_fmaf(sp[k].y, d.y, __builtin_fmaf(sp[k].z, d.z, pl.tinit)));
-        float w;
-        if (PRESCALED) {
-            w = __builtin_fmaf(sp[k].x, pl.osx, __builtin_fmaf(sp[k].y, pl.osy, __builtin_fmaf(sp[k].z, pl.osz, pl.qoe))) +
-                kp[k];
-        } else {
-            const float co = __builtin_fmaf(sp[k].x, pl.osx, __builtin_fmaf(sp[k].y, pl.osy, sp[k].z * pl.osz));
-            w = __builtin_fmaf(co, (float)(-2.0 * kFlatScale), pl.qoe) + kp[k];
-        }
+        const float w =
+            __builtin_fmaf(sp[k].x, pl.osx, __builtin_fmaf(sp[k].y, pl.osy, __builtin_fmaf(sp[k].z, pl.osz, pl.qoe))) + kp[k];
         pre[k] = __builtin_fminf(tcs, __builtin_fmaf(tcs, tcs, -w)) > 1e-3f;
     }
-#if SPT_PRE_ILP
     // all G pretests before the first branch (independent chains in flight
     // together), and one branch past the group when no lane passes any member
     unsigned long long pm[G], any = 0ull;
@@ -279,7 +213,6 @@ __device__ __forceinline__ void test_group_pre(const float4 (&sp)[G], const floa
         if (SPT_DIAG) dg.spheres += G;
         return;
     }
-#endif
 #pragma unroll
     for (int k = 0; k < G; ++k) {
         if (SPT_DIAG) {
@@ -287,11 +220,7 @@ __device__ __forceinline__ void test_group_pre(const float4 (&sp)[G], const floa
             dg.branches += __ballot(pre[k]) != 0ull ? 1 : 0;
             dg.passing += (unsigned long long)__popcll(__ballot(pre[k]));
         }
-#if SPT_PRE_ILP
         if (pm[k] != 0ull) {
-#else
-        if (__ballot(pre[k]) != 0ull) {
-#endif
             float tc, hh;
             const bool pass = ray_sphere(sp[k], o, d, tc, hh);
             if (__ballot(pass) != 0ull) update_member(pass, tc, hh, orig, slot + k, o, d, dod, h, dg);
@@ -313,28 +242,23 @@ __device__ __forceinline__ void test_leaf(cfloat *slots, const uint32_t *__restr
 }
 
 // Leaf test behind the member pretest: the S slots plus their S pretest constants.
-template <int S, bool PRESCALED>
+template <int S>
 __device__ __forceinline__ void test_leaf_pre(cfloat *slots, cfloat *kpre, const uint32_t *__restrict__ orig,
                                               uint32_t leaf_slot, const f3 &o, const f3 &d, float dod,
                                               const PreLane &pl, Hit &h, CastDiag &dg)
 {
     // 32-bit byte offsets off the table bases: the loads take them as SGPR offsets
     // (no 64-bit address arithmetic on the scalar unit)
-#if SPT_LEAF_BYTEOFF
     typedef __attribute__((address_space(4))) const char cchar;
     cfloat *cs = (cfloat *)((cchar *)slots + (leaf_slot << 4));
     cfloat *kb = (cfloat *)((cchar *)kpre + (leaf_slot << 2));
-#else
-    cfloat *cs = slots + 4 * leaf_slot;
-    cfloat *kb = kpre + leaf_slot;
-#endif
     float4 ms[S];
     float kp[S];
 #pragma unroll
     for (int k = 0; k < S; ++k) ms[k] = ld_uniform(cs, k);
 #pragma unroll
     for (int k = 0; k < S; ++k) kp[k] = kb[k];
-    test_group_pre<S, PRESCALED>(ms, kp, orig, leaf_slot, o, d, dod, pl, h, dg);
+    test_group_pre<S>(ms, kp, orig, leaf_slot, o, d, dod, pl, h, dg);
 }
 
 // FindClosestIntersectionSphere for every lane of the wave (Collision.hpp:87-109).
@@ -372,14 +296,6 @@ __device__ __forceinline__ Hit find_closest(const AccelView &ac, const f3 &o, co
 #pragma unroll
             for (int k = 0; k < SPT_GROUP; ++k) g4[k] = ld_uniform(slots, g * SPT_GROUP + k);
             test_group<SPT_GROUP>(g4, ac.orig, g * SPT_GROUP, o, d, dod, h, dg);
-#if SPT_DUP_ALWAYS
-            {  // timing experiment only: the always-list tested again
-                Hit h2 = h;
-                asm volatile("" : "+v"(h2.best));
-                test_group<SPT_GROUP>(g4, ac.orig, g * SPT_GROUP, o, d, dod, h2, dg);
-                asm volatile("" ::"v"(h2.idx), "v"(h2.best), "v"(h2.p.x));
-            }
-#endif
         }
     }
     const unsigned long long live_mask = __ballot(active);
@@ -413,7 +329,6 @@ __device__ __forceinline__ Hit find_closest(const AccelView &ac, const f3 &o, co
         // pass), so the ballot of the compare is the node mask: about 5 SALU per node
         // instead of 17.
         const float qoe = !active ? INFINITY : (no_cull ? -INFINITY : qo);
-#if SPT_PRETEST
         // member pretest terms: the node test's -2c o and qoe, plus the tc slack
         // mt = 2e-6 (pre_cm + |o|) + 1e-6 folded into -o.d
         const float olen = __builtin_amdgcn_sqrtf(oo) * 1.000001f;
@@ -423,7 +338,6 @@ __device__ __forceinline__ Hit find_closest(const AccelView &ac, const f3 &o, co
         pl.osz = osz;
         pl.qoe = qoe;
         pl.tinit = !active ? -INFINITY : (no_cull ? INFINITY : __builtin_fmaf(2e-6f, ac.pre_cm + olen, 1e-6f) - dod);
-#endif
         // c |Cb|^2 is left out of the sum: the node's threshold is K1'' = K1' - c |Cb|^2
         // (one rounding fewer)
         auto node_x = [&](const uint32_t *r) {
@@ -436,25 +350,12 @@ __device__ __forceinline__ Hit find_closest(const AccelView &ac, const f3 &o, co
         auto finish = [&](const uint32_t *r, float x) {
             const unsigned long long mm = __ballot(x <= __uint_as_float(r[6]));
             diag_node(mm);
-#if SPT_PRETEST
-            if (mm != 0ull) test_leaf_pre<LEAF, true>(slots, (cfloat *)ac.kpre, ac.orig, r[5], o, d, dod, pl, h, dg);
-#if SPT_DUP_LEAF
-            if (mm != 0ull) {  // timing experiment only: each entered leaf tested again
-                Hit h2 = h;
-                asm volatile("" : "+v"(h2.best));
-                test_leaf_pre<LEAF, true>(slots, (cfloat *)ac.kpre, ac.orig, r[5], o, d, dod, pl, h2, dg);
-                asm volatile("" ::"v"(h2.idx), "v"(h2.best), "v"(h2.p.x));
-            }
-#endif
-#else
-            if (mm != 0ull) test_leaf<LEAF>(slots, ac.orig, r[5], o, d, dod, h, dg);
-#endif
+            if (mm != 0ull) test_leaf_pre<LEAF>(slots, (cfloat *)ac.kpre, ac.orig, r[5], o, d, dod, pl, h, dg);
         };
         // The next record's load is issued only after this record's first use: a
         // scalar-load wait is lgkmcnt(0), so an earlier issue would be waited for here.
         cuint *p = nodes;
         uint32_t ra[8], rb[8];
-#if SPT_NODE_X8
         // the whole record in one s_load_dwordx8 (the compiler would load only the six
         // dwords the flat test uses, as four loads); the empty asm keeps all eight
         typedef uint32_t u32x8 __attribute__((ext_vector_type(8)));
@@ -465,42 +366,6 @@ __device__ __forceinline__ Hit find_closest(const AccelView &ac, const f3 &o, co
 #pragma unroll
             for (int i = 0; i < 8; ++i) r[i] = v[i];
         };
-#else
-        auto load_rec = [&](cuint *q, uint32_t(&r)[8]) {
-#pragma unroll
-            for (int i = 0; i < 8; ++i) r[i] = q[i];
-        };
-#endif
-#if SPT_NODE_X8 && SPT_FLAT_LATE_PIN
-        // the record's register pin (which waits for its load) after the previous
-        // node's branch instead of right at the load's issue
-        typedef uint32_t u32x8b __attribute__((ext_vector_type(8)));
-        typedef __attribute__((address_space(4))) const u32x8b cu32x8b;
-        auto pin = [&](u32x8b &v, uint32_t(&r)[8]) {
-            asm volatile("" : "+s"(v));
-#pragma unroll
-            for (int i = 0; i < 8; ++i) r[i] = v[i];
-        };
-        u32x8b va = *(cu32x8b *)p, vb;
-        pin(va, ra);
-        uint32_t left = ac.n_nodes;
-        while (left >= 2u) {
-            const float xa = node_x(ra);
-            __builtin_amdgcn_sched_barrier(0);
-            vb = *(cu32x8b *)(p + 8);
-            __builtin_amdgcn_sched_barrier(0);
-            finish(ra, xa);
-            pin(vb, rb);
-            const float xb = node_x(rb);
-            __builtin_amdgcn_sched_barrier(0);
-            va = *(cu32x8b *)(p + 16);
-            __builtin_amdgcn_sched_barrier(0);
-            finish(rb, xb);
-            pin(va, ra);
-            p += 16;
-            left -= 2u;
-        }
-#else
         load_rec(p, ra);
         uint32_t left = ac.n_nodes;
         while (left >= 2u) {
@@ -515,7 +380,6 @@ __device__ __forceinline__ Hit find_closest(const AccelView &ac, const f3 &o, co
             p += 16;
             left -= 2u;
         }
-#endif
         if (left != 0u) finish(ra, node_x(ra));
         return h;
     }
@@ -526,11 +390,7 @@ __device__ __forceinline__ Hit find_closest(const AccelView &ac, const f3 &o, co
         const uint32_t oct = (2u * (uint32_t)__popcll(__ballot(active && d.x < 0.f)) > nlive ? 1u : 0u) |
                              (2u * (uint32_t)__popcll(__ballot(active && d.y < 0.f)) > nlive ? 2u : 0u) |
                              (2u * (uint32_t)__popcll(__ballot(active && d.z < 0.f)) > nlive ? 4u : 0u);
-#if SPT_TREE_OCTANTS
         if (!LDSN) nodes += (size_t)8 * (ac.n_nodes + 1) * oct;
-#else
-        (void)oct;
-#endif
     }
     // Tree nodes {Cb, K1, skip, slot, F, c'|Cb|^2}: three conservative tests
     // (DESIGN.md §4.4), without a square root per node; a lane may need the node
@@ -549,14 +409,6 @@ __device__ __forceinline__ Hit find_closest(const AccelView &ac, const f3 &o, co
         return (__builtin_amdgcn_sqrtf(best * 1.0001f) * (1.0f + 0x1p-20f) + (2e-5f * olen + 1e-6f)) * kq;
     };
     float sbe = near_term(h.best);
-#if SPT_PRETEST && SPT_PRETEST_TREE
-    PreLane pl;  // member pretest terms (see the flat list above), o unscaled
-    pl.osx = o.x;
-    pl.osy = o.y;
-    pl.osz = o.z;
-    pl.qoe = !active ? INFINITY : (no_cull ? -INFINITY : qo);
-    pl.tinit = !active ? -INFINITY : (no_cull ? INFINITY : __builtin_fmaf(2e-6f, ac.pre_cm + olen * 1.000001f, 1e-6f) - dod);
-#endif
     // node record q of node j: a scalar load, or a broadcast LDS read
     auto ldn = [&](uint32_t j, int q) -> uint32_t { return LDSN ? lnodes[8 * j + q] : nodes[8 * j + q]; };
     uint32_t i = 0;
@@ -568,27 +420,15 @@ __device__ __forceinline__ Hit find_closest(const AccelView &ac, const f3 &o, co
         const float k1 = __uint_as_float(nb[3]), fr = __uint_as_float(nb[6]), cb2n = __uint_as_float(nb[7]);
         const uint32_t skip = LDSN ? __builtin_amdgcn_readfirstlane(nb[4]) : nb[4];
         const uint32_t leaf_slot = LDSN ? __builtin_amdgcn_readfirstlane(nb[5]) : nb[5];
-#if SPT_LDS_EARLY
         // LDS walk: this node's scalars before the successor's reads are issued (a
         // readfirstlane after them would wait for them: LDS waits are lgkmcnt(0))
         if (LDSN) asm volatile("" ::"s"(skip), "s"(leaf_slot));
-#endif
         // speculative prefetch of the preorder successor (prefetching the skip
         // target as well measured 4% slower on config 5)
 #pragma unroll
         for (int q = 0; q < 8; ++q) nb[q] = ldn(i + 1, q);
-#if SPT_LDS_SKIPPF
-        // LDS walk: the skip target's record as well (a leaf's skip is i + 1)
-        uint32_t ns[8];
-        if (LDSN) {
-#pragma unroll
-            for (int q = 0; q < 8; ++q) ns[q] = ldn(skip, q);
-        }
-#endif
-#if SPT_LDS_EARLY
         // LDS walk: keep the successor's ds_reads ahead of this node's tests
         if (LDSN) __builtin_amdgcn_sched_barrier(0);
-#endif
         const float tcb = __builtin_fmaf(bx, d.x, __builtin_fmaf(by, d.y, __builtin_fmaf(bz, d.z, -dod)));
         // Cb.o from o itself (not -2c o: two VGPRs fewer keep the kernel at 64)
         const float cbo = __builtin_fmaf(bx, o.x, __builtin_fmaf(by, o.y, bz * o.z));
@@ -598,12 +438,8 @@ __device__ __forceinline__ Hit find_closest(const AccelView &ac, const f3 &o, co
         const bool line = x <= k1;
         const bool front = __builtin_fmaf(1e-4f, olen, tcb) >= -fr;
         const bool near = !(w > sn * sn);
-#if SPT_TREE_BALLOTS
         // the AND of the three compare ballots: each is the compare's own lane mask
         const unsigned long long mm = (__ballot(line) & __ballot(front) & __ballot(near) & live_mask) | nocull_mask;
-#else
-        const unsigned long long mm = (__ballot(line && front && near) & live_mask) | nocull_mask;
-#endif
         const bool leaf = leaf_slot != kNoSlot;
         if (SPT_DIAG) {
             dg.nodes += 1;
@@ -614,21 +450,11 @@ __device__ __forceinline__ Hit find_closest(const AccelView &ac, const f3 &o, co
             }
         }
         if (mm != 0ull && leaf) {
-#if SPT_PRETEST && SPT_PRETEST_TREE
-            test_leaf_pre<LEAF, false>(slots, (cfloat *)ac.kpre, ac.orig, leaf_slot, o, d, dod, pl, h, dg);
-#else
             test_leaf<LEAF>(slots, ac.orig, leaf_slot, o, d, dod, h, dg);
-#endif
             sbe = near_term(h.best);
         }
         const uint32_t next = (mm != 0ull && !leaf) ? i + 1 : skip;
         if (next != i + 1) {
-#if SPT_LDS_SKIPPF
-            if (LDSN) {
-#pragma unroll
-                for (int q = 0; q < 8; ++q) nb[q] = ns[q];
-            } else
-#endif
             {
 #pragma unroll
                 for (int q = 0; q < 8; ++q) nb[q] = ldn(next, q);
@@ -813,19 +639,7 @@ __device__ __forceinline__ void shade_step(const RenderArgs &a, Path &ps, const 
         }
     }
     bool spec_event = false;
-#if SPT_COOP_BALL
     const f3 rv_coop = coop_ball_vector(ps.st, scatter, lds);
-#if SPT_DUP_BALL
-    {
-        uint64_t st2 = ps.st;  // timing experiment only: a second, discarded sampler run
-        asm volatile("" : "+v"(st2));
-        const f3 r2 = coop_ball_vector(st2, scatter, lds);
-        asm volatile("" ::"v"(r2.x), "v"(r2.y), "v"(r2.z));
-    }
-#endif
-#else
-    (void)lds;
-#endif
     if (scatter) {
         // contact point + normal + cube-minus-ball vector, shared by the diffuse
         // first hit (lines 23-26), the diffuse loop (30-33) and the mirror (41-43)
@@ -833,11 +647,7 @@ __device__ __forceinline__ void shade_step(const RenderArgs &a, Path &ps, const 
         const f3 C = mk(cs.x, cs.y, cs.z);
         ps.o = h.p;
         const f3 nrm = normalize(sub(ps.o, C));
-#if SPT_COOP_BALL
         f3 rv = rv_coop;
-#else
-        f3 rv = ball_vector(ps.st);
-#endif
         f3 base;
         if (dl) {
             ps.c = mul(ps.c, 0.5f);
@@ -886,27 +696,11 @@ __device__ __forceinline__ void start_path(const RenderArgs &a, uint32_t mine, u
 {
     // primary ray, SingleThreadPathTracer.hpp:123-130.  A claim of
     // consecutive items stays inside one 8x8 tile (ts_item).
-#if SPT_TS_ORDER
     uint32_t sl, lr, cx;
     ts_item(mine, a.map.width, rows, a.spp_batch, a.div_band, a.div_tile, sl, lr, cx);
     const uint32_t s = a.s0 + sl;
     ps.item = sl * a.npix + lr * a.map.width + cx;  // slot: [sample][row-major pixel]
     const uint32_t x = a.map.x0 + cx;
-#elif SPT_TILE
-    const uint32_t sl = mine / a.npix;
-    const uint32_t s = a.s0 + sl;
-    uint32_t lr, cx;
-    tile_pixel(mine - sl * a.npix, a.map.width, rows, lr, cx);
-    ps.item = sl * a.npix + lr * a.map.width + cx;  // slot: [sample][row-major pixel]
-    const uint32_t x = a.map.x0 + cx;
-#else
-    const uint32_t sl = mine / a.npix;
-    const uint32_t s = a.s0 + sl;
-    const uint32_t pl = mine - sl * a.npix;
-    ps.item = mine;
-    const uint32_t lr = pl / a.map.width;
-    const uint32_t x = a.map.x0 + (pl - lr * a.map.width);
-#endif
     const uint32_t y = a.map.parts == 1u ? a.map.y0 + lr : row_of_fast(a.map, lr, a.div_strip);
     ps.st = fmix64(a.seed_key ^ (((uint64_t)(y * a.width + x) << 32) | (uint64_t)s));
     const float un = (float)y + uniform(ps.st, -1.f, 1.f);

@@ -34,9 +34,26 @@ CONFIGS = {
     "c5": ("stress10k", 1920, 1080, 256, 50),
     "c1": ("cornell3", 200, 100, 4, 8),
 }
-VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12  # 78.64 T fp32 lane-ops/s (non-FMA)
+# VALU issue: a wave64 VALU instruction occupies its SIMD-32 for 2 cycles
+# (MI355X_MICROARCH.md: 4 SIMD-32 per CU), 1024 SIMDs at 2.4 GHz
+CLOCK_HZ = 2.4e9
+VALU_ISSUE_PEAK = 256 * 4 * CLOCK_HZ / 2  # 1.2288e12 wave-instructions/s
+VALU_PEAK_TOPS = 256 * 4 * 32 * CLOCK_HZ / 1e12  # 78.64 T fp32 lane-ops/s (non-FMA)
 HBM_PEAK_GBS = 8000.0
 FLOP_PER_TEST = 17  # RaySphereIntersection, Collision.hpp:9-17
+VALU_PER_PRETEST = 10  # the conservative member pretest
+# algorithmic HBM bytes per frame = 16 B/px float RGBA accumulator + 3 B/px
+# RGB8 + 48 B per sphere of scene tables
+ALGO_BYTES_PER_PIXEL, ALGO_BYTES_PER_SPHERE = 19, 48
+# Reference CPU path vs the restatement, both timed in the build container (8-core Xeon,
+# config 2 at 1200x800x100 spp, depth 50, 16 threads = 2*nproc, RenderImageParallelMain
+# tiling): reference from BASELINE.md (its clock-seam scene has N = 167), restatement
+# measured with `python tools/cpu_calibration.py` (keyed scene seed 1, N = 149)
+CPU_CALIBRATION = {"reference_msps": {"segment": 4.26, "task": 4.33},
+                   "restatement_msps": {"segment": 5.128, "task": 4.269},
+                   "host": "build container, Intel Xeon 8 cores, 16 threads, c2 at 100 spp",
+                   "note": "restatement/reference = 1.20 (segment) and 0.99 (task) raw; "
+                           "x149/167 sphere-count normalised: 1.07 and 0.88"}
 
 
 def make_scene(spt, name):
@@ -49,23 +66,81 @@ def make_scene(spt, name):
     raise ValueError(name)
 
 
-def cpu_baseline(scene, view, w, h, spp_sample, bounces, threads):
-    """The CPU restatement (oracle/, "port") timed with the reference's
-    RenderImageParallelMain tiling (threads x threads tiles, <= threads in
-    flight) on RenderSegmentTask, the TaskBasedPathTracer path of north_star."""
+def host_cores():
+    """CPUs this process may use: the job's share where one is set (OMP_NUM_THREADS on
+    the GPU box, whose os.cpu_count() is the whole machine), else the affinity mask."""
+    share = os.environ.get("OMP_NUM_THREADS")
+    if share and share.isdigit() and int(share) > 0:
+        return int(share)
+    return len(os.sched_getaffinity(0))
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(scene, view, w, h, spp_sample, bounces):
+    """The CPU restatement (oracle/, "port", gcc -O2 -msse4.1) timed with the
+    reference's RenderImageParallelMain tiling (Renderer.hpp:257-302: tc x tc tiles,
+    <= tc in flight) at tc = 2 * cores, the reference's hardware_concurrency() * 2
+    rule: RenderSegmentTask (TaskBasedPathTracer, north_star's CPU path) is `value`,
+    RenderSegment (the shipped default) is timed beside it."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle
     pyoracle.build()
     osc = pyoracle.OracleScene(scene.centers, scene.radii, scene.colors, scene.materials, scene.fuzz)
     fr = pyoracle.make_frame(view, [0, 1, -3, 0], [137, 207, 240, 0], w, h, spp_sample, bounces, 1)
-    t0 = time.perf_counter()
-    pyoracle.render_image_parallel(osc, fr, threads, mode=1, want_rgba=False)
-    dt = time.perf_counter() - t0
-    return {"value": round(w * h * spp_sample / dt / 1e6, 4), "unit": "Msamples/s", "cores": threads,
-            "kind": "port",
-            "sample": f"RenderSegmentTask (oracle C restatement, gcc -O2) via RenderImageParallelMain tiling "
-                      f"{threads}x{threads}, same scene/camera at {w}x{h}, {spp_sample} spp, depth {bounces}; "
-                      f"{dt:.2f} s wall on {threads} threads"}
+    cores = host_cores()
+    tc = 2 * cores
+    res = {}
+    for name, mode in (("task", 1), ("segment", 0)):
+        t0 = time.perf_counter()
+        pyoracle.render_image_parallel(osc, fr, tc, mode=mode, want_rgba=False)
+        dt = time.perf_counter() - t0
+        res[name] = (w * h * spp_sample / dt / 1e6, dt)
+    return {"value": round(res["task"][0], 4), "unit": "Msamples/s", "cores": cores, "kind": "port",
+            "segment_value": round(res["segment"][0], 4), "threads": tc, "nproc": os.cpu_count(),
+            "cpu_model": cpu_model(), "calibration": CPU_CALIBRATION,
+            "sample": f"RenderSegmentTask (value) and RenderSegment (segment_value) of the oracle C restatement "
+                      f"(gcc -O2 -msse4.1), RenderImageParallelMain tiling {tc}x{tc} with <= {tc} in flight on "
+                      f"{cores} cores, same scene/camera at {w}x{h}, {spp_sample} spp, depth {bounces}; "
+                      f"{res['task'][1]:.2f} s + {res['segment'][1]:.2f} s wall"}
+
+
+def dropin_bench(w, h, spp, bounces, frames, tcs):
+    """The C++ drop-in (include/spt/RenderSegmentShim.hpp) driven exactly like
+    RenderImageParallelMain (tools/dropin_harness.cpp): tc x tc RenderJob tiles, <= tc
+    threads in flight, host g_data, per tc the Msamples/s of `frames` timed frames."""
+    import subprocess
+    exe = os.path.join(ROOT, "simplepathtracer_amd", "lib", "spt_dropin_harness")
+    if not os.path.exists(exe):
+        return None
+    out = {}
+    for tc in tcs:
+        for task in (0, 1):
+            r = subprocess.run([exe, "/dev/null", str(w), str(h), str(spp), str(bounces), str(tc), str(task),
+                                str(frames)], capture_output=True, text=True, timeout=600)
+            if r.returncode != 0:
+                raise RuntimeError(f"dropin harness failed: {r.stderr[-400:]}")
+            sec = float(r.stdout.split("seconds=")[1].split()[0])
+            out[f"{'task' if task else 'segment'}_tc{tc}"] = round(w * h * spp * frames / sec / 1e6, 3)
+    return out
+
+
+def profile_record(config):
+    """Per-launch PMC counters and in-kernel lane counts of the render kernel for a
+    config, from profiles/counters.json (rocprofv3 --pmc passes and the SPT_DIAG build,
+    tools/profile.sh + tools/summarize_profile.py), or None."""
+    path = os.path.join(ROOT, "profiles", "counters.json")
+    if not os.path.exists(path):
+        return None
+    return json.load(open(path)).get(config)
 
 
 def main():
@@ -84,8 +159,9 @@ def main():
                          "2 when a frame is one workspace batch, else 1 (long multi-batch frames gain nothing "
                          "and would double the workspace)")
     ap.add_argument("--cpu-spp", type=int, default=32, help="spp of the bounded CPU-baseline sample")
-    ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-dropin", action="store_true", help="skip the C++ drop-in measurement (config 2)")
+    ap.add_argument("--dropin-frames", type=int, default=5)
     ap.add_argument("--dump", default="", help="write rank 0's final g_data bytes to this file")
     args = ap.parse_args()
 
@@ -181,18 +257,16 @@ def main():
         # device time; the span average is reported beside it
         avg_ms = st["render_busy_ms"] / launches
         span_ms = st["render_ms"] / launches
+        t_launch = avg_ms / 1e3
         rays_per_launch = st["casts"] / launches
-        algo_tflop = FLOP_PER_TEST * scene.n * rays_per_launch / 1e12
-        achieved = algo_tflop / (avg_ms / 1e3)
         samples_per_launch = st["samples"] / launches
-        slot_bytes = 12.0 if args.mode == "segment" else 16.0  # per-sample slot: rgb (+ counted flag in task mode)
-        hbm_bytes = slot_bytes * samples_per_launch  # written by the render kernel
-        traffic = None
-        tpath = os.path.join(ROOT, "profiles", "traffic.json")
-        if os.path.exists(tpath):
-            rec = json.load(open(tpath)).get(args.config, {}).get("render_kernel")
-            if rec and world == 1:
-                traffic = rec["fetch_bytes"] + rec["write_bytes"]
+        px_per_launch = samples_per_launch / spp  # every launch renders its pixels at full spp
+        # SURVEY §8(d) algorithmic bytes: 19 B per pixel (float RGBA + RGB8) + 48 B per sphere
+        algo_bytes = ALGO_BYTES_PER_PIXEL * px_per_launch + ALGO_BYTES_PER_SPHERE * scene.n
+        slot_bytes = (12.0 if args.mode == "segment" else 16.0) * samples_per_launch  # the design's sample slots
+        prof = profile_record(args.config) if world == 1 and args.engine == "megakernel" else None
+        rk = (prof or {}).get("render_kernel", {})
+        traffic = (rk["fetch_bytes"] + rk["write_bytes"]) if "fetch_bytes" in rk else None
         out = {
             "metric": "Msamples/s (pixels×spp/s), RTIOW random-sphere scene, 1/2/4/8 MI355X",
             "value": round(value, 3),
@@ -211,32 +285,64 @@ def main():
                        "width": W, "height": H, "spp": spp, "bounces": bounces, "spheres": scene.n,
                        "parallelism": f"row-strips{split.strip}x{world}" if world > 1 else "1 GPU",
                        "frames_in_flight": nst},
-            # contract form: the render kernel against HBM (12 B per sample slot written),
-            # as BASELINE.json's "fraction of HBM roofline" asks; the kernel is bound by
-            # VALU issue and latency instead (roofline_valu)
-            "roofline": {"bound": "hbm", "achieved": round(hbm_bytes / (avg_ms / 1e3) / 1e9, 3),
+            # contract form: the render kernel against HBM with SURVEY §8(d)'s algorithmic
+            # bytes; HBM does not bind this kernel (VALU issue + latency do: roofline_valu)
+            "roofline": {"bound": "hbm", "achieved": round(algo_bytes / t_launch / 1e9, 4),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(hbm_bytes / (avg_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 6), "traffic": traffic,
-                         "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE, profiles/traffic.json)",
-                         "algorithmic_bytes": hbm_bytes,
+                         "frac": round(algo_bytes / t_launch / 1e9 / HBM_PEAK_GBS, 7), "traffic": traffic,
+                         "traffic_unit": "HBM bytes per render launch (PMC FETCH_SIZE x2 + WRITE_SIZE, "
+                                         "profiles/counters.json)",
+                         "algorithmic_bytes": algo_bytes,
+                         "algorithmic_def": "19 B x pixels + 48 B x spheres per launch (SURVEY §8d)",
+                         "traffic_over_algorithmic": round(traffic / algo_bytes, 1) if traffic else None,
+                         "slot_bytes": slot_bytes,
+                         "slot_def": "the design's per-sample slots written by the render kernel (12 B/sample "
+                                     "segment mode) and read back once by the fold: the traffic above",
                          "kernel": "render_kernel", "avg_launch_ms": round(avg_ms, 4),
-                         "avg_launch_ms_def": "union of the render launches' HIP-event intervals (launch stream) / launches",
-                         "avg_launch_span_ms": round(span_ms, 4),
-                         "binding": "VALU issue + latency (see roofline_valu), not HBM"},
-            "roofline_valu": {"bound": "valu", "achieved": round(achieved, 3), "peak": round(VALU_PEAK_TOPS, 2),
-                              "unit": "TFLOP/s", "frac": round(achieved / VALU_PEAK_TOPS, 4),
-                              "flop_model": "17 FLOP per RaySphereIntersection x N spheres x rays counted in-kernel "
-                                            "(brute force; the culling skips most tests, so frac can pass 1)",
-                              "rays_per_launch": rays_per_launch,
-                              "flop_per_launch": FLOP_PER_TEST * scene.n * rays_per_launch},
+                         "avg_launch_ms_def": "union of the render launches' HIP-event intervals (launch stream) "
+                                              "/ launches",
+                         "avg_launch_span_ms": round(span_ms, 4)},
             "rays_per_sample": round(casts_all / max(samples_all, 1), 4),
             # with frames in flight the fold runs beside the next frame's render and its
             # own event span mostly measures waiting for CUs: reported for --streams 1 only
             "fold_ms_per_step": round(st["fold_ms"] / args.steps, 4) if nst == 1 else None,
         }
+        if prof and "SQ_INSTS_VALU" in rk:
+            # the binding resource: VALU issue.  Wave-instructions per launch from the PMC
+            # pass over this same command, against 1024 SIMDs x 2.4 GHz / 2 cycles per
+            # wave64 instruction; lane-level work from the SPT_DIAG build's in-kernel counts
+            issue = rk["SQ_INSTS_VALU"] / t_launch
+            rv = {"bound": "valu-issue", "achieved": round(issue / 1e12, 5), "peak": round(VALU_ISSUE_PEAK / 1e12, 5),
+                  "unit": "T wave64-VALU-instructions/s", "frac": round(issue / VALU_ISSUE_PEAK, 4),
+                  "valu_insts_per_launch": rk["SQ_INSTS_VALU"], "salu_insts_per_launch": rk.get("SQ_INSTS_SALU"),
+                  "source": rk.get("source")}
+            dg = (prof or {}).get("diag")
+            if dg:
+                lane_ops = (FLOP_PER_TEST * dg["lane_tests_per_ray"] + VALU_PER_PRETEST * dg["lane_pretests_per_ray"]) \
+                    * rays_per_launch
+                rv["useful"] = {"achieved": round(lane_ops / t_launch / 1e12, 3), "peak": round(VALU_PEAK_TOPS, 2),
+                                "unit": "T fp32 lane-ops/s", "frac": round(lane_ops / t_launch / 1e12 / VALU_PEAK_TOPS, 4),
+                                "tests_per_ray": dg["lane_tests_per_ray"],
+                                "pretests_per_ray": dg["lane_pretests_per_ray"],
+                                "brute_force_tests_per_ray": scene.n,
+                                "def": "17 FLOP per RaySphereIntersection + 10 per member pretest, evaluated for "
+                                       "live lanes (SPT_DIAG in-kernel counts, profiles/counters.json) x rays "
+                                       "counted in-kernel / launch time"}
+            for k in ("VALUUtilization", "VALUBusy", "occupancy_waves_per_simd", "sqc_dcache_miss_frac"):
+                if k in rk:
+                    rv[k] = rk[k]
+            out["roofline_valu"] = rv
         if world == 1 and not args.no_cpu_baseline:
             cw, ch = (W, H) if args.config != "c3" else (1920, 1080)
-            out["cpu_baseline"] = cpu_baseline(scene, view, cw, ch, args.cpu_spp, bounces, args.cpu_threads)
+            out["cpu_baseline"] = cpu_baseline(scene, view, cw, ch, args.cpu_spp, bounces)
+        if world == 1 and args.config == "c2" and not args.no_dropin and args.engine == "megakernel":
+            # the drop-in boundary itself: RenderSegment/RenderSegmentTask from RenderJob threads
+            d = dropin_bench(W, H, spp, bounces, args.dropin_frames, (4, 2 * host_cores()))
+            if d:
+                out["dropin"] = {"unit": "Msamples/s", **d,
+                                 "def": "C++ shim under RenderImageParallelMain tiling (tools/dropin_harness.cpp), "
+                                        "host g_data, tc=4 (shipped g_maxThreads) and tc=2*cores; "
+                                        f"{args.dropin_frames} timed frames each"}
         print(json.dumps(out), flush=True)
         if args.dump:
             torch.cuda.synchronize(dev)

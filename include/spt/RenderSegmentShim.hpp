@@ -13,7 +13,9 @@
 // (IOHelpers.hpp:17-22).  The reference has no error channel, so a failure is
 // reported on stderr and aborts.  Sampling uses the keyed per-(pixel, sample)
 // stream seeded with spt_shim::seed (default 1; SPT_SEED overrides) instead of
-// the clock-seeded thread_local splitmix (Random.hpp:86-93).
+// the clock-seeded thread_local splitmix (Random.hpp:86-93).  Concurrent RenderJob
+// threads run on the GPU together (each call gets its own stream and workspace);
+// SPT_DEVICES=0,1,... spreads them over several devices.
 #pragma once
 
 #include <spt_hip.h>
@@ -38,10 +40,23 @@ inline void check(spt_ctx *ctx, int rc, const char *what)
 
 inline spt_ctx *context()
 {
+    // SPT_DEVICES=0,1,...: a multi-device context (each RenderJob tile goes to the
+    // least busy device); else SPT_DEVICE (default 0)
     static spt_ctx *ctx = [] {
         spt_ctx *c = nullptr;
-        const char *dev = std::getenv("SPT_DEVICE");
-        check(nullptr, spt_ctx_create(dev ? std::atoi(dev) : 0, &c), "spt_ctx_create");
+        if (const char *list = std::getenv("SPT_DEVICES")) {
+            std::vector<int> devs;
+            for (const char *p = list; *p;) {
+                char *end = nullptr;
+                devs.push_back((int)std::strtol(p, &end, 10));
+                if (end == p) break;
+                p = *end == ',' ? end + 1 : end;
+            }
+            check(nullptr, spt_ctx_create_multi(devs.data(), (uint32_t)devs.size(), &c), "spt_ctx_create_multi");
+        } else {
+            const char *dev = std::getenv("SPT_DEVICE");
+            check(nullptr, spt_ctx_create(dev ? std::atoi(dev) : 0, &c), "spt_ctx_create");
+        }
         return c;
     }();
     return ctx;
@@ -111,7 +126,7 @@ inline void RenderSegment(RenderSegmentData segment)
                     "spt_render_segment");
 }
 
-// TaskBasedPathTracer.hpp:54-206 (exact for square tiles)
+// TaskBasedPathTracer.hpp:54-206 (non-square tiles alias pixels as the reference does)
 inline void RenderSegmentTask(RenderSegmentData segment)
 {
     spt_shim::sync_globals();

@@ -18,7 +18,9 @@
  *
  * Plain C types only.  Every function returns an spt_status; on failure
  * spt_last_error() describes why.  A context is safe to use from several host
- * threads (calls are serialised per context).
+ * threads: its state is guarded by a lock, and concurrent render calls (the
+ * reference's RenderJob threads) each get their own stream and workspace, so they
+ * run on the GPU together.
  */
 #ifndef SPT_HIP_H
 #define SPT_HIP_H
@@ -30,7 +32,7 @@
 extern "C" {
 #endif
 
-#define SPT_ABI_VERSION 2
+#define SPT_ABI_VERSION 3
 
 /* Only the functions below are exported from libspt_hip.so (built with
  * -fvisibility=hidden), so several builds can be loaded side by side. */
@@ -75,13 +77,15 @@ typedef struct spt_stats {
     double render_busy_ms; /* length of the union of the render launches' intervals: with
                               frames in flight on several streams launches overlap, and
                               this is the device time during which some render launch ran */
-    uint64_t diag[12];     /* diagnostic build only (-DSPT_DIAG=1): wave iterations,
+    uint64_t diag[14];     /* diagnostic build only (-DSPT_DIAG=1): wave iterations,
                               clusters entered, tree nodes tested, s_memtime cycles in
                               cast / shading / refill, (lane, cluster) pairs that may
                               pass, live lanes of entered clusters, spheres tested per
                               wave, their update branches taken (some lane passes),
                               lanes passing in those branches, branches that
-                              improve some lane's winner */
+                              improve some lane's winner, RaySphereIntersection
+                              evaluations for live lanes (lane-tests), member pretests
+                              for live lanes (lane-pretests) */
 } spt_stats;
 
 SPT_API int spt_abi_version(void);
@@ -91,6 +95,16 @@ SPT_API int spt_device_count(int *count);
 /* Context on one device.  Replaces nothing in the reference (its state is global);
  * it owns the device copies of Globals.hpp's scene/camera and a workspace. */
 SPT_API int spt_ctx_create(int device, spt_ctx **out);
+/* Context over several devices (one process driving the node's
+ * GPUs).  devices[0] is member 0; a device may be listed more than once (members on
+ * one device render concurrently on their own streams).  Every setter applies to all
+ * members (each keeps its own copy of the scene); spt_render_frame splits the frame
+ * over the members; spt_render_segment[_task] / spt_render_progressive send each
+ * call (a RenderJob tile) to the member with the fewest calls in flight; the other
+ * entry points (rows/assemble/samples/selftest) use member 0. */
+SPT_API int spt_ctx_create_multi(const int *devices, uint32_t n, spt_ctx **out);
+/* Members of ctx: on entry *n = capacity of devices (nullable), on return *n = count. */
+SPT_API int spt_ctx_devices(spt_ctx *ctx, uint32_t *n, int *devices);
 SPT_API void spt_ctx_destroy(spt_ctx *ctx);
 /* Last error of ctx, or of the calling thread when ctx is NULL. Never NULL. */
 SPT_API const char *spt_last_error(const spt_ctx *ctx);
@@ -141,7 +155,8 @@ SPT_API int spt_set_engine(spt_ctx *ctx, int engine);
 SPT_API int spt_set_workspace(spt_ctx *ctx, uint64_t bytes);
 
 /* ---- drop-in entry points (host memory, blocking) ----------------------------
- * Render pixels [yBegin,yEnd) x [xBegin,xEnd).
+ * Render pixels [yBegin,yEnd) x [xBegin,xEnd).  Concurrent calls on one context run
+ * on the GPU together (up to 8 in flight per device; SPT_HOST_SLOTS lowers it).
  * rgba_out (nullable): region-local row-major float4 per pixel = the reference's
  *   pixelColor after `*= 1/g_samples` (the value WritePixel receives).
  * g_data (nullable): full-frame width*height*3 bytes; the region's pixels are
@@ -149,13 +164,24 @@ SPT_API int spt_set_workspace(spt_ctx *ctx, uint64_t bytes);
  *   io::WritePixel does (IOHelpers.hpp:17-22), other bytes untouched. */
 SPT_API int spt_render_segment(spt_ctx *ctx, uint32_t yBegin, uint32_t yEnd, uint32_t xBegin, uint32_t xEnd,
                        float *rgba_out, uint8_t *g_data);
+/* The whole frame (RenderImage, Renderer.hpp:304-308, over every device of the
+ * context): member r of n renders the interleaved row strips r, r+n, ... (strip =
+ * the largest of 8/4/2/1 rows that deals the strips evenly) into a compact tile;
+ * member 0 pulls the tiles over xGMI (peer copies), scatters them into the frame and
+ * writes rgba_out (nullable, width*height float4, row-major) and g_data (nullable,
+ * the reference layout).  Pixels are keyed per (pixel, sample), so the frame is
+ * bit-identical for any member count.  Exception: in task mode a non-square frame
+ * (RenderImage's RenderSegmentTask({0, H, 0, W}) aliases pixels across rows,
+ * TaskBasedPathTracer.hpp:103,186) renders on member 0 alone.  Blocking. */
+SPT_API int spt_render_frame(spt_ctx *ctx, int mode, float *rgba_out, uint8_t *g_data);
 /* Progressive RenderSegment / RenderSegmentTask (the preview of RenderImageParallelMain,
  * Renderer.hpp:257-302): the region is rendered in passes of pass_spp samples; after
  * each pass rgba_out / g_data (either nullable) hold the render at the samples done so
  * far -- bit-identical to a render with g_samples = samples_done, since samples are
  * keyed per (pixel, sample) -- and cb(user, samples_done) runs on the calling thread
  * (nullable; a nonzero return stops the render there).  The last pass is the full
- * render.  cb must not call into the same context. */
+ * render.  cb runs with the context unlocked: it may read stats, pin buffers or render
+ * elsewhere, but setters of the same context called from it fail with SPT_ERR_STATE. */
 /* Page-lock a caller-owned host buffer -- typically g_data (Globals.hpp:19, malloc'd)
  * -- so the per-call device-to-host copy of the render is a direct DMA and the GL
  * thread's UpdateTexture (Renderer.hpp:157-164) reads the same pinned bytes.
@@ -225,7 +251,8 @@ SPT_API int spt_save_bmp(const char *path, uint32_t width, uint32_t height, uint
 /* ---- numerics self-test ------------------------------------------------------
  * Runs the device primitives the render path relies on over n inputs and
  * writes SPT_SELFTEST_COLS floats per input: a/b, sqrtf(a),
- * sqrt(double(a)) and pow5(double(a)) as two float words each, uniform(-1,1)
+ * glibc's powf(a, 5) and powf(c, 5) restated, powf(a, 2), the refraction scalar
+ * r*a - sqrt(1 - r*r*(1 - a*a)) (r = 1/1.5; -1e30 under total reflection), uniform(-1,1)
  * of bits, u8 of a, Normalize({a, b, c}) (3 floats), c/a, uniform(-0.5,0.5) and
  * uniform(0,1) of bits, with c the float whose bit pattern is bits. */
 #define SPT_SELFTEST_COLS 14

@@ -15,7 +15,7 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG_DIR, "lib", os.environ.get("SPT_LIB", "libspt_hip.so"))
 HEADER_PATH = os.path.join(os.path.dirname(PKG_DIR), "include", "spt_hip.h")
 
-ABI_VERSION = 2  # SPT_ABI_VERSION of include/spt_hip.h
+ABI_VERSION = 3  # SPT_ABI_VERSION of include/spt_hip.h
 SPT_OK = 0
 STATUS_NAMES = {0: "SPT_OK", 1: "SPT_ERR_ARG", 2: "SPT_ERR_STATE", 3: "SPT_ERR_HIP", 4: "SPT_ERR_NOMEM",
                 5: "SPT_ERR_NODEVICE"}
@@ -44,7 +44,7 @@ class Stats(ctypes.Structure):
         ("grid_blocks", ctypes.c_uint32),
         ("block_threads", ctypes.c_uint32),
         ("render_busy_ms", ctypes.c_double),
-        ("diag", ctypes.c_uint64 * 12),
+        ("diag", ctypes.c_uint64 * 14),
     ]
 
 
@@ -79,6 +79,9 @@ def lib() -> ctypes.CDLL:
         "spt_abi_version": ([], I),
         "spt_device_count": ([P], I),
         "spt_ctx_create": ([I, P], I),
+        "spt_ctx_create_multi": ([P, u32, P], I),
+        "spt_ctx_devices": ([P, P, P], I),
+        "spt_render_frame": ([P, I, P, P], I),
         "spt_ctx_destroy": ([P], None),
         "spt_last_error": ([P], ctypes.c_char_p),
         "spt_set_scene": ([P, P, P, P, P, P, u32], I),

@@ -12,7 +12,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
+#include <condition_variable>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -26,6 +28,8 @@
 namespace {
 
 thread_local std::string g_thread_error;
+// the context whose progress callback is running on this thread (spt_render_progressive)
+thread_local const spt_ctx *t_in_callback = nullptr;
 
 struct EventPair {
     hipEvent_t a = nullptr, b = nullptr;
@@ -34,7 +38,20 @@ struct EventPair {
 }  // namespace
 
 namespace {
-constexpr size_t kMaxWorkspaces = 4;
+// caller streams (spt_render_rows_async) + the host-call slots below
+constexpr size_t kMaxCallerStreams = 4;
+constexpr size_t kCounters = 18;  // device counters: casts, samples, dropped, -, diag[14]
+constexpr size_t kMaxHostSlots = 8;
+constexpr size_t kMaxWorkspaces = kMaxCallerStreams + kMaxHostSlots + 1;
+// One in-flight host call (spt_render_segment[_task] / spt_render_progressive): its own
+// stream (hence its own workspace) and output staging, so concurrent RenderJob tiles
+// (Renderer.hpp:242-302) run on the GPU together instead of one after another.
+struct HostSlot {
+    hipStream_t stream = nullptr;
+    float4 *d_stage = nullptr;  // region-local float4 output
+    size_t stage_cap = 0;
+    bool busy = false;
+};
 struct Workspace {
     hipStream_t stream = nullptr;  // key
     float *d_samples = nullptr;    // per-sample slots of the current batch
@@ -90,12 +107,25 @@ struct spt_ctx {
     // previous one drain)
     std::vector<Workspace> ws;
     unsigned long long *d_counters = nullptr;
-    float4 *d_stage = nullptr;
-    size_t stage_cap = 0;
     uint8_t *d_frame8 = nullptr;
     size_t frame8_cap = 0;
 
     std::vector<void *> pinned;  // host buffers registered by spt_pin_host
+
+    // host-call slots (render_segment_host), created on demand up to host_slots
+    std::vector<HostSlot *> slots;
+    std::condition_variable slot_cv;
+    uint32_t host_slots = kMaxHostSlots;
+    std::atomic<int> inflight{0};  // host calls in progress on this device
+
+    // multi-device context (spt_ctx_create_multi): member contexts of the other devices,
+    // each with its own scene copy; this context is member 0
+    std::vector<spt_ctx *> peers;
+    float4 *d_tile = nullptr;  // spt_render_frame: this member's strips (member 0: all members' strips)
+    size_t tile_cap = 0;
+    float4 *d_fullframe = nullptr;  // spt_render_frame: assembled float4 frame (member 0)
+    size_t fullframe_cap = 0;
+    hipEvent_t frame_ev = nullptr;
 
     // timing
     std::vector<EventPair> pending_render, pending_fold, pool;
@@ -162,11 +192,21 @@ EventPair get_pair(spt_ctx *ctx)
     return p;
 }
 
-// Harvest finished launch timings (blocking on their stop events).
-int collect_timings(spt_ctx *ctx)
+// Harvest launch timings: all of them (wait: blocking on their stop events), or only
+// those whose launches have finished (a host call must not wait for other callers').
+int collect_timings(spt_ctx *ctx, bool wait = true)
 {
     for (auto *vec : {&ctx->pending_render, &ctx->pending_fold}) {
+        std::vector<EventPair> keep;
         for (EventPair &p : *vec) {
+            if (!wait) {
+                const hipError_t q = hipEventQuery(p.b);
+                if (q == hipErrorNotReady) {
+                    keep.push_back(p);
+                    continue;
+                }
+                HIP_TRY(ctx, q);
+            }
             HIP_TRY(ctx, hipEventSynchronize(p.b));
             float ms = 0.f;
             HIP_TRY(ctx, hipEventElapsedTime(&ms, p.a, p.b));
@@ -181,7 +221,7 @@ int collect_timings(spt_ctx *ctx)
             }
             ctx->pool.push_back(p);
         }
-        vec->clear();
+        vec->swap(keep);
     }
     return SPT_OK;
 }
@@ -369,6 +409,8 @@ int render_impl(spt_ctx *ctx, int mode, const spt::RowMap &map, float4 *d_rgba, 
     fa.spp_total = ctx->spp;
     fa.mode = mode;
     fa.preview = pg ? 1 : 0;
+    // one rectangle in task mode = one RenderSegmentTask call: its colorIndex aliasing
+    fa.alias = mode == SPT_MODE_TASK && map.parts == 1u && rows != map.width ? 1 : 0;
 
     for (uint32_t s0 = 0; s0 < ctx->spp; s0 += spp_batch) {
         const uint32_t b = std::min(spp_batch, ctx->spp - s0);
@@ -475,7 +517,8 @@ int rebuild_accel(spt_ctx *ctx)
             shade[j] = ctx->h_shade[t.orig[j]];
             mat[j] = ctx->h_mat[t.orig[j]];
         }
-    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    // every stream: host calls and caller-stream renders may still read the tables
+    HIP_TRY(ctx, hipDeviceSynchronize());
     int rc = upload(ctx, &ctx->d_slots, &ctx->slots_cap, t.slots);
     if (!rc) rc = upload(ctx, &ctx->d_shade, &ctx->shade_cap, shade);
     if (!rc) rc = upload(ctx, &ctx->d_mat, &ctx->mat_cap, mat);
@@ -496,53 +539,257 @@ int check_region(spt_ctx *ctx, uint32_t yB, uint32_t yE, uint32_t xB, uint32_t x
     return SPT_OK;
 }
 
+// A free host-call slot of ctx (created on demand, at most ctx->host_slots; waits for
+// one to free up beyond that).  Called with ctx->mu held through lk.
+HostSlot *acquire_slot(spt_ctx *ctx, std::unique_lock<std::mutex> &lk)
+{
+    for (;;) {
+        for (HostSlot *h : ctx->slots)
+            if (!h->busy) {
+                h->busy = true;
+                return h;
+            }
+        if (ctx->slots.size() < ctx->host_slots) {
+            HostSlot *h = new HostSlot();
+            if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
+                delete h;
+                fail(ctx, SPT_ERR_HIP, "stream creation failed");
+                return nullptr;
+            }
+            h->busy = true;
+            ctx->slots.push_back(h);
+            return h;
+        }
+        ctx->slot_cv.wait(lk);
+    }
+}
+
+void release_slot(spt_ctx *ctx, HostSlot *h)
+{
+    h->busy = false;
+    ctx->slot_cv.notify_one();
+}
+
+// The member of a multi-device context with the fewest host calls in flight.
+spt_ctx *pick_member(spt_ctx *ctx)
+{
+    spt_ctx *best = ctx;
+    for (spt_ctx *p : ctx->peers)
+        if (p->inflight.load() < best->inflight.load()) best = p;
+    return best;
+}
+
 // RenderSegment / RenderSegmentTask with host outputs; with pass_spp > 0 progressively,
-// copying the outputs back and calling cb after every pass.
+// copying the outputs back and calling cb after every pass.  The context lock is held
+// only while launches are enqueued: each call renders on its own slot (stream,
+// workspace, staging), waits for its stream unlocked, so concurrent callers -- the
+// reference's RenderJob threads -- overlap on the GPU; cb runs unlocked too.
+// spread: a multi-device context sends the call to its least busy member (else member 0).
 int render_segment_host(spt_ctx *ctx, int mode, uint32_t yB, uint32_t yE, uint32_t xB, uint32_t xE, float *rgba,
-                        uint8_t *g_data, uint32_t pass_spp = 0, spt_progress_fn cb = nullptr, void *user = nullptr)
+                        uint8_t *g_data, uint32_t pass_spp = 0, spt_progress_fn cb = nullptr, void *user = nullptr,
+                        bool spread = true)
 {
     if (!ctx) return fail(nullptr, SPT_ERR_ARG, "null context");
-    std::lock_guard<std::mutex> lk(ctx->mu);
+    if (spread && !ctx->peers.empty()) ctx = pick_member(ctx);  // tiles go to the least busy device
+    std::unique_lock<std::mutex> lk(ctx->mu);
     int rc = check_ready(ctx);
     if (rc) return rc;
     if ((rc = check_region(ctx, yB, yE, xB, xE))) return rc;
     if (yB >= yE || xB >= xE) return SPT_OK;  // the reference's loops do nothing
     HIP_TRY(ctx, hipSetDevice(ctx->device));
+    HostSlot *hs = acquire_slot(ctx, lk);
+    if (!hs) return SPT_ERR_HIP;
+    ctx->inflight.fetch_add(1);
+    struct Release {
+        spt_ctx *c;
+        HostSlot *h;
+        ~Release()
+        {
+            c->inflight.fetch_sub(1);
+            release_slot(c, h);
+        }
+    } release{ctx, hs};  // runs with lk held (declared after it)
     const uint32_t w = xE - xB, h = yE - yB;
     const size_t npix = (size_t)w * h;
-    if ((rc = ensure(ctx, &ctx->d_stage, &ctx->stage_cap, npix))) return rc;
+    if ((rc = ensure(ctx, &hs->d_stage, &hs->stage_cap, npix))) return rc;
     uint8_t *d8 = nullptr;
     if (g_data) {
         if ((rc = ensure(ctx, &ctx->d_frame8, &ctx->frame8_cap, (size_t)ctx->W * ctx->H * 3))) return rc;
         d8 = ctx->d_frame8;
     }
+    const uint32_t W = ctx->W, H = ctx->H;
     spt::RowMap map{yB, yE, 1u, 1u, 0u, xB, w};
-    auto copy_out = [&]() -> int {
+    // enqueue the copy-back of the outputs, then wait for the slot's stream unlocked
+    auto copy_out_and_wait = [&]() -> int {
         if (rgba)
-            HIP_TRY(ctx, hipMemcpyAsync(rgba, ctx->d_stage, npix * sizeof(float4), hipMemcpyDeviceToHost, ctx->stream));
+            HIP_TRY(ctx, hipMemcpyAsync(rgba, hs->d_stage, npix * sizeof(float4), hipMemcpyDeviceToHost, hs->stream));
         if (g_data) {
             // rows y in [yB, yE) live at g_data rows H-1-y: one contiguous band, xB.. per row
-            const size_t pitch = (size_t)ctx->W * 3;
-            const size_t off = (size_t)(ctx->H - yE) * pitch + (size_t)xB * 3;
-            HIP_TRY(ctx, hipMemcpy2DAsync(g_data + off, pitch, ctx->d_frame8 + off, pitch, (size_t)w * 3, h,
-                                          hipMemcpyDeviceToHost, ctx->stream));
+            const size_t pitch = (size_t)W * 3;
+            const size_t off = (size_t)(H - yE) * pitch + (size_t)xB * 3;
+            HIP_TRY(ctx, hipMemcpy2DAsync(g_data + off, pitch, d8 + off, pitch, (size_t)w * 3, h,
+                                          hipMemcpyDeviceToHost, hs->stream));
         }
-        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        lk.unlock();
+        const hipError_t e = hipStreamSynchronize(hs->stream);
+        lk.lock();
+        if (e != hipSuccess) return fail(ctx, SPT_ERR_HIP, "hipStreamSynchronize failed: %s", hipGetErrorString(e));
         return SPT_OK;
     };
     if (pass_spp == 0) {
-        if ((rc = render_impl(ctx, mode, map, ctx->d_stage, d8, ctx->stream, false))) return rc;
+        if ((rc = render_impl(ctx, mode, map, hs->d_stage, d8, hs->stream, false))) return rc;
     } else {
         Progress pg{pass_spp, [&](uint32_t done) -> int {
-                        const int r = copy_out();
+                        const int r = copy_out_and_wait();
                         if (r) return -r;
-                        return cb ? (cb(user, done) != 0 ? 1 : 0) : 0;
+                        if (!cb) return 0;
+                        lk.unlock();
+                        t_in_callback = ctx;
+                        const int stop = cb(user, done);
+                        t_in_callback = nullptr;
+                        lk.lock();
+                        return stop != 0 ? 1 : 0;
                     }};
-        rc = render_impl(ctx, mode, map, ctx->d_stage, d8, ctx->stream, false, &pg);
+        rc = render_impl(ctx, mode, map, hs->d_stage, d8, hs->stream, false, &pg);
         if (rc) return rc < 0 ? -rc : rc;
     }
-    if ((rc = copy_out())) return rc;
-    return collect_timings(ctx);
+    if ((rc = copy_out_and_wait())) return rc;
+    return collect_timings(ctx, false);
+}
+
+// Setters must not run from a progress callback of the same context (the render in
+// progress reads the state they change).
+int check_not_in_callback(spt_ctx *ctx)
+{
+    if (t_in_callback == ctx) return fail(ctx, SPT_ERR_STATE, "called from a progress callback of this context");
+    return SPT_OK;
+}
+
+// Rows per strip of the multi-device frame split: the largest of 8, 4, 2, 1 that deals
+// the frame's strips evenly over the members, else 8 (simplepathtracer_amd/distributed.py
+// even_strip, the same rule as the one-process-per-GPU path).
+uint32_t even_strip(uint32_t height, uint32_t parts)
+{
+    for (uint32_t s : {8u, 4u, 2u, 1u})
+        if (height % s == 0 && (height / s) % parts == 0) return s;
+    return 8u;
+}
+
+// Apply a setter to the context and every member device of a multi-device context.
+template <class F>
+int for_members(spt_ctx *ctx, F &&f)
+{
+    if (!ctx) return fail(nullptr, SPT_ERR_ARG, "null context");
+    int rc = check_not_in_callback(ctx);
+    if (rc) return rc;
+    if ((rc = f(ctx))) return rc;
+    for (spt_ctx *p : ctx->peers)
+        if ((rc = f(p))) return fail(ctx, rc, "member device %d: %s", p->device, p->err.c_str());
+    return SPT_OK;
+}
+
+// Setters of one context; the exported setters apply them to every member device.
+int spt_set_scene_one(spt_ctx *ctx, const float *centers4, const float *radii, const float *colors4,
+                  const uint8_t *materials, const float *fuzz, uint32_t n)
+{
+    if (!ctx) return fail(nullptr, SPT_ERR_ARG, "null context");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    if (n > 0 && (!centers4 || !radii || !colors4 || !materials || !fuzz))
+        return fail(ctx, SPT_ERR_ARG, "null scene array");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    std::vector<float4> shade(n);
+    std::vector<uint32_t> mat(n);
+    for (uint32_t i = 0; i < n; ++i) {
+        shade[i] = make_float4(colors4[4 * i], colors4[4 * i + 1], colors4[4 * i + 2], fuzz[i]);
+        mat[i] = materials[i];
+    }
+    ctx->h_shade = std::move(shade);
+    ctx->h_mat = std::move(mat);
+    ctx->h_centers.assign(centers4, centers4 + 4 * (size_t)n);
+    ctx->h_radii.assign(radii, radii + n);
+    ctx->n = n;
+    int rc = rebuild_accel(ctx);
+    if (rc) return rc;
+    ctx->scene_set = true;
+    return SPT_OK;
+}
+
+int spt_set_camera_one(spt_ctx *ctx, const float view[16], const float eye[4], const float sky[4])
+{
+    if (!ctx) return fail(nullptr, SPT_ERR_ARG, "null context");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    if (!view || !eye || !sky) return fail(ctx, SPT_ERR_ARG, "null camera array");
+    for (int j = 12; j < 16; ++j)
+        if (view[j] != 0.0f)
+            return fail(ctx, SPT_ERR_ARG, "viewMatrix row 3 must be zero (CreateCameraBasisMatrix, Math.hpp:204-208)");
+    for (int j = 0; j < 12; ++j) ctx->cam.view[j] = view[j];
+    for (int j = 0; j < 3; ++j) {
+        ctx->cam.eye[j] = eye[j];
+        ctx->cam.sky[j] = sky[j];
+    }
+    ctx->cam_set = true;
+    return SPT_OK;
+}
+
+int spt_set_params_one(spt_ctx *ctx, uint32_t width, uint32_t height, uint32_t spp, uint32_t bounces, uint64_t seed)
+{
+    if (!ctx) return fail(nullptr, SPT_ERR_ARG, "null context");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    if (width == 0 || height == 0) return fail(ctx, SPT_ERR_ARG, "empty frame %ux%u", width, height);
+    if ((uint64_t)width * height * 3 > 0xFFFFFFFFull)
+        return fail(ctx, SPT_ERR_ARG, "frame %ux%u overflows the reference's uint32 g_size", width, height);
+    if (spp == 0) return fail(ctx, SPT_ERR_ARG, "spp must be >= 1 (1.f/0 samples)");
+    if (bounces == 0) return fail(ctx, SPT_ERR_ARG, "bounces must be >= 1 (--bounceCount never reaches 0)");
+    ctx->W = width;
+    ctx->H = height;
+    ctx->spp = spp;
+    ctx->bounces = bounces;
+    ctx->seed = seed;
+    ctx->params_set = true;
+    return SPT_OK;
+}
+
+int spt_set_cluster_size_one(spt_ctx *ctx, uint32_t k)
+{
+    if (!ctx) return fail(nullptr, SPT_ERR_ARG, "null context");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    if (k > spt::kClusterSlots && k != SPT_CLUSTER_AUTO)
+        return fail(ctx, SPT_ERR_ARG, "cluster size %u > %u", k, spt::kClusterSlots);
+    ctx->cluster_k = k;
+    if (!ctx->scene_set) return SPT_OK;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    return rebuild_accel(ctx);
+}
+
+int spt_set_cluster_tree_one(spt_ctx *ctx, uint32_t branching)
+{
+    if (!ctx) return fail(nullptr, SPT_ERR_ARG, "null context");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    if (branching == 1 || (branching > 64 && branching != SPT_TREE_AUTO))
+        return fail(ctx, SPT_ERR_ARG, "tree branching %u not in {0, 2..64, SPT_TREE_AUTO}", branching);
+    ctx->tree_branching = branching;
+    if (!ctx->scene_set) return SPT_OK;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    return rebuild_accel(ctx);
+}
+
+int spt_set_engine_one(spt_ctx *ctx, int engine)
+{
+    if (!ctx) return fail(nullptr, SPT_ERR_ARG, "null context");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    if (engine != SPT_ENGINE_MEGAKERNEL && engine != SPT_ENGINE_WAVEFRONT)
+        return fail(ctx, SPT_ERR_ARG, "unknown engine %d", engine);
+    ctx->engine = engine;
+    return SPT_OK;
+}
+
+int spt_set_workspace_one(spt_ctx *ctx, uint64_t bytes)
+{
+    if (!ctx) return fail(nullptr, SPT_ERR_ARG, "null context");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    if (bytes < sizeof(float4)) return fail(ctx, SPT_ERR_ARG, "workspace too small");
+    ctx->ws_bytes = bytes;
+    return SPT_OK;
 }
 
 }  // namespace
@@ -592,15 +839,64 @@ int spt_ctx_create(int device, spt_ctx **out)
     if (const char *e = std::getenv("SPT_TREE_B")) ctx->tree_branching = (uint32_t)std::max(0, std::atoi(e));
     if (const char *e = std::getenv("SPT_CLAIMS_PER_WAVE")) ctx->claims_per_wave = (uint32_t)std::max(1, std::atoi(e));
     if (const char *e = std::getenv("SPT_WF_CAP")) ctx->wf_cap = (uint32_t)std::max(1024, std::atoi(e));
+    if (const char *e = std::getenv("SPT_HOST_SLOTS"))
+        ctx->host_slots = (uint32_t)std::min<int>((int)kMaxHostSlots, std::max(1, std::atoi(e)));
     ctx->grid = (uint32_t)(per_cu * ctx->num_cu);
     ctx->grid_overlap = std::getenv("SPT_BLOCKS_PER_CU") || per_cu < 2 ? ctx->grid : (uint32_t)((per_cu - 1) * ctx->num_cu);
-    if (hipEventCreate(&ctx->ref_ev) != hipSuccess ||
-        hipMalloc((void **)&ctx->d_counters, 16 * sizeof(unsigned long long)) != hipSuccess ||
-        hipMemset(ctx->d_counters, 0, 16 * sizeof(unsigned long long)) != hipSuccess) {
+    if (hipEventCreate(&ctx->ref_ev) != hipSuccess || hipEventCreateWithFlags(&ctx->frame_ev, hipEventDisableTiming) != hipSuccess ||
+        hipMalloc((void **)&ctx->d_counters, kCounters * sizeof(unsigned long long)) != hipSuccess ||
+        hipMemset(ctx->d_counters, 0, kCounters * sizeof(unsigned long long)) != hipSuccess) {
         spt_ctx_destroy(ctx);
         return fail(nullptr, SPT_ERR_NOMEM, "workspace allocation failed");
     }
     *out = ctx;
+    return SPT_OK;
+}
+
+int spt_ctx_create_multi(const int *devices, uint32_t n, spt_ctx **out)
+{
+    if (!out) return fail(nullptr, SPT_ERR_ARG, "null out");
+    *out = nullptr;
+    if (!devices || n == 0) return fail(nullptr, SPT_ERR_ARG, "empty device list");
+    spt_ctx *ctx = nullptr;
+    int rc = spt_ctx_create(devices[0], &ctx);
+    if (rc) return rc;
+    for (uint32_t i = 1; i < n; ++i) {
+        spt_ctx *p = nullptr;
+        if ((rc = spt_ctx_create(devices[i], &p))) {
+            const std::string why = g_thread_error;
+            spt_ctx_destroy(ctx);
+            return fail(nullptr, rc, "member %u (device %d): %s", i, devices[i], why.c_str());
+        }
+        ctx->peers.push_back(p);
+        // member 0 pulls the members' strips over xGMI (hipMemcpyPeerAsync)
+        if (devices[i] != devices[0]) {
+            int can = 0;
+            if (hipDeviceCanAccessPeer(&can, devices[0], devices[i]) == hipSuccess && can) {
+                (void)hipSetDevice(devices[0]);
+                const hipError_t e = hipDeviceEnablePeerAccess(devices[i], 0);
+                if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) {
+                    spt_ctx_destroy(ctx);
+                    return fail(nullptr, SPT_ERR_HIP, "peer access %d -> %d: %s", devices[0], devices[i],
+                                hipGetErrorString(e));
+                }
+                (void)hipGetLastError();
+            }
+        }
+    }
+    *out = ctx;
+    return SPT_OK;
+}
+
+int spt_ctx_devices(spt_ctx *ctx, uint32_t *n, int *devices)
+{
+    if (!ctx || !n) return fail(ctx, SPT_ERR_ARG, "null argument");
+    const uint32_t cap = *n;
+    *n = 1u + (uint32_t)ctx->peers.size();
+    if (devices) {
+        if (cap >= 1) devices[0] = ctx->device;
+        for (uint32_t i = 1; i < *n && i < cap; ++i) devices[i] = ctx->peers[i - 1]->device;
+    }
     return SPT_OK;
 }
 
@@ -618,7 +914,7 @@ void spt_ctx_destroy(spt_ctx *ctx)
     for (void *p : ctx->pinned) (void)hipHostUnregister(p);
     if (ctx->ref_ev) (void)hipEventDestroy(ctx->ref_ev);
     void *bufs[] = {ctx->d_shade, ctx->d_mat, ctx->d_slots, ctx->d_orig, ctx->d_nodes,
-                    ctx->d_kpre, ctx->d_counters, ctx->d_stage, ctx->d_frame8};
+                    ctx->d_kpre, ctx->d_counters, ctx->d_frame8};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     for (Workspace &w : ctx->ws) {
@@ -630,7 +926,16 @@ void spt_ctx_destroy(spt_ctx *ctx)
             if (b) (void)hipFree(b);
         if (w.h_count) (void)hipHostFree(w.h_count);
     }
+    for (HostSlot *h : ctx->slots) {
+        if (h->d_stage) (void)hipFree(h->d_stage);
+        if (h->stream) (void)hipStreamDestroy(h->stream);
+        delete h;
+    }
+    for (void *b : {(void *)ctx->d_tile, (void *)ctx->d_fullframe})
+        if (b) (void)hipFree(b);
+    if (ctx->frame_ev) (void)hipEventDestroy(ctx->frame_ev);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    for (spt_ctx *p : ctx->peers) spt_ctx_destroy(p);
     delete ctx;
 }
 
@@ -643,85 +948,27 @@ const char *spt_last_error(const spt_ctx *ctx)
 int spt_set_scene(spt_ctx *ctx, const float *centers4, const float *radii, const float *colors4,
                   const uint8_t *materials, const float *fuzz, uint32_t n)
 {
-    if (!ctx) return fail(nullptr, SPT_ERR_ARG, "null context");
-    std::lock_guard<std::mutex> lk(ctx->mu);
-    if (n > 0 && (!centers4 || !radii || !colors4 || !materials || !fuzz))
-        return fail(ctx, SPT_ERR_ARG, "null scene array");
-    HIP_TRY(ctx, hipSetDevice(ctx->device));
-    std::vector<float4> shade(n);
-    std::vector<uint32_t> mat(n);
-    for (uint32_t i = 0; i < n; ++i) {
-        shade[i] = make_float4(colors4[4 * i], colors4[4 * i + 1], colors4[4 * i + 2], fuzz[i]);
-        mat[i] = materials[i];
-    }
-    ctx->h_shade = std::move(shade);
-    ctx->h_mat = std::move(mat);
-    ctx->h_centers.assign(centers4, centers4 + 4 * (size_t)n);
-    ctx->h_radii.assign(radii, radii + n);
-    ctx->n = n;
-    int rc = rebuild_accel(ctx);
-    if (rc) return rc;
-    ctx->scene_set = true;
-    return SPT_OK;
+    return for_members(ctx, [&](spt_ctx *c) { return spt_set_scene_one(c, centers4, radii, colors4, materials, fuzz, n); });
 }
 
 int spt_set_camera(spt_ctx *ctx, const float view[16], const float eye[4], const float sky[4])
 {
-    if (!ctx) return fail(nullptr, SPT_ERR_ARG, "null context");
-    std::lock_guard<std::mutex> lk(ctx->mu);
-    if (!view || !eye || !sky) return fail(ctx, SPT_ERR_ARG, "null camera array");
-    for (int j = 12; j < 16; ++j)
-        if (view[j] != 0.0f)
-            return fail(ctx, SPT_ERR_ARG, "viewMatrix row 3 must be zero (CreateCameraBasisMatrix, Math.hpp:204-208)");
-    for (int j = 0; j < 12; ++j) ctx->cam.view[j] = view[j];
-    for (int j = 0; j < 3; ++j) {
-        ctx->cam.eye[j] = eye[j];
-        ctx->cam.sky[j] = sky[j];
-    }
-    ctx->cam_set = true;
-    return SPT_OK;
+    return for_members(ctx, [&](spt_ctx *c) { return spt_set_camera_one(c, view, eye, sky); });
 }
 
 int spt_set_params(spt_ctx *ctx, uint32_t width, uint32_t height, uint32_t spp, uint32_t bounces, uint64_t seed)
 {
-    if (!ctx) return fail(nullptr, SPT_ERR_ARG, "null context");
-    std::lock_guard<std::mutex> lk(ctx->mu);
-    if (width == 0 || height == 0) return fail(ctx, SPT_ERR_ARG, "empty frame %ux%u", width, height);
-    if ((uint64_t)width * height * 3 > 0xFFFFFFFFull)
-        return fail(ctx, SPT_ERR_ARG, "frame %ux%u overflows the reference's uint32 g_size", width, height);
-    if (spp == 0) return fail(ctx, SPT_ERR_ARG, "spp must be >= 1 (1.f/0 samples)");
-    if (bounces == 0) return fail(ctx, SPT_ERR_ARG, "bounces must be >= 1 (--bounceCount never reaches 0)");
-    ctx->W = width;
-    ctx->H = height;
-    ctx->spp = spp;
-    ctx->bounces = bounces;
-    ctx->seed = seed;
-    ctx->params_set = true;
-    return SPT_OK;
+    return for_members(ctx, [&](spt_ctx *c) { return spt_set_params_one(c, width, height, spp, bounces, seed); });
 }
 
 int spt_set_cluster_size(spt_ctx *ctx, uint32_t k)
 {
-    if (!ctx) return fail(nullptr, SPT_ERR_ARG, "null context");
-    std::lock_guard<std::mutex> lk(ctx->mu);
-    if (k > spt::kClusterSlots && k != SPT_CLUSTER_AUTO)
-        return fail(ctx, SPT_ERR_ARG, "cluster size %u > %u", k, spt::kClusterSlots);
-    ctx->cluster_k = k;
-    if (!ctx->scene_set) return SPT_OK;
-    HIP_TRY(ctx, hipSetDevice(ctx->device));
-    return rebuild_accel(ctx);
+    return for_members(ctx, [&](spt_ctx *c) { return spt_set_cluster_size_one(c, k); });
 }
 
 int spt_set_cluster_tree(spt_ctx *ctx, uint32_t branching)
 {
-    if (!ctx) return fail(nullptr, SPT_ERR_ARG, "null context");
-    std::lock_guard<std::mutex> lk(ctx->mu);
-    if (branching == 1 || (branching > 64 && branching != SPT_TREE_AUTO))
-        return fail(ctx, SPT_ERR_ARG, "tree branching %u not in {0, 2..64, SPT_TREE_AUTO}", branching);
-    ctx->tree_branching = branching;
-    if (!ctx->scene_set) return SPT_OK;
-    HIP_TRY(ctx, hipSetDevice(ctx->device));
-    return rebuild_accel(ctx);
+    return for_members(ctx, [&](spt_ctx *c) { return spt_set_cluster_tree_one(c, branching); });
 }
 
 int spt_accel_check(const float *centers4, const float *radii, uint32_t n, uint32_t cluster_k, uint32_t branching,
@@ -741,21 +988,12 @@ int spt_accel_check(const float *centers4, const float *radii, uint32_t n, uint3
 
 int spt_set_engine(spt_ctx *ctx, int engine)
 {
-    if (!ctx) return fail(nullptr, SPT_ERR_ARG, "null context");
-    std::lock_guard<std::mutex> lk(ctx->mu);
-    if (engine != SPT_ENGINE_MEGAKERNEL && engine != SPT_ENGINE_WAVEFRONT)
-        return fail(ctx, SPT_ERR_ARG, "unknown engine %d", engine);
-    ctx->engine = engine;
-    return SPT_OK;
+    return for_members(ctx, [&](spt_ctx *c) { return spt_set_engine_one(c, engine); });
 }
 
 int spt_set_workspace(spt_ctx *ctx, uint64_t bytes)
 {
-    if (!ctx) return fail(nullptr, SPT_ERR_ARG, "null context");
-    std::lock_guard<std::mutex> lk(ctx->mu);
-    if (bytes < sizeof(float4)) return fail(ctx, SPT_ERR_ARG, "workspace too small");
-    ctx->ws_bytes = bytes;
-    return SPT_OK;
+    return for_members(ctx, [&](spt_ctx *c) { return spt_set_workspace_one(c, bytes); });
 }
 
 int spt_render_segment(spt_ctx *ctx, uint32_t yB, uint32_t yE, uint32_t xB, uint32_t xE, float *rgba, uint8_t *g_data)
@@ -800,6 +1038,85 @@ int spt_render_progressive(spt_ctx *ctx, int mode, uint32_t yB, uint32_t yE, uin
     if (mode != SPT_MODE_SEGMENT && mode != SPT_MODE_TASK) return fail(ctx, SPT_ERR_ARG, "bad mode %d", mode);
     if (pass_spp == 0) return fail(ctx, SPT_ERR_ARG, "pass_spp must be >= 1");
     return render_segment_host(ctx, mode, yB, yE, xB, xE, rgba, g_data, pass_spp, cb, user);
+}
+
+int spt_render_frame(spt_ctx *ctx, int mode, float *rgba_out, uint8_t *g_data)
+{
+    if (!ctx) return fail(nullptr, SPT_ERR_ARG, "null context");
+    if (mode != SPT_MODE_SEGMENT && mode != SPT_MODE_TASK) return fail(ctx, SPT_ERR_ARG, "bad mode %d", mode);
+    {
+        std::unique_lock<std::mutex> lk(ctx->mu);
+        int rc = check_ready(ctx);
+        if (rc) return rc;
+        const uint32_t W = ctx->W, H = ctx->H;
+        // RenderImage's RenderSegmentTask({0, H, 0, W}) on a non-square frame aliases
+        // pixels across rows (colorIndex, TaskBasedPathTracer.hpp:103,186), which a
+        // row-strip split cannot resolve locally: that frame renders on member 0 alone
+        if (ctx->peers.empty() || (mode == SPT_MODE_TASK && W != H)) {
+            lk.unlock();
+            return render_segment_host(ctx, mode, 0, H, 0, W, rgba_out, g_data, 0, nullptr, nullptr, false);
+        }
+    }
+    // every member renders its interleaved row strips into a compact tile; member 0
+    // pulls the tiles over xGMI (peer copies ordered after each member's render by an
+    // event), scatters them into the frame (assemble_kernel) and copies the frame back
+    std::vector<spt_ctx *> m{ctx};
+    m.insert(m.end(), ctx->peers.begin(), ctx->peers.end());
+    const uint32_t parts = (uint32_t)m.size();
+    std::vector<std::unique_lock<std::mutex>> locks;
+    for (spt_ctx *c : m) {
+        locks.emplace_back(c->mu);
+        int rc = check_ready(c);
+        if (rc) return c == ctx ? rc : fail(ctx, rc, "member device %d: %s", c->device, c->err.c_str());
+        if (c->W != ctx->W || c->H != ctx->H) return fail(ctx, SPT_ERR_STATE, "members disagree on the frame size");
+    }
+    const uint32_t W = ctx->W, H = ctx->H;
+    const uint32_t strip = even_strip(H, parts);
+    uint32_t max_rows = 0;
+    for (uint32_t r = 0; r < parts; ++r) max_rows = std::max(max_rows, spt::rows_owned(spt::RowMap{0, H, strip, parts, r, 0, W}));
+    const size_t tile = (size_t)max_rows * W;
+    int rc = ensure(ctx, &ctx->d_tile, &ctx->tile_cap, tile * parts);  // member 0: the gathered stack
+    if (rc) return rc;
+    for (uint32_t r = 0; r < parts; ++r) {
+        spt_ctx *c = m[r];
+        HIP_TRY(ctx, hipSetDevice(c->device));
+        if (r > 0 && (rc = ensure(c, &c->d_tile, &c->tile_cap, tile)))
+            return fail(ctx, rc, "member device %d: %s", c->device, c->err.c_str());
+        spt::RowMap map{0, H, strip, parts, r, 0, W};
+        float4 *dst = r == 0 ? ctx->d_tile : c->d_tile;
+        if ((rc = render_impl(c, mode, map, dst, nullptr, c->stream, false)))
+            return r == 0 ? rc : fail(ctx, rc, "member device %d: %s", c->device, c->err.c_str());
+        if (r > 0) HIP_TRY(ctx, hipEventRecord(c->frame_ev, c->stream));
+    }
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    for (uint32_t r = 1; r < parts; ++r) {
+        spt_ctx *c = m[r];
+        const size_t rows_r = spt::rows_owned(spt::RowMap{0, H, strip, parts, r, 0, W});
+        HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, c->frame_ev, 0));
+        HIP_TRY(ctx, hipMemcpyPeerAsync(ctx->d_tile + r * tile, ctx->device, c->d_tile, c->device,
+                                        rows_r * W * sizeof(float4), ctx->stream));
+    }
+    float4 *dframe = nullptr;
+    if (rgba_out) {
+        if ((rc = ensure(ctx, &ctx->d_fullframe, &ctx->fullframe_cap, (size_t)W * H))) return rc;
+        dframe = ctx->d_fullframe;
+    }
+    uint8_t *d8 = nullptr;
+    if (g_data) {
+        if ((rc = ensure(ctx, &ctx->d_frame8, &ctx->frame8_cap, (size_t)W * H * 3))) return rc;
+        d8 = ctx->d_frame8;
+    }
+    HIP_TRY(ctx, spt::launch_assemble(ctx->d_tile, max_rows, spt::RowMap{0, H, strip, parts, 0u, 0, W}, W, H, dframe,
+                                      d8, ctx->stream));
+    if (rgba_out)
+        HIP_TRY(ctx, hipMemcpyAsync(rgba_out, dframe, (size_t)W * H * sizeof(float4), hipMemcpyDeviceToHost, ctx->stream));
+    if (g_data) HIP_TRY(ctx, hipMemcpyAsync(g_data, d8, (size_t)W * H * 3, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    for (spt_ctx *c : m) {
+        HIP_TRY(ctx, hipSetDevice(c->device));
+        if ((rc = collect_timings(c, false))) return rc;
+    }
+    return SPT_OK;
 }
 
 int spt_rows_count(uint32_t yB, uint32_t yE, uint32_t strip, uint32_t parts, uint32_t part, uint32_t *rows)
@@ -851,6 +1168,12 @@ int spt_assemble_rows_async(spt_ctx *ctx, const void *d_tiles, uint32_t max_rows
 int spt_synchronize(spt_ctx *ctx)
 {
     if (!ctx) return fail(nullptr, SPT_ERR_ARG, "null context");
+    for (spt_ctx *c : ctx->peers) {
+        std::lock_guard<std::mutex> lk(c->mu);
+        HIP_TRY(ctx, hipSetDevice(c->device));
+        HIP_TRY(ctx, hipDeviceSynchronize());
+        if (collect_timings(c)) return fail(ctx, SPT_ERR_HIP, "member device %d: %s", c->device, c->err.c_str());
+    }
     std::lock_guard<std::mutex> lk(ctx->mu);
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     HIP_TRY(ctx, hipDeviceSynchronize());
@@ -880,24 +1203,27 @@ int spt_render_samples(spt_ctx *ctx, int mode, uint32_t yB, uint32_t yE, uint32_
         for (size_t s = 0; s < ctx->spp; ++s) {
             float *o = out + 4 * (p * ctx->spp + s);
             std::memcpy(o, &buf[(s * npix + p) * sf], sf * sizeof(float));
-            if (sf == 3) o[3] = 1.0f;  // segment mode: every sample counts
+            // segment mode: every sample counts; task mode: w holds the path's order key, 0 = dropped
+            uint32_t key;
+            std::memcpy(&key, &o[3], 4);
+            if (sf == 3 || key != 0) o[3] = 1.0f;
         }
     return collect_timings(ctx);
 }
 
-int spt_get_stats(spt_ctx *ctx, spt_stats *out)
+namespace {
+int stats_one(spt_ctx *ctx, spt_stats *out)
 {
-    if (!ctx || !out) return fail(ctx, SPT_ERR_ARG, "null argument");
     std::lock_guard<std::mutex> lk(ctx->mu);
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     int rc = collect_timings(ctx);
     if (rc) return rc;
-    unsigned long long c[16] = {0};
+    unsigned long long c[kCounters] = {0};
     HIP_TRY(ctx, hipMemcpy(c, ctx->d_counters, sizeof c, hipMemcpyDeviceToHost));
     out->casts = c[0];
     out->samples = c[1];
     out->dropped = c[2];
-    for (int i = 0; i < 12; ++i) out->diag[i] = c[4 + i];
+    for (int i = 0; i < 14; ++i) out->diag[i] = c[4 + i];
     out->launches = ctx->launches;
     out->render_ms = ctx->render_ms;
     out->fold_ms = ctx->fold_ms;
@@ -908,19 +1234,49 @@ int spt_get_stats(spt_ctx *ctx, spt_stats *out)
     return SPT_OK;
 }
 
-int spt_reset_stats(spt_ctx *ctx)
+int reset_one(spt_ctx *ctx)
 {
-    if (!ctx) return fail(nullptr, SPT_ERR_ARG, "null context");
     std::lock_guard<std::mutex> lk(ctx->mu);
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     int rc = collect_timings(ctx);
     if (rc) return rc;
-    HIP_TRY(ctx, hipMemset(ctx->d_counters, 0, 16 * sizeof(unsigned long long)));
+    HIP_TRY(ctx, hipMemset(ctx->d_counters, 0, kCounters * sizeof(unsigned long long)));
     ctx->render_ms = ctx->fold_ms = ctx->last_render_ms = 0;
     ctx->launches = 0;
     ctx->spans.clear();
     ctx->ref_recorded = false;
     return SPT_OK;
+}
+}  // namespace
+
+int spt_get_stats(spt_ctx *ctx, spt_stats *out)
+{
+    if (!ctx || !out) return fail(ctx, SPT_ERR_ARG, "null argument");
+    int rc = stats_one(ctx, out);
+    // a multi-device context sums the members' counters and device times; busy time is
+    // the longest member's (the devices run concurrently)
+    for (spt_ctx *p : ctx->peers) {
+        spt_stats q{};
+        if ((rc = stats_one(p, &q))) return fail(ctx, rc, "member device %d: %s", p->device, p->err.c_str());
+        out->casts += q.casts;
+        out->samples += q.samples;
+        out->dropped += q.dropped;
+        for (int i = 0; i < 14; ++i) out->diag[i] += q.diag[i];
+        out->launches += q.launches;
+        out->render_ms += q.render_ms;
+        out->fold_ms += q.fold_ms;
+        out->render_busy_ms = std::max(out->render_busy_ms, q.render_busy_ms);
+    }
+    return rc;
+}
+
+int spt_reset_stats(spt_ctx *ctx)
+{
+    if (!ctx) return fail(nullptr, SPT_ERR_ARG, "null context");
+    int rc = reset_one(ctx);
+    for (spt_ctx *p : ctx->peers)
+        if (!rc && (rc = reset_one(p))) return fail(ctx, rc, "member device %d: %s", p->device, p->err.c_str());
+    return rc;
 }
 
 int spt_selftest_numerics(spt_ctx *ctx, const float *a, const float *b, const uint32_t *bits, uint32_t n, float *out)

@@ -214,6 +214,8 @@ struct FoldArgs {
     uint32_t s_done;     // samples folded after this batch (s0 + spp_batch)
     int first, last, mode;
     int preview;         // write the outputs after every batch (progressive rendering)
+    int alias;           // task mode, one non-square rectangle: RenderSegmentTask's colorIndex
+                         // (dx + dy * segmentHeight, TaskBasedPathTracer.hpp:103,186) aliases pixels
 };
 
 hipError_t launch_render(const RenderArgs &a, uint32_t grid, uint32_t block, hipStream_t s);

@@ -188,6 +188,8 @@ __device__ __forceinline__ void render_body(const RenderArgs &a)
         atomicAdd(&a.counters[13], dg.branches);
         atomicAdd(&a.counters[14], dg.passing);
         atomicAdd(&a.counters[15], dg.improving);
+        atomicAdd(&a.counters[16], dg.lane_tests);
+        atomicAdd(&a.counters[17], dg.lane_pretests);
     }
 #endif
     (void)d_iters;
@@ -228,15 +230,47 @@ __global__ __launch_bounds__(256) void fold_kernel(FoldArgs a)
             acc.z = acc.z + c[2];
             acc.w = acc.w + 1.f;
         }
-    } else {
+    } else if (!a.alias) {
+        // RenderSegmentTask on a square tile: pixel p is colors[p]; w = 0 marks a dropped path
         const float4 *s = (const float4 *)a.samples + p;
         for (uint32_t k = 0; k < a.spp_batch; ++k) {
             const float4 c = s[(size_t)k * a.npix];
-            if (c.w != 0.f) {
+            if (__float_as_uint(c.w) != 0u) {
                 acc.x = acc.x + c.x;
                 acc.y = acc.y + c.y;
                 acc.z = acc.z + c.z;
                 acc.w = acc.w + 1.f;
+            }
+        }
+    } else {
+        // Non-square tile: colors[p] collects every pixel (dx, dy) of the tile with
+        // dx + dy * H == p (TaskBasedPathTracer.hpp:103,186; H = segmentHeight), and the
+        // resolve (196-205) writes colors[p] to pixel (p % W, p / W).  Within a sample
+        // the sources reach colors[p] in the order of their (key, pixel) (finish_step),
+        // so each sample's sources are added in that order.  No source: 0 samples, and
+        // 0 * (1.f / 0) is NaN, as in the reference.
+        const uint32_t W = a.map.width, H = a.npix / W;
+        const uint32_t dy_lo = p >= W ? (p - W + H) / H : 0u;
+        const uint32_t dy_hi = min(H - 1u, p / H);
+        const float4 *s = (const float4 *)a.samples;
+        for (uint32_t k = 0; k < a.spp_batch; ++k) {
+            const float4 *sk = s + (size_t)k * a.npix;
+            uint64_t prev = 0;  // (key << 32 | pixel) of the last source added
+            for (uint32_t t = dy_lo; t <= dy_hi; ++t) {
+                uint64_t best = ~0ull;
+                for (uint32_t dy = dy_lo; dy <= dy_hi; ++dy) {
+                    const uint32_t src = dy * W + (p - dy * H);
+                    const uint32_t key = __float_as_uint(sk[src].w);
+                    const uint64_t kp = ((uint64_t)key << 32) | src;
+                    if (key != 0u && kp > prev && kp < best) best = kp;
+                }
+                if (best == ~0ull) break;
+                const float4 c = sk[(uint32_t)best];
+                acc.x = acc.x + c.x;
+                acc.y = acc.y + c.y;
+                acc.z = acc.z + c.z;
+                acc.w = acc.w + 1.f;
+                prev = best;
             }
         }
     }

@@ -92,6 +92,10 @@ struct Hit {
 struct CastDiag {
     unsigned long long nodes = 0, leaves = 0, pairs = 0, live = 0;
     unsigned long long spheres = 0, branches = 0, passing = 0, improving = 0;
+    // lane-level work: RaySphereIntersection evaluations (17 FLOP each) and
+    // member pretests (10 VALU each) for the wave's live lanes
+    unsigned long long lane_tests = 0, lane_pretests = 0;
+    uint32_t live_now = 0;  // live lanes of the current cast
 };
 
 // The closest-contact / distance update of one member (Collision.hpp:19-27,49-56,
@@ -161,6 +165,7 @@ __device__ __forceinline__ void test_group(const float4 (&sp)[G], const uint32_t
     bool pass[G];
 #pragma unroll
     for (int k = 0; k < G; ++k) pass[k] = ray_sphere(sp[k], o, d, tcv[k], hv[k]);
+    if (SPT_DIAG) dg.lane_tests += (unsigned long long)G * dg.live_now;
 #pragma unroll
     for (int k = 0; k < G; ++k) {
         if (SPT_DIAG) {
@@ -209,6 +214,7 @@ __device__ __forceinline__ void test_group_pre(const float4 (&sp)[G], const floa
         any |= pm[k];
     }
     __builtin_amdgcn_sched_barrier(0);
+    if (SPT_DIAG) dg.lane_pretests += (unsigned long long)G * dg.live_now;
     if (any == 0ull) {
         if (SPT_DIAG) dg.spheres += G;
         return;
@@ -223,6 +229,7 @@ __device__ __forceinline__ void test_group_pre(const float4 (&sp)[G], const floa
         if (pm[k] != 0ull) {
             float tc, hh;
             const bool pass = ray_sphere(sp[k], o, d, tc, hh);
+            if (SPT_DIAG) dg.lane_tests += dg.live_now;
             if (__ballot(pass) != 0ull) update_member(pass, tc, hh, orig, slot + k, o, d, dod, h, dg);
         }
     }
@@ -289,6 +296,7 @@ __device__ __forceinline__ Hit find_closest(const AccelView &ac, const f3 &o, co
     const float qo = (float)(kFlatScale - 4.1e-6) * oo;
     const float m2c = (float)(-2.0 * kFlatScale);
     const float osx = m2c * o.x, osy = m2c * o.y, osz = m2c * o.z;
+    if (SPT_DIAG) dg.live_now = (uint32_t)__popcll(__ballot(active));
     // always-tested spheres (ground, large balls; every sphere when culling is off)
     {
         for (uint32_t g = 0; g < ac.always_groups; ++g) {
@@ -564,18 +572,33 @@ __device__ __forceinline__ void refract_event(const RenderArgs &a, Path &ps, uin
 
 // The tail of a shading step: the specular-event cap (RenderSegmentTask's pass limit,
 // the safety cap) and, for finishing paths, the sample slot write.
-__device__ __forceinline__ void finish_step(const RenderArgs &a, Path &ps, bool fin, bool spec_event, float counted,
-                                            f3 col, unsigned long long &done, unsigned long long &dropped)
+//
+// ps.spec: bits 0-15 count the path's specular events (= the RenderSegmentTask pass
+// it is in); in task mode bits 16-25 record which queue each of its first ten
+// events came from (bit 16 + k: 1 = refractive queue of pass k, 0 = reflective).
+// A task-mode slot's w is the path's position key inside its sample
+// (TaskBasedPathTracer.hpp:81-193): 1 + (pass << 11 | sky << 10 | queue bits), 0 for
+// a dropped path.  Within one sample RenderSegmentTask adds colours pass by pass,
+// the diffuse queue before the skybox queue, and a queue holds the tasks pushed by
+// the previous pass's reflective loop before those of its refractive loop, each in
+// its own queue order; so two paths of a sample reach `colors` in the order of
+// (key, pixel) -- which only matters where colorIndex aliases pixels (non-square
+// tiles, lines 103 and 186; fold_kernel).
+__device__ __forceinline__ void finish_step(const RenderArgs &a, Path &ps, bool fin, bool spec_event, bool refr_event,
+                                            bool sky, f3 col, unsigned long long &done, unsigned long long &dropped)
 {
+    bool counted = true;
     if (spec_event) {
+        const uint32_t k = ps.spec & 0xFFFFu;
+        if (a.mode == 1u && k < kTaskPasses && refr_event) ps.spec |= 1u << (16u + k);
         ++ps.spec;
-        if (a.mode == 1u && ps.spec >= kTaskPasses) {
+        if (a.mode == 1u && k + 1u >= kTaskPasses) {
             // RenderSegmentTask: this path would be processed in pass 10, which never runs
             fin = true;
-            counted = 0.f;
+            counted = false;
             col = mk(0.f, 0.f, 0.f);
             ++dropped;
-        } else if (ps.spec > kSpecularCap) {
+        } else if (k + 1u > kSpecularCap) {
             fin = true;
             col = mk(0.f, 0.f, 0.f);
         }
@@ -588,7 +611,9 @@ __device__ __forceinline__ void finish_step(const RenderArgs &a, Path &ps, bool 
             o3[1] = col.y;
             o3[2] = col.z;
         } else {
-            *(float4 *)(a.samples + (size_t)4 * ps.item) = make_float4(col.x, col.y, col.z, counted);
+            const uint32_t key =
+                counted ? 1u + (((ps.spec & 0xFFFFu) << 11) | (sky ? 1u << 10 : 0u) | ((ps.spec >> 16) & 0x3FFu)) : 0u;
+            *(float4 *)(a.samples + (size_t)4 * ps.item) = make_float4(col.x, col.y, col.z, __uint_as_float(key));
         }
         ps.phase = PH_IDLE;
         ps.d = mk(0.f, 0.f, 0.f);
@@ -610,7 +635,6 @@ __device__ __forceinline__ void shade_step(const RenderArgs &a, Path &ps, const 
     const uint32_t *__restrict__ mat = a.scene.mat;
     const uint32_t idx = h.idx;
     bool fin = false;
-    float counted = 1.f;
     f3 col = mk(0.f, 0.f, 0.f);
     const bool dl = ps.phase == PH_DLOOP;
     uint32_t m = SPT_SKYBOX_ID;
@@ -669,7 +693,7 @@ __device__ __forceinline__ void shade_step(const RenderArgs &a, Path &ps, const 
         refract_event(a, ps, idx);
         spec_event = true;
     }
-    finish_step(a, ps, fin, spec_event, counted, col, done, dropped);
+    finish_step(a, ps, fin, spec_event, refr, !dl, col, done, dropped);
 }
 
 

@@ -43,12 +43,20 @@ class RenderSegmentData:
 class Context:
     """One device context (spt_ctx) holding scene, camera and config."""
 
-    def __init__(self, device: int = 0):
+    def __init__(self, device: int = 0, devices=None):
+        """One device, or with `devices` (a list of ordinals, repeats allowed) a
+        multi-device context (spt_ctx_create_multi) whose member 0 is devices[0]."""
         L = _native.lib()
         h = ctypes.c_void_p()
-        _native.check(L.spt_ctx_create(device, ctypes.byref(h)))
+        if devices is None:
+            _native.check(L.spt_ctx_create(device, ctypes.byref(h)))
+            self.devices = [device]
+        else:
+            devs = np.ascontiguousarray(np.asarray(devices, np.int32))
+            _native.check(L.spt_ctx_create_multi(_p(devs), len(devs), ctypes.byref(h)))
+            self.devices = [int(d) for d in devs]
         self._h = h
-        self.device = device
+        self.device = self.devices[0]
 
     @property
     def handle(self):
@@ -81,6 +89,7 @@ class Context:
 
     def set_params(self, width: int, height: int, spp: int, bounces: int, seed: int = 1) -> None:
         self._check(_native.lib().spt_set_params(self._h, width, height, spp, bounces, seed))
+        self._frame = (width, height)
 
     def set_cluster_size(self, k: int) -> None:
         """Culling cluster size (0 = brute force over every sphere); results identical."""
@@ -108,6 +117,21 @@ class Context:
             gp = _p(g_data)
         self._check(fn(self._h, yB, yE, xB, xE, _p(rgba), gp))
         return rgba
+
+    def render_frame(self, g_data=None, task=False, rgba=True):
+        """The whole frame over every member device (spt_render_frame): returns the
+        row-major float4 frame (or None with rgba=False); writes g_data if given."""
+        L = _native.lib()
+        n = ctypes.c_uint32(0)
+        self._check(L.spt_ctx_devices(self._h, ctypes.byref(n), None))
+        w, h = self._frame
+        out = np.zeros((w * h, 4), np.float32) if rgba else None
+        gp = None
+        if g_data is not None:
+            assert g_data.dtype == np.uint8 and g_data.flags.c_contiguous and g_data.size == w * h * 3
+            gp = _p(g_data)
+        self._check(L.spt_render_frame(self._h, 1 if task else 0, _p(out) if rgba else None, gp))
+        return out
 
     def pin_host(self, arr: np.ndarray) -> None:
         """Page-lock a host array (e.g. g_data) for direct device-to-host copies."""
@@ -198,7 +222,8 @@ class Globals:
     """
 
     def __init__(self, scene: Scene, width=1440, height=1440, samples=100, bounces=10, seed=1, eye=DEFAULT_EYE,
-                 look_at=DEFAULT_LOOK_AT, up=DEFAULT_UP, init_color=INIT_COLOR, device=0, context=None):
+                 look_at=DEFAULT_LOOK_AT, up=DEFAULT_UP, init_color=INIT_COLOR, device=0, context=None,
+                 devices=None):
         self.g_width, self.g_height, self.g_samples, self.g_bounces = width, height, samples, bounces
         self.g_stride = 3
         self.g_size = width * height * 3
@@ -207,7 +232,7 @@ class Globals:
         self.viewMatrix = camera_basis(eye, look_at, up)
         self.scene = scene
         self.seed = seed
-        self.ctx = context or Context(device)
+        self.ctx = context or Context(device, devices=devices)
         self._lock = threading.Lock()
         self.sync()
 
@@ -236,8 +261,8 @@ def RenderSegment(segment: RenderSegmentData, g: Globals) -> np.ndarray:
 
 def RenderSegmentTask(segment: RenderSegmentData, g: Globals) -> np.ndarray:
     """TaskBasedPathTracer.hpp:54-206 semantics (10-pass cap, count-weighted
-    resolve).  Exact for square tiles; for non-square tiles the reference's
-    colorIndex stride (lines 103, 186) aliases pixels, which is not reproduced."""
+    resolve), including the colorIndex stride of non-square tiles (lines 103, 186:
+    rows strided by segmentHeight, so pixels alias and some indices stay empty)."""
     return g.ctx.render_segment(segment.yBegin, segment.yEnd, segment.xBegin, segment.xEnd, g.g_data, task=True)
 
 

@@ -12,7 +12,7 @@ def test_library_exports_every_declared_symbol(native):
     L = native.lib()
     missing = [n for n in names if not hasattr(L, n)]
     assert not missing, missing
-    assert L.spt_abi_version() == 2
+    assert L.spt_abi_version() == native.ABI_VERSION == 3
 
 
 def test_ctx_create_reports_no_device_without_gpu(native):
@@ -65,9 +65,9 @@ def _build_shim_harness(tmp_path):
     import subprocess
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     lib = os.path.join(root, "simplepathtracer_amd", "lib")
-    exe = str(tmp_path / "shim_harness")
-    subprocess.run(["g++", "-std=c++17", "-O2", "-Wall", "-Werror", f"-I{root}/include",
-                    os.path.join(root, "tests", "cpp", "shim_harness.cpp"), f"-L{lib}", "-lspt_hip",
+    exe = str(tmp_path / "dropin_harness")
+    subprocess.run(["g++", "-std=c++17", "-O2", "-Wall", "-Werror", "-pthread", f"-I{root}/include",
+                    os.path.join(root, "tools", "dropin_harness.cpp"), f"-L{lib}", "-lspt_hip",
                     f"-Wl,-rpath,{lib}", "-o", exe], check=True)
     return exe
 

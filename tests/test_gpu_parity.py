@@ -220,6 +220,48 @@ def test_task_mode_drops_deep_specular_paths(spt, ctx, oracle):
     assert_bitwise(got_seg[:, :3], want_seg[:, :3], "segment mode, deep specular chains")
 
 
+def _mirror_glass_lattice():
+    """The mirror lattice with every other sphere glass: paths of one sample finish
+    in different RenderSegmentTask passes and queues (TaskBasedPathTracer.hpp:81-193)."""
+    c, r, col, m, fz = _mirror_lattice()
+    m = m.copy()
+    m[2::2] = 2
+    return c, r, col, m, fz
+
+
+def same_bits_or_nan(got, want, what):
+    got, want = np.asarray(got, np.float32), np.asarray(want, np.float32)
+    nan = np.isnan(got) & np.isnan(want)
+    bad = (bits(got) != bits(want)) & ~nan
+    assert not bad.any(), f"{what}: {int(bad.sum())} lanes differ, first got {got[bad][:3]} want {want[bad][:3]}"
+
+
+@pytest.mark.parametrize("scene_name,y0,x0,w,h", [("random", 200, 300, 300, 200), ("random", 300, 500, 40, 90),
+                                                   ("lattice", 0, 0, 96, 20), ("lattice", 8, 4, 30, 50)])
+def test_task_mode_non_square_tiles_alias_like_the_reference(spt, ctx, oracle, golden_scenes, scene_name, y0, x0, w, h):
+    """RenderSegmentTask on a non-square tile strides colorIndex rows by segmentHeight
+    (TaskBasedPathTracer.hpp:103,186): pixel (p % W, p / W) gets colors[p], the sum of
+    every tile pixel (dx, dy) with dx + dy * H == p, added within each sample in the
+    reference's breadth-first order (pass, diffuse before skybox, queue order);
+    indices no pixel maps to resolve to 0 * (1/0) = NaN.  Config 2's own tiling
+    (1200x800, tc = 4) is 300x200; 96x20 has five sources per index."""
+    if scene_name == "random":
+        arrays = [golden_scenes[f"random_{k}"] for k in ("centers", "radii", "colors", "materials", "fuzz")]
+        view, fw, fh, spp, b, seed = golden_scenes["view"], 1200, 800, 3, 50, 4
+    else:
+        arrays = list(_mirror_glass_lattice())
+        view, fw, fh, spp, b, seed = spt.camera_basis(EYE, LOOK, UP), 128, 64, 12, 8, 9
+    setup(ctx, spt.Scene(*arrays), fw, fh, spp, b, seed=seed, view=view)
+    g = np.full(fw * fh * 3, 0xAB, np.uint8)
+    gw = g.copy()
+    got = ctx.render_segment(y0, y0 + h, x0, x0 + w, g, task=True)
+    fr = oracle.make_frame(view, EYE, SKY, fw, fh, spp, b, seed)
+    want, _ = oracle.render_segment(oracle.OracleScene(*arrays), fr, y0, y0 + h, x0, x0 + w, task=True, rgb8=gw)
+    same_bits_or_nan(got[:, :3], want[:, :3], f"task mode, {w}x{h} tile")
+    assert np.isnan(want[:, 0]).any() == (w != h)
+    assert np.array_equal(g, gw), "g_data bytes"
+
+
 # ---------------------------------------------------------------- edge cases
 
 def test_empty_region_is_a_noop(spt, ctx, golden_scenes):
@@ -361,16 +403,22 @@ def test_concurrent_render_jobs_share_a_context(spt, golden_scenes):
     g.ctx.close()
 
 
-@pytest.mark.parametrize("w,h,tc,task", [(1200, 800, 4, 0), (800, 800, 4, 1)])
-def test_cpp_dropin_shim_renders_like_the_context(spt, golden_scenes, tmp_path, w, h, tc, task):
+@pytest.mark.parametrize("w,h,tc,task,devices", [(1200, 800, 4, 0, None), (1200, 800, 4, 1, None),
+                                                  (1200, 800, 8, 0, "0,0")])
+def test_cpp_dropin_shim_renders_like_the_context(spt, golden_scenes, tmp_path, w, h, tc, task, devices):
     """The C++ RenderSegment/RenderSegmentTask shim, driven by RenderJob-style
-    concurrent threads over a tc x tc tile grid, writes the same g_data bytes as
-    a one-shot render through the context."""
+    concurrent threads over a tc x tc tile grid (config 2's 300x200 tiles at tc = 4,
+    non-square: task mode aliases), writes the same g_data bytes as tile renders
+    through the context; SPT_DEVICES spreads the tiles over a multi-device context."""
+    import os
     import subprocess
     from test_abi import _build_shim_harness
     exe = _build_shim_harness(tmp_path)
     out = tmp_path / "g_data.bin"
-    subprocess.run([exe, str(out), str(w), str(h), "6", "50", str(tc), str(task)], check=True, timeout=300)
+    env = dict(os.environ)
+    if devices:
+        env["SPT_DEVICES"] = devices
+    subprocess.run([exe, str(out), str(w), str(h), "6", "50", str(tc), str(task)], check=True, timeout=300, env=env)
     got = np.fromfile(out, np.uint8)
     c = spt.Context(0)
     setup(c, scene_from(spt, golden_scenes, "random"), w, h, 6, 50)
@@ -577,3 +625,89 @@ def test_config3_full_frame_batches_vs_oracle(spt, ctx, oracle, golden_scenes):
         assert_bitwise(a[y * 3840 + x, :3], want[0, :3], f"pixel {(x, y)}")
         i = 3 * ((2160 - 1 - y) * 3840 + x)
         assert np.array_equal(g[i:i + 3], gw[i:i + 3])
+
+
+# ---------------------------------------------------------------- multi-device context
+
+@pytest.mark.parametrize("devices,task", [([0, 0], False), ([0, 0, 0], False), ([0, 0], True)])
+def test_multi_device_frame_equals_one_device(spt, golden_scenes, devices, task):
+    """spt_render_frame over a device list (one process driving
+    several GPUs; here device 0 listed several times): interleaved strips per member,
+    peer-copy gather to member 0, assemble -- bit-identical to a one-device frame."""
+    W, H, spp = 360, 200, 6
+    one = spt.Context(0)
+    setup(one, scene_from(spt, golden_scenes, "random"), W, H, spp, 50)
+    g1 = np.zeros(W * H * 3, np.uint8)
+    want = one.render_frame(g1, task=task)
+    ref = one.render_segment(0, H, 0, W, task=task)
+    one.close()
+    same_bits_or_nan(want, ref, "one-device render_frame vs render_segment")
+    multi = spt.Context(devices=devices)
+    setup(multi, scene_from(spt, golden_scenes, "random"), W, H, spp, 50)
+    multi.reset_stats()
+    gm = np.zeros_like(g1)
+    got = multi.render_frame(gm, task=task)
+    st = multi.stats()
+    multi.close()
+    same_bits_or_nan(got[:, :3], want[:, :3], f"{len(devices)} members")
+    assert np.array_equal(gm, g1)
+    # task mode on a non-square frame aliases across rows: member 0 renders it alone
+    assert st["samples"] == W * H * spp and st["launches"] == (1 if task else len(devices))
+
+
+def test_multi_device_context_serves_render_jobs(spt, golden_scenes):
+    """RenderImageParallelMain's concurrent RenderJob tiles (Renderer.hpp:257-302) on a
+    two-member context: tiles go to the least busy member, same g_data bytes."""
+    g = spt.Globals(scene_from(spt, golden_scenes, "random"), width=240, height=160, samples=6, bounces=50)
+    spt.RenderSegment(spt.RenderSegmentData(0, 160, 0, 240), g)
+    want = g.g_data.copy()
+    g.ctx.close()
+    g2 = spt.Globals(scene_from(spt, golden_scenes, "random"), width=240, height=160, samples=6, bounces=50,
+                     devices=[0, 0])
+    spt.RenderImageParallelMain(g2, thread_count=8)
+    assert np.array_equal(g2.g_data, want)
+    g2.ctx.close()
+
+
+def test_progress_callback_may_call_into_the_context(spt, ctx, golden_scenes):
+    """The progress callback runs with the context unlocked (no self-deadlock): stats()
+    works from it, while a setter of the same context is refused (SPT_ERR_STATE)."""
+    setup(ctx, scene_from(spt, golden_scenes, "random"), 64, 48, 8, 50)
+    seen, errs = [], []
+
+    def cb(done):
+        seen.append(ctx.stats()["samples"])
+        try:
+            ctx.set_params(64, 48, 8, 50, 2)
+        except spt.SptError as e:
+            errs.append(e.code)
+
+    ctx.reset_stats()
+    ctx.render_progressive(0, 48, 0, 64, 4, None, cb)
+    assert seen == [64 * 48 * 4, 64 * 48 * 8]
+    assert errs == [2, 2]
+
+
+def test_concurrent_tiles_overlap_and_match(spt, ctx, golden_scenes):
+    """16 RenderJob-style threads on one context: each call gets its own stream and
+    workspace (at most 8 in flight); bytes equal the serial render."""
+    setup(ctx, scene_from(spt, golden_scenes, "random"), 320, 160, 4, 50)
+    want = np.zeros(320 * 160 * 3, np.uint8)
+    ctx.render_segment(0, 160, 0, 320, want)
+    got = np.zeros_like(want)
+    tiles = [(y, y + 40, x, x + 80) for y in range(0, 160, 40) for x in range(0, 320, 80)]
+    errors = []
+
+    def job(t):
+        try:
+            ctx.render_segment(*t, got)
+        except Exception as e:  # pragma: no cover
+            errors.append(e)
+
+    th = [threading.Thread(target=job, args=(t,)) for t in tiles]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errors
+    assert np.array_equal(got, want)

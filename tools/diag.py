@@ -6,10 +6,17 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import simplepathtracer_amd as spt  # noqa: E402
 
-cfg = sys.argv[1] if len(sys.argv) > 1 else "c2"
-W, H, spp, b = {"c2": (1200, 800, 100, 50), "c2s": (1200, 800, 8, 50), "c5s": (1920, 1080, 4, 50)}[cfg]
-if len(sys.argv) > 2:  # bounces override (1: casts are almost all primary rays)
-    b = int(sys.argv[2])
+args = [a for a in sys.argv[1:]]
+json_out = None
+if "--json" in args:
+    k = args.index("--json")
+    json_out = args[k + 1]
+    del args[k:k + 2]
+cfg = args[0] if args else "c2"
+W, H, spp, b = {"c2": (1200, 800, 100, 50), "c2s": (1200, 800, 8, 50), "c5": (1920, 1080, 256, 50),
+                "c5s": (1920, 1080, 4, 50), "c3": (3840, 2160, 1024, 50)}[cfg]
+if len(args) > 1:  # bounces override (1: casts are almost all primary rays)
+    b = int(args[1])
 ctx = spt.Context(0)
 scene = spt.generate_stress(1, 10000) if cfg.startswith("c5") else spt.generate_spheres(1)
 ctx.set_scene(scene)
@@ -32,4 +39,14 @@ sph, br, pas, imp = st["diag"][8:12]
 print(f"per wave cast: spheres tested={sph/max(it,1):.2f} update branches taken={br/max(it,1):.2f} "
       f"({br/max(sph,1):.3f} of tested); lanes passing per taken branch={pas/max(br,1):.2f}; "
       f"taken branches where some lane improves its winner={imp/max(br,1):.3f}")
+lt, lp = st["diag"][12:14]
+print(f"lane-level RaySphereIntersection evaluations per ray={lt/max(st['casts'],1):.2f} "
+      f"member pretests per ray={lp/max(st['casts'],1):.2f} (brute force: {scene.n})")
 print(f"render_ms={st['render_ms']:.3f}")
+if json_out:
+    import json
+    json.dump({"config": cfg, "frame": [W, H, spp, b], "spheres": scene.n, "casts": st["casts"],
+               "samples": st["samples"], "lane_tests_per_ray": lt / max(st["casts"], 1),
+               "lane_pretests_per_ray": lp / max(st["casts"], 1), "clusters_entered_per_wave_cast": leaves / max(it, 1),
+               "tree_nodes_per_wave_cast": nodes / max(it, 1), "live_lanes_per_iter": st["casts"] / max(it, 1),
+               "build": "SPT_DIAG=1 (libspt_hip_diag.so), counters only, never timed"}, open(json_out, "w"), indent=1)

@@ -1,0 +1,108 @@
+// Harness of the C++ drop-in (include/spt/RenderSegmentShim.hpp), for the parity
+// tests and for `bench.py --dropin`.  It declares globals with the names and types of
+// the reference's Globals.hpp / Definitions.hpp / Math.hpp (as the reference's own
+// translation unit would), includes the shim, and drives RenderSegment /
+// RenderSegmentTask from concurrent threads the way RenderImageParallelMain does
+// (Renderer.hpp:257-302: tc x tc tiles, at most tc RenderJob threads in flight).
+// Writes g_data to argv[1].
+// Usage: dropin_harness out.bin width height spp bounces threads task(0|1) [frames]
+//   frames > 0: render one untimed frame, then `frames` timed frames, and print
+//   "frames=K seconds=T" (wall clock of the K frames).  SPT_DEVICES=0,1,.. (shim)
+//   renders on a multi-device context.
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+namespace math {
+struct Vec4 { float xyzw[4]; };
+struct Mat4 { float array[16]; };
+}  // namespace math
+enum class Material : uint8_t { SKYBOX, REFLECTIVE, REFRACTIVE, DIFFUSE };
+struct RenderSegmentData { uint32_t yBegin = 0, yEnd = 0, xBegin = 0, xEnd = 0; };
+
+uint32_t g_width, g_height, g_samples, g_bounces;
+uint8_t *g_data;
+math::Mat4 viewMatrix;
+math::Vec4 eyePos = {{0, 1, -3, 0}}, lookAt = {{0, 1, 0, 0}}, upDir = {{0, 1, 0, 0}}, initColor = {{137, 207, 240, 0}};
+std::vector<math::Vec4> g_colors, g_spheres;
+std::vector<float> g_radii, g_diffuses;
+std::vector<Material> g_materials;
+uint32_t g_sphereNumber = 10;
+
+#include <spt/RenderSegmentShim.hpp>
+
+int main(int argc, char **argv)
+{
+    if (argc < 8) return 2;
+    g_width = atoi(argv[2]);
+    g_height = atoi(argv[3]);
+    g_samples = atoi(argv[4]);
+    g_bounces = atoi(argv[5]);
+    const uint32_t tc = atoi(argv[6]);
+    const bool task = atoi(argv[7]) != 0;
+    std::vector<uint8_t> frame((size_t)g_width * g_height * 3, 0);
+    g_data = frame.data();
+    // GenerateSpheres (SceneGenerators.hpp:6-66) through the library's producer
+    std::vector<float> c(4 * 4096), r(4096), col(4 * 4096), fz(4096);
+    std::vector<uint8_t> m(4096);
+    uint32_t n = 0;
+    if (spt_scene_generate_random(1, 4096, c.data(), r.data(), col.data(), m.data(), fz.data(), &n)) return 3;
+    g_sphereNumber = n;
+    for (uint32_t i = 0; i < n; ++i) {
+        g_spheres.push_back({{c[4 * i], c[4 * i + 1], c[4 * i + 2], 0}});
+        g_colors.push_back({{col[4 * i], col[4 * i + 1], col[4 * i + 2], 0}});
+        g_radii.push_back(r[i]);
+        g_diffuses.push_back(fz[i]);
+        g_materials.push_back(static_cast<Material>(m[i]));
+    }
+    if (spt_camera_basis(eyePos.xyzw, lookAt.xyzw, upDir.xyzw, viewMatrix.array)) return 4;
+    // RenderImageParallelMain: tc x tc tiles, at most tc in flight
+    auto frame_once = [&]() {
+        const uint32_t sw = g_width / tc, sh = g_height / tc;
+        std::atomic<int> free_threads((int)tc);
+        std::condition_variable cv;
+        std::mutex mu;
+        std::vector<std::thread> threads;
+        for (uint32_t j = 0; j < tc; ++j)
+            for (uint32_t i = 0; i < tc; ++i) {
+                RenderSegmentData seg{sh * j, sh * j + sh > g_height ? g_height : sh * j + sh, sw * i,
+                                      sw * i + sw > g_width ? g_width : sw * i + sw};
+                {
+                    std::unique_lock<std::mutex> lk(mu);
+                    cv.wait(lk, [&] { return free_threads.load() > 0; });
+                    free_threads.fetch_sub(1);
+                }
+                threads.emplace_back([seg, task, &free_threads, &cv, &mu] {
+                    if (task)
+                        RenderSegmentTask(seg);
+                    else
+                        RenderSegment(seg);
+                    {
+                        std::lock_guard<std::mutex> lk(mu);
+                        free_threads.fetch_add(1);
+                    }
+                    cv.notify_one();
+                });
+            }
+        for (auto &t : threads) t.join();
+    };
+    frame_once();
+    const int frames = argc > 8 ? atoi(argv[8]) : 0;
+    if (frames > 0) {
+        const auto t0 = std::chrono::steady_clock::now();
+        for (int k = 0; k < frames; ++k) frame_once();
+        const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        printf("frames=%d seconds=%.6f\n", frames, sec);
+    }
+    FILE *f = fopen(argv[1], "wb");
+    if (!f) return 5;
+    fwrite(frame.data(), 1, frame.size(), f);
+    fclose(f);
+    return 0;
+}

@@ -10,7 +10,8 @@ src, dst = sys.argv[1], sys.argv[2]
 timed = int(sys.argv[3]) if len(sys.argv) > 3 else 20  # bench --steps of the profiled run
 cmd = sys.argv[4] if len(sys.argv) > 4 else "(default arguments)"
 out = [f"# rocprofv3 summary: {os.path.basename(src)}\n",
-       "Command: `tools/profile.sh` = rocprofv3 --kernel-trace --stats and four separate --pmc passes over "
+       "Command: `tools/profile.sh` = rocprofv3 --kernel-trace --stats and separate --pmc passes (one counter "
+       "group each) over "
        f"`python3 bench.py {cmd}` (1x MI355X).\n",
        "## Kernel trace (--kernel-trace --stats)\n", "| kernel | calls | avg ms | min ms | max ms | % |",
        "|---|---|---|---|---|---|"]
@@ -46,7 +47,7 @@ if os.path.exists(trace):
         out.append(f"| `{k[:60]}` | {len(d)} | {sum(d)/len(d):.4f} | {min(d):.4f} | {max(d):.4f} | "
                    f"{tot/1e6/len(d):.4f} |")
 agg = collections.defaultdict(list)
-for d in ("pmc1", "pmc2", "pmc3", "pmc4"):
+for d in sorted(x for x in os.listdir(src) if x.startswith("pmc")):
     p = os.path.join(src, d, "run_counter_collection.csv")
     if not os.path.exists(p):
         continue
@@ -63,20 +64,43 @@ for (k, c), v in sorted(agg.items()):
         note = f" (KB = {val/1024:.1f} MB)"
     out.append(f"| `{k}` | {c} | {val:,.0f}{note} |")
 open(dst, "w").write("\n".join(out) + "\n")
-# profiles/traffic.json: HBM bytes per launch (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE,
-# KB -> bytes) that bench.py reports as roofline.traffic; SPT_TRAFFIC_CONFIG names the config
-tcfg = os.environ.get("SPT_TRAFFIC_CONFIG")
-if tcfg:
+# profiles/counters.json[config]: per-launch PMC values of the render and fold kernels
+# (FETCH_SIZE x2 gfx950 correction, KB -> bytes; derived VALU/occupancy figures) and
+# the SPT_DIAG lane counts (diag.json of tools/profile.sh) that bench.py reports in
+# roofline.traffic and roofline_valu; SPT_COUNTERS_CONFIG names the config
+ccfg = os.environ.get("SPT_COUNTERS_CONFIG")
+if ccfg:
     import json
-    tp = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "profiles", "traffic.json")
-    doc = json.load(open(tp)) if os.path.exists(tp) else {}
+    cp = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "profiles", "counters.json")
+    doc = json.load(open(cp)) if os.path.exists(cp) else {}
+    rel = os.path.relpath(os.path.abspath(dst), os.path.dirname(os.path.dirname(os.path.abspath(cp))))
     entry = {}
-    for kname, short in (("render_kernel", "render_kernel"), ("fold_kernel", "fold_kernel")):
-        f = [sum(v) / len(v) for (k, c), v in agg.items() if short in k and c == "FETCH_SIZE"]
-        w = [sum(v) / len(v) for (k, c), v in agg.items() if short in k and c == "WRITE_SIZE"]
-        if f and w:
-            entry[kname] = {"fetch_bytes": int(2 * f[0] * 1024), "write_bytes": int(w[0] * 1024),
-                            "source": os.path.relpath(os.path.abspath(dst), os.path.dirname(os.path.dirname(os.path.abspath(tp))))}
-    doc[tcfg] = entry
-    json.dump(doc, open(tp, "w"), indent=2)
+    for short in ("render_kernel", "fold_kernel"):
+        vals = {c: sum(v) / len(v) for (k, c), v in agg.items() if short in k}
+        if not vals:
+            continue
+        e = {"source": rel}
+        if "FETCH_SIZE" in vals and "WRITE_SIZE" in vals:
+            e["fetch_bytes"] = int(2 * vals["FETCH_SIZE"] * 1024)
+            e["write_bytes"] = int(vals["WRITE_SIZE"] * 1024)
+        for c in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_SMEM", "SQ_WAVES", "SQ_ACTIVE_INST_VALU",
+                  "SQ_THREAD_CYCLES_VALU", "SQC_DCACHE_HITS", "SQC_DCACHE_MISSES", "VALUUtilization", "VALUBusy",
+                  "MeanOccupancyPerCU"):
+            if c in vals:
+                e[c] = round(vals[c], 4) if vals[c] < 1e4 else int(vals[c])
+        if "VALUUtilization" not in e and "SQ_THREAD_CYCLES_VALU" in vals and vals.get("SQ_ACTIVE_INST_VALU"):
+            e["VALUUtilization"] = round(100 * vals["SQ_THREAD_CYCLES_VALU"] / (vals["SQ_ACTIVE_INST_VALU"] * 64), 2)
+        if "MeanOccupancyPerCU" in vals:
+            e["occupancy_waves_per_simd"] = round(vals["MeanOccupancyPerCU"] / 4, 3)
+        if vals.get("SQC_DCACHE_HITS") is not None and vals.get("SQC_DCACHE_MISSES") is not None:
+            tot = vals["SQC_DCACHE_HITS"] + vals["SQC_DCACHE_MISSES"]
+            e["sqc_dcache_miss_frac"] = round(vals["SQC_DCACHE_MISSES"] / tot, 4) if tot else None
+        entry[short] = e
+    dj = os.path.join(src, "diag.json")
+    if os.path.exists(dj):
+        d = json.load(open(dj))
+        d["source"] = rel
+        entry["diag"] = d
+    doc[ccfg] = entry
+    json.dump(doc, open(cp, "w"), indent=2)
 print("\n".join(out))

@@ -328,7 +328,9 @@ def main():
                                 "def": "17 FLOP per RaySphereIntersection + 10 per member pretest, evaluated for "
                                        "live lanes (SPT_DIAG in-kernel counts, profiles/counters.json) x rays "
                                        "counted in-kernel / launch time"}
-            for k in ("VALUUtilization", "VALUBusy", "occupancy_waves_per_simd", "sqc_dcache_miss_frac"):
+            # VALUUtilization: active lanes per VALU instruction (%); occupancy: mean resident
+            # waves per SIMD over the launch (MeanOccupancyPerCU / 4); scalar-cache miss rate
+            for k in ("VALUUtilization", "occupancy_waves_per_simd", "sqc_dcache_miss_frac"):
                 if k in rk:
                     rv[k] = rk[k]
             out["roofline_valu"] = rv

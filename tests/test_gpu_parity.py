@@ -711,3 +711,65 @@ def test_concurrent_tiles_overlap_and_match(spt, ctx, golden_scenes):
         t.join()
     assert not errors
     assert np.array_equal(got, want)
+
+
+# ---------------------------------------------------------------- configs 4 and 5 at full size
+
+def test_config4_eight_way_strip_split_equals_one_part(spt, ctx, golden_scenes):
+    """BASELINE config 4's split (3840x2160, the config-2 scene, 8 parts of
+    even_strip(2160, 8)-row interleaved strips, tiles gathered and assembled) rehearsed
+    on one GPU at 2 spp: bit-identical to the 1-part frame.  Both paths: the device
+    API (rows + assemble, what each bench rank runs) and spt_render_frame over an
+    8-member context (the C++ host's multi-device path)."""
+    import torch
+    from simplepathtracer_amd.distributed import even_strip
+    W, H, spp, parts = 3840, 2160, 2, 8
+    strip = even_strip(H, parts)
+    assert strip == 8 and (H // strip) % parts == 0
+    setup(ctx, scene_from(spt, golden_scenes, "random"), W, H, spp, 50, seed=3)
+    full = torch.zeros((W * H, 4), dtype=torch.float32, device="cuda")
+    g_full = torch.zeros(W * H * 3, dtype=torch.uint8, device="cuda")
+    ctx.render_rows_async(0, 0, H, 1, 1, 0, 0, W, full.data_ptr(), g_full.data_ptr())
+    ctx.synchronize()
+    rows = [spt.rows_count(0, H, strip, parts, p) for p in range(parts)]
+    assert rows == [H // parts] * parts
+    tiles = torch.zeros((parts, rows[0] * W, 4), dtype=torch.float32, device="cuda")
+    for p in range(parts):
+        ctx.render_rows_async(0, 0, H, strip, parts, p, 0, W, tiles[p].data_ptr(), 0)
+    frame = torch.zeros_like(full)
+    g = torch.zeros_like(g_full)
+    ctx.assemble_rows_async(tiles.data_ptr(), rows[0], 0, H, strip, parts, 0, W, frame.data_ptr(), g.data_ptr())
+    ctx.synchronize()
+    assert torch.equal(frame.view(torch.int32), full.view(torch.int32))
+    assert torch.equal(g, g_full)
+    multi = spt.Context(devices=[0] * parts)
+    setup(multi, scene_from(spt, golden_scenes, "random"), W, H, spp, 50, seed=3)
+    gm = np.zeros(W * H * 3, np.uint8)
+    fm = multi.render_frame(gm)
+    multi.close()
+    assert np.array_equal(fm.view(np.int32), full.cpu().numpy().view(np.int32))
+    assert np.array_equal(gm, g_full.cpu().numpy())
+
+
+def test_config5_full_frame_properties(spt, ctx, oracle):
+    """BASELINE config 5 at full size (10 000 spheres, 1920x1080, 256 spp, depth 50,
+    LDS tree kernel): every sample accounted for, deterministic, and sampled pixels
+    bit-exact vs the oracle's brute-force uint32 scan."""
+    s = spt.generate_stress(1, 10000)
+    W, H, spp = 1920, 1080, 256
+    setup(ctx, s, W, H, spp, 50)
+    ctx.reset_stats()
+    a = ctx.render_segment(0, H, 0, W)
+    st = ctx.stats()
+    assert st["samples"] == W * H * spp
+    assert 1.0 < st["casts"] / st["samples"] < 8.0
+    assert np.isfinite(a[:, :3]).all()
+    b = ctx.render_segment(0, H, 0, W)
+    assert_bitwise(a, b, "determinism")
+    osc = oracle.OracleScene(s.centers, s.radii, s.colors, s.materials, s.fuzz)
+    fr = oracle.make_frame(spt.camera_basis(EYE, LOOK, UP), EYE, SKY, W, H, spp, 50, 1)
+    rng = np.random.default_rng(5)
+    for _ in range(6):
+        x, y = int(rng.integers(0, W)), int(rng.integers(0, H))
+        want, _ = oracle.render_segment(osc, fr, y, y + 1, x, x + 1)
+        assert_bitwise(a[y * W + x, :3], want[0, :3], f"pixel {(x, y)}")

@@ -72,8 +72,9 @@ typedef struct spt_stats {
     double render_ms;      /* summed device time of render-kernel launches */
     double fold_ms;        /* summed device time of resolve (fold) launches */
     double last_render_ms; /* device time of the most recent render launch */
-    uint32_t grid_blocks;  /* persistent grid of the render kernel */
-    uint32_t block_threads;
+    uint32_t grid_blocks;  /* grid of the most recent render launch (the persistent grid
+                              before any launch) */
+    uint32_t block_threads; /* its block size (256; 1024 for the LDS tree kernel) */
     double render_busy_ms; /* length of the union of the render launches' intervals: with
                               frames in flight on several streams launches overlap, and
                               this is the device time during which some render launch ran */

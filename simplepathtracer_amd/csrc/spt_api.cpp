@@ -73,6 +73,7 @@ struct spt_ctx {
     uint32_t grid = 0, block = spt::kRenderBlock, claim = 0;  // 0 = per launch (claim_size)
     uint32_t claims_per_wave = 2;                              // render_grid (config 1: 2 > 1, 4)
     uint32_t grid_overlap = 0;  // grid while frames are in flight on several streams
+    uint32_t last_grid = 0, last_block = 0;  // shape of the most recent render launch
 
     // scene (Globals.hpp:31-37)
     float4 *d_shade = nullptr, *d_slots = nullptr;
@@ -116,6 +117,7 @@ struct spt_ctx {
     std::vector<HostSlot *> slots;
     std::condition_variable slot_cv;
     uint32_t host_slots = kMaxHostSlots;
+    uint32_t host_grid_div = 0;  // 0: half the slots in use (SPT_HOST_GRID_DIV overrides)
     std::atomic<int> inflight{0};  // host calls in progress on this device
 
     // multi-device context (spt_ctx_create_multi): member contexts of the other devices,
@@ -285,11 +287,13 @@ uint32_t claim_size(const spt_ctx *ctx, uint64_t items)
 // fewer claims than that grid has waves.  A wave without a claim only starts,
 // finds the counter exhausted and exits, and on config 1 (1250 claims, 8192
 // waves) those waves tripled the launch time.
-uint32_t render_grid(const spt_ctx *ctx, uint64_t items, uint32_t claim)
+// div: host calls sharing the GPU side by side (each gets 1/div of the grid).
+uint32_t render_grid(const spt_ctx *ctx, uint64_t items, uint32_t claim, uint32_t div)
 {
     const uint64_t claims = (items + claim - 1) / claim;
     const uint64_t per_block = (uint64_t)(ctx->block / 64) * ctx->claims_per_wave;
-    return (uint32_t)std::min<uint64_t>(full_grid(ctx), std::max<uint64_t>(1, (claims + per_block - 1) / per_block));
+    const uint64_t full = (full_grid(ctx) + div - 1) / div;
+    return (uint32_t)std::min<uint64_t>(full, std::max<uint64_t>(1, (claims + per_block - 1) / per_block));
 }
 
 // The workspace of stream s (created on first use, at most kMaxWorkspaces).
@@ -353,8 +357,9 @@ struct Progress {
     std::function<int(uint32_t)> after_pass;
 };
 
+// grid_div: concurrent host calls on this context share the GPU (render_grid)
 int render_impl(spt_ctx *ctx, int mode, const spt::RowMap &map, float4 *d_rgba, uint8_t *d_rgb8, hipStream_t s,
-                bool keep_samples, const Progress *pg = nullptr)
+                bool keep_samples, const Progress *pg = nullptr, uint32_t grid_div = 1)
 {
     const uint32_t rows = spt::rows_owned(map);
     const uint64_t npix64 = (uint64_t)rows * map.width;
@@ -449,7 +454,10 @@ int render_impl(spt_ctx *ctx, int mode, const spt::RowMap &map, float4 *d_rgba, 
                 ctx->ref_recorded = true;
             }
             HIP_TRY(ctx, hipEventRecord(ev.a, s));
-            HIP_TRY(ctx, spt::launch_render(ra, render_grid(ctx, ra.n_items, ra.claim), ctx->block, s));
+            spt::LaunchShape sh{render_grid(ctx, ra.n_items, ra.claim, grid_div), ctx->block, grid_div, 0, 0};
+            HIP_TRY(ctx, spt::launch_render(ra, sh, s));
+            ctx->last_grid = sh.ran_grid;
+            ctx->last_block = sh.ran_block;
             HIP_TRY(ctx, hipEventRecord(ev.b, s));
         }
         ctx->pending_render.push_back(ev);
@@ -636,8 +644,13 @@ int render_segment_host(spt_ctx *ctx, int mode, uint32_t yB, uint32_t yE, uint32
         if (e != hipSuccess) return fail(ctx, SPT_ERR_HIP, "hipStreamSynchronize failed: %s", hipGetErrorString(e));
         return SPT_OK;
     };
+    // concurrent callers (RenderJob threads) share the GPU side by side: with k slots in
+    // use each launch gets 2/k of the grid, so launches overlap and no single launch's
+    // tail idles the device (config 2 through the C++ shim, Msamples/s, grid divisor
+    // 1 / k/2 / k: tc = 4: 7 923 / 8 715 / 7 417; tc = 8: 4 117 / 6 303 / 5 769)
+    const uint32_t div = ctx->host_grid_div ? ctx->host_grid_div : std::max<uint32_t>(1u, (uint32_t)ctx->slots.size() / 2u);
     if (pass_spp == 0) {
-        if ((rc = render_impl(ctx, mode, map, hs->d_stage, d8, hs->stream, false))) return rc;
+        if ((rc = render_impl(ctx, mode, map, hs->d_stage, d8, hs->stream, false, nullptr, div))) return rc;
     } else {
         Progress pg{pass_spp, [&](uint32_t done) -> int {
                         const int r = copy_out_and_wait();
@@ -650,7 +663,7 @@ int render_segment_host(spt_ctx *ctx, int mode, uint32_t yB, uint32_t yE, uint32
                         lk.lock();
                         return stop != 0 ? 1 : 0;
                     }};
-        rc = render_impl(ctx, mode, map, hs->d_stage, d8, hs->stream, false, &pg);
+        rc = render_impl(ctx, mode, map, hs->d_stage, d8, hs->stream, false, &pg, div);
         if (rc) return rc < 0 ? -rc : rc;
     }
     if ((rc = copy_out_and_wait())) return rc;
@@ -839,6 +852,7 @@ int spt_ctx_create(int device, spt_ctx **out)
     if (const char *e = std::getenv("SPT_TREE_B")) ctx->tree_branching = (uint32_t)std::max(0, std::atoi(e));
     if (const char *e = std::getenv("SPT_CLAIMS_PER_WAVE")) ctx->claims_per_wave = (uint32_t)std::max(1, std::atoi(e));
     if (const char *e = std::getenv("SPT_WF_CAP")) ctx->wf_cap = (uint32_t)std::max(1024, std::atoi(e));
+    if (const char *e = std::getenv("SPT_HOST_GRID_DIV")) ctx->host_grid_div = (uint32_t)std::max(0, std::atoi(e));
     if (const char *e = std::getenv("SPT_HOST_SLOTS"))
         ctx->host_slots = (uint32_t)std::min<int>((int)kMaxHostSlots, std::max(1, std::atoi(e)));
     ctx->grid = (uint32_t)(per_cu * ctx->num_cu);
@@ -1229,8 +1243,8 @@ int stats_one(spt_ctx *ctx, spt_stats *out)
     out->fold_ms = ctx->fold_ms;
     out->last_render_ms = ctx->last_render_ms;
     out->render_busy_ms = busy_ms(ctx);
-    out->grid_blocks = ctx->grid;
-    out->block_threads = ctx->block;
+    out->grid_blocks = ctx->last_grid ? ctx->last_grid : ctx->grid;
+    out->block_threads = ctx->last_block ? ctx->last_block : ctx->block;
     return SPT_OK;
 }
 

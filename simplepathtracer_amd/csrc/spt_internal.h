@@ -218,7 +218,15 @@ struct FoldArgs {
                          // (dx + dy * segmentHeight, TaskBasedPathTracer.hpp:103,186) aliases pixels
 };
 
-hipError_t launch_render(const RenderArgs &a, uint32_t grid, uint32_t block, hipStream_t s);
+// Launch geometry of one render launch: the context's persistent grid for the
+// 256-thread kernels (`grid`, `block`), a divisor of every kernel's full grid (several
+// host calls in flight share the GPU side by side), and on return the grid and block
+// the chosen kernel ran with (the LDS tree kernel sizes its own: 1024-thread blocks).
+struct LaunchShape {
+    uint32_t grid, block, div;
+    uint32_t ran_grid, ran_block;
+};
+hipError_t launch_render(const RenderArgs &a, LaunchShape &sh, hipStream_t s);
 
 // Wavefront variant (spt_wavefront.hip): double-buffered ray queues of `cap`
 // rays, a hit record per ray, kWfCats category queues and their counters.

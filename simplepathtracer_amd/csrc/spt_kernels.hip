@@ -23,6 +23,8 @@
 // sequential reference loop whatever order the paths finished in.
 #include "spt_path.h"
 
+#include <mutex>
+
 namespace spt {
 
 
@@ -340,51 +342,56 @@ __global__ void selftest_kernel(const float *a, const float *b, const uint32_t *
     o[13] = uniform_bits(bits[i], 0.f, 1.f);
 }
 
-// Blocks per CU of the LDS tree variant and CUs of the device, queried once per
-// process (a thread-safe local static: RenderJob threads launch concurrently; every
-// device of the node is an MI355X).  per_cu = 0 disables the variant.
+// Blocks per CU of the LDS tree variant and CUs of a device, queried once per device
+// (thread-safe: RenderJob threads launch concurrently).  per_cu = 0 disables the variant.
 static void lds_tree_shape(int *per_cu, int *num_cu)
 {
-    struct Shape {
-        int pc = 0, nc = 0;
-    };
-    static const Shape shape = [] {
-        Shape r;
-        int dev = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&r.nc, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&r.pc, render_kernel_lds, (int)kLdsBlock, 0) != hipSuccess)
-            r.pc = 0;
-        return r;
-    }();
-    *per_cu = shape.pc;
-    *num_cu = shape.nc;
+    constexpr int kMaxDevices = 64;
+    static std::mutex mu;
+    static int pc[kMaxDevices], nc[kMaxDevices];
+    static bool known[kMaxDevices];
+    int dev = 0;
+    *per_cu = *num_cu = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return;
+    std::lock_guard<std::mutex> lk(mu);
+    if (!known[dev]) {
+        if (hipDeviceGetAttribute(&nc[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc[dev], render_kernel_lds, (int)kLdsBlock, 0) != hipSuccess)
+            pc[dev] = 0;
+        known[dev] = true;
+    }
+    *per_cu = pc[dev];
+    *num_cu = nc[dev];
 }
 
-hipError_t launch_render(const RenderArgs &a, uint32_t grid, uint32_t block, hipStream_t s)
+hipError_t launch_render(const RenderArgs &a, LaunchShape &sh, hipStream_t s)
 {
+    const uint32_t div = sh.div ? sh.div : 1u;
     if (a.scene.accel.tree && a.scene.accel.n_nodes + 1u <= kLdsNodeRecords) {
-        // all resident blocks, or fewer when the launch has under 2 claims per wave
-        // (render_grid's rule; a frame in flight on another stream only queues)
+        // all resident blocks (divided among the host calls in flight), or fewer when the
+        // launch has under 2 claims per wave (render_grid's rule)
         int per_cu = 0, num_cu = 0;
         lds_tree_shape(&per_cu, &num_cu);
         if (per_cu > 0) {
-            (void)grid;
-            (void)block;
             const uint64_t claims = ((uint64_t)a.n_items + a.claim - 1) / a.claim;
             const uint64_t per_block = 2 * (kLdsBlock / 64);
+            const uint64_t full = ((uint64_t)per_cu * num_cu + div - 1) / div;
             uint64_t g = (claims + per_block - 1) / per_block;
-            g = g < (uint64_t)per_cu * num_cu ? g : (uint64_t)per_cu * num_cu;
-            hipLaunchKernelGGL(render_kernel_lds, dim3((uint32_t)g), dim3(kLdsBlock), 0, s, a);
+            g = g < full ? g : full;
+            sh.ran_grid = (uint32_t)g;
+            sh.ran_block = kLdsBlock;
+            hipLaunchKernelGGL(render_kernel_lds, dim3(sh.ran_grid), dim3(kLdsBlock), 0, s, a);
             return hipGetLastError();
         }
     }
+    sh.ran_grid = sh.grid;
+    sh.ran_block = sh.block;
     if (a.scene.accel.tree)
-        hipLaunchKernelGGL((render_kernel<true, (int)kClusterSlots>), dim3(grid), dim3(block), 0, s, a);
+        hipLaunchKernelGGL((render_kernel<true, (int)kClusterSlots>), dim3(sh.grid), dim3(sh.block), 0, s, a);
     else if (a.scene.accel.leaf_slots == kFlatLeafSlots)
-        hipLaunchKernelGGL((render_kernel<false, (int)kFlatLeafSlots>), dim3(grid), dim3(block), 0, s, a);
+        hipLaunchKernelGGL((render_kernel<false, (int)kFlatLeafSlots>), dim3(sh.grid), dim3(sh.block), 0, s, a);
     else
-        hipLaunchKernelGGL((render_kernel<false, (int)kClusterSlots>), dim3(grid), dim3(block), 0, s, a);
+        hipLaunchKernelGGL((render_kernel<false, (int)kClusterSlots>), dim3(sh.grid), dim3(sh.block), 0, s, a);
     return hipGetLastError();
 }
 

@@ -7,7 +7,7 @@ megakernel, folded in sample order, written as float RGBA + RGB8 g_data.
 With N GPUs (torchrun, one process per GPU) the frame is split into interleaved
 row strips (8 rows, or fewer so the strips deal evenly: 4 at N = 8), rank r renders
 strips r, r+N, ...; the float tiles are gathered to rank 0 over RCCL
-(all_gather_into_tensor) and assembled there (strong scaling: the frame is fixed,
+(one gather: send/recv pairs over xGMI) and assembled there (strong scaling: the frame is fixed,
 per-GPU work shrinks with N).  Consecutive frames alternate over two HIP streams
 (`--streams`), each with its own workspace and output buffers, so one frame's last
 paths drain while the next frame fills the GPU and its gather overlaps rendering.
@@ -209,7 +209,8 @@ def main():
              "local": None, "gathered": None}
         if world > 1:
             b["local"] = torch.zeros((split.tile_pixels(), 4), dtype=torch.float32, device=dev)
-            b["gathered"] = torch.zeros((world * split.tile_pixels(), 4), dtype=torch.float32, device=dev)
+            if rank == 0:
+                b["gathered"] = torch.zeros((world * split.tile_pixels(), 4), dtype=torch.float32, device=dev)
         bufs.append(b)
     counter = [0]
 

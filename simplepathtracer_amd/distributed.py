@@ -3,8 +3,8 @@ with an RCCL gather of the per-tile framebuffers).
 
 One process per GPU.  The frame's rows are dealt in interleaved `strip`-row
 strips: rank r owns strips r, r+N, r+2N, ...  Each rank renders its rows into a
-compact float4 tile (spt_render_rows_async); one all_gather_into_tensor over
-RCCL/xGMI brings every tile to every rank and rank 0 scatters them into the frame
+compact float4 tile (spt_render_rows_async); one gather over RCCL/xGMI brings
+every tile to rank 0, which scatters them into the frame
 and the RGB8 g_data buffer (spt_assemble_rows_async).  Per-pixel results do not
 depend on the split (keyed per-(pixel, sample) RNG), so any N gives the 1-GPU frame.
 """
@@ -53,16 +53,24 @@ class FrameSplit:
 
 
 def gather_tiles(local_tile, gathered, group=None) -> None:
-    """All ranks' tiles -> gathered[world*max_rows*width, 4], rank-major (one
-    collective; the concatenated form is accepted by both RCCL and gloo)."""
+    """Every rank's tile -> rank 0's gathered[world*max_rows*width, 4], rank-major: one
+    gather to rank 0 (RCCL send/recv pairs over xGMI), so each tile crosses one link
+    once; other ranks pass gathered=None."""
     import torch.distributed as dist
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    dst = dist.get_global_rank(group, 0) if group is not None else 0
     if local_tile.is_cuda and dist.get_backend(group) != "nccl":
         # rehearsal path (several ranks on one GPU, gloo): exchange host copies
-        host = gathered.new_empty(gathered.shape, device="cpu")
-        dist.all_gather_into_tensor(host, local_tile.cpu(), group=group)
-        gathered.copy_(host)
+        host = local_tile.cpu()
+        parts = [host.new_empty(host.shape) for _ in range(world)] if rank == 0 else None
+        dist.gather(host, parts, dst=dst, group=group)
+        if rank == 0:
+            for r, p in enumerate(parts):
+                gathered[r * p.shape[0]:(r + 1) * p.shape[0]].copy_(p)
         return
-    dist.all_gather_into_tensor(gathered, local_tile, group=group)
+    parts = list(gathered.chunk(world)) if rank == 0 else None
+    dist.gather(local_tile, parts, dst=dst, group=group)
 
 
 def render_frame(ctx, split: FrameSplit, rank: int, mode: int, local_tile, gathered=None, frame=None,

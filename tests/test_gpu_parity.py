@@ -432,7 +432,7 @@ def test_cpp_dropin_shim_renders_like_the_context(spt, golden_scenes, tmp_path, 
 
 
 def test_bench_two_ranks_on_one_gpu_matches_one_rank(spt, tmp_path):
-    """bench.py's N>1 flow (strip split, all_gather_into_tensor, rank-0 assemble)
+    """bench.py's N>1 flow (strip split, gather to rank 0, rank-0 assemble)
     rehearsed with two gloo ranks sharing cuda:0: same g_data as N=1."""
     import os
     import subprocess

@@ -1,6 +1,6 @@
 """CPU tests of the N>1 path: world_size-2 `gloo` processes split the frame into
 interleaved strips, exchange their tiles with the same collective bench.py uses
-(all_gather_into_tensor), and rank 0 places them with the row map.  The per-rank
+(a gather to rank 0), and rank 0 places them with the row map.  The per-rank
 tiles come from the CPU oracle (test infrastructure standing in for the GPU
 render, which `test_gpu_parity.py::test_row_split_and_assemble_equals_full_frame`
 covers on the device)."""
@@ -48,7 +48,7 @@ def _worker(rank, world, port, strip, scene_arrays, view, q):
         tile = np.zeros((split.tile_pixels(), 4), np.float32)
         tile[:len(rows) * W] = _oracle_rows(rows, scene_arrays, view)
         local = torch.from_numpy(tile)
-        gathered = torch.zeros((world * split.tile_pixels(), 4), dtype=torch.float32)
+        gathered = torch.zeros((world * split.tile_pixels(), 4), dtype=torch.float32) if rank == 0 else None
         gather_tiles(local, gathered)
         if rank == 0:
             frame = np.zeros((H, W, 4), np.float32)

@@ -33,6 +33,7 @@
 #pragma clang fp contract(off)
 
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <cstring>
 #include <cstdio>
@@ -76,6 +77,63 @@ float pretest_k(const float4 &s)
 }
 
 const float4 kDummy = make_float4(0.f, 0.f, 0.f, -INFINITY);  // r*r = -inf: never passes
+
+// |C| + |r| of sphere i: Bm of a tree node is the largest over its members
+double member_reach(const float *centers4, const float *radii, uint32_t i)
+{
+    const double x = centers4[4 * i], y = centers4[4 * i + 1], z = centers4[4 * i + 2];
+    return std::sqrt(x * x + y * y + z * z) + std::fabs((double)radii[i]);
+}
+
+// Bm of the members idx[0..m) (0 when empty)
+double node_reach(const float *centers4, const float *radii, const uint32_t *idx, size_t m)
+{
+    double bm = 0;
+    for (size_t j = 0; j < m; ++j) bm = std::max(bm, member_reach(centers4, radii, idx[j]));
+    return bm;
+}
+
+// Tree node box of the members idx[0..m): lo = min (C - |r|) - kBoxS Bm
+// rounded down, hi = max (C + |r|) + kBoxS Bm rounded up.  Members beyond 1e15 from the
+// origin: the box is everything (the node never culls).
+AccelNode box_node(const float *centers4, const float *radii, const uint32_t *idx, size_t m)
+{
+    AccelNode nd{};
+    const double bm = node_reach(centers4, radii, idx, m);
+    double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (size_t j = 0; j < m; ++j)
+        for (int c = 0; c < 3; ++c) {
+            const double cc = centers4[4 * idx[j] + c], r = std::fabs((double)radii[idx[j]]);
+            lo[c] = std::min(lo[c], cc - r);
+            hi[c] = std::max(hi[c], cc + r);
+        }
+    float flo[3], fhi[3];
+    for (int c = 0; c < 3; ++c) {
+        const bool off = !(bm <= 1e15);
+        flo[c] = off ? -INFINITY : round_down(lo[c] - kBoxS * bm);
+        fhi[c] = off ? INFINITY : round_up(hi[c] + kBoxS * bm);
+    }
+    nd.lox = flo[0];
+    nd.loy = flo[1];
+    nd.loz = flo[2];
+    nd.hix = fhi[0];
+    nd.hiy = fhi[1];
+    nd.hiz = fhi[2];
+    return nd;
+}
+
+// the record one past a layout's last node (the kernels prefetch it; never tested)
+AccelNode pad_node(uint32_t skip)
+{
+    AccelNode nd{};
+    nd.cx = nd.cy = nd.cz = 0.f;
+    nd.k1 = -INFINITY;
+    nd.skip = skip;
+    nd.slot = kNoSlot;
+    nd.rb = -INFINITY;
+    nd.cb2 = 0.f;
+    return nd;
+}
 
 }  // namespace
 
@@ -162,8 +220,10 @@ AccelTables build_accel(const float *centers4, const float *radii, uint32_t n, u
             }
         t.depth = (uint32_t)levels.size();
 
-        // bounding sphere of the member spheres of leaves [c0, c1)
-        auto bound = [&](Span sp, AccelNode &nd) {
+        // bounding sphere (flat lists) or expanded box (trees) of the member spheres of
+        // leaves [c0, c1); `ctr` = centre of the members' centres (sibling order)
+        const bool tree = levels.size() > 1;
+        auto bound = [&](Span sp, AccelNode &nd, double *ctr) {
             const size_t j0 = (size_t)sp.c0 * k, j1 = std::min(sorted.size(), (size_t)sp.c1 * k);
             double clo[3] = {INFINITY, INFINITY, INFINITY}, chi[3] = {-INFINITY, -INFINITY, -INFINITY};
             for (size_t j = j0; j < j1; ++j)
@@ -171,8 +231,12 @@ AccelTables build_accel(const float *centers4, const float *radii, uint32_t n, u
                     clo[c] = std::min(clo[c], (double)centers4[4 * sorted[j] + c]);
                     chi[c] = std::max(chi[c], (double)centers4[4 * sorted[j] + c]);
                 }
-            const float cbf[3] = {(float)((clo[0] + chi[0]) / 2), (float)((clo[1] + chi[1]) / 2),
-                                  (float)((clo[2] + chi[2]) / 2)};
+            for (int c = 0; c < 3; ++c) ctr[c] = (clo[c] + chi[c]) / 2;
+            if (tree) {
+                nd = box_node(centers4, radii, sorted.data() + j0, j1 - j0);
+                return;
+            }
+            const float cbf[3] = {(float)ctr[0], (float)ctr[1], (float)ctr[2]};
             double rb = 0;
             for (size_t j = j0; j < j1; ++j) {
                 const uint32_t i = sorted[j];
@@ -187,19 +251,25 @@ AccelTables build_accel(const float *centers4, const float *radii, uint32_t n, u
             nd.cx = cbf[0];
             nd.cy = cbf[1];
             nd.cz = cbf[2];
-            nd.rb = round_up(rb);
-            nd.k1 = round_up(1.15 * (double)nd.rb * (double)nd.rb + 1e-5);
-            const double cb2 = (double)cbf[0] * cbf[0] + (double)cbf[1] * cbf[1] + (double)cbf[2] * cbf[2];
-            nd.cb2 = (float)cb2;
+            const float rbf = round_up(rb);
+            nd.k1 = round_up(1.15 * (double)rbf * (double)rbf + 1e-5);
+            // expanded line test (spt_path.h find_closest): K1'' = K1 +
+            // 4e-6 |Cb|^2 - c |Cb|^2 -- the kernel leaves c |Cb|^2 out of the per-lane sum
+            // and compares against K1'' instead (one add fewer)
+            const double cbb = (double)nd.cx * nd.cx + (double)nd.cy * nd.cy + (double)nd.cz * nd.cz;
+            nd.cb2 = (float)(kFlatScale * cbb);
+            nd.rb = round_up((double)nd.k1 + 4e-6 * cbb - (double)nd.cb2);
         };
         // Preorder emission, once per direction octant: siblings are ordered front to
         // back along the octant's diagonal, so a wave walking the layout of its
         // majority octant finds near hits first and the distance test culls more.
         // The top level sits under an implicit root (never tested).
         std::vector<std::vector<AccelNode>> bounds(levels.size());
+        std::vector<std::vector<std::array<double, 3>>> ctrs(levels.size());
         for (size_t lvl = 0; lvl < levels.size(); ++lvl) {
             bounds[lvl].resize(levels[lvl].size());
-            for (size_t j = 0; j < levels[lvl].size(); ++j) bound(levels[lvl][j], bounds[lvl][j]);
+            ctrs[lvl].resize(levels[lvl].size());
+            for (size_t j = 0; j < levels[lvl].size(); ++j) bound(levels[lvl][j], bounds[lvl][j], ctrs[lvl][j].data());
         }
         const uint32_t top = (uint32_t)levels.size() - 1;
         for (uint32_t oct = 0; oct < 8; ++oct) {
@@ -208,10 +278,10 @@ AccelTables build_accel(const float *centers4, const float *radii, uint32_t n, u
             auto ordered = [&](uint32_t lvl, size_t q0, size_t q1) {
                 std::vector<size_t> ix;
                 for (size_t q = q0; q < q1; ++q) ix.push_back(q);
-                if (levels.size() == 1) return ix;  // flat list: slot order (the kernel relies on it)
+                if (!tree) return ix;  // flat list: slot order (the kernel relies on it)
                 std::stable_sort(ix.begin(), ix.end(), [&](size_t a, size_t b) {
-                    const AccelNode &na = bounds[lvl][a], &nb = bounds[lvl][b];
-                    return sx * na.cx + sy * na.cy + sz * na.cz < sx * nb.cx + sy * nb.cy + sz * nb.cz;
+                    const std::array<double, 3> &ca = ctrs[lvl][a], &cb = ctrs[lvl][b];
+                    return sx * ca[0] + sy * ca[1] + sz * ca[2] < sx * cb[0] + sy * cb[1] + sz * cb[2];
                 });
                 return ix;
             };
@@ -230,25 +300,9 @@ AccelTables build_accel(const float *centers4, const float *radii, uint32_t n, u
                 t.nodes[me].skip = (uint32_t)(t.nodes.size() - base);
             };
             for (size_t j : ordered(top, 0, levels[top].size())) emit(emit, top, j);
-            // expanded node tests (spt_path.h find_closest): flat lists
-            // keep K1'' = K1' - c |Cb|^2 in rb and c |Cb|^2 in cb2; tree nodes F = Rb + 1e-4 (|Cb| + Rb)
-            // in rb and (c - kTreeNodeErr) |Cb|^2 in cb2
-            for (size_t q = base; q < t.nodes.size(); ++q) {
-                AccelNode &nd = t.nodes[q];
-                const double cbb = (double)nd.cx * nd.cx + (double)nd.cy * nd.cy + (double)nd.cz * nd.cz;
-                if (levels.size() == 1) {
-                    // K1'' = K1 + 4e-6 |Cb|^2 - c |Cb|^2: the kernel leaves c |Cb|^2 out of
-                    // the per-lane sum and compares against K1'' instead (one add fewer)
-                    nd.cb2 = (float)(kFlatScale * cbb);
-                    nd.rb = round_up((double)nd.k1 + 4e-6 * cbb - (double)nd.cb2);
-                } else {
-                    nd.rb = round_up((double)nd.rb + 1e-4 * (std::sqrt(cbb) + (double)nd.rb));
-                    nd.cb2 = (float)((kFlatScale - kTreeNodeErr) * cbb);
-                }
-            }
             if (oct == 0) t.n_nodes = (uint32_t)t.nodes.size();
             // pad node (the kernel prefetches one node past the layout)
-            t.nodes.push_back(AccelNode{0.f, 0.f, 0.f, -INFINITY, t.n_nodes + 1, kNoSlot, -INFINITY, 0.f});
+            t.nodes.push_back(pad_node(t.n_nodes + 1));
         }
     }
     // the kernel prefetches one always-group past the list and one node past the tree
@@ -257,7 +311,7 @@ AccelTables build_accel(const float *centers4, const float *radii, uint32_t n, u
         t.orig.push_back(0xFFFFFFFFu);
     }
     if (t.nodes.empty())  // no tree: one pad record per octant layout (n_nodes = 0)
-        for (int oct = 0; oct < 8; ++oct) t.nodes.push_back(AccelNode{0.f, 0.f, 0.f, -INFINITY, 1, kNoSlot, -INFINITY, 0.f});
+        for (int oct = 0; oct < 8; ++oct) t.nodes.push_back(pad_node(1));
     // member pretest constants of the cluster slots (dummies: K' = +inf never passes)
     t.kpre.assign(t.slots.size(), 0.f);
     double cm = 0;
@@ -268,8 +322,10 @@ AccelTables build_accel(const float *centers4, const float *radii, uint32_t n, u
         }
         const float4 &q = t.slots[j];
         t.kpre[j] = pretest_k(q);
-        cm = std::max(cm, std::sqrt((double)q.x * q.x + (double)q.y * q.y + (double)q.z * q.z) +
-                              std::sqrt((double)q.w));
+        // over the slot's r*r (the pretest) and the sphere's |r| (tree boxes' Bm)
+        cm = std::max({cm,
+                       std::sqrt((double)q.x * q.x + (double)q.y * q.y + (double)q.z * q.z) + std::sqrt((double)q.w),
+                       member_reach(centers4, radii, t.orig[j])});
     }
     t.pre_cm = round_up(cm * (1.0 + 1e-9));
     if (!(cm <= 1e15)) {
@@ -339,36 +395,49 @@ std::string validate_accel(const AccelTables &t, const float *centers4, const fl
                 if (nd.slot < cbase || (nd.slot - cbase) % t.leaf_slots || nd.slot + t.leaf_slots > t.slots.size())
                     return bad("layout %u node %u: leaf slot %u out of range", oct, i, nd.slot);
             }
-            // containment of every member below (Rb = max |Cm - Cb| + r over the members):
-            // flat lists: Rb <= sqrt((K1 - 1e-5) / 1.15), K1'' >= K1 + 4e-6 |Cb|^2 - cb2 and
-            // cb2 = c |Cb|^2; tree nodes: K1 >= 1.15 Rb^2 + 1e-5, F >= Rb + 1e-4 (|Cb| + Rb)
-            // and cb2 = (c - kTreeNodeErr) |Cb|^2
+            // containment of every member below.  Flat lists (Rb = max |Cm - Cb| + r over the
+            // members): Rb <= sqrt((K1 - 1e-5) / 1.15), K1'' >= K1 + 4e-6 |Cb|^2 - cb2 and
+            // cb2 = c |Cb|^2.  Trees: lo <= C - |r| - kBoxS Bm and hi >= C + |r| + kBoxS Bm on
+            // every axis, Bm = max |C| + |r| over the members (box_node's arithmetic)
             const bool flat = t.n_nodes == t.leaves;
-            const double cbb = (double)nd.cx * nd.cx + (double)nd.cy * nd.cy + (double)nd.cz * nd.cz;
-            if (flat && !(std::fabs((double)nd.cb2 - kFlatScale * cbb) <= 2e-7 * cbb &&
-                          (double)nd.rb >= (double)nd.k1 + 4e-6 * cbb - (double)nd.cb2))
-                return bad("layout %u node %u: flat-list |Cb|^2 or K1' wrong", oct, i);
-            if (!flat && !(std::fabs((double)nd.cb2 - (kFlatScale - kTreeNodeErr) * cbb) <= 1e-7 * cbb))
-                return bad("layout %u node %u: tree-node scaled |Cb|^2 wrong", oct, i);
-            double rbm = 0;
+            std::vector<uint32_t> below;
             for (uint32_t q = i; q < nd.skip; ++q) {
                 if (L[q].slot == kNoSlot) continue;
-                for (uint32_t k = 0; k < t.leaf_slots; ++k) {
-                    const uint32_t o = t.orig[L[q].slot + k];
-                    if (o == 0xFFFFFFFFu) continue;
-                    double d2 = 0;
-                    const double cb[3] = {nd.cx, nd.cy, nd.cz};
-                    for (int c = 0; c < 3; ++c) {
-                        const double dd = (double)centers4[4 * o + c] - cb[c];
-                        d2 += dd * dd;
-                    }
-                    rbm = std::max(rbm, std::sqrt(d2) + std::fabs((double)radii[o]));
-                }
+                for (uint32_t k = 0; k < t.leaf_slots; ++k)
+                    if (t.orig[L[q].slot + k] != 0xFFFFFFFFu) below.push_back(t.orig[L[q].slot + k]);
             }
-            const bool k1_ok = (double)nd.k1 >= 1.15 * rbm * rbm + 1e-5;
-            if (!k1_ok) return bad("layout %u node %u: a member lies outside the K1 bound", oct, i);
-            if (!flat && !((double)nd.rb >= rbm + 1e-4 * (std::sqrt(cbb) + rbm)))
-                return bad("layout %u node %u: a member lies outside the F bound", oct, i);
+            if (!flat) {
+                const double bm = node_reach(centers4, radii, below.data(), below.size());
+                const bool off = !(bm <= 1e15);
+                const float blo[3] = {nd.lox, nd.loy, nd.loz}, bhi[3] = {nd.hix, nd.hiy, nd.hiz};
+                for (uint32_t o : below)
+                    for (int c = 0; c < 3; ++c) {
+                        const double cc = centers4[4 * o + c], r = std::fabs((double)radii[o]);
+                        const bool in = off ? (blo[c] == -INFINITY && bhi[c] == INFINITY)
+                                            : ((double)blo[c] <= (cc - r) - kBoxS * bm &&
+                                               (double)bhi[c] >= (cc + r) + kBoxS * bm);
+                        if (!in) return bad("layout %u node %u: sphere %u outside the expanded box", oct, i, o);
+                    }
+                if (!(t.pre_cm >= bm || t.pre_cm == INFINITY))
+                    return bad("layout %u node %u: Bm above the scene bound", oct, i);
+                continue;
+            }
+            const double cbb = (double)nd.cx * nd.cx + (double)nd.cy * nd.cy + (double)nd.cz * nd.cz;
+            if (!(std::fabs((double)nd.cb2 - kFlatScale * cbb) <= 2e-7 * cbb &&
+                  (double)nd.rb >= (double)nd.k1 + 4e-6 * cbb - (double)nd.cb2))
+                return bad("layout %u node %u: flat-list |Cb|^2 or K1' wrong", oct, i);
+            double rbm = 0;
+            for (uint32_t o : below) {
+                double d2 = 0;
+                const double cb[3] = {nd.cx, nd.cy, nd.cz};
+                for (int c = 0; c < 3; ++c) {
+                    const double dd = (double)centers4[4 * o + c] - cb[c];
+                    d2 += dd * dd;
+                }
+                rbm = std::max(rbm, std::sqrt(d2) + std::fabs((double)radii[o]));
+            }
+            if (!((double)nd.k1 >= 1.15 * rbm * rbm + 1e-5))
+                return bad("layout %u node %u: a member lies outside the K1 bound", oct, i);
         }
         if (leaves != t.leaves) return bad("layout %u: %zu leaves, expected %u", oct, leaves, t.leaves);
         if (t.n_nodes == t.leaves)  // flat list: node i is leaf i, in slot order

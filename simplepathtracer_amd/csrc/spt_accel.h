@@ -10,19 +10,36 @@
 
 namespace spt {
 
-// One node of the cluster tree, 32 B (one s_load_dwordx8).  Nodes are stored in
-// depth-first preorder: the first child of an inner node is the next record, and
-// `skip` is the index just past the node's subtree.  Leaves are clusters.
+// One node of the cluster tree, 32 B (one s_load_dwordx8 or two ds_read_b128).
+// Nodes are stored in depth-first preorder: the first child of an inner node is the
+// next record, and `skip` is the index just past the node's subtree.  Leaves are
+// clusters.  Flat-list nodes (no inner nodes) carry a bounding sphere; tree nodes an
+// axis-aligned box.  skip/slot sit at dwords 4-5 in both forms.
 struct AccelNode {
-    float cx, cy, cz;  // bounding-sphere centre Cb
-    float k1;          // cull constant K1 = 1.15 Rb^2 + 1e-5 (rounded up)
-    uint32_t skip;     // next node when this one is culled (or is a leaf)
-    uint32_t slot;     // leaf: first of its leaf_slots slots; inner: kNoSlot
-    float rb;          // tree nodes: bounding radius Rb (rounded up);
-                       // flat lists: K1'' = K1 + 4e-6 |Cb|^2 - cb2 (rounded up), the expanded-form
-                       // margin less the node's c |Cb|^2 term
-    float cb2;         // |Cb|^2 (flat lists' expanded line test)
+    union {
+        struct {
+            float cx, cy, cz;  // flat list: bounding-sphere centre Cb
+            float k1;          // flat list: cull constant K1 = 1.15 Rb^2 + 1e-5 (rounded up)
+        };
+        struct {
+            float lox, loy, loz;  // tree: box lo = min (C - r) - kBoxS Bm (rounded down)
+            float hix;            // tree: box hi.x = max (C + r) + kBoxS Bm (rounded up)
+        };
+    };
+    uint32_t skip;  // next node when this one is culled (or is a leaf)
+    uint32_t slot;  // leaf: first of its leaf_slots slots; inner: kNoSlot
+    union {
+        struct {
+            float rb;   // flat list: K1'' = K1 + 4e-6 |Cb|^2 - cb2 (rounded up), the expanded-form
+                        // margin less the node's c |Cb|^2 term
+            float cb2;  // flat list: c |Cb|^2 (the expanded line test)
+        };
+        struct {
+            float hiy, hiz;  // tree: box hi.y, hi.z
+        };
+    };
 };
+static_assert(sizeof(AccelNode) == 32, "one 32-byte record per node");
 
 struct AccelTables {
     std::vector<float4> slots;      // {cx, cy, cz, r*r} in traversal order, dummy = r*r -inf

@@ -156,6 +156,15 @@ constexpr double kFlatScale = 1.0 - 1e-4;
 // Tree nodes store (kFlatScale - kTreeNodeErr) |Cb|^2: the near test's w is then a
 // lower bound of |Cb-o|^2 despite the expansion's rounding.
 constexpr double kTreeNodeErr = 3e-6;
+// Tree nodes are boxes expanded by kBoxS (|o| + Bm) on every side (Bm >= max |C| + r
+// over the node's members): a ray whose member test passes comes within
+// sqrt(r^2 + 2.6e-6 X^2) <= r + 1.6125e-3 X of the member's centre, X = |C - o|
+// <= |o| + Bm; the rest of the margin covers the slab arithmetic.
+// The node stores kBoxS Bm in its box, the lane adds kBoxS |o|.
+constexpr double kBoxS = 1.63e-3;
+// Reciprocal of a direction component: |d_i| is raised to at least 2^-20 first (no
+// inf/NaN in the slab arithmetic; sound by the margin argument of DESIGN.md §4.4).
+constexpr float kBoxMinDir = 0x1p-20f;
 constexpr uint32_t kNoSlot = 0xFFFFFFFFu;  // AccelNode::slot of inner nodes
 constexpr uint32_t kMiss = 0xFFFFFFFFu;    // Hit::idx when no sphere was hit
 

@@ -85,8 +85,16 @@ __device__ __forceinline__ uint32_t lane_rank(unsigned long long mask)
 struct Hit {
     uint32_t idx;        // slot of the winner (traversal order), kMiss = none
     float best;          // its squared distance
-    f3 p;                // its closest contact point
+    float t;             // its contact parameter: contact point o + d t (contact())
 };
+
+// CalculateRaySphereClosestContactPoint's point o + d t (Collision.hpp:49-56), in the
+// reference's operation order; recomputed after the cast from the winner's t (two
+// VGPRs fewer in the traversal than carrying the point), bit-identical
+__device__ __forceinline__ f3 contact(const f3 &o, const f3 &d, float t)
+{
+    return mk(o.x + d.x * t, o.y + d.y * t, o.z + d.z * t);
+}
 
 // Wave-diagnostic counters of the SPT_DIAG build.
 struct CastDiag {
@@ -109,7 +117,7 @@ __device__ __forceinline__ void update_member(bool pass, float tc, float hh, con
 {
     // CalculateRaySphereClosestContactPoint, Collision.hpp:19-27,49-56
     const float t = tc - sqrt_pos_normal(hh);
-    const f3 p = mk(o.x + d.x * t, o.y + d.y * t, o.z + d.z * t);
+    const f3 p = contact(o, d, t);
     const bool front = dod < dot(p, d);
     const bool ok = pass && front;
     const float ds = lensq(sub(o, p));
@@ -135,9 +143,7 @@ __device__ __forceinline__ void update_member(bool pass, float tc, float hh, con
     if (SPT_DIAG) dg.improving += __ballot(better) != 0ull ? 1 : 0;
     h.best = better ? ds : h.best;
     h.idx = better ? s : h.idx;
-    h.p.x = better ? p.x : h.p.x;
-    h.p.y = better ? p.y : h.p.y;
-    h.p.z = better ? p.z : h.p.z;
+    h.t = better ? t : h.t;
 }
 
 // RaySphereIntersection, Collision.hpp:9-17, in the reference's operation order:
@@ -283,7 +289,7 @@ __device__ __forceinline__ Hit find_closest(const AccelView &ac, const f3 &o, co
     Hit h;
     h.idx = kMiss;
     h.best = FLT_MAX;
-    h.p = o;
+    h.t = 0.f;
     const float dod = dot(o, d);
     cfloat *slots = (cfloat *)ac.slots;
     // Lanes whose direction is not unit length within 1e-6 (the glass branch
@@ -391,7 +397,8 @@ __device__ __forceinline__ Hit find_closest(const AccelView &ac, const f3 &o, co
         if (left != 0u) finish(ra, node_x(ra));
         return h;
     }
-    const float olen = __builtin_amdgcn_sqrtf(oo);  // |o|, for the front and near margins
+    // |o| (rounded up), for the box margin and the front and near slack
+    const float olen = __builtin_amdgcn_sqrtf(oo) * 1.000001f;
     if (TREE) {
         // the layout of the wave's majority direction octant (siblings front to back)
         const uint32_t nlive = (uint32_t)__popcll(live_mask);
@@ -400,23 +407,35 @@ __device__ __forceinline__ Hit find_closest(const AccelView &ac, const f3 &o, co
                              (2u * (uint32_t)__popcll(__ballot(active && d.z < 0.f)) > nlive ? 4u : 0u);
         if (!LDSN) nodes += (size_t)8 * (ac.n_nodes + 1) * oct;
     }
-    // Tree nodes {Cb, K1, skip, slot, F, c'|Cb|^2}: three conservative tests
-    // (DESIGN.md §4.4), without a square root per node; a lane may need the node
-    // only if all pass.  With tcb = Cb.d - o.d and
-    //   w = c' |Cb|^2 - 2c Cb.o + (c - 4.1e-6) |o|^2 <= c |Cb-o|^2   (c' = c - 3e-6),
-    //   line:  w - tcb^2 <= K1                (the ray's line passes within the bound)
-    //   front: tcb + 1e-4 |o| >= -F           (some member may lie in front, tc > 1e-3)
-    //   near:  w <= S^2,  S = (1.004 F + 2e-5 |o| + 1e-6 + sqrt(best (1 + 1e-4))) / 0.996
-    //          (some member's contact point may be closer than the lane's winner)
-    // with F >= Rb + 1e-4 (|Cb| + Rb).  15 VALU per node.
-    const float kq = (float)(1.0 / 0.996 * (1.0 + 1e-6));
-    const float c1004 = (float)(1.004 / 0.996 * (1.0 + 1e-6));
-    // near term of the lane's current winner, refreshed after every leaf test;
-    // inf while there is none (best = FLT_MAX: never culls)
-    auto near_term = [&](float best) {
-        return (__builtin_amdgcn_sqrtf(best * 1.0001f) * (1.0f + 0x1p-20f) + (2e-5f * olen + 1e-6f)) * kq;
+    // Tree nodes are boxes [lo, hi] already expanded by kBoxS Bm.  Per
+    // lane: the margin el = kBoxS |o| + 1e-6, the reciprocals ir of d (|d_i| raised to
+    // kBoxMinDir) and ql = -(o + el) ir, qh = (el - o) ir, so the entry and exit
+    // parameters of slab i along d are min / max of  fma(lo_i, ir_i, ql_i)  and
+    // fma(hi_i, ir_i, qh_i).  A lane may need the node iff
+    //   max(t_near, -eta) <= min(t_far, sbl)
+    // i.e. the slabs overlap (line), t_far >= -eta (front: a member may lie ahead) and
+    // t_near <= sbl (near: a member's contact point may be closer than the lane's
+    // winner), with eta = 1e-6 (|o| + Bs) + 1e-6 and
+    // sbl = sqrt(best) (1 + 1e-5) + 1e-5 (|o| + Bs) + 1e-6, Bs = pre_cm >= every Bm.
+    // 17 VALU per node.  Lanes with |o| > 1e15 never cull.
+    const float el = __builtin_fmaf((float)kBoxS, olen, 1e-6f);
+    auto rcp_dir = [](float x) {
+        const float m = __builtin_fmaxf(__builtin_fabsf(x), kBoxMinDir);
+        return __builtin_amdgcn_rcpf(__builtin_copysignf(m, x));
     };
-    float sbe = near_term(h.best);
+    const float irx = rcp_dir(d.x), iry = rcp_dir(d.y), irz = rcp_dir(d.z);
+    const float qlx = (-o.x - el) * irx, qly = (-o.y - el) * iry, qlz = (-o.z - el) * irz;
+    const float qhx = (el - o.x) * irx, qhy = (el - o.y) * iry, qhz = (el - o.z) * irz;
+    const float obs = olen + ac.pre_cm;
+    const float neta = -__builtin_fmaf(1e-6f, obs, 1e-6f);
+    const float kn = __builtin_fmaf(1e-5f, obs, 1e-6f);
+    const unsigned long long tree_nocull = nocull_mask | __ballot(active && !(oo <= 1e30f));
+    // near bound of the lane's current winner, refreshed after every leaf test;
+    // ~1.8e19 while there is none (best = FLT_MAX: never culls)
+    auto near_bound = [&](float best) {
+        return __builtin_fmaf(__builtin_amdgcn_sqrtf(best), 1.00001f, kn);
+    };
+    float sbl = near_bound(h.best);
     // node record q of node j: a scalar load, or a broadcast LDS read
     auto ldn = [&](uint32_t j, int q) -> uint32_t { return LDSN ? lnodes[8 * j + q] : nodes[8 * j + q]; };
     uint32_t i = 0;
@@ -424,8 +443,8 @@ __device__ __forceinline__ Hit find_closest(const AccelView &ac, const f3 &o, co
 #pragma unroll
     for (int q = 0; q < 8; ++q) nb[q] = ldn(0, q);
     while (i < ac.n_nodes) {
-        const float bx = __uint_as_float(nb[0]), by = __uint_as_float(nb[1]), bz = __uint_as_float(nb[2]);
-        const float k1 = __uint_as_float(nb[3]), fr = __uint_as_float(nb[6]), cb2n = __uint_as_float(nb[7]);
+        const float lx = __uint_as_float(nb[0]), ly = __uint_as_float(nb[1]), lz = __uint_as_float(nb[2]);
+        const float hx = __uint_as_float(nb[3]), hy = __uint_as_float(nb[6]), hz = __uint_as_float(nb[7]);
         const uint32_t skip = LDSN ? __builtin_amdgcn_readfirstlane(nb[4]) : nb[4];
         const uint32_t leaf_slot = LDSN ? __builtin_amdgcn_readfirstlane(nb[5]) : nb[5];
         // LDS walk: this node's scalars before the successor's reads are issued (a
@@ -437,17 +456,14 @@ __device__ __forceinline__ Hit find_closest(const AccelView &ac, const f3 &o, co
         for (int q = 0; q < 8; ++q) nb[q] = ldn(i + 1, q);
         // LDS walk: keep the successor's ds_reads ahead of this node's tests
         if (LDSN) __builtin_amdgcn_sched_barrier(0);
-        const float tcb = __builtin_fmaf(bx, d.x, __builtin_fmaf(by, d.y, __builtin_fmaf(bz, d.z, -dod)));
-        // Cb.o from o itself (not -2c o: two VGPRs fewer keep the kernel at 64)
-        const float cbo = __builtin_fmaf(bx, o.x, __builtin_fmaf(by, o.y, bz * o.z));
-        const float w = __builtin_fmaf(cbo, m2c, qo) + cb2n;
-        const float x = __builtin_fmaf(-tcb, tcb, w);
-        const float sn = __builtin_fmaf(fr, c1004, sbe);
-        const bool line = x <= k1;
-        const bool front = __builtin_fmaf(1e-4f, olen, tcb) >= -fr;
-        const bool near = !(w > sn * sn);
-        // the AND of the three compare ballots: each is the compare's own lane mask
-        const unsigned long long mm = (__ballot(line) & __ballot(front) & __ballot(near) & live_mask) | nocull_mask;
+        const float ax = __builtin_fmaf(lx, irx, qlx), bx = __builtin_fmaf(hx, irx, qhx);
+        const float ay = __builtin_fmaf(ly, iry, qly), by = __builtin_fmaf(hy, iry, qhy);
+        const float az = __builtin_fmaf(lz, irz, qlz), bz = __builtin_fmaf(hz, irz, qhz);
+        const float tn = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(ax, bx), __builtin_fminf(ay, by)),
+                                         __builtin_fmaxf(__builtin_fminf(az, bz), neta));
+        const float tf = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(ax, bx), __builtin_fmaxf(ay, by)),
+                                         __builtin_fminf(__builtin_fmaxf(az, bz), sbl));
+        const unsigned long long mm = (__ballot(tn <= tf) & live_mask) | tree_nocull;
         const bool leaf = leaf_slot != kNoSlot;
         if (SPT_DIAG) {
             dg.nodes += 1;
@@ -459,7 +475,7 @@ __device__ __forceinline__ Hit find_closest(const AccelView &ac, const f3 &o, co
         }
         if (mm != 0ull && leaf) {
             test_leaf<LEAF>(slots, ac.orig, leaf_slot, o, d, dod, h, dg);
-            sbe = near_term(h.best);
+            sbl = near_bound(h.best);
         }
         const uint32_t next = (mm != 0ull && !leaf) ? i + 1 : skip;
         if (next != i + 1) {
@@ -669,7 +685,7 @@ __device__ __forceinline__ void shade_step(const RenderArgs &a, Path &ps, const 
         // first hit (lines 23-26), the diffuse loop (30-33) and the mirror (41-43)
         const float4 cs = hit[idx];
         const f3 C = mk(cs.x, cs.y, cs.z);
-        ps.o = h.p;
+        ps.o = contact(ps.o, ps.d, h.t);
         const f3 nrm = normalize(sub(ps.o, C));
         f3 rv = rv_coop;
         f3 base;
@@ -689,7 +705,7 @@ __device__ __forceinline__ void shade_step(const RenderArgs &a, Path &ps, const 
         ps.d = normalize(add(base, rv));
     }
     if (refr) {
-        ps.o = h.p;
+        ps.o = contact(ps.o, ps.d, h.t);
         refract_event(a, ps, idx);
         spec_event = true;
     }

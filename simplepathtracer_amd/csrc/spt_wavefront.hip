@@ -110,7 +110,7 @@ __global__ __launch_bounds__(256) void wf_extend(WfArgs w, uint32_t n, uint32_t 
     const Hit h = find_closest<TREE, LEAF>(w.ra.scene.accel, o, d, act, dg);
     uint32_t cat = kWfCats;  // none
     if (act) {
-        w.hit[i] = make_float4(h.p.x, h.p.y, h.p.z, __uint_as_float(h.idx));
+        w.hit[i] = make_float4(h.t, 0.f, 0.f, __uint_as_float(h.idx));
         // category of the next shading step: the material switch of
         // TraceAndSampleColor (SingleThreadPathTracer.hpp:98-111) or the diffuse loop
         cat = 0;  // sky / miss / unknown material
@@ -158,7 +158,7 @@ __global__ __launch_bounds__(256) void wf_shade(WfArgs w, uint32_t cat, uint32_t
     Hit h;
     h.idx = __float_as_uint(h4.w);
     h.best = 0.f;
-    h.p = mk(h4.x, h4.y, h4.z);
+    h.t = h4.x;
     unsigned long long done = 0, dropped = 0;
     shade_step(w.ra, ps, h, act, done, dropped, s_lds + (threadIdx.x & ~63u));
     if (act) {

@@ -76,6 +76,35 @@ __device__ __forceinline__ float4 ld_uniform(cfloat *p, uint32_t i)
     return make_float4(p[4 * i + 0], p[4 * i + 1], p[4 * i + 2], p[4 * i + 3]);
 }
 
+// v_min/max(3)_f32 without the compiler's IEEE-mode canonicalisation of operands it
+// cannot prove canonical (loop-carried or negated values: one v_max_f32 x, x each per
+// use).  No operand here is a signalling NaN, so the raw instructions give the same
+// result as fminf/fmaxf.
+__device__ __forceinline__ float max_raw(float a, float b)
+{
+    float r;
+    asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ float min_raw(float a, float b)
+{
+    float r;
+    asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ float max3_raw(float a, float b, float c)
+{
+    float r;
+    asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+__device__ __forceinline__ float min3_raw(float a, float b, float c)
+{
+    float r;
+    asm("v_min3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
 __device__ __forceinline__ uint32_t lane_rank(unsigned long long mask)
 {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
@@ -418,7 +447,7 @@ __device__ __forceinline__ Hit find_closest(const AccelView &ac, const f3 &o, co
     // winner), with eta = 1e-6 (|o| + Bs) + 1e-6 and
     // sbl = sqrt(best) (1 + 1e-5) + 1e-5 (|o| + Bs) + 1e-6, Bs = pre_cm >= every Bm.
     // 17 VALU per node.  Lanes with |o| > 1e15 never cull.
-    const float el = __builtin_fmaf((float)kBoxS, olen, 1e-6f);
+        const float el = __builtin_fmaf((float)kBoxS, olen, 1e-6f);
     auto rcp_dir = [](float x) {
         const float m = __builtin_fmaxf(__builtin_fabsf(x), kBoxMinDir);
         return __builtin_amdgcn_rcpf(__builtin_copysignf(m, x));
@@ -459,10 +488,10 @@ __device__ __forceinline__ Hit find_closest(const AccelView &ac, const f3 &o, co
         const float ax = __builtin_fmaf(lx, irx, qlx), bx = __builtin_fmaf(hx, irx, qhx);
         const float ay = __builtin_fmaf(ly, iry, qly), by = __builtin_fmaf(hy, iry, qhy);
         const float az = __builtin_fmaf(lz, irz, qlz), bz = __builtin_fmaf(hz, irz, qhz);
-        const float tn = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(ax, bx), __builtin_fminf(ay, by)),
-                                         __builtin_fmaxf(__builtin_fminf(az, bz), neta));
-        const float tf = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(ax, bx), __builtin_fmaxf(ay, by)),
-                                         __builtin_fminf(__builtin_fmaxf(az, bz), sbl));
+        const float tn = max3_raw(__builtin_fminf(ax, bx), __builtin_fminf(ay, by),
+                                  max_raw(__builtin_fminf(az, bz), neta));
+        const float tf = min3_raw(__builtin_fmaxf(ax, bx), __builtin_fmaxf(ay, by),
+                                  min_raw(__builtin_fmaxf(az, bz), sbl));
         const unsigned long long mm = (__ballot(tn <= tf) & live_mask) | tree_nocull;
         const bool leaf = leaf_slot != kNoSlot;
         if (SPT_DIAG) {

@@ -7,26 +7,31 @@
 //  * "always" spheres (large radius: the ground r = 1e6, the three r = 3 balls of
 //    GenerateSpheres) are tested for every ray;
 //  * the small spheres are sorted along a Morton curve and cut into clusters of
-//    k <= 8 members (8 slots each, dummies pad), the leaves of a tree whose inner
-//    nodes group `branching` consecutive clusters; every node carries a bounding
-//    sphere of all member spheres below it (Cb, Rb >= |Cm - Cb| + r_m).  The tree
-//    is stored in preorder with skip links, so the wave-uniform traversal needs no
-//    stack: enter a node (next record) if any lane may pass, else jump to `skip`.
+//    k <= 8 members (8 slots each, dummies pad).  Up to 64 clusters form a flat list
+//    whose nodes carry a bounding sphere of their members (Cb, Rb >= |Cm - Cb| + r_m);
+//    beyond that the clusters are the leaves of a tree whose inner nodes group
+//    `branching` consecutive clusters, every tree node carrying an axis-aligned box
+//    of all member spheres below it, expanded by kBoxS Bm (Bm = max |C| + r over
+//    those members).  The tree is stored in preorder with skip links, so the
+//    wave-uniform traversal needs no stack: enter a node (next record) if any lane
+//    may pass, else jump to `skip`.
 //
 // Cull conditions, derived in DESIGN.md §4.4 from an fp32 error analysis of the
 // member test and of the node test for a ray whose computed |d|^2 is within 1e-6
 // of 1 (other lanes never cull):
-//   line:  keep iff d2b = |Cb-o|^2 - ((Cb-o).d)^2 <= K1 + 1e-4 |Cb-o|^2,
+//   flat line: keep iff d2b = |Cb-o|^2 - ((Cb-o).d)^2 <= K1 + 1e-4 |Cb-o|^2,
 //          K1 = 1.15 Rb^2 + 1e-5 (rounded up);  derived need 1.0835 Rb^2 + 3.6e-5 |Cb-o|^2
-//   front: cull iff (Cb-o).d < -(Rb + 1e-4 (|Cb-o| + Rb))      (tree nodes)
-//   near:  cull iff Lc > 0 and Lc^2 > best (1 + 1e-4),
-//          Lc = |Cb-o| - Rb - 4e-3 (|Cb-o| + Rb) - 2e-5 |o| - 1e-6   (tree nodes)
-// They use only the containment of the members (Rb >= |Cm - Cb| + r_m), so they
-// hold for inner nodes as for clusters; nodes failing them for every lane of a
-// wave are skipped with their subtree.  Tests run in traversal order, so the
-// closest hit is selected by the lexicographic (distance, original index)
-// minimum, which equals the reference's strict-'>' first-index-wins scan.
-// Eight preorder layouts, one per direction octant, differ only in sibling order.
+//   tree box: keep iff the ray's line crosses the box grown by kBoxS |o| more (a
+//          passing member's centre lies within r + 1.6125e-3 |C - o| of the line),
+//          at a parameter >= -1e-6 (|o| + Bs) (a member may lie ahead) and entering it
+//          at most sqrt(best) (1 + 1e-5) + 1e-5 (|o| + Bs) along the ray (a member's
+//          contact point may beat the lane's winner), Bs = pre_cm >= every Bm
+// They use only the containment of the members, so they hold for inner nodes as
+// for clusters; nodes failing them for every lane of a wave are skipped with their
+// subtree.  Tests run in traversal order, so the closest hit is selected by the
+// lexicographic (distance, original index) minimum, which equals the reference's
+// strict-'>' first-index-wins scan.  Eight preorder layouts, one per direction
+// octant, differ only in sibling order.
 #include "spt_accel.h"
 #include "spt_internal.h"
 

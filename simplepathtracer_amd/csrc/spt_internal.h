@@ -153,9 +153,6 @@ constexpr uint32_t kFlatLeafSlots = 4; // slots of a flat-list leaf holding <= 4
 // in by scaling the expanded |Cb-o|^2 by kFlatScale = 1 - 1e-4; nodes store
 // kFlatScale |Cb|^2.
 constexpr double kFlatScale = 1.0 - 1e-4;
-// Tree nodes store (kFlatScale - kTreeNodeErr) |Cb|^2: the near test's w is then a
-// lower bound of |Cb-o|^2 despite the expansion's rounding.
-constexpr double kTreeNodeErr = 3e-6;
 // Tree nodes are boxes expanded by kBoxS (|o| + Bm) on every side (Bm >= max |C| + r
 // over the node's members): a ray whose member test passes comes within
 // sqrt(r^2 + 2.6e-6 X^2) <= r + 1.6125e-3 X of the member's centre, X = |C - o|

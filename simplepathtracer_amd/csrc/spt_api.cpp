@@ -491,16 +491,17 @@ int upload(spt_ctx *ctx, T **p, size_t *cap, const std::vector<T> &v)
     return SPT_OK;
 }
 
-// Traversal shape for the current scene: a flat list of 4-sphere clusters for
-// small scenes (the wave enters most clusters anyway, and 4-slot leaves measured
-// faster there), a 4-ary tree of 8-sphere clusters once that list gets long.
+// Traversal shape for the current scene: a 4-ary tree of boxes over 8-sphere
+// clusters (config 2: 14 650 Msamples/s against 13 950 for round 1's flat list of
+// 4-sphere clusters under bounding spheres); the flat list remains
+// selectable (spt_set_cluster_tree(ctx, 0)).  Scenes of <= 32 spheres are tested
+// brute force (build_accel).
 struct Shape {
     uint32_t k, branching, leaf_slots;
 };
 Shape resolve_shape(const spt_ctx *ctx)
 {
-    const bool tree = ctx->tree_branching == SPT_TREE_AUTO ? ctx->n / spt::kClusterSlots > 64
-                                                           : ctx->tree_branching >= 2;
+    const bool tree = ctx->tree_branching == SPT_TREE_AUTO ? true : ctx->tree_branching >= 2;
     Shape sh;
     sh.k = ctx->cluster_k != SPT_CLUSTER_AUTO ? ctx->cluster_k : tree ? spt::kClusterSlots : spt::kFlatLeafSlots;
     sh.branching = tree ? (ctx->tree_branching == SPT_TREE_AUTO ? 4u : ctx->tree_branching) : 0u;

@@ -60,6 +60,9 @@ constexpr uint32_t kLdsBlock = SPT_LDS_BLOCK;
 #define SPT_LDS_NODES 2432
 #endif
 constexpr uint32_t kLdsNodeRecords = SPT_LDS_NODES;
+// smallest tree walked from LDS: below it the 8 octant layouts (64 nodes: 16 KiB) fit
+// the scalar cache
+constexpr uint32_t kLdsMinNodes = 64;
 
 // One kernel per traversal shape (flat list of 4- or 8-slot leaves, tree of
 // 8-slot leaves), each with its own register allocation; launch_render picks.
@@ -367,7 +370,10 @@ static void lds_tree_shape(int *per_cu, int *num_cu)
 hipError_t launch_render(const RenderArgs &a, LaunchShape &sh, hipStream_t s)
 {
     const uint32_t div = sh.div ? sh.div : 1u;
-    if (a.scene.accel.tree && a.scene.accel.n_nodes + 1u <= kLdsNodeRecords) {
+    // trees of >= kLdsMinNodes nodes walk an LDS copy of the node table (config 5);
+    // smaller ones stay in the scalar cache (all 8 octant layouts: config 2's 26-node
+    // tree is 6.7 KB), where the 256-thread kernel overlaps frames in flight better
+    if (a.scene.accel.tree && a.scene.accel.n_nodes >= kLdsMinNodes && a.scene.accel.n_nodes + 1u <= kLdsNodeRecords) {
         // all resident blocks (divided among the host calls in flight), or fewer when the
         // launch has under 2 claims per wave (render_grid's rule)
         int per_cu = 0, num_cu = 0;

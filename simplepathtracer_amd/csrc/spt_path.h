@@ -342,9 +342,6 @@ __device__ __forceinline__ Hit find_closest(const AccelView &ac, const f3 &o, co
         }
     }
     const unsigned long long live_mask = __ballot(active);
-    // node masks are formed as (ballot(test) & live) | nocull: the ballot of a
-    // compare is the compare's own lane mask, with no VALU round trip
-    const unsigned long long nocull_mask = __ballot(no_cull);
     cuint *nodes = (cuint *)ac.nodes;
     if (!TREE) {
         // flat list: node i is leaf i.  The line test in expanded form, with FMAs
@@ -458,7 +455,9 @@ __device__ __forceinline__ Hit find_closest(const AccelView &ac, const f3 &o, co
     const float obs = olen + ac.pre_cm;
     const float neta = -__builtin_fmaf(1e-6f, obs, 1e-6f);
     const float kn = __builtin_fmaf(1e-5f, obs, 1e-6f);
-    const unsigned long long tree_nocull = nocull_mask | __ballot(active && !(oo <= 1e30f));
+    // tree node masks are (ballot(test) & live) | nocull: the ballot of a compare is
+    // the compare's own lane mask, with no VALU round trip
+    const unsigned long long tree_nocull = __ballot(no_cull || (active && !(oo <= 1e30f)));
     // near bound of the lane's current winner, refreshed after every leaf test;
     // ~1.8e19 while there is none (best = FLT_MAX: never culls)
     auto near_bound = [&](float best) {

@@ -129,7 +129,12 @@ def dropin_bench(w, h, spp, bounces, frames, tcs):
             if r.returncode != 0:
                 raise RuntimeError(f"dropin harness failed: {r.stderr[-400:]}")
             sec = float(r.stdout.split("seconds=")[1].split()[0])
-            out[f"{'task' if task else 'segment'}_tc{tc}"] = round(w * h * spp * frames / sec / 1e6, 3)
+            key = f"{'task' if task else 'segment'}_tc{tc}"
+            out[key] = round(w * h * spp * frames / sec / 1e6, 3)
+            if "batches=" in r.stdout:  # calls per batched launch, over all frames run
+                calls = int(r.stdout.split("calls=")[1].split()[0])
+                batches = int(r.stdout.split("batches=")[1].split()[0])
+                out[key + "_calls_per_batch"] = round(calls / max(batches, 1), 2)
     return out
 
 

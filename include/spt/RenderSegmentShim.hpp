@@ -14,7 +14,8 @@
 // reported on stderr and aborts.  Sampling uses the keyed per-(pixel, sample)
 // stream seeded with spt_shim::seed (default 1; SPT_SEED overrides) instead of
 // the clock-seeded thread_local splitmix (Random.hpp:86-93).  Concurrent RenderJob
-// threads run on the GPU together (each call gets its own stream and workspace);
+// threads are rendered together (the library batches their tiles into shared
+// launches, and writes into the page-locked g_data in place);
 // SPT_DEVICES=0,1,... spreads them over several devices.
 #pragma once
 
@@ -108,7 +109,8 @@ inline void sync_globals()
     check(ctx, spt_set_camera(ctx, view, eye, sky), "spt_set_camera");
     check(ctx, spt_set_params(ctx, g_width, g_height, g_samples, g_bounces, seed), "spt_set_params");
     last.swap(key);
-    // page-lock g_data once (best effort): the per-call copy-back becomes a direct DMA
+    // page-lock g_data once (best effort): batched calls then write their tiles' bytes
+    // into it in place (no copy-back)
     static const void *pinned = nullptr;
     if (g_data && pinned != g_data && spt_pin_host(ctx, g_data, (size_t)g_width * g_height * 3) == SPT_OK)
         pinned = g_data;

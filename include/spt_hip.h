@@ -19,8 +19,8 @@
  * Plain C types only.  Every function returns an spt_status; on failure
  * spt_last_error() describes why.  A context is safe to use from several host
  * threads: its state is guarded by a lock, and concurrent render calls (the
- * reference's RenderJob threads) each get their own stream and workspace, so they
- * run on the GPU together.
+ * reference's RenderJob threads) are rendered together: the calls that arrive while
+ * one batch renders form the next (one render + one fold launch over their tiles).
  */
 #ifndef SPT_HIP_H
 #define SPT_HIP_H
@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define SPT_ABI_VERSION 3
+#define SPT_ABI_VERSION 4
 
 /* Only the functions below are exported from libspt_hip.so (built with
  * -fvisibility=hidden), so several builds can be loaded side by side. */
@@ -87,6 +87,8 @@ typedef struct spt_stats {
                               improve some lane's winner, RaySphereIntersection
                               evaluations for live lanes (lane-tests), member pretests
                               for live lanes (lane-pretests) */
+    uint64_t batches;       /* batched launches of concurrent spt_render_segment[_task] calls */
+    uint64_t batched_calls; /* calls rendered in them */
 } spt_stats;
 
 SPT_API int spt_abi_version(void);

@@ -52,6 +52,29 @@ struct HostSlot {
     size_t stage_cap = 0;
     bool busy = false;
 };
+// Batched host calls: concurrent spt_render_segment[_task] calls are rendered together,
+// one render + one fold launch per batch over a table of rectangles (BatchRect), so
+// the reference's RenderJob threads (Renderer.hpp:242-302) -- 16 tiles a frame at the
+// shipped g_maxThreads = 4, 1 024 at tc = 2 * 16 cores -- do not each pay a launch,
+// its fold, its tail and its own synchronisation.  Two batch sets: while one batch
+// renders, the calls arriving meanwhile form the next.
+constexpr uint32_t kMaxBatchSets = 8;
+struct BatchSet {
+    hipStream_t stream = nullptr;
+    spt::BatchRect *d_rects = nullptr, *h_rects = nullptr;  // device table, pinned host copy
+    size_t rects_cap = 0, h_rects_cap = 0;
+    float4 *d_stage = nullptr;  // float4 outputs of the batch's rectangles, concatenated
+    size_t stage_cap = 0;
+    bool busy = false;
+};
+struct BatchReq {
+    int mode;
+    uint32_t yB, yE, xB, xE;
+    float *rgba;
+    uint8_t *g_data;
+    int rc;
+    bool launched, done;
+};
 struct Workspace {
     hipStream_t stream = nullptr;  // key
     float *d_samples = nullptr;    // per-sample slots of the current batch
@@ -111,7 +134,13 @@ struct spt_ctx {
     uint8_t *d_frame8 = nullptr;
     size_t frame8_cap = 0;
 
-    std::vector<void *> pinned;  // host buffers registered by spt_pin_host
+    // host buffers registered by spt_pin_host, with their device-side addresses
+    struct Pinned {
+        void *ptr;
+        size_t bytes;
+        uint8_t *dev;
+    };
+    std::vector<Pinned> pinned;
 
     // host-call slots (render_segment_host), created on demand up to host_slots
     std::vector<HostSlot *> slots;
@@ -119,6 +148,14 @@ struct spt_ctx {
     uint32_t host_slots = kMaxHostSlots;
     uint32_t host_grid_div = 0;  // 0: half the slots in use (SPT_HOST_GRID_DIV overrides)
     std::atomic<int> inflight{0};  // host calls in progress on this device
+    // batched host calls (render_batched); SPT_BATCH=0 renders every call on its own
+    bool batching = true;
+    std::vector<BatchReq *> batch_pending;
+    bool batch_leader = false;  // a caller is assembling the next batch
+    BatchSet bsets[kMaxBatchSets];
+    uint32_t batch_sets = 2;  // batches in flight at once (SPT_BATCH_SETS)
+    std::condition_variable batch_cv;
+    uint64_t batches = 0, batched_calls = 0;
 
     // multi-device context (spt_ctx_create_multi): member contexts of the other devices,
     // each with its own scene copy; this context is member 0
@@ -588,6 +625,228 @@ spt_ctx *pick_member(spt_ctx *ctx)
     return best;
 }
 
+// Bytes of per-sample slots a rectangle needs in one batch (all spp samples at once).
+uint64_t batch_slot_bytes(const spt_ctx *ctx, int mode, uint64_t npix)
+{
+    return npix * ctx->spp * (mode == SPT_MODE_SEGMENT ? 3u : 4u) * sizeof(float);
+}
+
+// Enqueue one batch on bs->stream: rectangle table, render, fold, the copy-back of
+// every request's outputs.  Called with ctx->mu held.
+int launch_batch(spt_ctx *ctx, BatchSet *bs, const std::vector<BatchReq *> &batch)
+{
+    const int mode = batch[0]->mode;
+    const uint32_t slot_floats = mode == SPT_MODE_SEGMENT ? 3u : 4u;
+    const uint32_t spp = ctx->spp, W = ctx->W, H = ctx->H;
+    uint64_t items = 0, pix = 0;
+    bool any_rgba = false, any_g = false;
+    for (const BatchReq *r : batch) {
+        const uint64_t np = (uint64_t)(r->xE - r->xB) * (r->yE - r->yB);
+        items += np * spp;
+        pix += np;
+        any_rgba |= r->rgba != nullptr;
+        any_g |= r->g_data != nullptr;
+    }
+    const uint32_t claim = claim_size(ctx, items);
+    // rectangles' items start at claim multiples (a claim never spans two)
+    const size_t n = batch.size();
+    int rc = SPT_OK;
+    if (bs->h_rects_cap < n) {
+        if (bs->h_rects) HIP_TRY(ctx, hipHostFree(bs->h_rects));
+        bs->h_rects = nullptr;
+        bs->h_rects_cap = 0;
+        HIP_TRY(ctx, hipHostMalloc((void **)&bs->h_rects, n * sizeof(spt::BatchRect)));
+        bs->h_rects_cap = n;
+    }
+    if ((rc = ensure(ctx, &bs->d_rects, &bs->rects_cap, n))) return rc;
+    if (any_g && (rc = ensure(ctx, &ctx->d_frame8, &ctx->frame8_cap, (size_t)W * H * 3))) return rc;
+    uint64_t item = 0, slot = 0, px = 0;
+    for (size_t i = 0; i < n; ++i) {
+        const BatchReq *r = batch[i];
+        spt::BatchRect &b = bs->h_rects[i];
+        const uint32_t w = r->xE - r->xB, rows = r->yE - r->yB, np = w * rows;
+        item = (item + claim - 1) / claim * claim;
+        b.item_off = (uint32_t)item;
+        b.item_end = (uint32_t)(item + (uint64_t)np * spp);
+        b.slot_off = (uint32_t)slot;
+        b.pix_off = (uint32_t)px;
+        b.x0 = r->xB;
+        b.y0 = r->yB;
+        b.w = w;
+        b.rows = rows;
+        b.npix = np;
+        b.alias = mode == SPT_MODE_TASK && rows != w ? 1u : 0u;
+        // g_data inside a page-locked buffer (spt_pin_host; the C++ shim pins it): the
+        // fold writes the bytes in place, no copy-back
+        b.rgb8 = nullptr;
+        if (r->g_data) {
+            b.rgb8 = ctx->d_frame8;
+            const size_t fb = (size_t)W * H * 3;
+            for (const spt_ctx::Pinned &p : ctx->pinned) {
+                const uint8_t *base = (const uint8_t *)p.ptr;
+                if (p.dev && r->g_data >= base && r->g_data + fb <= base + p.bytes) {
+                    b.rgb8 = p.dev + (r->g_data - base);
+                    break;
+                }
+            }
+        }
+        b.div_band = spt::make_fastdiv(rows >= 8 ? 8u * w * spp : 1u);
+        b.div_tile = spt::make_fastdiv(64u * spp);
+        item = b.item_end;
+        slot += (uint64_t)np * spp;
+        px += np;
+    }
+    Workspace *w = workspace_for(ctx, bs->stream);
+    if (!w) return SPT_ERR_STATE;
+    if ((rc = ensure(ctx, &w->d_samples, &w->samples_cap, (size_t)slot * slot_floats))) return rc;
+    if (any_rgba && (rc = ensure(ctx, &bs->d_stage, &bs->stage_cap, (size_t)pix))) return rc;
+    const hipStream_t s = bs->stream;
+    HIP_TRY(ctx, hipMemcpyAsync(bs->d_rects, bs->h_rects, n * sizeof(spt::BatchRect), hipMemcpyHostToDevice, s));
+
+    spt::RenderArgs ra{};
+    ra.scene = spt::DeviceScene{ctx->d_shade, ctx->d_mat, ctx->n, ctx->accel};
+    ra.cam = ctx->cam;
+    ra.width = W;
+    ra.height = H;
+    ra.bounces = ctx->bounces;
+    ra.mode = (uint32_t)mode;
+    ra.seed_key = fmix64(ctx->seed);
+    ra.map = spt::RowMap{0u, 1u, 1u, 1u, 0u, 0u, 1u};  // per rectangle (BatchRect)
+    ra.div_strip = spt::make_fastdiv(1u);
+    ra.npix = (uint32_t)pix;
+    ra.spp_batch = spp;
+    ra.s0 = 0;
+    ra.n_items = (uint32_t)item;
+    ra.claim = claim;
+    ra.div_band = ra.div_tile = spt::make_fastdiv(1u);
+    ra.samples = w->d_samples;
+    ra.slot_floats = slot_floats;
+    ra.head = w->d_head;
+    ra.counters = ctx->d_counters;
+    ra.rects = bs->d_rects;
+    ra.n_rects = (uint32_t)n;
+
+    HIP_TRY(ctx, hipMemsetAsync(w->d_head, 0, sizeof(uint32_t), s));
+    if (!ctx->ref_recorded) {
+        HIP_TRY(ctx, hipEventRecord(ctx->ref_ev, s));
+        ctx->ref_recorded = true;
+    }
+    EventPair ev = get_pair(ctx);
+    HIP_TRY(ctx, hipEventRecord(ev.a, s));
+    spt::LaunchShape sh{render_grid(ctx, ra.n_items, claim, 1u), ctx->block, 1u, 0, 0};
+    HIP_TRY(ctx, spt::launch_render(ra, sh, s));
+    ctx->last_grid = sh.ran_grid;
+    ctx->last_block = sh.ran_block;
+    HIP_TRY(ctx, hipEventRecord(ev.b, s));
+    ctx->pending_render.push_back(ev);
+    ctx->launches++;
+
+    spt::FoldArgs fa{};
+    fa.samples = w->d_samples;
+    fa.slot_floats = slot_floats;
+    fa.out_rgba = any_rgba ? bs->d_stage : nullptr;
+    fa.out_rgb8 = any_g ? ctx->d_frame8 : nullptr;
+    fa.width = W;
+    fa.height = H;
+    fa.npix = (uint32_t)pix;
+    fa.spp_batch = spp;
+    fa.spp_total = spp;
+    fa.s_done = spp;
+    fa.first = fa.last = 1;
+    fa.mode = mode;
+    fa.rects = bs->d_rects;
+    fa.n_rects = (uint32_t)n;
+    EventPair ef = get_pair(ctx);
+    HIP_TRY(ctx, hipEventRecord(ef.a, s));
+    HIP_TRY(ctx, spt::launch_fold(fa, s));
+    HIP_TRY(ctx, hipEventRecord(ef.b, s));
+    ctx->pending_fold.push_back(ef);
+
+    for (size_t i = 0; i < n; ++i) {
+        const BatchReq *r = batch[i];
+        const spt::BatchRect &b = bs->h_rects[i];
+        if (r->rgba)
+            HIP_TRY(ctx, hipMemcpyAsync(r->rgba, bs->d_stage + b.pix_off, (size_t)b.npix * sizeof(float4),
+                                        hipMemcpyDeviceToHost, s));
+        if (r->g_data && b.rgb8 == ctx->d_frame8) {
+            // rows y in [yB, yE) live at g_data rows H-1-y: one band, xB.. per row
+            const size_t pitch = (size_t)W * 3;
+            const size_t off = (size_t)(H - r->yE) * pitch + (size_t)r->xB * 3;
+            HIP_TRY(ctx, hipMemcpy2DAsync(r->g_data + off, pitch, ctx->d_frame8 + off, pitch, (size_t)b.w * 3, b.rows,
+                                          hipMemcpyDeviceToHost, s));
+        }
+    }
+    return SPT_OK;
+}
+
+// One RenderSegment / RenderSegmentTask call through the batcher: the call joins the
+// pending list; a caller that finds no batch being assembled becomes the leader,
+// waits for a free batch set, takes every pending call of the first one's mode (up
+// to the workspace), launches them as one batch and waits for it unlocked, then
+// marks them done.  Called with ctx->mu held through lk.
+int render_batched(spt_ctx *ctx, std::unique_lock<std::mutex> &lk, int mode, uint32_t yB, uint32_t yE, uint32_t xB,
+                   uint32_t xE, float *rgba, uint8_t *g_data)
+{
+    BatchReq req{mode, yB, yE, xB, xE, rgba, g_data, SPT_OK, false, false};
+    ctx->batch_pending.push_back(&req);
+    while (!req.done) {
+        if (ctx->batch_leader || req.launched) {
+            ctx->batch_cv.wait(lk);
+            continue;
+        }
+        ctx->batch_leader = true;
+        BatchSet *bs = nullptr;
+        for (;;) {
+            for (uint32_t q = 0; q < ctx->batch_sets; ++q)
+                if (!ctx->bsets[q].busy) {
+                    bs = &ctx->bsets[q];
+                    break;
+                }
+            if (bs) break;
+            ctx->batch_cv.wait(lk);
+        }
+        // FIFO, the first pending call's mode, within the workspace and 2^31 items
+        std::vector<BatchReq *> batch, rest;
+        uint64_t bytes = 0, items = 0;
+        const int bmode = ctx->batch_pending.front()->mode;
+        for (BatchReq *r : ctx->batch_pending) {
+            const uint64_t np = (uint64_t)(r->xE - r->xB) * (r->yE - r->yB);
+            const uint64_t b = batch_slot_bytes(ctx, bmode, np), it = np * ctx->spp + 1024;
+            const bool fits = batch.empty() || (bytes + b <= ctx->ws_bytes && items + it < 0x7FFFFFFFull);
+            if (r->mode != bmode || !fits || r->yE > ctx->H || r->xE > ctx->W) {
+                rest.push_back(r);
+                continue;
+            }
+            batch.push_back(r);
+            bytes += b;
+            items += it;
+        }
+        ctx->batch_pending.swap(rest);
+        for (BatchReq *r : batch) r->launched = true;
+        bs->busy = true;
+        ctx->batch_leader = false;
+        ctx->batch_cv.notify_all();  // the next caller may assemble the next batch
+        if (!bs->stream && hipStreamCreateWithFlags(&bs->stream, hipStreamNonBlocking) != hipSuccess) bs->stream = nullptr;
+        int rc = bs->stream ? launch_batch(ctx, bs, batch) : fail(ctx, SPT_ERR_HIP, "stream creation failed");
+        if (rc == SPT_OK) {
+            lk.unlock();
+            const hipError_t e = hipStreamSynchronize(bs->stream);
+            lk.lock();
+            if (e != hipSuccess) rc = fail(ctx, SPT_ERR_HIP, "hipStreamSynchronize failed: %s", hipGetErrorString(e));
+        }
+        ctx->batches++;
+        ctx->batched_calls += batch.size();
+        for (BatchReq *r : batch) {
+            r->rc = rc;
+            r->done = true;
+        }
+        bs->busy = false;
+        if (rc == SPT_OK) rc = collect_timings(ctx, false);
+        ctx->batch_cv.notify_all();
+    }
+    return req.rc;
+}
+
 // RenderSegment / RenderSegmentTask with host outputs; with pass_spp > 0 progressively,
 // copying the outputs back and calling cb after every pass.  The context lock is held
 // only while launches are enqueued: each call renders on its own slot (stream,
@@ -606,6 +865,16 @@ int render_segment_host(spt_ctx *ctx, int mode, uint32_t yB, uint32_t yE, uint32
     if ((rc = check_region(ctx, yB, yE, xB, xE))) return rc;
     if (yB >= yE || xB >= xE) return SPT_OK;  // the reference's loops do nothing
     HIP_TRY(ctx, hipSetDevice(ctx->device));
+    // one-shot calls join a batch unless one call's samples exceed the workspace (then
+    // it renders alone, in sample batches)
+    if (pass_spp == 0 && ctx->batching && ctx->engine == SPT_ENGINE_MEGAKERNEL &&
+        batch_slot_bytes(ctx, mode, (uint64_t)(xE - xB) * (yE - yB)) <= ctx->ws_bytes &&
+        (uint64_t)(xE - xB) * (yE - yB) * ctx->spp < 0x7FFF0000ull) {
+        ctx->inflight.fetch_add(1);
+        rc = render_batched(ctx, lk, mode, yB, yE, xB, xE, rgba, g_data);
+        ctx->inflight.fetch_sub(1);
+        return rc;
+    }
     HostSlot *hs = acquire_slot(ctx, lk);
     if (!hs) return SPT_ERR_HIP;
     ctx->inflight.fetch_add(1);
@@ -854,6 +1123,9 @@ int spt_ctx_create(int device, spt_ctx **out)
     if (const char *e = std::getenv("SPT_CLAIMS_PER_WAVE")) ctx->claims_per_wave = (uint32_t)std::max(1, std::atoi(e));
     if (const char *e = std::getenv("SPT_WF_CAP")) ctx->wf_cap = (uint32_t)std::max(1024, std::atoi(e));
     if (const char *e = std::getenv("SPT_HOST_GRID_DIV")) ctx->host_grid_div = (uint32_t)std::max(0, std::atoi(e));
+    if (const char *e = std::getenv("SPT_BATCH")) ctx->batching = std::atoi(e) != 0;
+    if (const char *e = std::getenv("SPT_BATCH_SETS"))
+        ctx->batch_sets = (uint32_t)std::min<int>((int)kMaxBatchSets, std::max(1, std::atoi(e)));
     if (const char *e = std::getenv("SPT_HOST_SLOTS"))
         ctx->host_slots = (uint32_t)std::min<int>((int)kMaxHostSlots, std::max(1, std::atoi(e)));
     ctx->grid = (uint32_t)(per_cu * ctx->num_cu);
@@ -926,7 +1198,7 @@ void spt_ctx_destroy(spt_ctx *ctx)
             (void)hipEventDestroy(p.b);
         }
     (void)hipDeviceSynchronize();  // async renders on caller streams
-    for (void *p : ctx->pinned) (void)hipHostUnregister(p);
+    for (const spt_ctx::Pinned &p : ctx->pinned) (void)hipHostUnregister(p.ptr);
     if (ctx->ref_ev) (void)hipEventDestroy(ctx->ref_ev);
     void *bufs[] = {ctx->d_shade, ctx->d_mat, ctx->d_slots, ctx->d_orig, ctx->d_nodes,
                     ctx->d_kpre, ctx->d_counters, ctx->d_frame8};
@@ -945,6 +1217,12 @@ void spt_ctx_destroy(spt_ctx *ctx)
         if (h->d_stage) (void)hipFree(h->d_stage);
         if (h->stream) (void)hipStreamDestroy(h->stream);
         delete h;
+    }
+    for (BatchSet &b : ctx->bsets) {
+        if (b.d_rects) (void)hipFree(b.d_rects);
+        if (b.h_rects) (void)hipHostFree(b.h_rects);
+        if (b.d_stage) (void)hipFree(b.d_stage);
+        if (b.stream) (void)hipStreamDestroy(b.stream);
     }
     for (void *b : {(void *)ctx->d_tile, (void *)ctx->d_fullframe})
         if (b) (void)hipFree(b);
@@ -1027,10 +1305,13 @@ int spt_pin_host(spt_ctx *ctx, void *ptr, size_t bytes)
     if (!ctx) return fail(nullptr, SPT_ERR_ARG, "null context");
     std::lock_guard<std::mutex> lk(ctx->mu);
     if (!ptr || bytes == 0) return fail(ctx, SPT_ERR_ARG, "null or empty host buffer");
-    if (std::find(ctx->pinned.begin(), ctx->pinned.end(), ptr) != ctx->pinned.end()) return SPT_OK;
+    for (const spt_ctx::Pinned &p : ctx->pinned)
+        if (p.ptr == ptr) return SPT_OK;
     HIP_TRY(ctx, hipSetDevice(ctx->device));
-    HIP_TRY(ctx, hipHostRegister(ptr, bytes, hipHostRegisterDefault));
-    ctx->pinned.push_back(ptr);
+    HIP_TRY(ctx, hipHostRegister(ptr, bytes, hipHostRegisterMapped));
+    void *dev = nullptr;
+    if (hipHostGetDevicePointer(&dev, ptr, 0) != hipSuccess) dev = nullptr;
+    ctx->pinned.push_back(spt_ctx::Pinned{ptr, bytes, (uint8_t *)dev});
     return SPT_OK;
 }
 
@@ -1038,10 +1319,11 @@ int spt_unpin_host(spt_ctx *ctx, void *ptr)
 {
     if (!ctx) return fail(nullptr, SPT_ERR_ARG, "null context");
     std::lock_guard<std::mutex> lk(ctx->mu);
-    auto it = std::find(ctx->pinned.begin(), ctx->pinned.end(), ptr);
+    auto it = std::find_if(ctx->pinned.begin(), ctx->pinned.end(), [&](const spt_ctx::Pinned &p) { return p.ptr == ptr; });
     if (it == ctx->pinned.end()) return fail(ctx, SPT_ERR_ARG, "buffer %p was not pinned", ptr);
     HIP_TRY(ctx, hipSetDevice(ctx->device));
-    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    // batched calls may be writing into it directly
+    HIP_TRY(ctx, hipDeviceSynchronize());
     HIP_TRY(ctx, hipHostUnregister(ptr));
     ctx->pinned.erase(it);
     return SPT_OK;
@@ -1246,6 +1528,8 @@ int stats_one(spt_ctx *ctx, spt_stats *out)
     out->render_busy_ms = busy_ms(ctx);
     out->grid_blocks = ctx->last_grid ? ctx->last_grid : ctx->grid;
     out->block_threads = ctx->last_block ? ctx->last_block : ctx->block;
+    out->batches = ctx->batches;
+    out->batched_calls = ctx->batched_calls;
     return SPT_OK;
 }
 
@@ -1258,6 +1542,7 @@ int reset_one(spt_ctx *ctx)
     HIP_TRY(ctx, hipMemset(ctx->d_counters, 0, kCounters * sizeof(unsigned long long)));
     ctx->render_ms = ctx->fold_ms = ctx->last_render_ms = 0;
     ctx->launches = 0;
+    ctx->batches = ctx->batched_calls = 0;
     ctx->spans.clear();
     ctx->ref_recorded = false;
     return SPT_OK;
@@ -1278,6 +1563,8 @@ int spt_get_stats(spt_ctx *ctx, spt_stats *out)
         out->dropped += q.dropped;
         for (int i = 0; i < 14; ++i) out->diag[i] += q.diag[i];
         out->launches += q.launches;
+        out->batches += q.batches;
+        out->batched_calls += q.batched_calls;
         out->render_ms += q.render_ms;
         out->fold_ms += q.fold_ms;
         out->render_busy_ms = std::max(out->render_busy_ms, q.render_busy_ms);

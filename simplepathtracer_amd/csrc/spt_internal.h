@@ -190,6 +190,24 @@ struct Camera {
     float sky[3];
 };
 
+// One rectangle of a batched launch (several concurrent RenderSegment calls rendered
+// by one render + one fold launch, spt_api.cpp Batcher).  Its items are
+// [item_off, item_end) of the launch, in the order of a single-rectangle launch
+// (ts_item over w x rows pixels and all spp samples); item_off is a multiple of the
+// launch's claim size, so a claim never spans two rectangles, and items in
+// [item_end, next item_off) are padding (no path).  Its per-sample slots are
+// [slot_off, slot_off + npix * spp), [sample][row-major pixel]; its fold output sits at
+// pixels [pix_off, pix_off + npix) of the batch's staging.
+struct BatchRect {
+    uint32_t item_off, item_end, slot_off, pix_off;
+    uint32_t x0, y0, w, rows;
+    uint32_t npix, alias;  // alias: task mode on a non-square tile (fold_kernel)
+    uint8_t *rgb8;         // the call's g_data as the device sees it (its page-locked host buffer,
+                           // written in place, or the context's device frame), or null
+    FastDiv div_band, div_tile;  // ts_item divisors 8*w*spp and 64*spp
+};
+static_assert(sizeof(BatchRect) == 72, "BatchRect layout");
+
 struct RenderArgs {
     DeviceScene scene;
     Camera cam;
@@ -207,6 +225,8 @@ struct RenderArgs {
     uint32_t slot_floats;  // 3 or 4
     uint32_t *head;      // queue head (zeroed before launch)
     unsigned long long *counters;  // [0] casts, [1] samples, [2] dropped
+    const BatchRect *rects;  // batched launch: n_rects rectangles (map/npix/div_* unused); else null
+    uint32_t n_rects;
 };
 
 struct FoldArgs {
@@ -222,6 +242,8 @@ struct FoldArgs {
     int preview;         // write the outputs after every batch (progressive rendering)
     int alias;           // task mode, one non-square rectangle: RenderSegmentTask's colorIndex
                          // (dx + dy * segmentHeight, TaskBasedPathTracer.hpp:103,186) aliases pixels
+    const BatchRect *rects;  // batched fold: n_rects rectangles over npix = their total pixels
+    uint32_t n_rects;        // (map and alias per rectangle; spp_batch = spp_total, first = last = 1)
 };
 
 // Launch geometry of one render launch: the context's persistent grid for the

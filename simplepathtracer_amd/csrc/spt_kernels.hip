@@ -66,7 +66,10 @@ constexpr uint32_t kLdsMinNodes = 64;
 
 // One kernel per traversal shape (flat list of 4- or 8-slot leaves, tree of
 // 8-slot leaves), each with its own register allocation; launch_render picks.
-template <bool TREE, int LEAF, bool LDSN, uint32_t BLOCK>
+// BATCH: the launch renders a.n_rects rectangles (a.rects, concurrent host calls
+// batched by spt_api.cpp); each refill then serves lanes from one claim only, and a
+// claim's rectangle is looked up once per claim.
+template <bool TREE, int LEAF, bool LDSN, uint32_t BLOCK, bool BATCH = false>
 __device__ __forceinline__ void render_body(const RenderArgs &a)
 {
     const uint32_t lane = __lane_id();
@@ -98,6 +101,8 @@ __device__ __forceinline__ void render_body(const RenderArgs &a)
     // keeps the next claim in flight (lane 0) so the atomic's latency is hidden.
     uint32_t blk_cur = 0, blk_end = 0;
     uint32_t pend = 0;
+    uint32_t rect = 0;  // BATCH: rectangle of the current claim
+    (void)rect;
     if (lane == 0) pend = atomicAdd(a.head, a.claim);
     bool exhausted = false;
     unsigned long long casts = 0, done = 0, dropped = 0;
@@ -120,7 +125,32 @@ __device__ __forceinline__ void render_body(const RenderArgs &a)
     for (;;) {
         // ---- refill: hand out (pixel, sample) items to idle lanes (ballot + prefix)
         const unsigned long long need = __ballot(ps.phase == PH_IDLE);
-        if (need != 0ull && !exhausted) {
+        if (BATCH && need != 0ull && !exhausted) {
+            if (blk_cur == blk_end) {
+                // the claim in flight becomes current, the next one goes in flight
+                const uint32_t nb = __builtin_amdgcn_readfirstlane(pend);
+                if (nb < a.n_items && lane == 0) pend = atomicAdd(a.head, a.claim);
+                if (nb >= a.n_items) {
+                    exhausted = true;
+                } else {
+                    blk_cur = nb;
+                    blk_end = min(nb + a.claim, a.n_items);
+#if defined(__HIP_DEVICE_COMPILE__)
+                    rect = find_rect(nb);
+#endif
+                }
+            }
+            if (!exhausted) {
+                const uint32_t take = min((uint32_t)__popcll(need), blk_end - blk_cur);
+                const uint32_t rank = lane_rank(need);
+                const uint32_t mine = blk_cur + rank;
+                (void)mine;
+                blk_cur += take;
+#if defined(__HIP_DEVICE_COMPILE__)
+                if (ps.phase == PH_IDLE && rank < take) start_path_rect(mine, rect, ps);
+#endif
+            }
+        } else if (!BATCH && need != 0ull && !exhausted) {
             const uint32_t cnt = (uint32_t)__popcll(need);
             const uint32_t rank = lane_rank(need);
             const uint32_t avail = blk_end - blk_cur;
@@ -210,6 +240,13 @@ __global__ __launch_bounds__(kRenderBlock) SPT_RENDER_ATTR void render_kernel(Re
     render_body<TREE, LEAF, false, kRenderBlock>(a);
 }
 
+// batched launches (RenderArgs::rects): concurrent RenderSegment calls in one launch
+template <bool TREE, int LEAF>
+__global__ __launch_bounds__(kRenderBlock) SPT_RENDER_ATTR void render_kernel_batch(RenderArgs a)
+{
+    render_body<TREE, LEAF, false, kRenderBlock, true>(a);
+}
+
 // its own register budget: 1024-thread blocks, two per CU, need 8 waves per SIMD
 #ifndef SPT_LDS_NUM_SGPR
 #define SPT_LDS_NUM_SGPR 80
@@ -219,27 +256,34 @@ __global__ __launch_bounds__(kLdsBlock)
 {
     render_body<true, (int)kClusterSlots, true, kLdsBlock>(a);
 }
-
-__global__ __launch_bounds__(256) void fold_kernel(FoldArgs a)
+__global__ __launch_bounds__(kLdsBlock)
+    __attribute__((amdgpu_num_sgpr(SPT_LDS_NUM_SGPR), amdgpu_waves_per_eu(2 * kLdsBlock / 256))) void render_kernel_lds_batch(RenderArgs a)
 {
-    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= a.npix) return;
+    render_body<true, (int)kClusterSlots, true, kLdsBlock, true>(a);
+}
+
+// RenderSegment's / RenderSegmentTask's resolve of pixel p of a region (map, npix
+// pixels, alias: task mode on a non-square tile) whose slots start at `samples`;
+// local float4 output at out_rgba[p].
+__device__ __forceinline__ void fold_pixel(const FoldArgs &a, const float *samples, const RowMap &map, uint32_t npix,
+                                           int alias, uint32_t p, float4 *out_rgba, uint8_t *out_rgb8)
+{
     float4 acc = a.first ? make_float4(0.f, 0.f, 0.f, 0.f) : a.acc[p];
     if (a.mode == 0) {
         // RenderSegment: 12-byte slots, every sample counts
-        const float *s = a.samples + (size_t)3 * p;
+        const float *s = samples + (size_t)3 * p;
         for (uint32_t k = 0; k < a.spp_batch; ++k) {
-            const float *c = s + (size_t)3 * k * a.npix;  // [sample][pixel]: coalesced across lanes
+            const float *c = s + (size_t)3 * k * npix;  // [sample][pixel]: coalesced across lanes
             acc.x = acc.x + c[0];
             acc.y = acc.y + c[1];
             acc.z = acc.z + c[2];
             acc.w = acc.w + 1.f;
         }
-    } else if (!a.alias) {
+    } else if (!alias) {
         // RenderSegmentTask on a square tile: pixel p is colors[p]; w = 0 marks a dropped path
-        const float4 *s = (const float4 *)a.samples + p;
+        const float4 *s = (const float4 *)samples + p;
         for (uint32_t k = 0; k < a.spp_batch; ++k) {
-            const float4 c = s[(size_t)k * a.npix];
+            const float4 c = s[(size_t)k * npix];
             if (__float_as_uint(c.w) != 0u) {
                 acc.x = acc.x + c.x;
                 acc.y = acc.y + c.y;
@@ -254,12 +298,12 @@ __global__ __launch_bounds__(256) void fold_kernel(FoldArgs a)
         // the sources reach colors[p] in the order of their (key, pixel) (finish_step),
         // so each sample's sources are added in that order.  No source: 0 samples, and
         // 0 * (1.f / 0) is NaN, as in the reference.
-        const uint32_t W = a.map.width, H = a.npix / W;
+        const uint32_t W = map.width, H = npix / W;
         const uint32_t dy_lo = p >= W ? (p - W + H) / H : 0u;
         const uint32_t dy_hi = min(H - 1u, p / H);
-        const float4 *s = (const float4 *)a.samples;
+        const float4 *s = (const float4 *)samples;
         for (uint32_t k = 0; k < a.spp_batch; ++k) {
-            const float4 *sk = s + (size_t)k * a.npix;
+            const float4 *sk = s + (size_t)k * npix;
             uint64_t prev = 0;  // (key << 32 | pixel) of the last source added
             for (uint32_t t = dy_lo; t <= dy_hi; ++t) {
                 uint64_t best = ~0ull;
@@ -288,16 +332,39 @@ __global__ __launch_bounds__(256) void fold_kernel(FoldArgs a)
     // s_done samples is the render at g_samples = s_done, bit for bit (keyed samples).
     const float scale = a.mode == 0 ? 1.f / (float)a.s_done : 1.f / acc.w;
     const float r = acc.x * scale, g = acc.y * scale, b = acc.z * scale;
-    if (a.out_rgba) a.out_rgba[p] = make_float4(r, g, b, 0.f);
-    if (a.out_rgb8) {
-        const uint32_t lr = p / a.map.width;
-        const uint32_t x = a.map.x0 + (p - lr * a.map.width);
-        const uint32_t y = row_of(a.map, lr);
+    if (out_rgba) out_rgba[p] = make_float4(r, g, b, 0.f);
+    if (out_rgb8) {
+        const uint32_t lr = p / map.width;
+        const uint32_t x = map.x0 + (p - lr * map.width);
+        const uint32_t y = row_of(map, lr);
         const size_t gi = (size_t)3 * ((size_t)(a.height - 1u - y) * a.width + x);
-        a.out_rgb8[gi + 0] = gamma_byte(r);
-        a.out_rgb8[gi + 1] = gamma_byte(g);
-        a.out_rgb8[gi + 2] = gamma_byte(b);
+        out_rgb8[gi + 0] = gamma_byte(r);
+        out_rgb8[gi + 1] = gamma_byte(g);
+        out_rgb8[gi + 2] = gamma_byte(b);
     }
+}
+
+__global__ __launch_bounds__(256) void fold_kernel(FoldArgs a)
+{
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= a.npix) return;
+    fold_pixel(a, a.samples, a.map, a.npix, a.alias, p, a.out_rgba, a.out_rgb8);
+}
+
+// Batched fold (FoldArgs::rects): pixel p of the batch's concatenated rectangles.
+__global__ __launch_bounds__(256) void fold_kernel_batch(FoldArgs a)
+{
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= a.npix) return;
+    uint32_t lo = 0, hi = a.n_rects;
+    while (hi - lo > 1u) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (a.rects[mid].pix_off <= p) lo = mid; else hi = mid;
+    }
+    const BatchRect &r = a.rects[lo];
+    const RowMap map{r.y0, r.y0 + r.rows, 1u, 1u, 0u, r.x0, r.w};
+    fold_pixel(a, a.samples + (size_t)a.slot_floats * r.slot_off, map, r.npix, (int)r.alias, p - r.pix_off,
+               a.out_rgba ? a.out_rgba + r.pix_off : nullptr, r.rgb8);
 }
 
 __global__ __launch_bounds__(256) void assemble_kernel(const float4 *tiles, uint32_t max_rows, RowMap base,
@@ -370,6 +437,7 @@ static void lds_tree_shape(int *per_cu, int *num_cu)
 hipError_t launch_render(const RenderArgs &a, LaunchShape &sh, hipStream_t s)
 {
     const uint32_t div = sh.div ? sh.div : 1u;
+    const bool batch = a.rects != nullptr;
     // trees of >= kLdsMinNodes nodes walk an LDS copy of the node table (config 5);
     // smaller ones stay in the scalar cache (all 8 octant layouts: config 2's 26-node
     // tree is 6.7 KB), where the 256-thread kernel overlaps frames in flight better
@@ -386,13 +454,23 @@ hipError_t launch_render(const RenderArgs &a, LaunchShape &sh, hipStream_t s)
             g = g < full ? g : full;
             sh.ran_grid = (uint32_t)g;
             sh.ran_block = kLdsBlock;
-            hipLaunchKernelGGL(render_kernel_lds, dim3(sh.ran_grid), dim3(kLdsBlock), 0, s, a);
+            if (batch)
+                hipLaunchKernelGGL(render_kernel_lds_batch, dim3(sh.ran_grid), dim3(kLdsBlock), 0, s, a);
+            else
+                hipLaunchKernelGGL(render_kernel_lds, dim3(sh.ran_grid), dim3(kLdsBlock), 0, s, a);
             return hipGetLastError();
         }
     }
     sh.ran_grid = sh.grid;
     sh.ran_block = sh.block;
-    if (a.scene.accel.tree)
+    if (batch) {
+        if (a.scene.accel.tree)
+            hipLaunchKernelGGL((render_kernel_batch<true, (int)kClusterSlots>), dim3(sh.grid), dim3(sh.block), 0, s, a);
+        else if (a.scene.accel.leaf_slots == kFlatLeafSlots)
+            hipLaunchKernelGGL((render_kernel_batch<false, (int)kFlatLeafSlots>), dim3(sh.grid), dim3(sh.block), 0, s, a);
+        else
+            hipLaunchKernelGGL((render_kernel_batch<false, (int)kClusterSlots>), dim3(sh.grid), dim3(sh.block), 0, s, a);
+    } else if (a.scene.accel.tree)
         hipLaunchKernelGGL((render_kernel<true, (int)kClusterSlots>), dim3(sh.grid), dim3(sh.block), 0, s, a);
     else if (a.scene.accel.leaf_slots == kFlatLeafSlots)
         hipLaunchKernelGGL((render_kernel<false, (int)kFlatLeafSlots>), dim3(sh.grid), dim3(sh.block), 0, s, a);
@@ -404,7 +482,10 @@ hipError_t launch_render(const RenderArgs &a, LaunchShape &sh, hipStream_t s)
 hipError_t launch_fold(const FoldArgs &a, hipStream_t s)
 {
     if (a.npix == 0) return hipSuccess;
-    hipLaunchKernelGGL(fold_kernel, dim3((a.npix + 255) / 256), dim3(256), 0, s, a);
+    if (a.rects)
+        hipLaunchKernelGGL(fold_kernel_batch, dim3((a.npix + 255) / 256), dim3(256), 0, s, a);
+    else
+        hipLaunchKernelGGL(fold_kernel, dim3((a.npix + 255) / 256), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 

@@ -820,6 +820,49 @@ __device__ __forceinline__ void start_path_kernarg(uint32_t mine, uint32_t rows,
     start_path(a, mine, rows, recip((float)a.width), recip((float)a.height),
                mk(k.cam.eye[0], k.cam.eye[1], k.cam.eye[2]), ps);
 }
+
+// Batched launches (RenderArgs::rects): the rectangle holding item `nb` (the first
+// item of a claim; claims never span two rectangles), by binary search over the
+// rectangles' item_off with scalar loads (nb is wave-uniform).
+typedef __attribute__((address_space(4))) const BatchRect crect_t;
+__device__ __forceinline__ uint32_t find_rect(uint32_t nb)
+{
+    kargs_t &k = *kernarg_args();
+    crect_t *r = (crect_t *)k.rects;
+    uint32_t lo = 0, hi = k.n_rects;
+    while (hi - lo > 1u) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (r[mid].item_off <= nb) lo = mid; else hi = mid;
+    }
+    return lo;
+}
+
+// start_path for item `mine` of a batched launch, in rectangle `ri` (wave-uniform):
+// the rectangle's own region, item order and slot range.  Items past its item_end
+// (claim padding) start nothing: the lane stays idle.
+__device__ __forceinline__ void start_path_rect(uint32_t mine, uint32_t ri, Path &ps)
+{
+    kargs_t &k = *kernarg_args();
+    crect_t &r = ((crect_t *)k.rects)[ri];
+    if (mine >= r.item_end) return;
+    RenderArgs a;
+    a.map = RowMap{r.y0, r.y0 + r.rows, 1u, 1u, 0u, r.x0, r.w};
+    a.width = k.width;
+    a.height = k.height;
+    a.bounces = k.bounces;
+    a.npix = r.npix;
+    a.spp_batch = k.spp_batch;
+    a.s0 = k.s0;
+    a.seed_key = k.seed_key;
+    a.div_band = FastDiv{r.div_band.d, r.div_band.m, r.div_band.s};
+    a.div_tile = FastDiv{r.div_tile.d, r.div_tile.m, r.div_tile.s};
+    a.div_strip = FastDiv{1u, 0u, 0u};
+#pragma unroll
+    for (int q = 0; q < 12; ++q) a.cam.view[q] = k.cam.view[q];
+    start_path(a, mine - r.item_off, r.rows, recip((float)a.width), recip((float)a.height),
+               mk(k.cam.eye[0], k.cam.eye[1], k.cam.eye[2]), ps);
+    ps.item += r.slot_off;
+}
 #endif
 
 }  // namespace

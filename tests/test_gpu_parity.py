@@ -689,8 +689,8 @@ def test_progress_callback_may_call_into_the_context(spt, ctx, golden_scenes):
 
 
 def test_concurrent_tiles_overlap_and_match(spt, ctx, golden_scenes):
-    """16 RenderJob-style threads on one context: each call gets its own stream and
-    workspace (at most 8 in flight); bytes equal the serial render."""
+    """16 RenderJob-style threads on one context (their calls batched into shared
+    launches); bytes equal the serial render."""
     setup(ctx, scene_from(spt, golden_scenes, "random"), 320, 160, 4, 50)
     want = np.zeros(320 * 160 * 3, np.uint8)
     ctx.render_segment(0, 160, 0, 320, want)
@@ -711,6 +711,57 @@ def test_concurrent_tiles_overlap_and_match(spt, ctx, golden_scenes):
         t.join()
     assert not errors
     assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("task", [False, True])
+def test_batched_calls_match_single_calls(spt, golden_scenes, monkeypatch, task):
+    """Concurrent spt_render_segment[_task] calls are rendered in batches (one render
+    and one fold launch over a table of rectangles, spt_api.cpp render_batched): float
+    pixels and g_data bytes of every tile equal the same calls rendered one by one
+    without batching (SPT_BATCH=0), for square and non-square tiles (task mode: the
+    colorIndex aliasing per tile) and ragged sizes; the stats count every call."""
+    scene = scene_from(spt, golden_scenes, "random")
+    W, H, spp = 330, 170, 3
+    tiles = [(0, 40, 0, 100), (0, 40, 100, 140), (40, 170, 0, 33), (40, 97, 33, 330), (97, 170, 33, 200),
+             (97, 170, 200, 330), (0, 40, 140, 330)]
+    n_part = len(tiles)  # a partition of the frame: these write g_data
+    tiles = tiles + [(y, y + 13, x, x + 13) for y, x in ((150, 10), (0, 300), (60, 60))]  # overlapping repeats
+    monkeypatch.setenv("SPT_BATCH", "0")
+    ref = spt.Context(0)
+    monkeypatch.delenv("SPT_BATCH")
+    setup(ref, scene, W, H, spp, 50)
+    want8 = np.zeros(W * H * 3, np.uint8)
+    want = [ref.render_segment(*t, want8 if k < n_part else None, task=task) for k, t in enumerate(tiles)]
+    assert ref.stats()["batches"] == 0
+    ref.close()
+    c = spt.Context(0)
+    setup(c, scene, W, H, spp, 50)
+    c.reset_stats()
+    got8 = np.zeros_like(want8)
+    got = [None] * len(tiles)
+    errors = []
+    go = threading.Barrier(len(tiles))
+
+    def job(k):
+        try:
+            go.wait()
+            got[k] = c.render_segment(*tiles[k], got8 if k < n_part else None, task=task)
+        except Exception as e:  # pragma: no cover
+            errors.append(e)
+
+    th = [threading.Thread(target=job, args=(k,)) for k in range(len(tiles))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    st = c.stats()
+    c.close()
+    assert not errors
+    for k, t in enumerate(tiles):
+        assert_bitwise(got[k], want[k], f"tile {t}")
+    assert np.array_equal(got8, want8)
+    assert st["batched_calls"] == len(tiles) and 1 <= st["batches"] <= len(tiles)
+    assert st["launches"] == st["batches"]
 
 
 # ---------------------------------------------------------------- configs 4 and 5 at full size

@@ -98,7 +98,11 @@ int main(int argc, char **argv)
         const auto t0 = std::chrono::steady_clock::now();
         for (int k = 0; k < frames; ++k) frame_once();
         const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-        printf("frames=%d seconds=%.6f\n", frames, sec);
+        spt_stats st{};
+        spt_get_stats(spt_shim::context(), &st);  // since the context's creation (no reset)
+        printf("frames=%d seconds=%.6f calls=%llu batches=%llu render_ms=%.3f busy_ms=%.3f fold_ms=%.3f\n", frames, sec,
+               (unsigned long long)st.batched_calls, (unsigned long long)st.batches, st.render_ms, st.render_busy_ms,
+               st.fold_ms);
     }
     FILE *f = fopen(argv[1], "wb");
     if (!f) return 5;

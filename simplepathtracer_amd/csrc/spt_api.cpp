@@ -808,12 +808,19 @@ int render_batched(spt_ctx *ctx, std::unique_lock<std::mutex> &lk, int mode, uin
         // FIFO, the first pending call's mode, within the workspace and 2^31 items
         std::vector<BatchReq *> batch, rest;
         uint64_t bytes = 0, items = 0;
-        const int bmode = ctx->batch_pending.front()->mode;
+        const int bmode = ctx->batch_pending.empty() ? req.mode : ctx->batch_pending.front()->mode;
         for (BatchReq *r : ctx->batch_pending) {
             const uint64_t np = (uint64_t)(r->xE - r->xB) * (r->yE - r->yB);
+            if (r->yE > ctx->H || r->xE > ctx->W || np * ctx->spp >= 0x7FFF0000ull) {
+                // the frame shrank or spp grew (spt_set_params) after the call was checked
+                r->rc = fail(ctx, SPT_ERR_ARG, "region [%u,%u)x[%u,%u) no longer fits the %ux%u frame at %u spp",
+                             r->yB, r->yE, r->xB, r->xE, ctx->W, ctx->H, ctx->spp);
+                r->launched = r->done = true;
+                continue;
+            }
             const uint64_t b = batch_slot_bytes(ctx, bmode, np), it = np * ctx->spp + 1024;
             const bool fits = batch.empty() || (bytes + b <= ctx->ws_bytes && items + it < 0x7FFFFFFFull);
-            if (r->mode != bmode || !fits || r->yE > ctx->H || r->xE > ctx->W) {
+            if (r->mode != bmode || !fits) {
                 rest.push_back(r);
                 continue;
             }
@@ -822,6 +829,11 @@ int render_batched(spt_ctx *ctx, std::unique_lock<std::mutex> &lk, int mode, uin
             items += it;
         }
         ctx->batch_pending.swap(rest);
+        if (batch.empty()) {  // every pending call failed the checks above
+            ctx->batch_leader = false;
+            ctx->batch_cv.notify_all();
+            continue;
+        }
         for (BatchReq *r : batch) r->launched = true;
         bs->busy = true;
         ctx->batch_leader = false;
@@ -833,6 +845,8 @@ int render_batched(spt_ctx *ctx, std::unique_lock<std::mutex> &lk, int mode, uin
             const hipError_t e = hipStreamSynchronize(bs->stream);
             lk.lock();
             if (e != hipSuccess) rc = fail(ctx, SPT_ERR_HIP, "hipStreamSynchronize failed: %s", hipGetErrorString(e));
+        } else if (bs->stream) {
+            (void)hipStreamSynchronize(bs->stream);  // whatever was enqueued before the failure
         }
         ctx->batches++;
         ctx->batched_calls += batch.size();

@@ -42,7 +42,8 @@ namespace {
 constexpr size_t kMaxCallerStreams = 4;
 constexpr size_t kCounters = 18;  // device counters: casts, samples, dropped, -, diag[14]
 constexpr size_t kMaxHostSlots = 8;
-constexpr size_t kMaxWorkspaces = kMaxCallerStreams + kMaxHostSlots + 1;
+constexpr uint32_t kMaxBatchSets = 8;  // batches of host calls in flight (BatchSet below)
+constexpr size_t kMaxWorkspaces = kMaxCallerStreams + kMaxHostSlots + kMaxBatchSets + 1;
 // One in-flight host call (spt_render_segment[_task] / spt_render_progressive): its own
 // stream (hence its own workspace) and output staging, so concurrent RenderJob tiles
 // (Renderer.hpp:242-302) run on the GPU together instead of one after another.
@@ -58,7 +59,6 @@ struct HostSlot {
 // shipped g_maxThreads = 4, 1 024 at tc = 2 * 16 cores -- do not each pay a launch,
 // its fold, its tail and its own synchronisation.  Two batch sets: while one batch
 // renders, the calls arriving meanwhile form the next.
-constexpr uint32_t kMaxBatchSets = 8;
 struct BatchSet {
     hipStream_t stream = nullptr;
     spt::BatchRect *d_rects = nullptr, *h_rects = nullptr;  // device table, pinned host copy

@@ -44,9 +44,9 @@ constexpr size_t kCounters = 18;  // device counters: casts, samples, dropped, -
 constexpr size_t kMaxHostSlots = 8;
 constexpr uint32_t kMaxBatchSets = 8;  // batches of host calls in flight (BatchSet below)
 constexpr size_t kMaxWorkspaces = kMaxCallerStreams + kMaxHostSlots + kMaxBatchSets + 1;
-// One in-flight host call (spt_render_segment[_task] / spt_render_progressive): its own
-// stream (hence its own workspace) and output staging, so concurrent RenderJob tiles
-// (Renderer.hpp:242-302) run on the GPU together instead of one after another.
+// One in-flight unbatched host call (spt_render_progressive, or any call with
+// SPT_BATCH=0 or too large for one batch): its own stream (hence its own workspace) and
+// output staging, so such calls run on the GPU together instead of one after another.
 struct HostSlot {
     hipStream_t stream = nullptr;
     float4 *d_stage = nullptr;  // region-local float4 output
@@ -57,8 +57,8 @@ struct HostSlot {
 // one render + one fold launch per batch over a table of rectangles (BatchRect), so
 // the reference's RenderJob threads (Renderer.hpp:242-302) -- 16 tiles a frame at the
 // shipped g_maxThreads = 4, 1 024 at tc = 2 * 16 cores -- do not each pay a launch,
-// its fold, its tail and its own synchronisation.  Two batch sets: while one batch
-// renders, the calls arriving meanwhile form the next.
+// its fold, its tail and its own synchronisation.  Two batch sets by default
+// (SPT_BATCH_SETS): while one batch renders, the calls arriving meanwhile form the next.
 struct BatchSet {
     hipStream_t stream = nullptr;
     spt::BatchRect *d_rects = nullptr, *h_rects = nullptr;  // device table, pinned host copy

@@ -404,12 +404,15 @@ def test_concurrent_render_jobs_share_a_context(spt, golden_scenes):
 
 
 @pytest.mark.parametrize("w,h,tc,task,devices", [(1200, 800, 4, 0, None), (1200, 800, 4, 1, None),
-                                                  (1200, 800, 8, 0, "0,0")])
+                                                  (1200, 800, 8, 0, "0,0"), (320, 160, 16, 0, None),
+                                                  (320, 160, 16, 1, None)])
 def test_cpp_dropin_shim_renders_like_the_context(spt, golden_scenes, tmp_path, w, h, tc, task, devices):
     """The C++ RenderSegment/RenderSegmentTask shim, driven by RenderJob-style
     concurrent threads over a tc x tc tile grid (config 2's 300x200 tiles at tc = 4,
-    non-square: task mode aliases), writes the same g_data bytes as tile renders
-    through the context; SPT_DEVICES spreads the tiles over a multi-device context."""
+    non-square: task mode aliases; 256 tiles of 20x10 at tc = 16, batched many to a
+    launch), writes the same g_data bytes as tile renders through the context (its
+    page-locked g_data written in place by the batched fold); SPT_DEVICES spreads the
+    tiles over a multi-device context."""
     import os
     import subprocess
     from test_abi import _build_shim_harness

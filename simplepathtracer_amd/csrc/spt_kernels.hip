@@ -12,9 +12,12 @@
 //
 // Sphere data is read with wave-uniform scalar loads (s_load) -- the sphere
 // index of the hot loop is the same for all lanes.  Small spheres sit in 8-slot
-// clusters under a tree of bounding spheres walked by the whole wave without a
+// clusters under a tree of expanded boxes walked by the whole wave without a
 // stack (preorder + skip links); a subtree is skipped when no lane can pass any
-// member's test (spt_accel.cpp).
+// member's test or beat its current winner (spt_accel.cpp).
+// render_kernel_lds walks large trees from a per-block LDS copy of the node table;
+// the *_batch kernels render several host calls' rectangles in one launch
+// (spt_api.cpp render_batched).
 //
 // fold_kernel: RenderSegment's `pixelColor += sample` in sample order followed by
 // `*= 1/g_samples` (SingleThreadPathTracer.hpp:121-134) or RenderSegmentTask's

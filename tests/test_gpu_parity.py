@@ -367,6 +367,31 @@ def test_row_split_and_assemble_equals_full_frame(spt, ctx, golden_scenes):
     assert torch.equal(g, g_full)
 
 
+def test_config2_every_pixel_vs_oracle(spt, ctx, oracle, golden_scenes):
+    """The whole config-2 frame (1200x800, the box-tree default traversal) at 4 spp,
+    every pixel's float RGB and g_data bytes against the oracle's
+    RenderImageParallelMain (16x16 tiles, 16 threads); and RenderImage's
+    RenderSegmentTask over the whole non-square frame (colorIndex aliasing across the
+    frame) at 1 spp against the oracle's single-rectangle task render."""
+    W, H = 1200, 800
+    sc = oscene_from(oracle, golden_scenes, "random")
+    setup(ctx, scene_from(spt, golden_scenes, "random"), W, H, 4, 50, seed=11)
+    g = np.zeros(W * H * 3, np.uint8)
+    got = ctx.render_segment(0, H, 0, W, g)
+    fr = oracle.make_frame(golden_scenes["view"], EYE, SKY, W, H, 4, 50, 11)
+    want, want8 = oracle.render_image_parallel(sc, fr, 16, mode=0)
+    assert_bitwise(got[:, :3], want[:, :3], "config 2, every pixel, 4 spp")
+    assert np.array_equal(g, want8)
+    setup(ctx, scene_from(spt, golden_scenes, "random"), W, H, 1, 50, seed=12)
+    g = np.zeros(W * H * 3, np.uint8)
+    got = ctx.render_segment(0, H, 0, W, g, task=True)
+    fr = oracle.make_frame(golden_scenes["view"], EYE, SKY, W, H, 1, 50, 12)
+    g_want = np.zeros_like(g)
+    want, _ = oracle.render_segment(sc, fr, 0, H, 0, W, task=True, rgb8=g_want)
+    same_or_nan(got[:, :3], want[:, :3], "RenderImage (task mode, whole non-square frame)")
+    assert np.array_equal(g, g_want)
+
+
 def test_config2_full_frame_properties(spt, ctx, oracle, golden_scenes):
     """BASELINE config 2 at full size: every sample accounted for, deterministic,
     and random pixels bit-exact vs the oracle."""

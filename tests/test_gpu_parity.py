@@ -830,6 +830,30 @@ def test_config4_eight_way_strip_split_equals_one_part(spt, ctx, golden_scenes):
     assert np.array_equal(gm, g_full.cpu().numpy())
 
 
+def test_config5_box_tree_equals_brute_force(spt, ctx):
+    """The config-5 scene (10 000 spheres in a flat layer: the grazing rays the box
+    margins exist for) over the whole 1920x1080 frame at 2 spp, rendered through the box tree
+    walked from LDS, through the scalar-load walk of the octant layouts (a 2-ary tree
+    of 8-sphere clusters has more than the LDS kernel's 2 431 nodes) and brute force
+    (every sphere tested for every ray, the reference's scan): the same float bits and
+    the same ray count."""
+    s = spt.generate_stress(1, 10000)
+    W, H = 1920, 1080
+    setup(ctx, s, W, H, 2, 50, seed=21)
+    outs = []
+    for k, b in ((spt._native.CLUSTER_AUTO, spt._native.TREE_AUTO), (8, 2), (0, 0)):
+        ctx.set_cluster_size(k)
+        ctx.set_cluster_tree(b)
+        ctx.reset_stats()
+        outs.append(((k, b), ctx.render_segment(0, H, 0, W), ctx.stats()))
+    ctx.set_cluster_size(spt._native.CLUSTER_AUTO)
+    ctx.set_cluster_tree(spt._native.TREE_AUTO)
+    assert outs[0][2]["block_threads"] == 1024 and outs[1][2]["block_threads"] == 256  # LDS / scalar walk
+    for kb, img, st in outs[:2]:
+        assert_bitwise(img, outs[2][1], f"config 5 scene, culling {kb} vs brute force")
+        assert st["casts"] == outs[2][2]["casts"]
+
+
 def test_config5_full_frame_properties(spt, ctx, oracle):
     """BASELINE config 5 at full size (10 000 spheres, 1920x1080, 256 spp, depth 50,
     LDS tree kernel): every sample accounted for, deterministic, and sampled pixels

@@ -830,6 +830,35 @@ def test_config4_eight_way_strip_split_equals_one_part(spt, ctx, golden_scenes):
     assert np.array_equal(gm, g_full.cpu().numpy())
 
 
+def test_culling_is_exact_with_exact_distance_ties(spt, ctx, golden_scenes):
+    """Every small sphere of the config-2 scene duplicated (same centre and radius,
+    another colour and material, a higher index): each hit is an exact distance tie,
+    which the reference's strict '>' scan gives to the lower index.  The box tree
+    (near test: strict, so ties are never culled) and the flat list keep that winner:
+    frames and ray counts equal brute force."""
+    base = scene_from(spt, golden_scenes, "random")
+    c, r = np.asarray(base.centers, np.float32), np.asarray(base.radii, np.float32)
+    col, m, f = np.asarray(base.colors, np.float32), np.asarray(base.materials), np.asarray(base.fuzz, np.float32)
+    small = np.nonzero(r < 0.5)[0]
+    col2 = col[small].copy()
+    col2[:, :3] = 255.0 - col2[:, :3]
+    m2 = np.where(m[small] == 3, 1, 3).astype(m.dtype)  # diffuse <-> mirror
+    scene = spt.Scene(np.concatenate([c, c[small]]), np.concatenate([r, r[small]]), np.concatenate([col, col2]),
+                      np.concatenate([m, m2]), np.concatenate([f, f[small]]))
+    setup(ctx, scene, 320, 200, 8, 50, seed=4)
+    outs = []
+    for k, b in ((0, 0), (spt._native.CLUSTER_AUTO, spt._native.TREE_AUTO), (4, 0), (8, 2)):
+        ctx.set_cluster_size(k)
+        ctx.set_cluster_tree(b)
+        ctx.reset_stats()
+        outs.append(((k, b), ctx.render_segment(0, 200, 0, 320), ctx.stats()["casts"]))
+    ctx.set_cluster_size(spt._native.CLUSTER_AUTO)
+    ctx.set_cluster_tree(spt._native.TREE_AUTO)
+    for kb, img, casts in outs[1:]:
+        assert_bitwise(img, outs[0][1], f"duplicated spheres, culling {kb} vs brute force")
+        assert casts == outs[0][2]
+
+
 def test_config5_box_tree_equals_brute_force(spt, ctx):
     """The config-5 scene (10 000 spheres in a flat layer: the grazing rays the box
     margins exist for) over the whole 1920x1080 frame at 2 spp, rendered through the box tree

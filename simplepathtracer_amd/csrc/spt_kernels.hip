@@ -66,6 +66,11 @@ constexpr uint32_t kLdsNodeRecords = SPT_LDS_NODES;
 // smallest tree walked from LDS: below it the 8 octant layouts (64 nodes: 16 KiB) fit
 // the scalar cache
 constexpr uint32_t kLdsMinNodes = 64;
+// 1: the LDS tree is walked lane by lane (find_closest_lane; 0: the whole wave walks
+// the union of its lanes' paths, find_closest)
+#ifndef SPT_LANE_WALK
+#define SPT_LANE_WALK 1
+#endif
 
 // One kernel per traversal shape (flat list of 4- or 8-slot leaves, tree of
 // 8-slot leaves), each with its own register allocation; launch_render picks.
@@ -194,7 +199,9 @@ __device__ __forceinline__ void render_body(const RenderArgs &a)
         ++d_iters;
         // ---- one cast + one shading step ----
         const bool act = ps.phase != PH_IDLE;
-        const Hit h = find_closest<TREE, LEAF, LDSN>(a.scene.accel, ps.o, ps.d, act, dg, (const uint32_t *)s_nodes);
+        const Hit h = (LDSN && SPT_LANE_WALK)
+                          ? find_closest_lane<LEAF>(a.scene.accel, ps.o, ps.d, act, dg, (const uint32_t *)s_nodes)
+                          : find_closest<TREE, LEAF, LDSN>(a.scene.accel, ps.o, ps.d, act, dg, (const uint32_t *)s_nodes);
         SPT_STAMP(d_cyc_cast);
         shade_step(a, ps, h, act, done, dropped, s_lds + (threadIdx.x & ~63u));
         SPT_STAMP(d_cyc_shade);

@@ -524,6 +524,146 @@ __device__ __forceinline__ Hit find_closest(const AccelView &ac, const f3 &o, co
     return h;
 }
 
+// The closest-contact / distance update of one member for one lane (update_member
+// for lane-divergent walks): the lane passed RaySphereIntersection with tc, hh.
+// Exact ties go to the lower original index (vector loads, behind a divergent branch).
+__device__ __forceinline__ void update_member_lane(float tc, float hh, const uint32_t *__restrict__ orig,
+                                                   uint32_t s, const f3 &o, const f3 &d, float dod, Hit &h)
+{
+    const float t = tc - sqrt_pos_normal(hh);
+    const f3 p = contact(o, d, t);
+    const bool front = dod < dot(p, d);
+    const float ds = lensq(sub(o, p));
+    bool better = front && ds < h.best;
+    if (__builtin_expect(front && ds == h.best && h.idx != kMiss, 0)) better = orig[s] < orig[h.idx];
+    h.best = better ? ds : h.best;
+    h.idx = better ? s : h.idx;
+    h.t = better ? t : h.t;
+}
+
+// Lane-divergent walk of the LDS box tree (SPT_LANE_WALK, render_kernel_lds): every
+// lane follows its own preorder/skip path through the node records (two ds_read_b128
+// per lane and node) and tests only the leaves its own ray may need, their member
+// records read by vector loads.  A lane parks the leaves it meets (two at most; it
+// stops walking at the second) and the wave tests the parked leaves together once at
+// least SPT_LANE_LEAF_T lanes hold one or no lane can walk on (Aila & Laine's
+// postponed leaves).  The wave walk (find_closest) pays for the union of its lanes'
+// leaves -- on config 5 a lane needs ~10% of the members the wave tests.  Node test,
+// margins and near bound are find_closest's, per lane; leaves are
+// tested in a lane-dependent order, and the winner is still the lexicographic minimum
+// of (distance, original index), which does not depend on the order.
+// SPT_DIAG counters here: nodes = lane node visits, live = walk iterations, leaves =
+// leaf passes, pairs = lane leaf tests.
+#ifndef SPT_LANE_LEAF_T
+#define SPT_LANE_LEAF_T 8
+#endif
+#ifndef SPT_LANE_GROUP
+#define SPT_LANE_GROUP 2
+#endif
+template <int LEAF>
+__device__ __forceinline__ Hit find_closest_lane(const AccelView &ac, const f3 &o, const f3 &d, bool active,
+                                                 CastDiag &dg, const uint32_t *lnodes)
+{
+    Hit h;
+    h.idx = kMiss;
+    h.best = FLT_MAX;
+    h.t = 0.f;
+    const float dod = dot(o, d);
+    cfloat *slots = (cfloat *)ac.slots;
+    const float ddev = lensq(d) - 1.0f;
+    const bool no_cull = active && !(ddev <= 1e-6f && ddev >= -1e-6f);
+    const float oo = lensq(o);
+    if (SPT_DIAG) dg.live_now = (uint32_t)__popcll(__ballot(active));
+    for (uint32_t g = 0; g < ac.always_groups; ++g) {
+        float4 g4[SPT_GROUP];
+#pragma unroll
+        for (int k = 0; k < SPT_GROUP; ++k) g4[k] = ld_uniform(slots, g * SPT_GROUP + k);
+        test_group<SPT_GROUP>(g4, ac.orig, g * SPT_GROUP, o, d, dod, h, dg);
+    }
+    const float olen = __builtin_amdgcn_sqrtf(oo) * 1.000001f;
+    const float el = __builtin_fmaf((float)kBoxS, olen, 1e-6f);
+    auto rcp_dir = [](float x) {
+        const float m = __builtin_fmaxf(__builtin_fabsf(x), kBoxMinDir);
+        return __builtin_amdgcn_rcpf(__builtin_copysignf(m, x));
+    };
+    const float irx = rcp_dir(d.x), iry = rcp_dir(d.y), irz = rcp_dir(d.z);
+    const float qlx = (-o.x - el) * irx, qly = (-o.y - el) * iry, qlz = (-o.z - el) * irz;
+    const float qhx = (el - o.x) * irx, qhy = (el - o.y) * iry, qhz = (el - o.z) * irz;
+    const float obs = olen + ac.pre_cm;
+    const float neta = -__builtin_fmaf(1e-6f, obs, 1e-6f);
+    const float kn = __builtin_fmaf(1e-5f, obs, 1e-6f);
+    const bool nocull = no_cull || (active && !(oo <= 1e30f));
+    auto near_bound = [&](float best) { return __builtin_fmaf(__builtin_amdgcn_sqrtf(best), 1.00001f, kn); };
+    float sbl = near_bound(h.best);
+    const uint4 *ln = (const uint4 *)lnodes;
+    const float4 *__restrict__ gs = ac.slots;
+    const uint32_t n = ac.n_nodes;
+    uint32_t i = active ? 0u : n;
+    // parked leaves (first slots), kNoSlot = none: a lane keeps walking while one
+    // leaf is parked and stops at the second
+    uint32_t leaf = kNoSlot, leaf2 = kNoSlot;
+    for (;;) {
+        const bool tr = i < n && leaf2 == kNoSlot;
+        const unsigned long long mt = __ballot(tr);
+        const unsigned long long mp = __ballot(leaf != kNoSlot);
+        if ((mt | mp) == 0ull) break;
+        if (mp != 0ull && (mt == 0ull || __popcll(mp) >= SPT_LANE_LEAF_T)) {
+            if (SPT_DIAG) {
+                dg.leaves += 1;
+                dg.pairs += (unsigned long long)__popcll(mp);
+                dg.lane_tests += (unsigned long long)LEAF * __popcll(mp);
+            }
+            if (leaf != kNoSlot) {
+                // members SPT_LANE_GROUP at a time (8 waves/SIMD: 64 VGPRs; loading a
+                // whole leaf at once spills)
+#pragma unroll 1
+                for (int k0 = 0; k0 < LEAF; k0 += SPT_LANE_GROUP) {
+                    float4 m[SPT_LANE_GROUP];
+#pragma unroll
+                    for (int k = 0; k < SPT_LANE_GROUP; ++k) m[k] = gs[leaf + k0 + k];
+#pragma unroll
+                    for (int k = 0; k < SPT_LANE_GROUP; ++k) {
+                        float tc, hh;
+                        if (ray_sphere(m[k], o, d, tc, hh))
+                            update_member_lane(tc, hh, ac.orig, leaf + k0 + k, o, d, dod, h);
+                    }
+                }
+                sbl = near_bound(h.best);
+                leaf = leaf2;
+                leaf2 = kNoSlot;
+            }
+            continue;
+        }
+        if (SPT_DIAG) {
+            dg.nodes += (unsigned long long)__popcll(mt);
+            dg.live += 1;
+        }
+        if (tr) {
+            const uint4 ra = ln[2 * i], rb = ln[2 * i + 1];
+            const float ax = __builtin_fmaf(__uint_as_float(ra.x), irx, qlx);
+            const float bx = __builtin_fmaf(__uint_as_float(ra.w), irx, qhx);
+            const float ay = __builtin_fmaf(__uint_as_float(ra.y), iry, qly);
+            const float by = __builtin_fmaf(__uint_as_float(rb.z), iry, qhy);
+            const float az = __builtin_fmaf(__uint_as_float(ra.z), irz, qlz);
+            const float bz = __builtin_fmaf(__uint_as_float(rb.w), irz, qhz);
+            const float tn = max3_raw(__builtin_fminf(ax, bx), __builtin_fminf(ay, by),
+                                      max_raw(__builtin_fminf(az, bz), neta));
+            const float tf = min3_raw(__builtin_fmaxf(ax, bx), __builtin_fmaxf(ay, by),
+                                      min_raw(__builtin_fmaxf(az, bz), sbl));
+            const bool hit = tn <= tf || nocull;
+            const bool is_leaf = rb.y != kNoSlot;
+            if (hit && is_leaf) {
+                if (leaf != kNoSlot)
+                    leaf2 = rb.y;
+                else
+                    leaf = rb.y;
+            }
+            i = (hit && !is_leaf) ? i + 1 : rb.x;
+        }
+    }
+    return h;
+}
+
 // Per-lane path state of the flattened recursion.
 struct Path {
     uint32_t phase, item, bounce, spec;

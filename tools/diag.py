@@ -43,6 +43,7 @@ lt, lp = st["diag"][12:14]
 print(f"lane-level RaySphereIntersection evaluations per ray={lt/max(st['casts'],1):.2f} "
       f"member pretests per ray={lp/max(st['casts'],1):.2f} (brute force: {scene.n})")
 print(f"render_ms={st['render_ms']:.3f}")
+print("raw diag", list(st["diag"]))
 if json_out:
     import json
     json.dump({"config": cfg, "frame": [W, H, spp, b], "spheres": scene.n, "casts": st["casts"],

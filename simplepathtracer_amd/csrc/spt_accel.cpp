@@ -42,6 +42,7 @@
 #include <cmath>
 #include <cstring>
 #include <cstdio>
+#include <cstdlib>
 #include <numeric>
 #include <string>
 
@@ -201,35 +202,107 @@ AccelTables build_accel(const float *centers4, const float *radii, uint32_t n, u
         std::vector<uint32_t> sorted(keyed.size());
         for (size_t j = 0; j < keyed.size(); ++j) sorted[j] = keyed[j].second;
 
-        // leaves: k consecutive spheres each, leaf_slots slots each
+        // Tree over leaves of k consecutive spheres of `sorted`: node = a contiguous run
+        // of leaves [c0, c1) and its children.  Flat lists (branching 0, or at most
+        // `branching` leaves): the Morton leaves in slot order.  Trees: built top down,
+        // each node's run split into up to `branching` parts by repeated halving of the
+        // part with the most leaves along the longest axis of its centres' extent (the
+        // spheres of a part reordered so that both halves stay contiguous and leaf
+        // boundaries stay at multiples of k).
         const uint32_t leaves = (uint32_t)((sorted.size() + k - 1) / k);
+        t.leaves = leaves;
+        struct TNode {
+            uint32_t c0, c1;
+            std::vector<uint32_t> kids;
+        };
+        std::vector<TNode> tn;
+        const bool tree = branching >= 2 && leaves > branching;
+        const bool topdown = tree && !(std::getenv("SPT_TREE_MORTON") && std::atoi(std::getenv("SPT_TREE_MORTON")));
+        auto sph_end = [&](uint32_t c) { return std::min(sorted.size(), (size_t)c * k); };
+        std::vector<uint32_t> top;  // children of the implicit root
+        if (!tree) {
+            for (uint32_t c = 0; c < leaves; ++c) {
+                top.push_back((uint32_t)tn.size());
+                tn.push_back({c, c + 1, {}});
+            }
+        } else if (topdown) {
+            auto halve = [&](uint32_t c0, uint32_t c1) {  // split point (a leaf index)
+                const size_t j0 = (size_t)c0 * k, j1 = sph_end(c1);
+                double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+                for (size_t j = j0; j < j1; ++j)
+                    for (int c = 0; c < 3; ++c) {
+                        lo[c] = std::min(lo[c], (double)centers4[4 * sorted[j] + c]);
+                        hi[c] = std::max(hi[c], (double)centers4[4 * sorted[j] + c]);
+                    }
+                int ax = 0;
+                for (int c = 1; c < 3; ++c)
+                    if (hi[c] - lo[c] > hi[ax] - lo[ax]) ax = c;
+                const uint32_t cm = c0 + (c1 - c0 + 1) / 2;
+                // stable order for equal keys: ties broken by the Morton position
+                std::stable_sort(sorted.begin() + j0, sorted.begin() + j1, [&](uint32_t a, uint32_t b) {
+                    return centers4[4 * a + ax] < centers4[4 * b + ax];
+                });
+                return cm;
+            };
+            auto build = [&](auto &&self, uint32_t c0, uint32_t c1) -> uint32_t {
+                const uint32_t me = (uint32_t)tn.size();
+                tn.push_back({c0, c1, {}});
+                if (c1 - c0 <= 1) return me;
+                std::vector<std::pair<uint32_t, uint32_t>> parts{{c0, c1}};
+                while (parts.size() < branching) {
+                    size_t p = 0;
+                    for (size_t q = 1; q < parts.size(); ++q)
+                        if (parts[q].second - parts[q].first > parts[p].second - parts[p].first) p = q;
+                    const auto [a0, a1] = parts[p];
+                    if (a1 - a0 <= 1) break;
+                    const uint32_t m = halve(a0, a1);
+                    parts[p] = {a0, m};
+                    parts.insert(parts.begin() + p + 1, {m, a1});
+                }
+                for (const auto &pr : parts) {
+                    const uint32_t kid = self(self, pr.first, pr.second);
+                    tn[me].kids.push_back(kid);
+                }
+                return me;
+            };
+            const uint32_t root = build(build, 0, leaves);
+            top = tn[root].kids;
+        } else {
+            // bottom up over the Morton order: `branching` consecutive nodes per parent
+            std::vector<uint32_t> level;
+            for (uint32_t c = 0; c < leaves; ++c) {
+                level.push_back((uint32_t)tn.size());
+                tn.push_back({c, c + 1, {}});
+            }
+            while (level.size() > branching) {
+                std::vector<uint32_t> up;
+                for (size_t j = 0; j < level.size(); j += branching) {
+                    TNode nd{tn[level[j]].c0, tn[level[std::min(level.size(), j + branching) - 1]].c1, {}};
+                    for (size_t q = j; q < std::min(level.size(), j + branching); ++q) nd.kids.push_back(level[q]);
+                    up.push_back((uint32_t)tn.size());
+                    tn.push_back(std::move(nd));
+                }
+                level = std::move(up);
+            }
+            top = level;
+        }
+        // leaves in slot order: k spheres each, leaf_slots slots each
         for (uint32_t c = 0; c < leaves; ++c) {
-            for (size_t j = (size_t)c * k; j < std::min(sorted.size(), (size_t)(c + 1) * k); ++j) push_slot(sorted[j]);
+            for (size_t j = (size_t)c * k; j < sph_end(c + 1); ++j) push_slot(sorted[j]);
             pad_to(leaf_slots, cbase);
         }
-        t.leaves = leaves;
-
-        // tree levels over consecutive leaves: level 0 = leaves, each node = [c0, c1)
-        struct Span {
-            uint32_t c0, c1;
+        auto depth_of = [&](auto &&self, uint32_t q) -> uint32_t {
+            uint32_t dd = 0;
+            for (uint32_t kq : tn[q].kids) dd = std::max(dd, self(self, kq));
+            return dd + 1;
         };
-        std::vector<std::vector<Span>> levels(1);
-        for (uint32_t c = 0; c < leaves; ++c) levels[0].push_back({c, c + 1});
-        if (branching >= 2)
-            while (levels.back().size() > branching) {
-                const std::vector<Span> &below = levels.back();
-                std::vector<Span> up;
-                for (size_t j = 0; j < below.size(); j += branching)
-                    up.push_back({below[j].c0, below[std::min(below.size(), j + branching) - 1].c1});
-                levels.push_back(std::move(up));
-            }
-        t.depth = (uint32_t)levels.size();
+        t.depth = 0;
+        for (uint32_t q : top) t.depth = std::max(t.depth, depth_of(depth_of, q));
 
         // bounding sphere (flat lists) or expanded box (trees) of the member spheres of
         // leaves [c0, c1); `ctr` = centre of the members' centres (sibling order)
-        const bool tree = levels.size() > 1;
-        auto bound = [&](Span sp, AccelNode &nd, double *ctr) {
-            const size_t j0 = (size_t)sp.c0 * k, j1 = std::min(sorted.size(), (size_t)sp.c1 * k);
+        auto bound = [&](const TNode &sp, AccelNode &nd, double *ctr) {
+            const size_t j0 = (size_t)sp.c0 * k, j1 = sph_end(sp.c1);
             double clo[3] = {INFINITY, INFINITY, INFINITY}, chi[3] = {-INFINITY, -INFINITY, -INFINITY};
             for (size_t j = j0; j < j1; ++j)
                 for (int c = 0; c < 3; ++c) {
@@ -269,42 +342,33 @@ AccelTables build_accel(const float *centers4, const float *radii, uint32_t n, u
         // back along the octant's diagonal, so a wave walking the layout of its
         // majority octant finds near hits first and the distance test culls more.
         // The top level sits under an implicit root (never tested).
-        std::vector<std::vector<AccelNode>> bounds(levels.size());
-        std::vector<std::vector<std::array<double, 3>>> ctrs(levels.size());
-        for (size_t lvl = 0; lvl < levels.size(); ++lvl) {
-            bounds[lvl].resize(levels[lvl].size());
-            ctrs[lvl].resize(levels[lvl].size());
-            for (size_t j = 0; j < levels[lvl].size(); ++j) bound(levels[lvl][j], bounds[lvl][j], ctrs[lvl][j].data());
-        }
-        const uint32_t top = (uint32_t)levels.size() - 1;
+        std::vector<AccelNode> bounds(tn.size());
+        std::vector<std::array<double, 3>> ctrs(tn.size());
+        for (size_t q = 0; q < tn.size(); ++q) bound(tn[q], bounds[q], ctrs[q].data());
         for (uint32_t oct = 0; oct < 8; ++oct) {
             const double sx = (oct & 1) ? -1.0 : 1.0, sy = (oct & 2) ? -1.0 : 1.0, sz = (oct & 4) ? -1.0 : 1.0;
             const size_t base = t.nodes.size();
-            auto ordered = [&](uint32_t lvl, size_t q0, size_t q1) {
-                std::vector<size_t> ix;
-                for (size_t q = q0; q < q1; ++q) ix.push_back(q);
+            auto ordered = [&](const std::vector<uint32_t> &kids) {
+                std::vector<uint32_t> ix = kids;
                 if (!tree) return ix;  // flat list: slot order (the kernel relies on it)
-                std::stable_sort(ix.begin(), ix.end(), [&](size_t a, size_t b) {
-                    const std::array<double, 3> &ca = ctrs[lvl][a], &cb = ctrs[lvl][b];
+                std::stable_sort(ix.begin(), ix.end(), [&](uint32_t a, uint32_t b) {
+                    const std::array<double, 3> &ca = ctrs[a], &cb = ctrs[b];
                     return sx * ca[0] + sy * ca[1] + sz * ca[2] < sx * cb[0] + sy * cb[1] + sz * cb[2];
                 });
                 return ix;
             };
-            auto emit = [&](auto &&self, uint32_t lvl, size_t j) -> void {
-                const Span sp = levels[lvl][j];
+            auto emit = [&](auto &&self, uint32_t q) -> void {
                 const size_t me = t.nodes.size();
-                t.nodes.push_back(bounds[lvl][j]);
-                if (lvl == 0) {
-                    t.nodes[me].slot = (uint32_t)(cbase + (size_t)sp.c0 * leaf_slots);
+                t.nodes.push_back(bounds[q]);
+                if (tn[q].kids.empty()) {
+                    t.nodes[me].slot = (uint32_t)(cbase + (size_t)tn[q].c0 * leaf_slots);
                 } else {
                     t.nodes[me].slot = kNoSlot;
-                    const size_t nb = levels[lvl - 1].size();
-                    for (size_t q : ordered(lvl - 1, j * branching, std::min(nb, (j + 1) * branching)))
-                        self(self, lvl - 1, q);
+                    for (uint32_t kq : ordered(tn[q].kids)) self(self, kq);
                 }
                 t.nodes[me].skip = (uint32_t)(t.nodes.size() - base);
             };
-            for (size_t j : ordered(top, 0, levels[top].size())) emit(emit, top, j);
+            for (uint32_t q : ordered(top)) emit(emit, q);
             if (oct == 0) t.n_nodes = (uint32_t)t.nodes.size();
             // pad node (the kernel prefetches one node past the layout)
             t.nodes.push_back(pad_node(t.n_nodes + 1));

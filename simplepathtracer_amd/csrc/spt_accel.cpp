@@ -9,12 +9,13 @@
 //  * the small spheres are sorted along a Morton curve and cut into clusters of
 //    k <= 8 members (8 slots each, dummies pad).  Up to 64 clusters form a flat list
 //    whose nodes carry a bounding sphere of their members (Cb, Rb >= |Cm - Cb| + r_m);
-//    beyond that the clusters are the leaves of a tree whose inner nodes group
-//    `branching` consecutive clusters, every tree node carrying an axis-aligned box
-//    of all member spheres below it, expanded by kBoxS Bm (Bm = max |C| + r over
-//    those members).  The tree is stored in preorder with skip links, so the
-//    wave-uniform traversal needs no stack: enter a node (next record) if any lane
-//    may pass, else jump to `skip`.
+//    beyond that the clusters are the leaves of a tree built top down by the
+//    surface-area heuristic (up to `branching` children per node, spheres regrouped
+//    into the leaves it chooses), every tree node carrying an axis-aligned box of all
+//    member spheres below it, expanded by kBoxS Bm (Bm = max |C| + r over those
+//    members).  The tree is stored in preorder with skip links, so the traversal
+//    needs no stack: enter a node (next record) if the ray (wave walk: any lane) may
+//    pass, else jump to `skip`.
 //
 // Cull conditions, derived in DESIGN.md §4.4 from an fp32 error analysis of the
 // member test and of the node test for a ray whose computed |d|^2 is within 1e-6
@@ -42,7 +43,6 @@
 #include <cmath>
 #include <cstring>
 #include <cstdio>
-#include <cstdlib>
 #include <numeric>
 #include <string>
 
@@ -206,9 +206,10 @@ AccelTables build_accel(const float *centers4, const float *radii, uint32_t n, u
         // of leaves [c0, c1) and its children.  Flat lists (branching 0, or at most
         // `branching` leaves): the Morton leaves in slot order.  Trees: built top down,
         // each node's run split into up to `branching` parts by repeated halving of the
-        // part with the most leaves along the longest axis of its centres' extent (the
-        // spheres of a part reordered so that both halves stay contiguous and leaf
-        // boundaries stay at multiples of k).
+        // part with the most leaves (halve: SAH over leaf-aligned cuts; the spheres of a
+        // part are reordered so that both halves stay contiguous and leaf boundaries stay
+        // at multiples of k).  Config 5: 118 ms per frame against 170 for the bottom-up
+        // grouping of consecutive Morton leaves, 114 for median splits.
         const uint32_t leaves = (uint32_t)((sorted.size() + k - 1) / k);
         t.leaves = leaves;
         struct TNode {
@@ -217,7 +218,6 @@ AccelTables build_accel(const float *centers4, const float *radii, uint32_t n, u
         };
         std::vector<TNode> tn;
         const bool tree = branching >= 2 && leaves > branching;
-        const bool topdown = tree && !(std::getenv("SPT_TREE_MORTON") && std::atoi(std::getenv("SPT_TREE_MORTON")));
         auto sph_end = [&](uint32_t c) { return std::min(sorted.size(), (size_t)c * k); };
         std::vector<uint32_t> top;  // children of the implicit root
         if (!tree) {
@@ -225,24 +225,57 @@ AccelTables build_accel(const float *centers4, const float *radii, uint32_t n, u
                 top.push_back((uint32_t)tn.size());
                 tn.push_back({c, c + 1, {}});
             }
-        } else if (topdown) {
-            auto halve = [&](uint32_t c0, uint32_t c1) {  // split point (a leaf index)
+        } else {
+            // split point (a leaf index) of leaves [c0, c1): the surface-area heuristic
+            // over leaf-aligned cuts along each axis (spheres sorted by that centre
+            // coordinate): min of area(left) leaves(left) + area(right) leaves(right),
+            // areas of the members' boxes; the spheres end up in the chosen axis' order
+            auto halve = [&](uint32_t c0, uint32_t c1) {
                 const size_t j0 = (size_t)c0 * k, j1 = sph_end(c1);
-                double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
-                for (size_t j = j0; j < j1; ++j)
-                    for (int c = 0; c < 3; ++c) {
-                        lo[c] = std::min(lo[c], (double)centers4[4 * sorted[j] + c]);
-                        hi[c] = std::max(hi[c], (double)centers4[4 * sorted[j] + c]);
+                {
+                    double best = INFINITY;
+                    int bax = 0;
+                    uint32_t bcut = c0 + (c1 - c0 + 1) / 2;
+                    auto area = [](const double *lo, const double *hi) {
+                        const double dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
+                        return dx * dy + dy * dz + dz * dx;
+                    };
+                    for (int ax = 0; ax < 3; ++ax) {
+                        std::stable_sort(sorted.begin() + j0, sorted.begin() + j1, [&](uint32_t a, uint32_t b) {
+                            return centers4[4 * a + ax] < centers4[4 * b + ax];
+                        });
+                        const uint32_t nl = c1 - c0;
+                        std::vector<double> left(nl + 1);  // area of leaves [c0, c0 + q)
+                        double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+                        auto grow = [&](size_t j) {
+                            const uint32_t i = sorted[j];
+                            const double r = std::fabs((double)radii[i]);
+                            for (int c = 0; c < 3; ++c) {
+                                lo[c] = std::min(lo[c], (double)centers4[4 * i + c] - r);
+                                hi[c] = std::max(hi[c], (double)centers4[4 * i + c] + r);
+                            }
+                        };
+                        for (uint32_t q = 1; q <= nl; ++q) {
+                            for (size_t j = (size_t)(c0 + q - 1) * k; j < sph_end(c0 + q); ++j) grow(j);
+                            left[q] = area(lo, hi);
+                        }
+                        std::fill(lo, lo + 3, INFINITY);
+                        std::fill(hi, hi + 3, -INFINITY);
+                        for (uint32_t q = nl - 1; q >= 1; --q) {
+                            for (size_t j = (size_t)(c0 + q) * k; j < sph_end(c0 + q + 1); ++j) grow(j);
+                            const double cost = left[q] * q + area(lo, hi) * (nl - q);
+                            if (cost < best) {
+                                best = cost;
+                                bax = ax;
+                                bcut = c0 + q;
+                            }
+                        }
                     }
-                int ax = 0;
-                for (int c = 1; c < 3; ++c)
-                    if (hi[c] - lo[c] > hi[ax] - lo[ax]) ax = c;
-                const uint32_t cm = c0 + (c1 - c0 + 1) / 2;
-                // stable order for equal keys: ties broken by the Morton position
-                std::stable_sort(sorted.begin() + j0, sorted.begin() + j1, [&](uint32_t a, uint32_t b) {
-                    return centers4[4 * a + ax] < centers4[4 * b + ax];
-                });
-                return cm;
+                    std::stable_sort(sorted.begin() + j0, sorted.begin() + j1, [&](uint32_t a, uint32_t b) {
+                        return centers4[4 * a + bax] < centers4[4 * b + bax];
+                    });
+                    return bcut;
+                }
             };
             auto build = [&](auto &&self, uint32_t c0, uint32_t c1) -> uint32_t {
                 const uint32_t me = (uint32_t)tn.size();
@@ -267,24 +300,6 @@ AccelTables build_accel(const float *centers4, const float *radii, uint32_t n, u
             };
             const uint32_t root = build(build, 0, leaves);
             top = tn[root].kids;
-        } else {
-            // bottom up over the Morton order: `branching` consecutive nodes per parent
-            std::vector<uint32_t> level;
-            for (uint32_t c = 0; c < leaves; ++c) {
-                level.push_back((uint32_t)tn.size());
-                tn.push_back({c, c + 1, {}});
-            }
-            while (level.size() > branching) {
-                std::vector<uint32_t> up;
-                for (size_t j = 0; j < level.size(); j += branching) {
-                    TNode nd{tn[level[j]].c0, tn[level[std::min(level.size(), j + branching) - 1]].c1, {}};
-                    for (size_t q = j; q < std::min(level.size(), j + branching); ++q) nd.kids.push_back(level[q]);
-                    up.push_back((uint32_t)tn.size());
-                    tn.push_back(std::move(nd));
-                }
-                level = std::move(up);
-            }
-            top = level;
         }
         // leaves in slot order: k spheres each, leaf_slots slots each
         for (uint32_t c = 0; c < leaves; ++c) {

@@ -528,8 +528,8 @@ int upload(spt_ctx *ctx, T **p, size_t *cap, const std::vector<T> &v)
     return SPT_OK;
 }
 
-// Traversal shape for the current scene: a 4-ary tree of boxes over 8-sphere
-// clusters (config 2: 14 650 Msamples/s against 13 950 for round 1's flat list of
+// Traversal shape for the current scene: a 4-ary (3-ary above 512 spheres) tree of
+// boxes over 8-sphere clusters (config 2: 14 650 Msamples/s against 13 950 for round 1's flat list of
 // 4-sphere clusters under bounding spheres); the flat list remains
 // selectable (spt_set_cluster_tree(ctx, 0)).  Scenes of <= 32 spheres are tested
 // brute force (build_accel).
@@ -541,7 +541,9 @@ Shape resolve_shape(const spt_ctx *ctx)
     const bool tree = ctx->tree_branching == SPT_TREE_AUTO ? true : ctx->tree_branching >= 2;
     Shape sh;
     sh.k = ctx->cluster_k != SPT_CLUSTER_AUTO ? ctx->cluster_k : tree ? spt::kClusterSlots : spt::kFlatLeafSlots;
-    sh.branching = tree ? (ctx->tree_branching == SPT_TREE_AUTO ? 4u : ctx->tree_branching) : 0u;
+    // auto: 4 children per node; 3 for large scenes, whose trees the LDS kernel walks
+    // lane by lane (config 5: 107 ms per frame against 110 for 4)
+    sh.branching = tree ? (ctx->tree_branching == SPT_TREE_AUTO ? (ctx->n > 512 ? 3u : 4u) : ctx->tree_branching) : 0u;
     sh.leaf_slots = !tree && sh.k <= spt::kFlatLeafSlots ? spt::kFlatLeafSlots : spt::kClusterSlots;
     return sh;
 }

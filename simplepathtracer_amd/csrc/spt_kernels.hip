@@ -65,7 +65,10 @@ constexpr uint32_t kLdsBlock = SPT_LDS_BLOCK;
 constexpr uint32_t kLdsNodeRecords = SPT_LDS_NODES;
 // smallest tree walked from LDS: below it the 8 octant layouts (64 nodes: 16 KiB) fit
 // the scalar cache
-constexpr uint32_t kLdsMinNodes = 64;
+#ifndef SPT_LDS_MIN_NODES
+#define SPT_LDS_MIN_NODES 64
+#endif
+constexpr uint32_t kLdsMinNodes = SPT_LDS_MIN_NODES;
 // 1: the LDS tree is walked lane by lane (find_closest_lane; 0: the whole wave walks
 // the union of its lanes' paths, find_closest)
 #ifndef SPT_LANE_WALK

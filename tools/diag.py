@@ -44,10 +44,22 @@ print(f"lane-level RaySphereIntersection evaluations per ray={lt/max(st['casts']
       f"member pretests per ray={lp/max(st['casts'],1):.2f} (brute force: {scene.n})")
 print(f"render_ms={st['render_ms']:.3f}")
 print("raw diag", list(st["diag"]))
+# the LDS kernel (1024-thread blocks) walks lane by lane (spt_path.h find_closest_lane):
+# nodes = lane node visits, live = walk iterations, leaves = leaf passes, pairs = lane leaf tests
+lane_walk = st["block_threads"] == 1024
+if lane_walk:
+    print(f"lane walk: node visits per ray={nodes/max(st['casts'],1):.2f} walk iterations per wave cast="
+          f"{live/max(it,1):.2f} leaf passes per wave cast={leaves/max(it,1):.2f} leaves per ray="
+          f"{pairs/max(st['casts'],1):.2f} lanes per leaf pass={pairs/max(leaves,1):.2f}")
 if json_out:
     import json
     json.dump({"config": cfg, "frame": [W, H, spp, b], "spheres": scene.n, "casts": st["casts"],
                "samples": st["samples"], "lane_tests_per_ray": lt / max(st["casts"], 1),
                "lane_pretests_per_ray": lp / max(st["casts"], 1), "clusters_entered_per_wave_cast": leaves / max(it, 1),
                "tree_nodes_per_wave_cast": nodes / max(it, 1), "live_lanes_per_iter": st["casts"] / max(it, 1),
-               "build": "SPT_DIAG=1 (libspt_hip_diag.so), counters only, never timed"}, open(json_out, "w"), indent=1)
+               "build": "SPT_DIAG=1 (libspt_hip_diag.so), counters only, never timed",
+               **({"walk": "lane", "lane_node_visits_per_ray": nodes / max(st["casts"], 1),
+                   "walk_iters_per_wave_cast": live / max(it, 1), "leaf_passes_per_wave_cast": leaves / max(it, 1),
+                   "leaves_per_ray": pairs / max(st["casts"], 1), "lanes_per_leaf_pass": pairs / max(leaves, 1),
+                   "note": "lane walk: clusters_entered/tree_nodes per wave cast count leaf passes and lane "
+                           "node visits"} if lane_walk else {"walk": "wave"})}, open(json_out, "w"), indent=1)

@@ -134,9 +134,11 @@ SPT_API int spt_set_params(spt_ctx *ctx, uint32_t width, uint32_t height, uint32
  * ray (the reference's brute force).  Results are identical either way. */
 #define SPT_CLUSTER_AUTO 0xFFFFFFFFu
 SPT_API int spt_set_cluster_size(spt_ctx *ctx, uint32_t k);
-/* Clusters are the leaves of a tree of bounding spheres walked by the whole wave;
- * `branching` children per inner node, 0 = flat list of clusters, SPT_TREE_AUTO
- * (default) = flat while n / 8 <= 64, else 4.  Results are identical for any value. */
+/* Clusters are the leaves of a tree of expanded boxes (built top down by the
+ * surface-area heuristic); `branching` children per inner node at most, 0 = flat list
+ * of clusters under bounding spheres, SPT_TREE_AUTO (default) = a tree with 4 (scenes
+ * of <= 512 spheres) or 3 children.  Trees of 64..2431 nodes are walked lane by lane
+ * from LDS, others by the whole wave.  Results are identical for any value. */
 #define SPT_TREE_AUTO 0xFFFFFFFFu
 SPT_API int spt_set_cluster_tree(spt_ctx *ctx, uint32_t branching);
 /* Host-only check (no device needed): build the traversal tables for a scene and

@@ -545,9 +545,9 @@ __device__ __forceinline__ void update_member_lane(float tc, float hh, const uin
 // lane follows its own preorder/skip path through the node records (two ds_read_b128
 // per lane and node) and tests only the leaves its own ray may need, their member
 // records read by vector loads.  A lane parks the leaves it meets (two at most; it
-// stops walking at the second) and the wave tests the parked leaves together once at
-// least SPT_LANE_LEAF_T lanes hold one or no lane can walk on (Aila & Laine's
-// postponed leaves).  The wave walk (find_closest) pays for the union of its lanes'
+// stops walking at the second) and the wave tests the parked leaves -- each lane all
+// of its own -- once SPT_LANE_LEAF_T lanes hold one (64: every lane) or no lane can
+// walk on (Aila & Laine's postponed leaves, while-while).  The wave walk (find_closest) pays for the union of its lanes'
 // leaves -- on config 5 a lane needs ~10% of the members the wave tests.  Node test,
 // margins and near bound are find_closest's, per lane; leaves are
 // tested in a lane-dependent order, and the winner is still the lexicographic minimum
@@ -555,7 +555,7 @@ __device__ __forceinline__ void update_member_lane(float tc, float hh, const uin
 // SPT_DIAG counters here: nodes = lane node visits, live = walk iterations, leaves =
 // leaf passes, pairs = lane leaf tests.
 #ifndef SPT_LANE_LEAF_T
-#define SPT_LANE_LEAF_T 24
+#define SPT_LANE_LEAF_T 64
 #endif
 #ifndef SPT_LANE_GROUP
 #define SPT_LANE_GROUP 2
@@ -614,23 +614,25 @@ __device__ __forceinline__ Hit find_closest_lane(const AccelView &ac, const f3 &
                 dg.lane_tests += (unsigned long long)LEAF * __popcll(mp);
             }
             if (leaf != kNoSlot) {
-                // members SPT_LANE_GROUP at a time (8 waves/SIMD: 64 VGPRs; loading a
-                // whole leaf at once spills)
+                // the lane's parked leaves (one or two) as one run of members, taken
+                // SPT_LANE_GROUP at a time (8 waves/SIMD: 64 VGPRs; loading a whole
+                // leaf at once spills)
+                const int lim = leaf2 != kNoSlot ? 2 * LEAF : LEAF;
 #pragma unroll 1
-                for (int k0 = 0; k0 < LEAF; k0 += SPT_LANE_GROUP) {
+                for (int k0 = 0; k0 < lim; k0 += SPT_LANE_GROUP) {
+                    const uint32_t base = k0 < LEAF ? leaf + k0 : leaf2 + (k0 - LEAF);
                     float4 m[SPT_LANE_GROUP];
 #pragma unroll
-                    for (int k = 0; k < SPT_LANE_GROUP; ++k) m[k] = gs[leaf + k0 + k];
+                    for (int k = 0; k < SPT_LANE_GROUP; ++k) m[k] = gs[base + k];
 #pragma unroll
                     for (int k = 0; k < SPT_LANE_GROUP; ++k) {
                         float tc, hh;
                         if (ray_sphere(m[k], o, d, tc, hh))
-                            update_member_lane(tc, hh, ac.orig, leaf + k0 + k, o, d, dod, h);
+                            update_member_lane(tc, hh, ac.orig, base + k, o, d, dod, h);
                     }
                 }
                 sbl = near_bound(h.best);
-                leaf = leaf2;
-                leaf2 = kNoSlot;
+                leaf = leaf2 = kNoSlot;
             }
             continue;
         }

@@ -539,6 +539,53 @@ def test_culling_is_exact_far_and_scaled(spt, ctx, golden_scenes, shift, scale):
         assert casts == outs[0][2]
 
 
+@pytest.mark.parametrize("case", ["ties", "far", "small", "large"])
+def test_lane_walk_is_exact(spt, ctx, case):
+    """The lane walk of the LDS box tree (find_closest_lane: each lane its own path and
+    leaves, per-lane tie-break by original index) on a 1 500-sphere
+    stress scene: with every small sphere duplicated (exact distance ties: the lower
+    index wins, as in the reference's strict scan), moved 3600 units from the origin,
+    shrunk 1000x and enlarged 30x.  Frames and ray counts equal brute force, and the
+    tree run really took the 1 024-thread LDS kernel."""
+    base = spt.generate_stress(7, 1500)
+    c, r = np.asarray(base.centers, np.float32).copy(), np.asarray(base.radii, np.float32).copy()
+    col, m, f = np.asarray(base.colors, np.float32), np.asarray(base.materials), np.asarray(base.fuzz, np.float32)
+    shift, scale = (0.0, 0.0, 0.0), 1.0
+    if case == "ties":
+        small = np.nonzero(r < 0.5)[0]
+        col2 = col[small].copy()
+        col2[:, :3] = 255.0 - col2[:, :3]
+        m2 = np.where(m[small] == 3, 1, 3).astype(m.dtype)
+        c, r = np.concatenate([c, c[small]]), np.concatenate([r, r[small]])
+        col, m, f = np.concatenate([col, col2]), np.concatenate([m, m2]), np.concatenate([f, f[small]])
+    else:
+        shift, scale = {"far": ((3000.0, 0.0, -2000.0), 1.0), "small": ((0.0, 0.0, 0.0), 1e-3),
+                        "large": ((-40.0, 7.0, 55.0), 30.0)}[case]
+        c[:, :3] = (c[:, :3] * np.float32(scale) + np.float32(shift)).astype(np.float32)
+        r = (r * np.float32(scale)).astype(np.float32)
+    scene = spt.Scene(c, r, col, m, f)
+    eye = [(e * scale + s) for e, s in zip(EYE[:3], shift)] + [0]
+    look = [(e * scale + s) for e, s in zip(LOOK[:3], shift)] + [0]
+    ctx.set_scene(scene)
+    ctx.set_camera(spt.camera_basis(eye, look, UP), eye, SKY)
+    ctx.set_params(320, 200, 4, 50, 5)
+    outs = []
+    for k, b in ((0, 0), (spt._native.CLUSTER_AUTO, spt._native.TREE_AUTO), (8, 4)):
+        ctx.set_cluster_size(k)
+        ctx.set_cluster_tree(b)
+        ctx.reset_stats()
+        img = ctx.render_segment(0, 200, 0, 320)
+        st = ctx.stats()
+        if k != 0:
+            assert st["block_threads"] == 1024, (k, b, st["block_threads"])
+        outs.append(((k, b), img, st["casts"]))
+    ctx.set_cluster_size(spt._native.CLUSTER_AUTO)
+    ctx.set_cluster_tree(spt._native.TREE_AUTO)
+    for kb, img, casts in outs[1:]:
+        assert_bitwise(img, outs[0][1], f"lane walk {case}, culling {kb} vs brute force")
+        assert casts == outs[0][2]
+
+
 @pytest.mark.parametrize("task", [False, True])
 def test_progressive_passes_equal_lower_spp_renders(spt, ctx, golden_scenes, task):
     """spt_render_progressive (the preview of RenderImageParallelMain): after every pass

@@ -553,7 +553,7 @@ __device__ __forceinline__ void update_member_lane(float tc, float hh, const uin
 // tested in a lane-dependent order, and the winner is still the lexicographic minimum
 // of (distance, original index), which does not depend on the order.
 // SPT_DIAG counters here: nodes = lane node visits, live = walk iterations, leaves =
-// leaf passes, pairs = lane leaf tests.
+// leaf passes, pairs = (lane, leaf) tests.
 #ifndef SPT_LANE_LEAF_T
 #define SPT_LANE_LEAF_T 64
 #endif
@@ -609,9 +609,10 @@ __device__ __forceinline__ Hit find_closest_lane(const AccelView &ac, const f3 &
         if ((mt | mp) == 0ull) break;
         if (mp != 0ull && (mt == 0ull || __popcll(mp) >= SPT_LANE_LEAF_T)) {
             if (SPT_DIAG) {
+                const unsigned long long nl = (unsigned long long)(__popcll(mp) + __popcll(__ballot(leaf2 != kNoSlot)));
                 dg.leaves += 1;
-                dg.pairs += (unsigned long long)__popcll(mp);
-                dg.lane_tests += (unsigned long long)LEAF * __popcll(mp);
+                dg.pairs += nl;
+                dg.lane_tests += (unsigned long long)LEAF * nl;
             }
             if (leaf != kNoSlot) {
                 // the lane's parked leaves (one or two) as one run of members, taken

@@ -50,7 +50,7 @@ lane_walk = st["block_threads"] == 1024
 if lane_walk:
     print(f"lane walk: node visits per ray={nodes/max(st['casts'],1):.2f} walk iterations per wave cast="
           f"{live/max(it,1):.2f} leaf passes per wave cast={leaves/max(it,1):.2f} leaves per ray="
-          f"{pairs/max(st['casts'],1):.2f} lanes per leaf pass={pairs/max(leaves,1):.2f}")
+          f"{pairs/max(st['casts'],1):.2f} lane leaves per leaf pass={pairs/max(leaves,1):.2f}")
 if json_out:
     import json
     json.dump({"config": cfg, "frame": [W, H, spp, b], "spheres": scene.n, "casts": st["casts"],
@@ -60,6 +60,6 @@ if json_out:
                "build": "SPT_DIAG=1 (libspt_hip_diag.so), counters only, never timed",
                **({"walk": "lane", "lane_node_visits_per_ray": nodes / max(st["casts"], 1),
                    "walk_iters_per_wave_cast": live / max(it, 1), "leaf_passes_per_wave_cast": leaves / max(it, 1),
-                   "leaves_per_ray": pairs / max(st["casts"], 1), "lanes_per_leaf_pass": pairs / max(leaves, 1),
+                   "leaves_per_ray": pairs / max(st["casts"], 1), "lane_leaves_per_leaf_pass": pairs / max(leaves, 1),
                    "note": "lane walk: clusters_entered/tree_nodes per wave cast count leaf passes and lane "
                            "node visits"} if lane_walk else {"walk": "wave"})}, open(json_out, "w"), indent=1)

@@ -213,7 +213,7 @@ __device__ __forceinline__ void render_body(const RenderArgs &a)
                           ? find_closest_lane<LEAF>(a.scene.accel, ps.o, ps.d, act, dg, (const uint32_t *)s_nodes)
                           : find_closest<TREE, LEAF, LDSN>(a.scene.accel, ps.o, ps.d, act, dg, (const uint32_t *)s_nodes);
         SPT_STAMP(d_cyc_cast);
-        shade_step(a, ps, h, act, done, dropped, s_lds + (threadIdx.x & ~63u));
+        shade_step<true>(a, ps, h, act, done, dropped, s_lds + (threadIdx.x & ~63u));
         SPT_STAMP(d_cyc_shade);
     }
 

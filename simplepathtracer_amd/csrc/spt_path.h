@@ -730,11 +730,26 @@ __device__ __forceinline__ f3 coop_ball_vector(uint64_t &st, bool need, uint32_t
     return r;
 }
 
+#if defined(__HIP_DEVICE_COMPILE__)
+// The kernel's RenderArgs in the kernarg segment, behind an opaque zero offset: the
+// refill-only fields read through it are loaded (scalar cache) where they are used
+// instead of being hoisted into SGPRs for the kernel's lifetime.  Only valid in a
+// kernel whose first argument is a RenderArgs (render_kernel: start_path<true>).
+typedef __attribute__((address_space(4))) const RenderArgs kargs_t;
+__device__ __forceinline__ kargs_t *kernarg_args()
+{
+    uint32_t z;
+    asm volatile("s_mov_b32 %0, 0" : "=s"(z));
+    typedef __attribute__((address_space(4))) const char kchar;
+    return (kargs_t *)((kchar *)__builtin_amdgcn_kernarg_segment_ptr() + z);
+}
+#endif
+
 // SampleColorRefractive (SingleThreadPathTracer.hpp:48-92) for a lane whose ray hit
 // the glass slot idx at the contact point ps.o: new ps.o (exit point) and ps.d.
-__device__ __forceinline__ void refract_event(const RenderArgs &a, Path &ps, uint32_t idx)
+__device__ __forceinline__ void refract_event(const float4 *__restrict__ slots, Path &ps, uint32_t idx)
 {
-    const float4 cs = a.scene.accel.slots[idx];
+    const float4 cs = slots[idx];
     const f3 C = mk(cs.x, cs.y, cs.z);
     const f3 nrm = normalize(sub(ps.o, C));
     const f3 d = ps.d;
@@ -778,15 +793,16 @@ __device__ __forceinline__ void refract_event(const RenderArgs &a, Path &ps, uin
 // its own queue order; so two paths of a sample reach `colors` in the order of
 // (key, pixel) -- which only matters where colorIndex aliases pixels (non-square
 // tiles, lines 103 and 186; fold_kernel).
-__device__ __forceinline__ void finish_step(const RenderArgs &a, Path &ps, bool fin, bool spec_event, bool refr_event,
-                                            bool sky, f3 col, unsigned long long &done, unsigned long long &dropped)
+__device__ __forceinline__ void finish_step(uint32_t mode, float *samples, Path &ps, bool fin, bool spec_event,
+                                            bool refr_event, bool sky, f3 col, unsigned long long &done,
+                                            unsigned long long &dropped)
 {
     bool counted = true;
     if (spec_event) {
         const uint32_t k = ps.spec & 0xFFFFu;
-        if (a.mode == 1u && k < kTaskPasses && refr_event) ps.spec |= 1u << (16u + k);
+        if (mode == 1u && k < kTaskPasses && refr_event) ps.spec |= 1u << (16u + k);
         ++ps.spec;
-        if (a.mode == 1u && k + 1u >= kTaskPasses) {
+        if (mode == 1u && k + 1u >= kTaskPasses) {
             // RenderSegmentTask: this path would be processed in pass 10, which never runs
             fin = true;
             counted = false;
@@ -798,16 +814,16 @@ __device__ __forceinline__ void finish_step(const RenderArgs &a, Path &ps, bool 
         }
     }
     if (fin) {
-        if (a.mode == 0u) {
+        if (mode == 0u) {
             // RenderSegment counts every sample: 12-byte slots
-            float *o3 = a.samples + (size_t)3 * ps.item;
+            float *o3 = samples + (size_t)3 * ps.item;
             o3[0] = col.x;
             o3[1] = col.y;
             o3[2] = col.z;
         } else {
             const uint32_t key =
                 counted ? 1u + (((ps.spec & 0xFFFFu) << 11) | (sky ? 1u << 10 : 0u) | ((ps.spec >> 16) & 0x3FFu)) : 0u;
-            *(float4 *)(a.samples + (size_t)4 * ps.item) = make_float4(col.x, col.y, col.z, __uint_as_float(key));
+            *(float4 *)(samples + (size_t)4 * ps.item) = make_float4(col.x, col.y, col.z, __uint_as_float(key));
         }
         ps.phase = PH_IDLE;
         ps.d = mk(0.f, 0.f, 0.f);
@@ -820,6 +836,7 @@ __device__ __forceinline__ void finish_step(const RenderArgs &a, Path &ps, bool 
 // bounce loop (21-37) in PH_DLOOP.  Finishing paths write their sample slot.
 // Called by every lane of the wave (`act` = the lane holds a path), so the
 // cooperative cube-minus-ball sampler runs in uniform control flow.
+template <bool KARG = false>
 __device__ __forceinline__ void shade_step(const RenderArgs &a, Path &ps, const Hit &h, bool act,
                                            unsigned long long &done, unsigned long long &dropped, uint32_t *lds)
 {
@@ -827,6 +844,24 @@ __device__ __forceinline__ void shade_step(const RenderArgs &a, Path &ps, const 
     const float4 *__restrict__ hit = a.scene.accel.slots;
     const float4 *__restrict__ shade = a.scene.shade;
     const uint32_t *__restrict__ mat = a.scene.mat;
+    float *samples = a.samples;
+    uint32_t mode = a.mode;
+    float sky0 = a.cam.sky[0], sky1 = a.cam.sky[1], sky2 = a.cam.sky[2];
+#if defined(__HIP_DEVICE_COMPILE__)
+    if constexpr (KARG) {
+        // render kernels: read at the point of use from the kernarg segment (scalar
+        // loads) instead of holding them in SGPRs across the loop
+        kargs_t &k = *kernarg_args();
+        hit = k.scene.accel.slots;
+        shade = k.scene.shade;
+        mat = k.scene.mat;
+        samples = k.samples;
+        mode = k.mode;
+        sky0 = k.cam.sky[0];
+        sky1 = k.cam.sky[1];
+        sky2 = k.cam.sky[2];
+    }
+#endif
     const uint32_t idx = h.idx;
     bool fin = false;
     f3 col = mk(0.f, 0.f, 0.f);
@@ -852,7 +887,7 @@ __device__ __forceinline__ void shade_step(const RenderArgs &a, Path &ps, const 
         if (!scatter && !refr) {
             // SampleColorSkybox, lines 11-14
             const float k = ps.d.y + 1.f;
-            col = mul(mk(a.cam.sky[0] * k, a.cam.sky[1] * k, a.cam.sky[2] * k), 0.5f);
+            col = mul(mk(sky0 * k, sky1 * k, sky2 * k), 0.5f);
             fin = true;
         }
     }
@@ -884,30 +919,16 @@ __device__ __forceinline__ void shade_step(const RenderArgs &a, Path &ps, const 
     }
     if (refr) {
         ps.o = contact(ps.o, ps.d, h.t);
-        refract_event(a, ps, idx);
+        refract_event(hit, ps, idx);
         spec_event = true;
     }
-    finish_step(a, ps, fin, spec_event, refr, !dl, col, done, dropped);
+    finish_step(mode, samples, ps, fin, spec_event, refr, !dl, col, done, dropped);
 }
 
 
 // Start the path of batch item `mine`: its (pixel, sample), keyed RNG stream and
 // primary ray (SingleThreadPathTracer.hpp:123-130).  rw, rh: shared reciprocals
 // of g_width, g_height (div_core); `rows` = rows of the region.
-#if defined(__HIP_DEVICE_COMPILE__)
-// The kernel's RenderArgs in the kernarg segment, behind an opaque zero offset: the
-// refill-only fields read through it are loaded (scalar cache) where they are used
-// instead of being hoisted into SGPRs for the kernel's lifetime.  Only valid in a
-// kernel whose first argument is a RenderArgs (render_kernel: start_path<true>).
-typedef __attribute__((address_space(4))) const RenderArgs kargs_t;
-__device__ __forceinline__ kargs_t *kernarg_args()
-{
-    uint32_t z;
-    asm volatile("s_mov_b32 %0, 0" : "=s"(z));
-    typedef __attribute__((address_space(4))) const char kchar;
-    return (kargs_t *)((kchar *)__builtin_amdgcn_kernarg_segment_ptr() + z);
-}
-#endif
 
 __device__ __forceinline__ void start_path(const RenderArgs &a, uint32_t mine, uint32_t rows, const Recip &rw,
                                            const Recip &rh, const f3 &eye, Path &ps)

@@ -26,6 +26,7 @@
 // sequential reference loop whatever order the paths finished in.
 #include "spt_path.h"
 
+#include <algorithm>
 #include <mutex>
 
 namespace spt {
@@ -69,6 +70,14 @@ constexpr uint32_t kLdsNodeRecords = SPT_LDS_NODES;
 #define SPT_LDS_MIN_NODES 64
 #endif
 constexpr uint32_t kLdsMinNodes = SPT_LDS_MIN_NODES;
+// largest tree walked lane by lane from global memory; larger ones take the wave walk
+// (stress scenes at 16 spp, lane / wave walk: 20 000 spheres, 4 083 nodes, 12.7 / 18.6
+// ms; 30 000, 6 104: 15.6 / 20.1; 40 000, 8 115: 17.7 / 20.2; 50 000, 10 053: 23.8 /
+// 21.2 -- the per-lane node reads outgrow the caches)
+#ifndef SPT_GLANE_MAX_NODES
+#define SPT_GLANE_MAX_NODES 9000
+#endif
+constexpr uint32_t kGlaneMaxNodes = SPT_GLANE_MAX_NODES;
 #ifndef SPT_REFILL_MIN
 #define SPT_REFILL_MIN 16
 #endif
@@ -83,7 +92,7 @@ constexpr uint32_t kLdsMinNodes = SPT_LDS_MIN_NODES;
 // BATCH: the launch renders a.n_rects rectangles (a.rects, concurrent host calls
 // batched by spt_api.cpp); each refill then serves lanes from one claim only, and a
 // claim's rectangle is looked up once per claim.
-template <bool TREE, int LEAF, bool LDSN, uint32_t BLOCK, bool BATCH = false>
+template <bool TREE, int LEAF, bool LDSN, uint32_t BLOCK, bool BATCH = false, bool GLANE = false>
 __device__ __forceinline__ void render_body(const RenderArgs &a)
 {
     const uint32_t lane = __lane_id();
@@ -209,8 +218,11 @@ __device__ __forceinline__ void render_body(const RenderArgs &a)
         ++d_iters;
         // ---- one cast + one shading step ----
         const bool act = ps.phase != PH_IDLE;
+        // GLANE: the lane walk over layout 0 in global memory (trees too large for LDS)
         const Hit h = (LDSN && SPT_LANE_WALK)
                           ? find_closest_lane<LEAF>(a.scene.accel, ps.o, ps.d, act, dg, (const uint32_t *)s_nodes)
+                      : GLANE
+                          ? find_closest_lane<LEAF>(a.scene.accel, ps.o, ps.d, act, dg, (const uint32_t *)a.scene.accel.nodes)
                           : find_closest<TREE, LEAF, LDSN>(a.scene.accel, ps.o, ps.d, act, dg, (const uint32_t *)s_nodes);
         SPT_STAMP(d_cyc_cast);
         shade_step<true>(a, ps, h, act, done, dropped, s_lds + (threadIdx.x & ~63u));
@@ -265,6 +277,17 @@ template <bool TREE, int LEAF>
 __global__ __launch_bounds__(kRenderBlock) SPT_RENDER_ATTR void render_kernel_batch(RenderArgs a)
 {
     render_body<TREE, LEAF, false, kRenderBlock, true>(a);
+}
+
+// trees of kLdsNodeRecords to kGlaneMaxNodes nodes: the lane walk reading layout 0 from
+// global memory (L1/L2), in the 256-thread kernel's shape
+__global__ __launch_bounds__(kRenderBlock) SPT_RENDER_ATTR void render_kernel_glane(RenderArgs a)
+{
+    render_body<true, (int)kClusterSlots, false, kRenderBlock, false, true>(a);
+}
+__global__ __launch_bounds__(kRenderBlock) SPT_RENDER_ATTR void render_kernel_glane_batch(RenderArgs a)
+{
+    render_body<true, (int)kClusterSlots, false, kRenderBlock, true, true>(a);
 }
 
 // its own register budget: 1024-thread blocks, two per CU, need 8 waves per SIMD
@@ -483,6 +506,13 @@ hipError_t launch_render(const RenderArgs &a, LaunchShape &sh, hipStream_t s)
     }
     sh.ran_grid = sh.grid;
     sh.ran_block = sh.block;
+    if (a.scene.accel.tree && a.scene.accel.n_nodes >= kLdsMinNodes && a.scene.accel.n_nodes <= kGlaneMaxNodes) {
+        if (batch)
+            hipLaunchKernelGGL(render_kernel_glane_batch, dim3(sh.grid), dim3(sh.block), 0, s, a);
+        else
+            hipLaunchKernelGGL(render_kernel_glane, dim3(sh.grid), dim3(sh.block), 0, s, a);
+        return hipGetLastError();
+    }
     if (batch) {
         if (a.scene.accel.tree)
             hipLaunchKernelGGL((render_kernel_batch<true, (int)kClusterSlots>), dim3(sh.grid), dim3(sh.block), 0, s, a);
@@ -529,14 +559,15 @@ uint32_t render_group_size() { return SPT_GROUP; }
 
 hipError_t render_occupancy(uint32_t block, int *blocks_per_cu)
 {
-    // the smallest occupancy of the three shapes sizes the persistent grid
-    int a = 0, b = 0, c = 0;
+    // the smallest occupancy of the four shapes sizes the persistent grid
+    int a = 0, b = 0, c = 0, g = 0;
     hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, render_kernel<true, (int)kClusterSlots>, (int)block, 0);
     if (e == hipSuccess)
         e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, render_kernel<false, (int)kFlatLeafSlots>, (int)block, 0);
     if (e == hipSuccess)
         e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&c, render_kernel<false, (int)kClusterSlots>, (int)block, 0);
-    *blocks_per_cu = a < b ? (a < c ? a : c) : (b < c ? b : c);
+    if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&g, render_kernel_glane, (int)block, 0);
+    *blocks_per_cu = std::min(std::min(a, b), std::min(c, g));
     // the occupancy API reports one block per CU too many at 81-96 and 97-112 SGPRs
     // (MI355X_MICROARCH.md, Correctness boundaries): waves per SIMD are bounded by
     // 800 / (ceil(sgpr / 16) * 16 + 16) SGPRs; 256-thread blocks = 1 wave per SIMD

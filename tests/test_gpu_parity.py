@@ -654,11 +654,12 @@ def test_config5_scene_region_vs_oracle(spt, ctx, oracle):
     assert_bitwise(got[:, :3], want[:, :3], "config-5 scene region")
 
 
-@pytest.mark.parametrize("n", [10000, 20000])
+@pytest.mark.parametrize("n", [10000, 20000, 60000])
 def test_tree_kernels_lds_and_scalar_vs_oracle(spt, ctx, oracle, n):
-    """Both tree kernels: up to 2431 nodes the walk reads layout 0 from the block's LDS
-    copy (render_kernel_lds); a 20 000-sphere scene has more nodes and
-    takes the scalar-load kernel over the 8 octant layouts.  A 16x8 region at 4 spp,
+    """The three tree walks: up to 2431 nodes each lane walks layout 0
+    from the block's LDS copy (render_kernel_lds); up to 9000 nodes (20 000 spheres)
+    from global memory (render_kernel_glane); a 60 000-sphere tree is walked by the
+    whole wave with scalar loads over the 8 octant layouts.  A 16x8 region at 4 spp,
     bit-exact against the oracle's brute-force scan, and the same ray count."""
     import ctypes
     s = spt.generate_stress(3, n)
@@ -666,9 +667,11 @@ def test_tree_kernels_lds_and_scalar_vs_oracle(spt, ctx, oracle, n):
     r = np.ascontiguousarray(s.radii, np.float32)
     nodes = ctypes.c_uint32(0)
     P = ctypes.c_void_p
-    assert spt.lib().spt_accel_check(c.ctypes.data_as(P), r.ctypes.data_as(P), len(r), 8, 4,
+    assert spt.lib().spt_accel_check(c.ctypes.data_as(P), r.ctypes.data_as(P), len(r), 8, 3,
                                             ctypes.byref(nodes)) == 0
-    assert (nodes.value + 1 <= 2432) == (n == 10000), nodes.value
+    want_walk = {10000: "lds", 20000: "global", 60000: "wave"}[n]
+    walk = "lds" if nodes.value + 1 <= 2432 else "global" if nodes.value <= 9000 else "wave"
+    assert walk == want_walk, nodes.value
     setup(ctx, s, 1920, 1080, 4, 50)
     region = (500, 508, 944, 960)
     ctx.reset_stats()

@@ -138,7 +138,8 @@ SPT_API int spt_set_cluster_size(spt_ctx *ctx, uint32_t k);
  * surface-area heuristic); `branching` children per inner node at most, 0 = flat list
  * of clusters under bounding spheres, SPT_TREE_AUTO (default) = a tree with 4 (scenes
  * of <= 512 spheres) or 3 children.  Trees of 64..2431 nodes are walked lane by lane
- * from LDS, others by the whole wave.  Results are identical for any value. */
+ * from LDS, up to 9000 nodes lane by lane from global memory, others by the whole
+ * wave.  Results are identical for any value. */
 #define SPT_TREE_AUTO 0xFFFFFFFFu
 SPT_API int spt_set_cluster_tree(spt_ctx *ctx, uint32_t branching);
 /* Host-only check (no device needed): build the traversal tables for a scene and

@@ -539,15 +539,17 @@ def test_culling_is_exact_far_and_scaled(spt, ctx, golden_scenes, shift, scale):
         assert casts == outs[0][2]
 
 
+@pytest.mark.parametrize("n", [1500, 15000])
 @pytest.mark.parametrize("case", ["ties", "far", "small", "large"])
-def test_lane_walk_is_exact(spt, ctx, case):
-    """The lane walk of the LDS box tree (find_closest_lane: each lane its own path and
-    leaves, per-lane tie-break by original index) on a 1 500-sphere
-    stress scene: with every small sphere duplicated (exact distance ties: the lower
-    index wins, as in the reference's strict scan), moved 3600 units from the origin,
-    shrunk 1000x and enlarged 30x.  Frames and ray counts equal brute force, and the
-    tree run really took the 1 024-thread LDS kernel."""
-    base = spt.generate_stress(7, 1500)
+def test_lane_walk_is_exact(spt, ctx, case, n):
+    """The lane walk of the box tree (find_closest_lane: each lane its own path and
+    leaves, per-lane tie-break by original index) from LDS (1 500
+    spheres: the 1 024-thread kernel) and from global memory (15 000: the 256-thread
+    render_kernel_glane) on a stress scene: with every small sphere duplicated (exact
+    distance ties: the lower index wins, as in the reference's strict scan), moved 3600
+    units from the origin, shrunk 1000x and enlarged 30x.  Frames and ray counts equal
+    brute force."""
+    base = spt.generate_stress(7, n)
     c, r = np.asarray(base.centers, np.float32).copy(), np.asarray(base.radii, np.float32).copy()
     col, m, f = np.asarray(base.colors, np.float32), np.asarray(base.materials), np.asarray(base.fuzz, np.float32)
     shift, scale = (0.0, 0.0, 0.0), 1.0
@@ -577,7 +579,7 @@ def test_lane_walk_is_exact(spt, ctx, case):
         img = ctx.render_segment(0, 200, 0, 320)
         st = ctx.stats()
         if k != 0:
-            assert st["block_threads"] == 1024, (k, b, st["block_threads"])
+            assert st["block_threads"] == (1024 if n == 1500 else 256), (k, b, st["block_threads"])
         outs.append(((k, b), img, st["casts"]))
     ctx.set_cluster_size(spt._native.CLUSTER_AUTO)
     ctx.set_cluster_tree(spt._native.TREE_AUTO)

@@ -661,8 +661,9 @@ def test_tree_kernels_lds_and_scalar_vs_oracle(spt, ctx, oracle, n):
     """The three tree walks: up to 2431 nodes each lane walks layout 0
     from the block's LDS copy (render_kernel_lds); up to 9000 nodes (20 000 spheres)
     from global memory (render_kernel_glane); a 60 000-sphere tree is walked by the
-    whole wave with scalar loads over the 8 octant layouts.  A 16x8 region at 4 spp,
-    bit-exact against the oracle's brute-force scan, and the same ray count."""
+    whole wave with scalar loads over the 8 octant layouts.  A 16x8 region at 4 spp
+    through the batched drop-in path and the device-resident path, bit-exact against
+    the oracle's brute-force scan, and the same ray count."""
     import ctypes
     s = spt.generate_stress(3, n)
     c = np.ascontiguousarray(s.centers, np.float32)
@@ -683,6 +684,13 @@ def test_tree_kernels_lds_and_scalar_vs_oracle(spt, ctx, oracle, n):
     want, casts = oracle.render_segment(osc, fr, *region)
     assert_bitwise(got[:, :3], want[:, :3], f"{n}-sphere region")
     assert ctx.stats()["casts"] == casts
+    # the device-resident path (spt_render_rows_async: the unbatched kernels)
+    import torch
+    yB, yE, xB, xE = region
+    d = torch.zeros(((yE - yB) * (xE - xB), 4), dtype=torch.float32, device="cuda")
+    ctx.render_rows_async(0, yB, yE, 1, 1, 0, xB, xE, d.data_ptr(), 0)
+    ctx.synchronize()
+    assert_bitwise(d.cpu().numpy()[:, :3], want[:, :3], f"{n}-sphere region, device-resident")
 
 
 def test_config3_full_frame_batches_vs_oracle(spt, ctx, oracle, golden_scenes):

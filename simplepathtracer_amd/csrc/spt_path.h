@@ -560,14 +560,23 @@ __device__ __forceinline__ void update_member_lane(float tc, float hh, const uin
 #ifndef SPT_LANE_GROUP
 #define SPT_LANE_GROUP 2
 #endif
+// The lane walk as a resumable cast: `fresh` lanes start (winner none, node 0); the
+// others continue from their saved node, parked leaves and winner.  The always-list is
+// re-tested for every lane (idempotent: a sphere tested twice cannot replace itself --
+// equal distance and index).  Runs at most `budget` walk iterations and leaf passes;
+// returns whether the lane's cast is complete (inactive lanes: true).
 template <int LEAF>
-__device__ __forceinline__ Hit find_closest_lane(const AccelView &ac, const f3 &o, const f3 &d, bool active,
-                                                 CastDiag &dg, const uint32_t *lnodes)
+__device__ __forceinline__ bool lane_cast(const AccelView &ac, const f3 &o, const f3 &d, bool active, CastDiag &dg,
+                                          const uint32_t *lnodes, bool fresh, uint32_t budget, Hit &h, uint32_t &i,
+                                          uint32_t &leaf, uint32_t &leaf2)
 {
-    Hit h;
-    h.idx = kMiss;
-    h.best = FLT_MAX;
-    h.t = 0.f;
+    if (fresh) {
+        h.idx = kMiss;
+        h.best = FLT_MAX;
+        h.t = 0.f;
+        i = active ? 0u : ac.n_nodes;
+        leaf = leaf2 = kNoSlot;
+    }
     const float dod = dot(o, d);
     cfloat *slots = (cfloat *)ac.slots;
     const float ddev = lensq(d) - 1.0f;
@@ -598,11 +607,11 @@ __device__ __forceinline__ Hit find_closest_lane(const AccelView &ac, const f3 &
     const uint4 *ln = (const uint4 *)lnodes;
     const float4 *__restrict__ gs = ac.slots;
     const uint32_t n = ac.n_nodes;
-    uint32_t i = active ? 0u : n;
     // parked leaves (first slots), kNoSlot = none: a lane keeps walking while one
     // leaf is parked and stops at the second
-    uint32_t leaf = kNoSlot, leaf2 = kNoSlot;
+    uint32_t it = 0;
     for (;;) {
+        if (++it > budget) break;
         const bool tr = i < n && leaf2 == kNoSlot;
         const unsigned long long mt = __ballot(tr);
         const unsigned long long mp = __ballot(leaf != kNoSlot);
@@ -664,6 +673,17 @@ __device__ __forceinline__ Hit find_closest_lane(const AccelView &ac, const f3 &
             i = (hit && !is_leaf) ? i + 1 : rb.x;
         }
     }
+    return !(i < n || leaf != kNoSlot);
+}
+
+// One-shot lane walk (the whole cast in one call).
+template <int LEAF>
+__device__ __forceinline__ Hit find_closest_lane(const AccelView &ac, const f3 &o, const f3 &d, bool active,
+                                                 CastDiag &dg, const uint32_t *lnodes)
+{
+    Hit h;
+    uint32_t i, leaf, leaf2;
+    (void)lane_cast<LEAF>(ac, o, d, active, dg, lnodes, true, 0xFFFFFFFFu, h, i, leaf, leaf2);
     return h;
 }
 

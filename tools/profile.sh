@@ -11,7 +11,7 @@ set -o pipefail
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 TAG=${1:-prof}
 CFG=${2:-c2}
-shift 2 || true
+[ $# -ge 2 ] && shift 2 || shift $#
 ARGS="$*"
 [ -z "$ARGS" ] && ARGS="--no-dropin --no-cpu-baseline"
 OUT="$R/gpurun_out/$TAG"

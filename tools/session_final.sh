@@ -19,6 +19,6 @@ run bench_c2 300 python bench.py
 run bench_c1 200 python bench.py --config c1 --steps 20 --warmup 3
 run bench_c3 300 python bench.py --config c3 --steps 2 --warmup 1 --no-cpu-baseline
 run bench_c5 300 python bench.py --config c5 --steps 2 --warmup 1 --no-cpu-baseline
-bash tools/profile.sh "${1:-prof}" > gpurun_out/profile.log 2>&1 || { tail gpurun_out/profile.log; exit 3; }
+bash tools/profile.sh "${1:-prof}" c2 > gpurun_out/profile.log 2>&1 || { tail gpurun_out/profile.log; exit 3; }
 make -s -C simplepathtracer_amd/csrc diag > gpurun_out/diag_build.log 2>&1 || exit 3
 SPT_LIB=libspt_hip_diag.so run diag_c2 200 python tools/diag.py c2

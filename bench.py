@@ -309,9 +309,9 @@ def main():
                                               "/ launches",
                          "avg_launch_span_ms": round(span_ms, 4)},
             "rays_per_sample": round(casts_all / max(samples_all, 1), 4),
-            # with frames in flight the fold runs beside the next frame's render and its
-            # own event span mostly measures waiting for CUs: reported for --streams 1 only
-            "fold_ms_per_step": round(st["fold_ms"] / args.steps, 4) if nst == 1 else None,
+            # a fold overlapped by another stream's render (frames in flight, or the double-buffered
+            # sample batches of a multi-batch frame) spans its wait for free CU slots: not reported
+            "fold_ms_per_step": round(st["fold_ms"] / args.steps, 4) if nst == 1 and one_batch else None,
         }
         if prof and "SQ_INSTS_VALU" in rk:
             # the binding resource: VALU issue.  Wave-instructions per launch from the PMC

@@ -43,7 +43,10 @@ constexpr size_t kMaxCallerStreams = 4;
 constexpr size_t kCounters = 18;  // device counters: casts, samples, dropped, -, diag[14]
 constexpr size_t kMaxHostSlots = 8;
 constexpr uint32_t kMaxBatchSets = 8;  // batches of host calls in flight (BatchSet below)
-constexpr size_t kMaxWorkspaces = kMaxCallerStreams + kMaxHostSlots + kMaxBatchSets + 1;
+// + one companion stream per caller stream / host slot for double-buffered sample
+// batches (render_impl)
+constexpr size_t kMaxCompanions = kMaxCallerStreams + kMaxHostSlots;
+constexpr size_t kMaxWorkspaces = kMaxCallerStreams + kMaxHostSlots + kMaxBatchSets + 1 + kMaxCompanions;
 // One in-flight unbatched host call (spt_render_progressive, or any call with
 // SPT_BATCH=0 or too large for one batch): its own stream (hence its own workspace) and
 // output staging, so such calls run on the GPU together instead of one after another.
@@ -129,7 +132,13 @@ struct spt_ctx {
     // one workspace per stream, so renders on different streams can be in flight
     // together (the next frame's blocks fill the GPU while the last paths of the
     // previous one drain)
-    std::vector<Workspace> ws;
+    std::vector<Workspace> ws;  // reserved to kMaxWorkspaces: pointers into it stay valid
+    // frames of several sample batches: batch j renders on the caller's stream (j even)
+    // or its companion (j odd), each with its own workspace, so one batch renders while
+    // the other's samples are folded (render_impl); SPT_BATCH_DBUF=0 turns it off
+    bool batch_dbuf = true;
+    std::vector<std::pair<hipStream_t, hipStream_t>> companions;  // (caller stream, companion)
+    hipEvent_t dbuf_start = nullptr, dbuf_fold = nullptr;
     unsigned long long *d_counters = nullptr;
     uint8_t *d_frame8 = nullptr;
     size_t frame8_cap = 0;
@@ -352,6 +361,21 @@ Workspace *workspace_for(spt_ctx *ctx, hipStream_t s)
     return &ctx->ws.back();
 }
 
+// The companion stream of caller stream s (created on first use), or nullptr.
+hipStream_t companion_for(spt_ctx *ctx, hipStream_t s)
+{
+    for (const auto &c : ctx->companions)
+        if (c.first == s) return c.second;
+    if (ctx->companions.size() >= kMaxCompanions) return nullptr;
+    if (!ctx->dbuf_start && (hipEventCreateWithFlags(&ctx->dbuf_start, hipEventDisableTiming) != hipSuccess ||
+                             hipEventCreateWithFlags(&ctx->dbuf_fold, hipEventDisableTiming) != hipSuccess))
+        return nullptr;
+    hipStream_t c = nullptr;
+    if (hipStreamCreateWithFlags(&c, hipStreamNonBlocking) != hipSuccess) return nullptr;
+    ctx->companions.emplace_back(s, c);
+    return c;
+}
+
 // Queues of the wavefront engine in workspace w, for `cap` rays.
 int ensure_wavefront(spt_ctx *ctx, Workspace *w, uint32_t cap)
 {
@@ -420,6 +444,24 @@ int render_impl(spt_ctx *ctx, int mode, const spt::RowMap &map, float4 *d_rgba, 
         rc = ensure(ctx, &w->d_acc, &w->acc_cap, npix);
         if (rc) return rc;
     }
+    // several batches: odd batches render on the companion stream into its own
+    // workspace, so batch j+1 renders while batch j is folded and the GPU never waits
+    // for a batch's last paths (config 3: 6 batches per frame).  The folds stay in
+    // batch order (each waits for the previous one): the sums are unchanged.
+    hipStream_t s2 = nullptr;
+    Workspace *w2 = nullptr;
+    if (spp_batch < ctx->spp && !pg && !keep_samples && ctx->batch_dbuf && ctx->engine == SPT_ENGINE_MEGAKERNEL &&
+        (s2 = companion_for(ctx, s)) != nullptr && (w2 = workspace_for(ctx, s2)) != nullptr) {
+        if ((rc = ensure(ctx, &w2->d_samples, &w2->samples_cap, items_max * slot_floats))) return rc;
+        // the companion starts after the work already queued on the caller's stream
+        HIP_TRY(ctx, hipEventRecord(ctx->dbuf_start, s));
+        HIP_TRY(ctx, hipStreamWaitEvent(s2, ctx->dbuf_start, 0));
+    } else {
+        s2 = nullptr;
+        w2 = nullptr;
+    }
+    const hipStream_t s_caller = s;
+    Workspace *const w_caller = w;
 
     spt::RenderArgs ra{};
     ra.scene = spt::DeviceScene{ctx->d_shade, ctx->d_mat, ctx->n, ctx->accel};
@@ -454,8 +496,16 @@ int render_impl(spt_ctx *ctx, int mode, const spt::RowMap &map, float4 *d_rgba, 
     // one rectangle in task mode = one RenderSegmentTask call: its colorIndex aliasing
     fa.alias = mode == SPT_MODE_TASK && map.parts == 1u && rows != map.width ? 1 : 0;
 
-    for (uint32_t s0 = 0; s0 < ctx->spp; s0 += spp_batch) {
+    uint32_t j = 0;
+    for (uint32_t s0 = 0; s0 < ctx->spp; s0 += spp_batch, ++j) {
         const uint32_t b = std::min(spp_batch, ctx->spp - s0);
+        if (s2) {
+            s = (j & 1u) ? s2 : s_caller;
+            w = (j & 1u) ? w2 : w_caller;
+            ra.samples = w->d_samples;
+            fa.samples = w->d_samples;
+            ra.head = w->d_head;
+        }
         ra.spp_batch = b;
         ra.s0 = s0;
         ra.n_items = npix * b;
@@ -505,9 +555,12 @@ int render_impl(spt_ctx *ctx, int mode, const spt::RowMap &map, float4 *d_rgba, 
         fa.last = s0 + b >= ctx->spp;
         fa.s_done = s0 + b;
         EventPair ef = get_pair(ctx);
+        // double-buffered: fold j after fold j-1 (the other stream; shared accumulator)
+        if (s2 && j > 0) HIP_TRY(ctx, hipStreamWaitEvent(s, ctx->dbuf_fold, 0));
         HIP_TRY(ctx, hipEventRecord(ef.a, s));
         HIP_TRY(ctx, spt::launch_fold(fa, s));
         HIP_TRY(ctx, hipEventRecord(ef.b, s));
+        if (s2) HIP_TRY(ctx, hipEventRecord(ctx->dbuf_fold, s));
         ctx->pending_fold.push_back(ef);
         if (pg && pg->after_pass) {
             const int r = pg->after_pass(s0 + b);
@@ -515,6 +568,8 @@ int render_impl(spt_ctx *ctx, int mode, const spt::RowMap &map, float4 *d_rgba, 
             if (r > 0) break;  // the caller stopped the render
         }
     }
+    // the caller's stream continues after the last fold (and with it every batch)
+    if (s2 && s != s_caller) HIP_TRY(ctx, hipStreamWaitEvent(s_caller, ctx->dbuf_fold, 0));
     if (ctx->pending_render.size() > 256) return collect_timings(ctx);
     return SPT_OK;
 }
@@ -1121,6 +1176,7 @@ int spt_ctx_create(int device, spt_ctx **out)
     if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
         return fail(nullptr, SPT_ERR_NODEVICE, "device %d is %s, this build targets gfx950", device, prop.gcnArchName);
     spt_ctx *ctx = new spt_ctx();
+    ctx->ws.reserve(kMaxWorkspaces);
     ctx->device = device;
     ctx->num_cu = prop.multiProcessorCount;
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
@@ -1140,6 +1196,7 @@ int spt_ctx_create(int device, spt_ctx **out)
     if (const char *e = std::getenv("SPT_WF_CAP")) ctx->wf_cap = (uint32_t)std::max(1024, std::atoi(e));
     if (const char *e = std::getenv("SPT_HOST_GRID_DIV")) ctx->host_grid_div = (uint32_t)std::max(0, std::atoi(e));
     if (const char *e = std::getenv("SPT_BATCH")) ctx->batching = std::atoi(e) != 0;
+    if (const char *e = std::getenv("SPT_BATCH_DBUF")) ctx->batch_dbuf = std::atoi(e) != 0;
     if (const char *e = std::getenv("SPT_BATCH_SETS"))
         ctx->batch_sets = (uint32_t)std::min<int>((int)kMaxBatchSets, std::max(1, std::atoi(e)));
     if (const char *e = std::getenv("SPT_HOST_SLOTS"))
@@ -1243,6 +1300,9 @@ void spt_ctx_destroy(spt_ctx *ctx)
     for (void *b : {(void *)ctx->d_tile, (void *)ctx->d_fullframe})
         if (b) (void)hipFree(b);
     if (ctx->frame_ev) (void)hipEventDestroy(ctx->frame_ev);
+    for (const auto &c : ctx->companions) (void)hipStreamDestroy(c.second);
+    for (hipEvent_t e : {ctx->dbuf_start, ctx->dbuf_fold})
+        if (e) (void)hipEventDestroy(e);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     for (spt_ctx *p : ctx->peers) spt_ctx_destroy(p);
     delete ctx;

@@ -337,13 +337,29 @@ def test_invalid_arguments_raise(spt, ctx, golden_scenes):
 
 # ---------------------------------------------------------------- full-size properties
 
-def test_workspace_batches_fold_in_order(spt, ctx, golden_scenes):
+@pytest.mark.parametrize("task", [False, True])
+def test_workspace_batches_fold_in_order(spt, ctx, golden_scenes, task):
+    """Several sample batches (odd ones on the companion stream, double-buffered) fold in
+    batch order: bit-identical to one batch; again on a caller stream of its own."""
+    import torch
+    def render(*r):
+        return ctx.render_segment(*r, task=task)
+
     setup(ctx, scene_from(spt, golden_scenes, "random"), 1200, 800, 10, 50, seed=4)
-    a = ctx.render_segment(200, 264, 100, 228)
-    ctx.set_workspace(64 * 128 * 3 * 16)  # forces 4 batches of <= 3 samples
-    b = ctx.render_segment(200, 264, 100, 228)
+    a = render(200, 264, 100, 228)
+    ctx.set_workspace(64 * 128 * 12 * 3)  # 4 (segment) / 5 (task) batches
+    b = render(200, 264, 100, 228)
+    ctx.reset_stats()
+    st = torch.cuda.Stream()
+    out = torch.zeros((64 * 128, 4), dtype=torch.float32, device="cuda")
+    ctx.render_rows_async(spt.MODE_TASK if task else spt.MODE_SEGMENT, 200, 264, 1, 1, 0, 100, 228,
+                          out.data_ptr(), 0, st.cuda_stream)
+    st.synchronize()
+    launches = ctx.stats()["launches"]
     ctx.set_workspace(4 << 30)
     assert_bitwise(b, a, "batched vs single-batch")
+    assert_bitwise(out.cpu().numpy(), a, "batched on a caller stream vs single-batch")
+    assert launches == (5 if task else 4)
 
 
 def test_row_split_and_assemble_equals_full_frame(spt, ctx, golden_scenes):

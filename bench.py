@@ -205,7 +205,18 @@ def main():
     split = FrameSplit(W, H, world, args.strip or even_strip(H, world))
     slot_bytes = 12 if args.mode == "segment" else 16
     one_batch = W * H * spp * slot_bytes <= (16 << 30)  # the context's default workspace
-    nst = args.streams if args.streams > 0 else (2 if one_batch else 1)
+    nst = args.streams
+    if nst <= 0:
+        nst = 1
+        if one_batch:
+            # frames in flight pay off on the 256-thread kernels; the LDS tree kernel's
+            # 1024-thread blocks (two per CU, config 5) leave the next frame no slot:
+            # one stream there (config 5: 91.9 vs 93.1 ms per frame).  Probe which kernel
+            # the scene takes with a one-row render on the current stream.
+            cur = torch.cuda.current_stream(dev)
+            ctx.render_rows_async(mode, 0, 1, 1, 1, 0, 0, min(W, 64), 0, 0, cur.cuda_stream)
+            cur.synchronize()
+            nst = 2 if ctx.stats()["block_threads"] <= 256 else 1
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(nst - 1)]
     bufs = []
     for _ in range(nst):  # per-stream frame buffers: frames in flight do not share outputs

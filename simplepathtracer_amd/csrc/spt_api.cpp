@@ -1177,6 +1177,7 @@ int spt_ctx_create(int device, spt_ctx **out)
         return fail(nullptr, SPT_ERR_NODEVICE, "device %d is %s, this build targets gfx950", device, prop.gcnArchName);
     spt_ctx *ctx = new spt_ctx();
     ctx->ws.reserve(kMaxWorkspaces);
+    ctx->block = spt::render_block_size();
     ctx->device = device;
     ctx->num_cu = prop.multiProcessorCount;
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {

@@ -288,6 +288,11 @@ uint32_t render_group_size();  // spheres per group of the hot loop (SPT_GROUP)
 
 constexpr uint32_t kSpecularCap = 1024;  // see spt_oracle.h SPO_SPECULAR_CAP
 constexpr uint32_t kTaskPasses = 10;     // TaskBasedPathTracer.hpp:81
-constexpr uint32_t kRenderBlock = 256;
+// threads per block of the 256-thread render kernels (the LDS tree kernel has its own)
+#ifndef SPT_RENDER_BLOCK
+#define SPT_RENDER_BLOCK 256
+#endif
+constexpr uint32_t kRenderBlock = SPT_RENDER_BLOCK;
+uint32_t render_block_size();  // kRenderBlock of the kernel object (the launch uses it)
 
 }  // namespace spt

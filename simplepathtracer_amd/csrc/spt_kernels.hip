@@ -587,6 +587,7 @@ hipError_t launch_selftest(const float *a, const float *b, const uint32_t *bits,
 }
 
 uint32_t render_group_size() { return SPT_GROUP; }
+uint32_t render_block_size() { return kRenderBlock; }
 
 hipError_t render_occupancy(uint32_t block, int *blocks_per_cu)
 {
@@ -601,11 +602,12 @@ hipError_t render_occupancy(uint32_t block, int *blocks_per_cu)
     *blocks_per_cu = std::min(std::min(a, b), std::min(c, g));
     // the occupancy API reports one block per CU too many at 81-96 and 97-112 SGPRs
     // (MI355X_MICROARCH.md, Correctness boundaries): waves per SIMD are bounded by
-    // 800 / (ceil(sgpr / 16) * 16 + 16) SGPRs; 256-thread blocks = 1 wave per SIMD
+    // 800 / (ceil(sgpr / 16) * 16 + 16) SGPRs; a block of w waves takes w/4 wave slots per SIMD
     if (SPT_NUM_SGPR > 0) {
         // .sgpr_count = the cap minus the 2 VCC registers
-        const int cap = 800 / (((SPT_NUM_SGPR - 2 + 15) / 16) * 16 + 16);
-        if (*blocks_per_cu > cap) *blocks_per_cu = cap;
+        const int cap = 800 / (((SPT_NUM_SGPR - 2 + 15) / 16) * 16 + 16);  // waves per SIMD
+        const int cap_blocks = cap * 4 / (int)(block / 64u);                 // 4 SIMDs per CU
+        if (*blocks_per_cu > cap_blocks) *blocks_per_cu = cap_blocks;
     }
     return e;
 }

@@ -317,16 +317,18 @@ uint32_t full_grid(const spt_ctx *ctx)
     return ctx->ws.size() > 1 ? ctx->grid_overlap : ctx->grid;
 }
 
-// Items per claim from the global counter: whole 8x8 tiles, up to 4 of them (a
-// wave's live paths then stay within one compact patch), fewer only when the
-// launch has under 4 claims per wave (the tail would unbalance).  A 1/8 rank share
-// of config 2 runs 1.38 ms with 128-item claims and 1.19 ms with 256.
+// Items per claim from the global counter: up to 512 (8 samples of one 8x8 tile), fewer
+// only when the launch has under 4 claims per wave (the tail would unbalance).  Every
+// claim is one device-scope atomic on one address, and those serialise: config 2 at
+// 192 / 256 / 512 / 1024 items per claim runs 6.86 / 6.00 / 5.25 / 5.34 ms per frame,
+// config 3 502.5 -> 424.0 ms from 256 to 512 (bench, two rounds interleaved).  A 1/8
+// rank share of config 2 ran 1.38 ms with 128-item claims and 1.19 ms with 256.
 uint32_t claim_size(const spt_ctx *ctx, uint64_t items)
 {
     if (ctx->claim) return ctx->claim;
     const uint64_t waves = (uint64_t)full_grid(ctx) * (ctx->block / 64);
     const uint64_t fair = items / std::max<uint64_t>(waves * 4, 1);
-    return (uint32_t)std::min<uint64_t>(256, std::max<uint64_t>(64, fair / 64 * 64));
+    return (uint32_t)std::min<uint64_t>(512, std::max<uint64_t>(64, fair / 64 * 64));
 }
 
 // Blocks of one render launch: the persistent grid, or fewer when the launch has

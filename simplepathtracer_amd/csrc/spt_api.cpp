@@ -98,6 +98,7 @@ struct spt_ctx {
     int num_cu = 0;
     uint32_t grid = 0, block = spt::kRenderBlock, claim = 0;  // 0 = per launch (claim_size)
     uint32_t claims_per_wave = 2;                              // render_grid (config 1: 2 > 1, 4)
+    uint32_t queues = spt::kMaxQueues;                         // claim counters (RenderArgs::n_queues)
     uint32_t grid_overlap = 0;  // grid while frames are in flight on several streams
     uint32_t last_grid = 0, last_block = 0;  // shape of the most recent render launch
 
@@ -317,12 +318,12 @@ uint32_t full_grid(const spt_ctx *ctx)
     return ctx->ws.size() > 1 ? ctx->grid_overlap : ctx->grid;
 }
 
-// Items per claim from the global counter: up to 512 (8 samples of one 8x8 tile), fewer
-// only when the launch has under 4 claims per wave (the tail would unbalance).  Every
-// claim is one device-scope atomic on one address, and those serialise: config 2 at
-// 192 / 256 / 512 / 1024 items per claim runs 6.86 / 6.00 / 5.25 / 5.34 ms per frame,
-// config 3 502.5 -> 424.0 ms from 256 to 512 (bench, two rounds interleaved).  A 1/8
-// rank share of config 2 ran 1.38 ms with 128-item claims and 1.19 ms with 256.
+// Items per claim: up to 512 (8 samples of one 8x8 tile), fewer only when the launch has
+// under 4 claims per wave (the tail would unbalance).  Every claim is one device-scope
+// atomic, and atomics on one address serialise: with a single counter config 2 at
+// 128 / 256 / 512 items per claim ran 8.66 / 6.04 / 5.29 ms per frame.  Claims now
+// come from one counter per XCD (RenderArgs::n_queues): 5.46 / 5.32 / 5.28 ms, and the
+// drop-in path's small batched launches gained 7-20%.
 uint32_t claim_size(const spt_ctx *ctx, uint64_t items)
 {
     if (ctx->claim) return ctx->claim;
@@ -355,7 +356,7 @@ Workspace *workspace_for(spt_ctx *ctx, hipStream_t s)
     }
     Workspace w;
     w.stream = s;
-    if (hipMalloc((void **)&w.d_head, sizeof(uint32_t)) != hipSuccess) {
+    if (hipMalloc((void **)&w.d_head, sizeof(uint32_t) * spt::kMaxQueues * spt::kQueueStride) != hipSuccess) {
         fail(ctx, SPT_ERR_NOMEM, "workspace allocation failed");
         return nullptr;
     }
@@ -511,6 +512,11 @@ int render_impl(spt_ctx *ctx, int mode, const spt::RowMap &map, float4 *d_rgba, 
         ra.spp_batch = b;
         ra.s0 = s0;
         ra.n_items = npix * b;
+        ra.n_queues = ctx->queues;
+        {
+            const uint32_t per = (ra.n_items + ra.n_queues - 1u) / ra.n_queues;
+            ra.queue_items = (per + ra.claim - 1u) / ra.claim * ra.claim;
+        }
         ra.div_band = spt::make_fastdiv(rows >= 8 ? 8u * map.width * b : 1u);
         ra.div_tile = spt::make_fastdiv(64u * b);
         EventPair ev = get_pair(ctx);
@@ -537,7 +543,7 @@ int render_impl(spt_ctx *ctx, int mode, const spt::RowMap &map, float4 *d_rgba, 
             }
             HIP_TRY(ctx, hipEventRecord(ev.b, s));
         } else {
-            HIP_TRY(ctx, hipMemsetAsync(w->d_head, 0, sizeof(uint32_t), s));
+            HIP_TRY(ctx, hipMemsetAsync(w->d_head, 0, sizeof(uint32_t) * spt::kQueueStride * ra.n_queues, s));
             if (!ctx->ref_recorded) {
                 HIP_TRY(ctx, hipEventRecord(ctx->ref_ev, s));
                 ctx->ref_recorded = true;
@@ -777,6 +783,12 @@ int launch_batch(spt_ctx *ctx, BatchSet *bs, const std::vector<BatchReq *> &batc
     ra.s0 = 0;
     ra.n_items = (uint32_t)item;
     ra.claim = claim;
+    // queues of claim multiples: a claim still never spans two rectangles
+    ra.n_queues = ctx->queues;
+    {
+        const uint32_t per = (ra.n_items + ra.n_queues - 1u) / ra.n_queues;
+        ra.queue_items = (per + claim - 1u) / claim * claim;
+    }
     ra.div_band = ra.div_tile = spt::make_fastdiv(1u);
     ra.samples = w->d_samples;
     ra.slot_floats = slot_floats;
@@ -785,7 +797,7 @@ int launch_batch(spt_ctx *ctx, BatchSet *bs, const std::vector<BatchReq *> &batc
     ra.rects = bs->d_rects;
     ra.n_rects = (uint32_t)n;
 
-    HIP_TRY(ctx, hipMemsetAsync(w->d_head, 0, sizeof(uint32_t), s));
+    HIP_TRY(ctx, hipMemsetAsync(w->d_head, 0, sizeof(uint32_t) * spt::kQueueStride * ra.n_queues, s));
     if (!ctx->ref_recorded) {
         HIP_TRY(ctx, hipEventRecord(ctx->ref_ev, s));
         ctx->ref_recorded = true;
@@ -1196,6 +1208,8 @@ int spt_ctx_create(int device, spt_ctx **out)
     if (const char *e = std::getenv("SPT_CLUSTER_K")) ctx->cluster_k = (uint32_t)std::max(0, std::atoi(e));
     if (const char *e = std::getenv("SPT_TREE_B")) ctx->tree_branching = (uint32_t)std::max(0, std::atoi(e));
     if (const char *e = std::getenv("SPT_CLAIMS_PER_WAVE")) ctx->claims_per_wave = (uint32_t)std::max(1, std::atoi(e));
+    if (const char *e = std::getenv("SPT_QUEUES"))
+        ctx->queues = (uint32_t)std::min<int>((int)spt::kMaxQueues, std::max(1, std::atoi(e)));
     if (const char *e = std::getenv("SPT_WF_CAP")) ctx->wf_cap = (uint32_t)std::max(1024, std::atoi(e));
     if (const char *e = std::getenv("SPT_HOST_GRID_DIV")) ctx->host_grid_div = (uint32_t)std::max(0, std::atoi(e));
     if (const char *e = std::getenv("SPT_BATCH")) ctx->batching = std::atoi(e) != 0;

@@ -227,7 +227,13 @@ struct RenderArgs {
     unsigned long long *counters;  // [0] casts, [1] samples, [2] dropped
     const BatchRect *rects;  // batched launch: n_rects rectangles (map/npix/div_* unused); else null
     uint32_t n_rects;
+    // claims come from n_queues counters head[k * kQueueStride], queue k
+    // handing out items [k * queue_items, (k + 1) * queue_items) (claim multiples)
+    uint32_t n_queues, queue_items;
 };
+
+// claim counters: at most one per XCD, 256 bytes apart (separate cache lines)
+constexpr uint32_t kMaxQueues = 8, kQueueStride = 64;
 
 struct FoldArgs {
     const float *samples;  // slot_floats per slot, [sample][pixel]

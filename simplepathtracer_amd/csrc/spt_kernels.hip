@@ -95,6 +95,27 @@ constexpr uint32_t kGlaneMaxNodes = SPT_GLANE_MAX_NODES;
 // BATCH: the launch renders a.n_rects rectangles (a.rects, concurrent host calls
 // batched by spt_api.cpp); each refill then serves lanes from one claim only, and a
 // claim's rectangle is looked up once per claim.
+// The next claim of a launch (lane 0).  Items come from a.n_queues counters,
+// one per XCD: queue k hands out [k * queue_items, (k + 1) * queue_items), so the
+// device-scope atomics of the grid spread over 8 addresses instead of serialising on
+// one.  A wave starts on queue `home` (blockIdx % n_queues: its XCD under round-robin
+// dispatch) and moves on to the next queue when one is dry; n_items when all are.
+__device__ __forceinline__ uint32_t claim_next(const RenderArgs &a, uint32_t home, uint32_t &qi)
+{
+    while (qi < a.n_queues) {
+        uint32_t k = home + qi;
+        if (k >= a.n_queues) k -= a.n_queues;
+        const uint32_t lo = k * a.queue_items;
+        const uint32_t len = lo < a.n_items ? min(a.queue_items, a.n_items - lo) : 0u;
+        if (len != 0u) {
+            const uint32_t c = atomicAdd(a.head + k * kQueueStride, a.claim);
+            if (c < len) return lo + c;
+        }
+        ++qi;
+    }
+    return a.n_items;
+}
+
 template <bool TREE, int LEAF, bool LDSN, uint32_t BLOCK, bool BATCH = false, bool GLANE = false>
 __device__ __forceinline__ void render_body(const RenderArgs &a)
 {
@@ -129,7 +150,9 @@ __device__ __forceinline__ void render_body(const RenderArgs &a)
     uint32_t pend = 0;
     uint32_t rect = 0;  // BATCH: rectangle of the current claim
     (void)rect;
-    if (lane == 0) pend = atomicAdd(a.head, a.claim);
+    const uint32_t home = blockIdx.x % a.n_queues;
+    uint32_t qi = 0;  // queues tried after the home queue ran dry (lane 0)
+    if (lane == 0) pend = claim_next(a, home, qi);
     bool exhausted = false;
     unsigned long long casts = 0, done = 0, dropped = 0;
     unsigned long long d_iters = 0, d_cyc_cast = 0, d_cyc_shade = 0, d_cyc_refill = 0;
@@ -171,7 +194,7 @@ __device__ __forceinline__ void render_body(const RenderArgs &a)
             if (blk_cur == blk_end) {
                 // the claim in flight becomes current, the next one goes in flight
                 const uint32_t nb = __builtin_amdgcn_readfirstlane(pend);
-                if (nb < a.n_items && lane == 0) pend = atomicAdd(a.head, a.claim);
+                if (nb < a.n_items && lane == 0) pend = claim_next(a, home, qi);
                 if (nb >= a.n_items) {
                     exhausted = true;
                 } else {
@@ -203,7 +226,7 @@ __device__ __forceinline__ void render_body(const RenderArgs &a)
             } else {
                 // switch to the claim in flight and put the next one in flight
                 const uint32_t nb = __builtin_amdgcn_readfirstlane(pend);
-                if (nb < a.n_items && lane == 0) pend = atomicAdd(a.head, a.claim);
+                if (nb < a.n_items && lane == 0) pend = claim_next(a, home, qi);
                 if (nb >= a.n_items) {
                     exhausted = true;
                     blk_cur = blk_end = 0;

@@ -981,3 +981,36 @@ def test_config5_full_frame_properties(spt, ctx, oracle):
         x, y = int(rng.integers(0, W)), int(rng.integers(0, H))
         want, _ = oracle.render_segment(osc, fr, y, y + 1, x, x + 1)
         assert_bitwise(a[y * W + x, :3], want[0, :3], f"pixel {(x, y)}")
+
+
+@pytest.mark.parametrize("task", [False, True])
+def test_claim_queues_render_the_same(spt, golden_scenes, monkeypatch, task):
+    """Claims come from one counter per XCD (RenderArgs::n_queues, spt_kernels.hip
+    claim_next): 1, 3 and 8 queues give bit-identical frames and count every sample,
+    on a full region, on launches with fewer claims than queues (the trailing queues
+    are empty) and through the batched drop-in path."""
+    scene = scene_from(spt, golden_scenes, "random")
+    regions = [(0, 120, 0, 200), (37, 45, 90, 98), (5, 6, 7, 8)]
+    out = {}
+    for q in ("1", "3", "8"):
+        monkeypatch.setenv("SPT_QUEUES", q)
+        c = spt.Context(0)
+        setup(c, scene, 200, 120, 5, 50, seed=3)
+        c.reset_stats()
+        out[q] = [c.render_segment(*r, task=task) for r in regions]
+        st = c.stats()
+        got8 = np.zeros(200 * 120 * 3, np.uint8)
+        tiles = [(y, y + 40, x, x + 50) for y in range(0, 120, 40) for x in range(0, 200, 50)]
+        th = [threading.Thread(target=c.render_segment, args=(*t, got8), kwargs={"task": task}) for t in tiles]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        out[q].append(got8)
+        c.close()
+        if not task:
+            assert st["samples"] == 5 * sum((r[1] - r[0]) * (r[3] - r[2]) for r in regions)
+    monkeypatch.delenv("SPT_QUEUES")
+    for q in ("3", "8"):
+        for k, (a, b) in enumerate(zip(out[q], out["1"])):
+            assert_bitwise(a, b, f"queues {q} vs 1, part {k}")

@@ -323,13 +323,17 @@ uint32_t full_grid(const spt_ctx *ctx)
 // atomic, and atomics on one address serialise: with a single counter config 2 at
 // 128 / 256 / 512 items per claim ran 8.66 / 6.04 / 5.29 ms per frame.  Claims now
 // come from one counter per XCD (RenderArgs::n_queues): 5.46 / 5.32 / 5.28 ms, and the
-// drop-in path's small batched launches gained 7-20%.
+// drop-in path's small batched launches gained 7-20%.  Trees walked lane by
+// lane (config 5) take at most kLaneClaim: their paths vary most in length, and smaller
+// claims even out the launch's tail (config 5 at 256 / 512 / 1024: 89.5 / 91.9 / 95.7 ms).
+constexpr uint32_t kLaneClaim = 256;
 uint32_t claim_size(const spt_ctx *ctx, uint64_t items)
 {
     if (ctx->claim) return ctx->claim;
     const uint64_t waves = (uint64_t)full_grid(ctx) * (ctx->block / 64);
     const uint64_t fair = items / std::max<uint64_t>(waves * 4, 1);
-    return (uint32_t)std::min<uint64_t>(512, std::max<uint64_t>(64, fair / 64 * 64));
+    const uint32_t cap = spt::lane_walk_tree(ctx->accel) ? kLaneClaim : 512u;
+    return (uint32_t)std::min<uint64_t>(cap, std::max<uint64_t>(64, fair / 64 * 64));
 }
 
 // Blocks of one render launch: the persistent grid, or fewer when the launch has

@@ -300,5 +300,7 @@ constexpr uint32_t kTaskPasses = 10;     // TaskBasedPathTracer.hpp:81
 #endif
 constexpr uint32_t kRenderBlock = SPT_RENDER_BLOCK;
 uint32_t render_block_size();  // kRenderBlock of the kernel object (the launch uses it)
+// true when launch_render walks this tree lane by lane (LDS or global-memory lane walk)
+bool lane_walk_tree(const AccelView &ac);
 
 }  // namespace spt

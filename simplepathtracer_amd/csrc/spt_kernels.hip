@@ -611,6 +611,10 @@ hipError_t launch_selftest(const float *a, const float *b, const uint32_t *bits,
 
 uint32_t render_group_size() { return SPT_GROUP; }
 uint32_t render_block_size() { return kRenderBlock; }
+bool lane_walk_tree(const AccelView &ac)
+{
+    return ac.tree && ac.n_nodes >= kLdsMinNodes && (ac.n_nodes + 1u <= kLdsNodeRecords || ac.n_nodes <= kGlaneMaxNodes);
+}
 
 hipError_t render_occupancy(uint32_t block, int *blocks_per_cu)
 {

@@ -319,22 +319,25 @@ uint32_t full_grid(const spt_ctx *ctx)
 }
 
 // Items per claim: 256, or 512 for launches of at least 64 Ki items per wave (config 3's
-// sample batches: 424.4 vs 429.0 ms per frame), fewer only when the launch has under 4
-// claims per wave.  Every claim is one device-scope atomic, and atomics on one address
+// sample batches: 424.4 vs 429.0 ms per frame), 192 below 4 Ki items per wave (config 2's
+// 1/8 rank share: 0.78 vs 0.82 ms), fewer only when the launch has under 4 claims per
+// wave.  Every claim is one device-scope atomic, and atomics on one address
 // serialise: with a single counter config 2 at 128 / 256 / 512 items per claim ran
 // 8.66 / 6.04 / 5.29 ms per frame.  Claims now come from one counter per XCD
 // (RenderArgs::n_queues), where small claims cost little and even out the tail: config 2
 // at 128 / 192 / 256 / 384 / 512 items 5.43 / 5.32 / 5.29 / 5.28 / 5.32 ms, its 1/8
 // rank share 0.78 / 0.78 / 0.80 / 0.91 / 1.03 ms (tools/scaling_probe.py), config 5
 // (lane walk) 89.1 / 88.8 / 89.3 / - / 91.8 ms.
-constexpr uint32_t kClaim = 256, kBigClaim = 512;
+constexpr uint32_t kSmallClaim = 192, kClaim = 256, kBigClaim = 512;
 uint32_t claim_size(const spt_ctx *ctx, uint64_t items)
 {
     if (ctx->claim) return ctx->claim;
     const uint64_t waves = std::max<uint64_t>((uint64_t)full_grid(ctx) * (ctx->block / 64), 1);
     const uint64_t fair = items / (waves * 4);
-    const bool big = items / waves >= 65536u && !spt::lane_walk_tree(ctx->accel);
-    return (uint32_t)std::min<uint64_t>(big ? kBigClaim : kClaim, std::max<uint64_t>(64, fair / 64 * 64));
+    const uint64_t per_wave = items / waves;
+    const uint32_t cap = per_wave < 4096u ? kSmallClaim
+                       : (per_wave >= 65536u && !spt::lane_walk_tree(ctx->accel)) ? kBigClaim : kClaim;
+    return (uint32_t)std::min<uint64_t>(cap, std::max<uint64_t>(64, fair / 64 * 64));
 }
 
 // Blocks of one render launch: the persistent grid, or fewer when the launch has

@@ -53,8 +53,14 @@ for d in sorted(x for x in os.listdir(src) if x.startswith("pmc")):
         continue
     for r in csv.DictReader(open(p)):
         if "spt::" in r["Kernel_Name"]:
-            agg[(r["Kernel_Name"].split("(")[0].replace("void ", ""), r["Counter_Name"])].append(float(r["Counter_Value"]))
-out += ["", "## PMC counters (average per dispatch, separate passes)\n", "| kernel | counter | value |", "|---|---|---|"]
+            agg[(r["Kernel_Name"].split("(")[0].replace("void ", ""), r["Counter_Name"])].append(
+                (int(r["Dispatch_Id"]), float(r["Counter_Value"])))
+# the timed dispatches only (the last `timed` of each kernel, as in the trace section): the
+# bench's probe render (one row) and warmup frames would otherwise pull the average down
+for key, v in agg.items():
+    agg[key] = [x for _, x in sorted(v)[-timed:]]
+out += ["", f"## PMC counters (average per dispatch over the last {timed} dispatches of each kernel, separate passes)\n",
+        "| kernel | counter | value |", "|---|---|---|"]
 for (k, c), v in sorted(agg.items()):
     val = sum(v) / len(v)
     note = ""

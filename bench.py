@@ -148,6 +148,59 @@ def profile_record(config):
     return json.load(open(path)).get(config)
 
 
+def free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(args, argv) -> int:
+    """`--gpus N` (N > 1) run without a launcher: start the N rank processes as children
+    (torch.distributed.run, one process per GPU, rendezvous on 127.0.0.1) and return
+    their exit code.  Nothing here touches the GPU (counting devices does not initialise
+    HIP on this image), so no process that initialised the GPU ever execs.  The GPU
+    count is checked first: N ranks over RCCL need N visible GPUs, and the run is
+    refused (exit 2) rather than silently rendering on fewer; SPT_DIST_BACKEND=gloo is
+    the rehearsal backend, whose ranks may share a GPU (rank r uses GPU r % count)."""
+    import subprocess
+    import torch
+    backend = os.environ.get("SPT_DIST_BACKEND", "nccl")
+    have = torch.cuda.device_count()
+    if not args.launch_check and backend == "nccl" and args.gpus > have:
+        print(f"bench.py: --gpus {args.gpus} needs {args.gpus} GPUs, {have} visible", file=sys.stderr, flush=True)
+        return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def launch_check(args) -> None:
+    """--launch-check: each rank joins the process group (SPT_DIST_BACKEND, gloo on a
+    CPU-only host) and rank 0 prints what the group sees; no GPU work."""
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    backend = os.environ.get("SPT_DIST_BACKEND", "gloo")
+    if world > 1:
+        dist.init_process_group(backend)
+        ids = torch.zeros((world, 2), dtype=torch.int64)
+        ids[rank] = torch.tensor([rank, local])
+        dist.all_reduce(ids)
+        seen = {"world_size": dist.get_world_size(), "backend": dist.get_backend(), "ranks": ids[:, 0].tolist(),
+                "local_ranks": ids[:, 1].tolist()}
+        dist.destroy_process_group()
+    else:
+        seen = {"world_size": 1, "backend": None, "ranks": [0], "local_ranks": [0]}
+    if rank == 0:
+        print(json.dumps({"launch_check": True, "n_gpus": args.gpus, **seen}), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -168,7 +221,16 @@ def main():
     ap.add_argument("--no-dropin", action="store_true", help="skip the C++ drop-in measurement (config 2)")
     ap.add_argument("--dropin-frames", type=int, default=5)
     ap.add_argument("--dump", default="", help="write rank 0's final g_data bytes to this file")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="only start the ranks and report the process group (launcher test; no GPU work)")
     args = ap.parse_args()
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        raise SystemExit(launch_ranks(args, sys.argv[1:]))
+    if args.launch_check:
+        launch_check(args)
+        return
 
     import torch
     import torch.distributed as dist
@@ -177,11 +239,14 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.gpus != world and world > 1:
+    if args.gpus != world:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     # SPT_DIST_BACKEND=gloo rehearses the N>1 flow with several ranks on one GPU
     backend = os.environ.get("SPT_DIST_BACKEND", "nccl")
-    local = local % max(torch.cuda.device_count(), 1)
+    ndev = torch.cuda.device_count()
+    if backend == "nccl" and world > ndev:
+        raise SystemExit(f"{world} ranks over RCCL need {world} GPUs, {ndev} visible")
+    local = local % max(ndev, 1)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
@@ -229,14 +294,20 @@ def main():
                 b["gathered"] = torch.zeros((world * split.tile_pixels(), 4), dtype=torch.float32, device=dev)
         bufs.append(b)
     counter = [0]
+    # gather timing of the timed steps (N > 1): events around each step's gather
+    gev = []
 
-    def step():
+    def step(timed=False):
         k = counter[0] % nst
         counter[0] += 1
         b = bufs[k]
+        ev = None
+        if timed and world > 1:
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            gev.append(ev)
         with torch.cuda.stream(streams[k]):  # RCCL collectives follow the current stream
             render_frame(ctx, split, rank, mode, b["local"], b["gathered"], b["frame"], b["g_data"],
-                         streams[k].cuda_stream)
+                         streams[k].cuda_stream, gather_events=ev)
 
     for _ in range(args.warmup):
         step()
@@ -247,12 +318,16 @@ def main():
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step()
+        step(timed=True)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     st = ctx.stats()
+    # this rank's render device time per step (union of its launches' intervals)
+    rank_render_ms = st["render_busy_ms"] / args.steps
+    rank_gather_ms = sum(a.elapsed_time(b) for a, b in gev) / max(len(gev), 1)
+    per_rank = None
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -260,8 +335,15 @@ def main():
         tot = torch.tensor([st["casts"], st["samples"]], dtype=torch.float64, device=dev)
         dist.all_reduce(tot)
         casts_all, samples_all = float(tot[0]), float(tot[1])
+        pr = torch.zeros((2, world), dtype=torch.float64, device=dev)
+        pr[0, rank] = rank_render_ms
+        pr[1, rank] = rank_gather_ms
+        dist.all_reduce(pr)
+        per_rank = pr.cpu().tolist()
+        world_seen, backend_seen = dist.get_world_size(), dist.get_backend()
     else:
         casts_all, samples_all = float(st["casts"]), float(st["samples"])
+        world_seen, backend_seen = 1, None
 
     total_samples = W * H * spp * args.steps
     value = total_samples / elapsed / 1e6
@@ -319,11 +401,19 @@ def main():
                          "avg_launch_ms_def": "union of the render launches' HIP-event intervals (launch stream) "
                                               "/ launches",
                          "avg_launch_span_ms": round(span_ms, 4)},
+            "world_size": world_seen,
+            "backend": backend_seen,
             "rays_per_sample": round(casts_all / max(samples_all, 1), 4),
             # a fold overlapped by another stream's render (frames in flight, or the double-buffered
             # sample batches of a multi-batch frame) spans its wait for free CU slots: not reported
             "fold_ms_per_step": round(st["fold_ms"] / args.steps, 4) if nst == 1 and one_batch else None,
         }
+        if per_rank is not None:
+            out["ranks"] = {"render_ms": [round(v, 4) for v in per_rank[0]],
+                            "gather_ms": [round(v, 4) for v in per_rank[1]],
+                            "def": "per rank and step: render device time (union of its render launches' HIP-event "
+                                   "intervals) and the gather (HIP events on the step's stream around dist.gather; "
+                                   "includes waiting for the slowest rank)"}
         if prof and "SQ_INSTS_VALU" in rk:
             # the binding resource: VALU issue.  Wave-instructions per launch from the PMC
             # pass over this same command, against 1024 SIMDs x 2.4 GHz / 2 cycles per

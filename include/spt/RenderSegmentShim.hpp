@@ -46,12 +46,19 @@ inline spt_ctx *context()
     static spt_ctx *ctx = [] {
         spt_ctx *c = nullptr;
         if (const char *list = std::getenv("SPT_DEVICES")) {
+            // a comma-separated list of ordinals; anything else aborts (a typo must not
+            // turn into extra members on device 0)
             std::vector<int> devs;
-            for (const char *p = list; *p;) {
+            for (const char *p = list;;) {
                 char *end = nullptr;
-                devs.push_back((int)std::strtol(p, &end, 10));
-                if (end == p) break;
-                p = *end == ',' ? end + 1 : end;
+                const long d = std::strtol(p, &end, 10);
+                if (end == p || (*end != ',' && *end != '\0') || d < 0) {
+                    std::fprintf(stderr, "spt: malformed SPT_DEVICES=\"%s\" (want e.g. 0,1,2)\n", list);
+                    std::abort();
+                }
+                devs.push_back((int)d);
+                if (*end == '\0') break;
+                p = end + 1;
             }
             check(nullptr, spt_ctx_create_multi(devs.data(), (uint32_t)devs.size(), &c), "spt_ctx_create_multi");
         } else {

@@ -228,6 +228,17 @@ int ensure(spt_ctx *ctx, T **p, size_t *cap, size_t count)
     return SPT_OK;
 }
 
+// A device buffer of ctx must live on ctx->device (multi-device contexts switch the
+// current device between members).
+int check_on_device(spt_ctx *ctx, const void *p, const char *what)
+{
+    hipPointerAttribute_t at{};
+    HIP_TRY(ctx, hipPointerGetAttributes(&at, p));
+    if (at.device != ctx->device)
+        return fail(ctx, SPT_ERR_STATE, "%s is on device %d, not on member 0's device %d", what, at.device, ctx->device);
+    return SPT_OK;
+}
+
 EventPair get_pair(spt_ctx *ctx)
 {
     if (!ctx->pool.empty()) {
@@ -1473,8 +1484,12 @@ int spt_render_frame(spt_ctx *ctx, int mode, float *rgba_out, uint8_t *g_data)
     uint32_t max_rows = 0;
     for (uint32_t r = 0; r < parts; ++r) max_rows = std::max(max_rows, spt::rows_owned(spt::RowMap{0, H, strip, parts, r, 0, W}));
     const size_t tile = (size_t)max_rows * W;
+    // member 0's buffers live on member 0's device: the setters (for_members) and the
+    // previous frame leave another member's device current
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
     int rc = ensure(ctx, &ctx->d_tile, &ctx->tile_cap, tile * parts);  // member 0: the gathered stack
     if (rc) return rc;
+    if ((rc = check_on_device(ctx, ctx->d_tile, "the gathered tile stack"))) return rc;
     for (uint32_t r = 0; r < parts; ++r) {
         spt_ctx *c = m[r];
         HIP_TRY(ctx, hipSetDevice(c->device));
@@ -1497,11 +1512,13 @@ int spt_render_frame(spt_ctx *ctx, int mode, float *rgba_out, uint8_t *g_data)
     float4 *dframe = nullptr;
     if (rgba_out) {
         if ((rc = ensure(ctx, &ctx->d_fullframe, &ctx->fullframe_cap, (size_t)W * H))) return rc;
+        if ((rc = check_on_device(ctx, ctx->d_fullframe, "the assembled frame"))) return rc;
         dframe = ctx->d_fullframe;
     }
     uint8_t *d8 = nullptr;
     if (g_data) {
         if ((rc = ensure(ctx, &ctx->d_frame8, &ctx->frame8_cap, (size_t)W * H * 3))) return rc;
+        if ((rc = check_on_device(ctx, ctx->d_frame8, "g_data's device copy"))) return rc;
         d8 = ctx->d_frame8;
     }
     HIP_TRY(ctx, spt::launch_assemble(ctx->d_tile, max_rows, spt::RowMap{0, H, strip, parts, 0u, 0, W}, W, H, dframe,
@@ -1514,6 +1531,7 @@ int spt_render_frame(spt_ctx *ctx, int mode, float *rgba_out, uint8_t *g_data)
         HIP_TRY(ctx, hipSetDevice(c->device));
         if ((rc = collect_timings(c, false))) return rc;
     }
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
     return SPT_OK;
 }
 

@@ -618,7 +618,10 @@ bool lane_walk_tree(const AccelView &ac)
 
 hipError_t render_occupancy(uint32_t block, int *blocks_per_cu)
 {
-    // the smallest occupancy of the four shapes sizes the persistent grid
+    // the smallest occupancy of the four shapes sizes the persistent grid.  All four
+    // compile to the same register budget (SPT_RENDER_ATTR: 94 SGPRs, 72 VGPRs at the
+    // 96-SGPR cap, `make asm`), so the minimum equals each kernel's own occupancy and the
+    // global-memory lane walk does not shrink the grid of the other shapes
     int a = 0, b = 0, c = 0, g = 0;
     hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, render_kernel<true, (int)kClusterSlots>, (int)block, 0);
     if (e == hipSuccess)

@@ -74,9 +74,12 @@ def gather_tiles(local_tile, gathered, group=None) -> None:
 
 
 def render_frame(ctx, split: FrameSplit, rank: int, mode: int, local_tile, gathered=None, frame=None,
-                 g_data=None, stream=0, group=None) -> None:
+                 g_data=None, stream=0, group=None, gather_events=None) -> None:
     """One distributed frame: render own rows, gather, assemble on rank 0.
-    Tensors are device tensors; `stream` is the hipStream_t the launches use."""
+    Tensors are device tensors; `stream` is the hipStream_t the launches use (the
+    current torch stream: the collective follows it).  gather_events: an optional
+    pair of torch.cuda.Event recorded on that stream around the gather (its time
+    includes waiting for the slowest rank's render)."""
     if split.world == 1:
         ctx.render_rows_async(mode, 0, split.height, 1, 1, 0, 0, split.width,
                               frame.data_ptr() if frame is not None else 0,
@@ -84,7 +87,11 @@ def render_frame(ctx, split: FrameSplit, rank: int, mode: int, local_tile, gathe
         return
     ctx.render_rows_async(mode, 0, split.height, split.strip, split.world, rank, 0, split.width,
                           local_tile.data_ptr(), 0, stream)
+    if gather_events is not None:
+        gather_events[0].record()
     gather_tiles(local_tile, gathered, group)
+    if gather_events is not None:
+        gather_events[1].record()
     if rank == 0:
         ctx.assemble_rows_async(gathered.data_ptr(), split.max_rows, 0, split.height, split.strip, split.world, 0,
                                 split.width, frame.data_ptr() if frame is not None else 0,

@@ -57,6 +57,7 @@ class Context:
             self.devices = [int(d) for d in devs]
         self._h = h
         self.device = self.devices[0]
+        self._frame = None  # (width, height) after set_params
 
     @property
     def handle(self):
@@ -122,8 +123,9 @@ class Context:
         """The whole frame over every member device (spt_render_frame): returns the
         row-major float4 frame (or None with rgba=False); writes g_data if given."""
         L = _native.lib()
-        n = ctypes.c_uint32(0)
-        self._check(L.spt_ctx_devices(self._h, ctypes.byref(n), None))
+        if self._frame is None:
+            # SPT_ERR_STATE, as the library reports it to its own callers
+            raise _native.SptError(2, "params not set (set_params)")
         w, h = self._frame
         out = np.zeros((w * h, 4), np.float32) if rgba else None
         gp = None

@@ -477,18 +477,24 @@ def test_cpp_dropin_shim_renders_like_the_context(spt, golden_scenes, tmp_path, 
 
 def test_bench_two_ranks_on_one_gpu_matches_one_rank(spt, tmp_path):
     """bench.py's N>1 flow (strip split, gather to rank 0, rank-0 assemble)
-    rehearsed with two gloo ranks sharing cuda:0: same g_data as N=1."""
+    rehearsed with two gloo ranks sharing cuda:0, launched by bench.py itself
+    (`--gpus 2`, no torchrun): the line says 2 ranks and g_data equals N=1's."""
+    import json
     import os
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     one, two = tmp_path / "one.bin", tmp_path / "two.bin"
-    base = [sys.executable, os.path.join(root, "bench.py"), "--steps", "1", "--warmup", "0", "--no-cpu-baseline"]
-    subprocess.run(base + ["--dump", str(one)], check=True, timeout=300, cwd=root)
-    env = dict(os.environ, SPT_DIST_BACKEND="gloo")
-    subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
-                    "--master-addr=127.0.0.1", "--master-port=29533"] + base[1:] + ["--gpus", "2", "--dump", str(two)],
-                   check=True, timeout=300, cwd=root, env=env)
+    base = [sys.executable, os.path.join(root, "bench.py"), "--steps", "1", "--warmup", "0", "--no-cpu-baseline",
+            "--no-dropin"]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    subprocess.run(base + ["--dump", str(one)], check=True, timeout=300, cwd=root, env=env)
+    env["SPT_DIST_BACKEND"] = "gloo"
+    r = subprocess.run(base + ["--gpus", "2", "--dump", str(two)], check=True, timeout=300, cwd=root, env=env,
+                       capture_output=True, text=True)
+    line = json.loads([s for s in r.stdout.splitlines() if s.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["world_size"] == 2 and line["backend"] == "gloo"
+    assert len(line["ranks"]["render_ms"]) == 2 and min(line["ranks"]["render_ms"]) > 0
     a, b = np.fromfile(one, np.uint8), np.fromfile(two, np.uint8)
     assert a.size == b.size == 1200 * 800 * 3
     bad = np.nonzero(a != b)[0]

@@ -61,6 +61,44 @@ def _worker(rank, world, port, strip, scene_arrays, view, q):
         dist.destroy_process_group()
 
 
+def _bench_env():
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    return env
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_bench_launches_its_own_ranks(world):
+    """`bench.py --gpus N` without a launcher starts N rank processes itself (the
+    driver's scaling runs call it that way); --launch-check stops after the process
+    group forms, so this runs on a CPU-only host over gloo."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(_bench_env(), SPT_DIST_BACKEND="gloo")
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", str(world), "--launch-check"],
+                       capture_output=True, text=True, timeout=240, cwd=root, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads([s for s in r.stdout.splitlines() if s.startswith("{")][-1])
+    assert line["n_gpus"] == world and line["world_size"] == world and line["backend"] == "gloo"
+    assert line["ranks"] == list(range(world)) and sorted(line["local_ranks"]) == list(range(world))
+
+
+def test_bench_refuses_more_ranks_than_gpus():
+    """RCCL ranks need one GPU each: `--gpus N` with fewer GPUs visible exits non-zero
+    instead of rendering on fewer ranks."""
+    import subprocess
+    import sys
+    import torch
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    n = torch.cuda.device_count() + 1
+    env = dict(_bench_env(), SPT_DIST_BACKEND="nccl")
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", str(max(n, 2))],
+                       capture_output=True, text=True, timeout=240, cwd=root, env=env)
+    assert r.returncode == 2, (r.returncode, r.stderr[-2000:])
+    assert "GPUs" in r.stderr and "{" not in r.stdout
+
+
 @pytest.mark.parametrize("world,strip", [(2, 8), (2, 3), (3, 4)])
 def test_strip_split_gather_assemble_equals_full_frame(oracle, native, world, strip):
     import simplepathtracer_amd as spt

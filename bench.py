@@ -88,9 +88,11 @@ def cpu_model():
 def cpu_baseline(scene, view, w, h, spp_sample, bounces):
     """The CPU restatement (oracle/, "port", gcc -O2 -msse4.1) timed with the
     reference's RenderImageParallelMain tiling (Renderer.hpp:257-302: tc x tc tiles,
-    <= tc in flight) at tc = 2 * cores, the reference's hardware_concurrency() * 2
-    rule: RenderSegmentTask (TaskBasedPathTracer, north_star's CPU path) is `value`,
-    RenderSegment (the shipped default) is timed beside it."""
+    <= tc in flight) at the two thread counts SURVEY §8(d) names: tc = 2 * cores, the
+    reference's hardware_concurrency() * 2 rule, and tc = 4, the shipped g_maxThreads
+    (Globals.hpp:11; Renderer.hpp:261-262 takes min(2 * hw, g_maxThreads)).
+    RenderSegmentTask (TaskBasedPathTracer, north_star's CPU path) at 2 * cores is
+    `value`; RenderSegment (the shipped default generation type) beside it."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle
     pyoracle.build()
@@ -98,19 +100,23 @@ def cpu_baseline(scene, view, w, h, spp_sample, bounces):
     fr = pyoracle.make_frame(view, [0, 1, -3, 0], [137, 207, 240, 0], w, h, spp_sample, bounces, 1)
     cores = host_cores()
     tc = 2 * cores
-    res = {}
-    for name, mode in (("task", 1), ("segment", 0)):
-        t0 = time.perf_counter()
-        pyoracle.render_image_parallel(osc, fr, tc, mode=mode, want_rgba=False)
-        dt = time.perf_counter() - t0
-        res[name] = (w * h * spp_sample / dt / 1e6, dt)
-    return {"value": round(res["task"][0], 4), "unit": "Msamples/s", "cores": cores, "kind": "port",
-            "segment_value": round(res["segment"][0], 4), "threads": tc, "nproc": os.cpu_count(),
-            "cpu_model": cpu_model(), "calibration": CPU_CALIBRATION,
+    res, wall = {}, 0.0
+    for threads in (tc, 4):
+        for name, mode in (("task", 1), ("segment", 0)):
+            t0 = time.perf_counter()
+            pyoracle.render_image_parallel(osc, fr, threads, mode=mode, want_rgba=False)
+            dt = time.perf_counter() - t0
+            wall += dt
+            res[(name, threads)] = round(w * h * spp_sample / dt / 1e6, 4)
+    return {"value": res[("task", tc)], "unit": "Msamples/s", "cores": cores, "kind": "port",
+            "segment_value": res[("segment", tc)], "threads": tc,
+            "shipped_tc4": {"task": res[("task", 4)], "segment": res[("segment", 4)],
+                            "def": "tc = 4 (g_maxThreads, Globals.hpp:11): 4x4 tiles, <= 4 threads in flight"},
+            "nproc": os.cpu_count(), "cpu_model": cpu_model(), "calibration": CPU_CALIBRATION,
             "sample": f"RenderSegmentTask (value) and RenderSegment (segment_value) of the oracle C restatement "
                       f"(gcc -O2 -msse4.1), RenderImageParallelMain tiling {tc}x{tc} with <= {tc} in flight on "
-                      f"{cores} cores, same scene/camera at {w}x{h}, {spp_sample} spp, depth {bounces}; "
-                      f"{res['task'][1]:.2f} s + {res['segment'][1]:.2f} s wall"}
+                      f"{cores} cores, and the shipped tc = 4; same scene/camera at {w}x{h}, {spp_sample} spp, "
+                      f"depth {bounces}; {wall:.1f} s wall for the four runs"}
 
 
 def dropin_bench(w, h, spp, bounces, frames, tcs):
@@ -216,7 +222,8 @@ def main():
                          "the previous one's last paths drain; each stream has its own workspace); 0 = auto: "
                          "2 when a frame is one workspace batch, else 1 (long multi-batch frames gain nothing "
                          "and would double the workspace)")
-    ap.add_argument("--cpu-spp", type=int, default=32, help="spp of the bounded CPU-baseline sample")
+    ap.add_argument("--cpu-spp", type=int, default=0,
+                    help="spp of the CPU-baseline sample (0: the config's own spp on config 2, scaled down on others)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-dropin", action="store_true", help="skip the C++ drop-in measurement (config 2)")
     ap.add_argument("--dropin-frames", type=int, default=5)
@@ -442,8 +449,12 @@ def main():
                     rv[k] = rk[k]
             out["roofline_valu"] = rv
         if world == 1 and not args.no_cpu_baseline:
-            cw, ch = (W, H) if args.config != "c3" else (1920, 1080)
-            out["cpu_baseline"] = cpu_baseline(scene, view, cw, ch, args.cpu_spp, bounces)
+            # config 2 at its own 100 spp; the larger configs at their scene and depth, on
+            # config 2's frame, with spp scaled down to a bounded sample (c5's 10 000
+            # spheres are scanned brute force by the reference's loop)
+            cpu_spp = args.cpu_spp or (spp if args.config == "c2" else max(1, round(100 * 149 / scene.n)))
+            cw, ch = (W, H) if args.config in ("c1", "c2") else (1200, 800)
+            out["cpu_baseline"] = cpu_baseline(scene, view, cw, ch, cpu_spp, bounces)
         if world == 1 and args.config == "c2" and not args.no_dropin and args.engine == "megakernel":
             # the drop-in boundary itself: RenderSegment/RenderSegmentTask from RenderJob threads
             d = dropin_bench(W, H, spp, bounces, args.dropin_frames, (4, 2 * host_cores()))

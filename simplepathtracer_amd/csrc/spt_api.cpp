@@ -80,7 +80,7 @@ struct BatchReq {
 };
 struct Workspace {
     hipStream_t stream = nullptr;  // key
-    float *d_samples = nullptr;    // per-sample slots of the current batch
+    uint32_t *d_samples = nullptr; // per-sample slots of the current batch (sample words)
     size_t samples_cap = 0;
     float4 *d_acc = nullptr;       // ordered partial sums when a frame is batched
     size_t acc_cap = 0;
@@ -110,6 +110,7 @@ struct spt_ctx {
     size_t shade_cap = 0, mat_cap = 0, slots_cap = 0, orig_cap = 0, nodes_cap = 0, kpre_cap = 0;
     spt::AccelTables tables;
     uint32_t n = 0;
+    uint32_t code_shift = 0;  // slot bits of a diffuse sample code (spt_internal.h code_word)
     bool scene_set = false;
     // host copy of the hit geometry, to rebuild the traversal tables
     std::vector<float> h_centers, h_radii;
@@ -148,7 +149,8 @@ struct spt_ctx {
     struct Pinned {
         void *ptr;
         size_t bytes;
-        uint8_t *dev;
+        uint8_t *dev;  // the buffer as this member's device sees it
+        bool owner;    // registered by this context (member 0 of a multi-device context)
     };
     std::vector<Pinned> pinned;
 
@@ -430,6 +432,19 @@ int ensure_wavefront(spt_ctx *ctx, Workspace *w, uint32_t cap)
     return SPT_OK;
 }
 
+// Fold arguments shared by every fold of ctx: the slots and the decode tables of the
+// sample words (shading table, sky colour, slot bits).
+spt::FoldArgs fold_args(const spt_ctx *ctx, const uint32_t *samples, uint32_t slot_words)
+{
+    spt::FoldArgs fa{};
+    fa.samples = samples;
+    fa.slot_words = slot_words;
+    fa.shade = ctx->d_shade;
+    for (int j = 0; j < 3; ++j) fa.sky[j] = ctx->cam.sky[j];
+    fa.code_shift = ctx->code_shift;
+    return fa;
+}
+
 // Render the rows of `map` and fold them into d_rgba (local pixel order) and/or
 // d_rgb8 (full frame).  keep_samples: leave the per-sample colours of a single
 // batch in d_samples (debug path).
@@ -449,8 +464,8 @@ int render_impl(spt_ctx *ctx, int mode, const spt::RowMap &map, float4 *d_rgba, 
     if (npix64 == 0) return SPT_OK;
     if (npix64 > 0x7FFFFFFFull) return fail(ctx, SPT_ERR_ARG, "region too large (%llu pixels)", (unsigned long long)npix64);
     const uint32_t npix = (uint32_t)npix64;
-    const uint32_t slot_floats = mode == SPT_MODE_SEGMENT ? 3u : 4u;  // task mode keeps the counted flag
-    uint64_t budget = std::max<uint64_t>(ctx->ws_bytes / (slot_floats * sizeof(float)), 1);
+    const uint32_t slot_words = mode == SPT_MODE_SEGMENT ? 1u : 2u;  // task mode keeps the path's order key
+    uint64_t budget = std::max<uint64_t>(ctx->ws_bytes / (slot_words * sizeof(uint32_t)), 1);
     budget = std::min<uint64_t>(budget, 0x7FFFFFFFull);
     uint64_t per = std::max<uint64_t>(1, budget / npix);
     uint32_t spp_batch = (uint32_t)std::min<uint64_t>(ctx->spp, per);
@@ -460,7 +475,7 @@ int render_impl(spt_ctx *ctx, int mode, const spt::RowMap &map, float4 *d_rgba, 
     const uint64_t items_max = (uint64_t)npix * spp_batch;
     Workspace *w = workspace_for(ctx, s);
     if (!w) return SPT_ERR_STATE;
-    int rc = ensure(ctx, &w->d_samples, &w->samples_cap, items_max * slot_floats);
+    int rc = ensure(ctx, &w->d_samples, &w->samples_cap, items_max * slot_words);
     if (rc) return rc;
     if (spp_batch < ctx->spp) {
         rc = ensure(ctx, &w->d_acc, &w->acc_cap, npix);
@@ -474,7 +489,7 @@ int render_impl(spt_ctx *ctx, int mode, const spt::RowMap &map, float4 *d_rgba, 
     Workspace *w2 = nullptr;
     if (spp_batch < ctx->spp && !pg && !keep_samples && ctx->batch_dbuf && ctx->engine == SPT_ENGINE_MEGAKERNEL &&
         (s2 = companion_for(ctx, s)) != nullptr && (w2 = workspace_for(ctx, s2)) != nullptr) {
-        if ((rc = ensure(ctx, &w2->d_samples, &w2->samples_cap, items_max * slot_floats))) return rc;
+        if ((rc = ensure(ctx, &w2->d_samples, &w2->samples_cap, items_max * slot_words))) return rc;
         // the companion starts after the work already queued on the caller's stream
         HIP_TRY(ctx, hipEventRecord(ctx->dbuf_start, s));
         HIP_TRY(ctx, hipStreamWaitEvent(s2, ctx->dbuf_start, 0));
@@ -486,7 +501,7 @@ int render_impl(spt_ctx *ctx, int mode, const spt::RowMap &map, float4 *d_rgba, 
     Workspace *const w_caller = w;
 
     spt::RenderArgs ra{};
-    ra.scene = spt::DeviceScene{ctx->d_shade, ctx->d_mat, ctx->n, ctx->accel};
+    ra.scene = spt::DeviceScene{ctx->d_shade, ctx->d_mat, ctx->n, ctx->code_shift, ctx->accel};
     ra.cam = ctx->cam;
     ra.width = ctx->W;
     ra.height = ctx->H;
@@ -498,13 +513,11 @@ int render_impl(spt_ctx *ctx, int mode, const spt::RowMap &map, float4 *d_rgba, 
     ra.npix = npix;
     ra.claim = claim_size(ctx, (uint64_t)npix * spp_batch);
     ra.samples = w->d_samples;
-    ra.slot_floats = slot_floats;
+    ra.slot_words = slot_words;
     ra.head = w->d_head;
     ra.counters = ctx->d_counters;
 
-    spt::FoldArgs fa{};
-    fa.samples = w->d_samples;
-    fa.slot_floats = slot_floats;
+    spt::FoldArgs fa = fold_args(ctx, w->d_samples, slot_words);
     fa.acc = w->d_acc;
     fa.out_rgba = d_rgba;
     fa.out_rgb8 = d_rgb8;
@@ -639,6 +652,12 @@ int rebuild_accel(spt_ctx *ctx)
                                           sh.leaf_slots);
     const std::string bad = spt::validate_accel(t, ctx->h_centers.data(), ctx->h_radii.data(), ctx->n);
     if (!bad.empty()) return fail(ctx, SPT_ERR_STATE, "traversal tables invalid: %s", bad.c_str());
+    // a diffuse sample's code holds its slot in code_shift bits (code_word)
+    uint32_t shift = 0;
+    while (shift < 32 && (1ull << shift) < t.slots.size()) ++shift;
+    if (shift > spt::kCodeMaxShift)
+        return fail(ctx, SPT_ERR_ARG, "%zu sphere slots exceed the sample code's %u slot bits", t.slots.size(),
+                    spt::kCodeMaxShift);
     // shading tables in slot order: the kernel keeps the winner's slot, not its index
     std::vector<float4> shade(t.slots.size(), make_float4(0.f, 0.f, 0.f, 0.f));
     std::vector<uint32_t> mat(t.slots.size(), SPT_SKYBOX);
@@ -659,6 +678,7 @@ int rebuild_accel(spt_ctx *ctx)
     ctx->accel = spt::AccelView{ctx->d_slots, ctx->d_orig, ctx->d_nodes, t.always_groups, t.n_nodes,
                                 t.n_nodes > t.leaves ? 1u : 0u, t.leaf_slots, ctx->d_kpre, t.pre_cm};
     ctx->tables = std::move(t);
+    ctx->code_shift = shift;
     return SPT_OK;
 }
 
@@ -712,7 +732,7 @@ spt_ctx *pick_member(spt_ctx *ctx)
 // Bytes of per-sample slots a rectangle needs in one batch (all spp samples at once).
 uint64_t batch_slot_bytes(const spt_ctx *ctx, int mode, uint64_t npix)
 {
-    return npix * ctx->spp * (mode == SPT_MODE_SEGMENT ? 3u : 4u) * sizeof(float);
+    return npix * ctx->spp * (mode == SPT_MODE_SEGMENT ? 1u : 2u) * sizeof(uint32_t);
 }
 
 // Enqueue one batch on bs->stream: rectangle table, render, fold, the copy-back of
@@ -720,7 +740,7 @@ uint64_t batch_slot_bytes(const spt_ctx *ctx, int mode, uint64_t npix)
 int launch_batch(spt_ctx *ctx, BatchSet *bs, const std::vector<BatchReq *> &batch)
 {
     const int mode = batch[0]->mode;
-    const uint32_t slot_floats = mode == SPT_MODE_SEGMENT ? 3u : 4u;
+    const uint32_t slot_words = mode == SPT_MODE_SEGMENT ? 1u : 2u;
     const uint32_t spp = ctx->spp, W = ctx->W, H = ctx->H;
     uint64_t items = 0, pix = 0;
     bool any_rgba = false, any_g = false;
@@ -782,13 +802,13 @@ int launch_batch(spt_ctx *ctx, BatchSet *bs, const std::vector<BatchReq *> &batc
     }
     Workspace *w = workspace_for(ctx, bs->stream);
     if (!w) return SPT_ERR_STATE;
-    if ((rc = ensure(ctx, &w->d_samples, &w->samples_cap, (size_t)slot * slot_floats))) return rc;
+    if ((rc = ensure(ctx, &w->d_samples, &w->samples_cap, (size_t)slot * slot_words))) return rc;
     if (any_rgba && (rc = ensure(ctx, &bs->d_stage, &bs->stage_cap, (size_t)pix))) return rc;
     const hipStream_t s = bs->stream;
     HIP_TRY(ctx, hipMemcpyAsync(bs->d_rects, bs->h_rects, n * sizeof(spt::BatchRect), hipMemcpyHostToDevice, s));
 
     spt::RenderArgs ra{};
-    ra.scene = spt::DeviceScene{ctx->d_shade, ctx->d_mat, ctx->n, ctx->accel};
+    ra.scene = spt::DeviceScene{ctx->d_shade, ctx->d_mat, ctx->n, ctx->code_shift, ctx->accel};
     ra.cam = ctx->cam;
     ra.width = W;
     ra.height = H;
@@ -810,7 +830,7 @@ int launch_batch(spt_ctx *ctx, BatchSet *bs, const std::vector<BatchReq *> &batc
     }
     ra.div_band = ra.div_tile = spt::make_fastdiv(1u);
     ra.samples = w->d_samples;
-    ra.slot_floats = slot_floats;
+    ra.slot_words = slot_words;
     ra.head = w->d_head;
     ra.counters = ctx->d_counters;
     ra.rects = bs->d_rects;
@@ -831,9 +851,7 @@ int launch_batch(spt_ctx *ctx, BatchSet *bs, const std::vector<BatchReq *> &batc
     ctx->pending_render.push_back(ev);
     ctx->launches++;
 
-    spt::FoldArgs fa{};
-    fa.samples = w->d_samples;
-    fa.slot_floats = slot_floats;
+    spt::FoldArgs fa = fold_args(ctx, w->d_samples, slot_words);
     fa.out_rgba = any_rgba ? bs->d_stage : nullptr;
     fa.out_rgb8 = any_g ? ctx->d_frame8 : nullptr;
     fa.width = W;
@@ -1307,7 +1325,8 @@ void spt_ctx_destroy(spt_ctx *ctx)
             (void)hipEventDestroy(p.b);
         }
     (void)hipDeviceSynchronize();  // async renders on caller streams
-    for (const spt_ctx::Pinned &p : ctx->pinned) (void)hipHostUnregister(p.ptr);
+    for (const spt_ctx::Pinned &p : ctx->pinned)
+        if (p.owner) (void)hipHostUnregister(p.ptr);
     if (ctx->ref_ev) (void)hipEventDestroy(ctx->ref_ev);
     void *bufs[] = {ctx->d_shade, ctx->d_mat, ctx->d_slots, ctx->d_orig, ctx->d_nodes,
                     ctx->d_kpre, ctx->d_counters, ctx->d_frame8};
@@ -1415,29 +1434,54 @@ int spt_render_segment_task(spt_ctx *ctx, uint32_t yB, uint32_t yE, uint32_t xB,
 int spt_pin_host(spt_ctx *ctx, void *ptr, size_t bytes)
 {
     if (!ctx) return fail(nullptr, SPT_ERR_ARG, "null context");
-    std::lock_guard<std::mutex> lk(ctx->mu);
     if (!ptr || bytes == 0) return fail(ctx, SPT_ERR_ARG, "null or empty host buffer");
-    for (const spt_ctx::Pinned &p : ctx->pinned)
-        if (p.ptr == ptr) return SPT_OK;
+    {
+        std::lock_guard<std::mutex> lk(ctx->mu);
+        for (const spt_ctx::Pinned &p : ctx->pinned)
+            if (p.ptr == ptr) return SPT_OK;
+        HIP_TRY(ctx, hipSetDevice(ctx->device));
+        // portable: every member device of a multi-device context writes its tiles' bytes
+        // into the buffer in place (none copies them back over the others' writes)
+        HIP_TRY(ctx, hipHostRegister(ptr, bytes, hipHostRegisterMapped | hipHostRegisterPortable));
+        void *dev = nullptr;
+        if (hipHostGetDevicePointer(&dev, ptr, 0) != hipSuccess) dev = nullptr;
+        ctx->pinned.push_back(spt_ctx::Pinned{ptr, bytes, (uint8_t *)dev, true});
+    }
+    for (spt_ctx *m : ctx->peers) {
+        std::lock_guard<std::mutex> lk(m->mu);
+        HIP_TRY(ctx, hipSetDevice(m->device));
+        void *dev = nullptr;
+        if (hipHostGetDevicePointer(&dev, ptr, 0) != hipSuccess) dev = nullptr;
+        m->pinned.push_back(spt_ctx::Pinned{ptr, bytes, (uint8_t *)dev, false});
+    }
     HIP_TRY(ctx, hipSetDevice(ctx->device));
-    HIP_TRY(ctx, hipHostRegister(ptr, bytes, hipHostRegisterMapped));
-    void *dev = nullptr;
-    if (hipHostGetDevicePointer(&dev, ptr, 0) != hipSuccess) dev = nullptr;
-    ctx->pinned.push_back(spt_ctx::Pinned{ptr, bytes, (uint8_t *)dev});
     return SPT_OK;
 }
 
 int spt_unpin_host(spt_ctx *ctx, void *ptr)
 {
     if (!ctx) return fail(nullptr, SPT_ERR_ARG, "null context");
+    auto find = [&](spt_ctx *c) {
+        return std::find_if(c->pinned.begin(), c->pinned.end(), [&](const spt_ctx::Pinned &p) { return p.ptr == ptr; });
+    };
+    {
+        std::lock_guard<std::mutex> lk(ctx->mu);
+        if (find(ctx) == ctx->pinned.end() || !find(ctx)->owner)
+            return fail(ctx, SPT_ERR_ARG, "buffer %p was not pinned", ptr);
+    }
+    // batched calls of any member may be writing into it directly
+    for (spt_ctx *m : ctx->peers) {
+        std::lock_guard<std::mutex> lk(m->mu);
+        HIP_TRY(ctx, hipSetDevice(m->device));
+        HIP_TRY(ctx, hipDeviceSynchronize());
+        auto it = find(m);
+        if (it != m->pinned.end()) m->pinned.erase(it);
+    }
     std::lock_guard<std::mutex> lk(ctx->mu);
-    auto it = std::find_if(ctx->pinned.begin(), ctx->pinned.end(), [&](const spt_ctx::Pinned &p) { return p.ptr == ptr; });
-    if (it == ctx->pinned.end()) return fail(ctx, SPT_ERR_ARG, "buffer %p was not pinned", ptr);
     HIP_TRY(ctx, hipSetDevice(ctx->device));
-    // batched calls may be writing into it directly
     HIP_TRY(ctx, hipDeviceSynchronize());
     HIP_TRY(ctx, hipHostUnregister(ptr));
-    ctx->pinned.erase(it);
+    ctx->pinned.erase(find(ctx));
     return SPT_OK;
 }
 
@@ -1608,22 +1652,19 @@ int spt_render_samples(spt_ctx *ctx, int mode, uint32_t yB, uint32_t yE, uint32_
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     spt::RowMap map{yB, yE, 1u, 1u, 0u, xB, xE - xB};
     if ((rc = render_impl(ctx, mode, map, nullptr, nullptr, ctx->stream, true))) return rc;
+    // decode the sample words on the device: out[p * spp + s] = {r, g, b, counted}
     const size_t npix = (size_t)(xE - xB) * (yE - yB);
-    const size_t sf = mode == SPT_MODE_SEGMENT ? 3 : 4;
-    std::vector<float> buf(npix * ctx->spp * sf);  // device order [sample][pixel], sf floats per slot
-    HIP_TRY(ctx, hipMemcpyAsync(buf.data(), workspace_for(ctx, ctx->stream)->d_samples, buf.size() * sizeof(float),
-                                hipMemcpyDeviceToHost,
-                                ctx->stream));
-    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-    for (size_t p = 0; p < npix; ++p)
-        for (size_t s = 0; s < ctx->spp; ++s) {
-            float *o = out + 4 * (p * ctx->spp + s);
-            std::memcpy(o, &buf[(s * npix + p) * sf], sf * sizeof(float));
-            // segment mode: every sample counts; task mode: w holds the path's order key, 0 = dropped
-            uint32_t key;
-            std::memcpy(&key, &o[3], 4);
-            if (sf == 3 || key != 0) o[3] = 1.0f;
-        }
+    float4 *d_out = nullptr;
+    HIP_TRY(ctx, hipMalloc((void **)&d_out, npix * ctx->spp * sizeof(float4)));
+    spt::FoldArgs fa = fold_args(ctx, workspace_for(ctx, ctx->stream)->d_samples, mode == SPT_MODE_SEGMENT ? 1u : 2u);
+    fa.map = map;
+    fa.npix = (uint32_t)npix;
+    fa.spp_batch = ctx->spp;
+    hipError_t e = spt::launch_expand(fa, d_out, ctx->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(out, d_out, npix * ctx->spp * sizeof(float4), hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    (void)hipFree(d_out);
+    if (e != hipSuccess) return fail(ctx, SPT_ERR_HIP, "spt_render_samples: %s", hipGetErrorString(e));
     return collect_timings(ctx);
 }
 

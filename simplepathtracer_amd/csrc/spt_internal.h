@@ -146,6 +146,54 @@ __host__ __device__ inline void ts_item(uint32_t q, uint32_t width, uint32_t row
     col = c0 + (pix - row * wt);
 }
 
+// Inverse of ts_item for one pixel: the item index (= slot) of sample 0 of local pixel
+// (lr, col) and the step between its consecutive samples.  Slots are stored in item
+// order, so a claim's paths write one contiguous run of slots; the fold reads sample s
+// of a pixel at q0 + s * step (64 consecutive slots for the 64 pixels of a full 8x8 tile).
+__host__ __device__ inline void ts_slot_base(uint32_t lr, uint32_t col, uint32_t width, uint32_t rows, uint32_t S,
+                                             uint32_t &q0, uint32_t &step)
+{
+    const uint32_t band = lr >> 3;
+    const uint32_t h = rows - (band << 3) < 8u ? rows - (band << 3) : 8u;
+    const uint32_t ft = width >> 3, wr = width & 7u;
+    const uint32_t t = col >> 3;
+    const uint32_t tc = t < ft ? t : ft;  // full-width tile, or the ragged right one
+    const uint32_t wt = t < ft ? 8u : wr;
+    q0 = band * 8u * width * S + tc * h * 8u * S + (lr - (band << 3)) * wt + (col - (tc << 3));
+    step = h * wt;
+}
+
+// Sample codes: one 32-bit word per sample instead of its colour.  A
+// sample's colour is one of
+//   * the sky, initColor * k * 0.5 with k = d.y + 1.f of the final ray
+//     (SampleColorSkybox, SingleThreadPathTracer.hpp:11-14): the word is k's bits;
+//   * a diffuse albedo halved 1 + j times (SampleColorDiffuse, lines 21-37: the first
+//     diffuse hit's colour * 0.5, then * 0.5 per further bounce): a code naming the
+//     first hit's slot and j;
+//   * 0 (the specular-event cap; RenderSegmentTask's dropped paths).
+// A finite k is 0 or at least 2^-24 in magnitude (fl(y + 1) for float y: only y = -1
+// lies within 2^-24 of -1), so the words whose magnitude as a float is below 2^-24 and
+// nonzero never hold a k: they carry the codes c in [1, 2 (kCodeSmall - 1)], positive
+// words first, then the same magnitudes with the sign bit.  c = 1 is the colour 0,
+// c = 2 + (j << shift | slot) a diffuse sample; after kCodeSat halvings every finite
+// albedo is 0 (and inf / NaN stay themselves), so j saturates there.  The fold rebuilds
+// the colour with the render kernel's own operations: bit-identical.
+constexpr uint32_t kCodeSmall = 0x33800000u;  // bits of 2^-24
+constexpr uint32_t kCodeSat = 280;            // 2^-280 * FLT_MAX rounds to 0
+constexpr uint32_t kCodeMaxShift = 22;        // (kCodeSat + 1) << 22 codes fit
+__host__ __device__ inline uint32_t code_word(uint32_t c)
+{
+    return c < kCodeSmall ? c : 0x80000000u | (c - kCodeSmall + 1u);
+}
+// the code of a word, 0 for a sky word
+__host__ __device__ inline uint32_t word_code(uint32_t w)
+{
+    const uint32_t a = w & 0x7FFFFFFFu;
+    if (a == 0u || a >= kCodeSmall) return 0u;
+    return (w >> 31) ? a + kCodeSmall - 1u : a;
+}
+constexpr uint32_t kZeroWord = 1u;  // code_word(1): the colour 0
+
 constexpr uint32_t kMaxGroup = 16;     // sphere-table padding granule (>= SPT_GROUP)
 constexpr uint32_t kClusterSlots = 8;  // max members per cluster = slots of a tree leaf
 constexpr uint32_t kFlatLeafSlots = 4; // slots of a flat-list leaf holding <= 4 members
@@ -181,6 +229,7 @@ struct DeviceScene {
     const float4 *shade;    // {red, green, blue, fuzz} per slot (hit geometry: accel.slots)
     const uint32_t *mat;    // material id per slot
     uint32_t n;
+    uint32_t code_shift;    // slot bits of a diffuse sample code (code_word)
     AccelView accel;
 };
 
@@ -196,7 +245,7 @@ struct Camera {
 // (ts_item over w x rows pixels and all spp samples); item_off is a multiple of the
 // launch's claim size, so a claim never spans two rectangles, and items in
 // [item_end, next item_off) are padding (no path).  Its per-sample slots are
-// [slot_off, slot_off + npix * spp), [sample][row-major pixel]; its fold output sits at
+// [slot_off, slot_off + npix * spp), in its own item order; its fold output sits at
 // pixels [pix_off, pix_off + npix) of the batch's staging.
 struct BatchRect {
     uint32_t item_off, item_end, slot_off, pix_off;
@@ -221,8 +270,9 @@ struct RenderArgs {
     uint32_t claim;      // items per queue claim
     FastDiv div_band, div_tile;  // ts_item divisors 8*width*spp_batch and 64*spp_batch
     FastDiv div_strip;           // row_of_fast divisor map.strip
-    float *samples;      // [n_items] per-sample colour: {r, g, b} (segment mode) or {r, g, b, counted} (task mode)
-    uint32_t slot_floats;  // 3 or 4
+    uint32_t *samples;   // [n_items] per-sample slots in item order: the sample word (segment mode) or
+                         // {word, key} (task mode; key 0 = dropped path)
+    uint32_t slot_words;  // 1 or 2
     uint32_t *head;      // queue head (zeroed before launch)
     unsigned long long *counters;  // [0] casts, [1] samples, [2] dropped
     const BatchRect *rects;  // batched launch: n_rects rectangles (map/npix/div_* unused); else null
@@ -236,8 +286,11 @@ struct RenderArgs {
 constexpr uint32_t kMaxQueues = 8, kQueueStride = 64;
 
 struct FoldArgs {
-    const float *samples;  // slot_floats per slot, [sample][pixel]
-    uint32_t slot_floats;
+    const uint32_t *samples;  // slot_words per slot, in item order (ts_slot_base)
+    uint32_t slot_words;
+    const float4 *shade;      // the scene's shading table (diffuse codes name its slots)
+    float sky[3];             // initColor (sky words)
+    uint32_t code_shift;
     float4 *acc;         // persistent accumulator (w = sample count)
     float4 *out_rgba;    // nullable, local pixel order
     uint8_t *out_rgb8;   // nullable, full frame (g_data layout)
@@ -285,6 +338,7 @@ size_t wavefront_scan_bytes(uint32_t cap);
 hipError_t launch_wavefront_pass(const WavefrontBuffers &b, const RenderArgs &a, uint32_t cur, uint32_t n_cur,
                                  uint32_t gen_base, uint32_t gen_n, hipStream_t s);
 hipError_t launch_fold(const FoldArgs &a, hipStream_t s);
+hipError_t launch_expand(const FoldArgs &a, float4 *out, hipStream_t s);  // spt_render_samples
 hipError_t launch_assemble(const float4 *tiles, uint32_t max_rows, RowMap base, uint32_t width, uint32_t height,
                            float4 *frame, uint8_t *rgb8, hipStream_t s);
 hipError_t launch_selftest(const float *a, const float *b, const uint32_t *bits, uint32_t n, float *out,

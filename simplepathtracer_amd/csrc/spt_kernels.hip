@@ -142,7 +142,8 @@ __device__ __forceinline__ void render_body(const RenderArgs &a)
     ps.phase = PH_IDLE;
     ps.item = ps.bounce = ps.spec = 0;
     ps.st = 0;
-    ps.o = ps.d = ps.c = mk(0.f, 0.f, 0.f);
+    ps.o = ps.d = mk(0.f, 0.f, 0.f);
+    ps.slot = 0;
 
     // Items are handed out in claims of a.claim from one global counter; each wave
     // keeps the next claim in flight (lane 0) so the atomic's latency is hidden.
@@ -359,29 +360,64 @@ __global__ __launch_bounds__(kLdsBlock)
     render_body<true, (int)kClusterSlots, true, kLdsBlock, true>(a);
 }
 
-// RenderSegment's / RenderSegmentTask's resolve of pixel p of a region (map, npix
-// pixels, alias: task mode on a non-square tile) whose slots start at `samples`;
-// local float4 output at out_rgba[p].
-__device__ __forceinline__ void fold_pixel(const FoldArgs &a, const float *samples, const RowMap &map, uint32_t npix,
-                                           int alias, uint32_t p, float4 *out_rgba, uint8_t *out_rgb8)
+// The colour of a sample word (code_word, spt_internal.h), with the render kernel's own
+// operations: the sky as SampleColorSkybox computes it (SingleThreadPathTracer.hpp:11-14),
+// a diffuse sample as the albedo * 0.5 (line 24) halved once more per further bounce
+// (line 31), bit for bit.  Halving is exact while the value stays normal, so j halvings
+// are one multiply by 2^-j when the result is normal (or 0 / inf / NaN); otherwise (a
+// denormal result: each halving may round) they are done one at a time.
+__device__ __forceinline__ float halve_n(float x, uint32_t j)
 {
+    if (j <= 126u) {
+        const float r = x * __uint_as_float((127u - j) << 23);
+        if (__builtin_fabsf(r) >= 0x1p-126f || x == 0.f || !__builtin_isfinite(x)) return r;
+    }
+    for (uint32_t i = 0; i < j; ++i) x = x * 0.5f;
+    return x;
+}
+__device__ __forceinline__ f3 decode_sample(const FoldArgs &a, uint32_t w)
+{
+    const uint32_t c = word_code(w);
+    if (c == 0u) {
+        const float k = __uint_as_float(w);
+        return mul(mk(a.sky[0] * k, a.sky[1] * k, a.sky[2] * k), 0.5f);
+    }
+    if (c == 1u) return mk(0.f, 0.f, 0.f);
+    const uint32_t v = c - 2u;
+    const uint32_t slot = v & ((1u << a.code_shift) - 1u), j = v >> a.code_shift;
+    const float4 sh = a.shade[slot];
+    return mk(halve_n(sh.x * 0.5f, j), halve_n(sh.y * 0.5f, j), halve_n(sh.z * 0.5f, j));
+}
+
+// RenderSegment's / RenderSegmentTask's resolve of local pixel (lr, col) of a region
+// (map, `rows` rows, alias: task mode on a non-square tile) whose slots start at
+// `samples` (item order of a batch of a.spp_batch samples: ts_slot_base); local float4
+// output at out_rgba[lr * width + col].
+__device__ __forceinline__ void fold_pixel(const FoldArgs &a, const uint32_t *samples, const RowMap &map,
+                                           uint32_t rows, int alias, uint32_t lr, uint32_t col, float4 *out_rgba,
+                                           uint8_t *out_rgb8)
+{
+    const uint32_t W = map.width, S = a.spp_batch;
+    const uint32_t p = lr * W + col;
     float4 acc = a.first ? make_float4(0.f, 0.f, 0.f, 0.f) : a.acc[p];
+    uint32_t q0, step;
+    ts_slot_base(lr, col, W, rows, S, q0, step);
     if (a.mode == 0) {
-        // RenderSegment: 12-byte slots, every sample counts
-        const float *s = samples + (size_t)3 * p;
-        for (uint32_t k = 0; k < a.spp_batch; ++k) {
-            const float *c = s + (size_t)3 * k * npix;  // [sample][pixel]: coalesced across lanes
-            acc.x = acc.x + c[0];
-            acc.y = acc.y + c[1];
-            acc.z = acc.z + c[2];
+        // RenderSegment: one word per slot, every sample counts
+        for (uint32_t k = 0; k < S; ++k) {
+            const f3 c = decode_sample(a, samples[q0 + k * step]);
+            acc.x = acc.x + c.x;
+            acc.y = acc.y + c.y;
+            acc.z = acc.z + c.z;
             acc.w = acc.w + 1.f;
         }
     } else if (!alias) {
-        // RenderSegmentTask on a square tile: pixel p is colors[p]; w = 0 marks a dropped path
-        const float4 *s = (const float4 *)samples + p;
-        for (uint32_t k = 0; k < a.spp_batch; ++k) {
-            const float4 c = s[(size_t)k * npix];
-            if (__float_as_uint(c.w) != 0u) {
+        // RenderSegmentTask on a square tile: pixel p is colors[p]; key 0 marks a dropped path
+        const uint2 *s2 = (const uint2 *)samples;
+        for (uint32_t k = 0; k < S; ++k) {
+            const uint2 v = s2[q0 + k * step];
+            if (v.y != 0u) {
+                const f3 c = decode_sample(a, v.x);
                 acc.x = acc.x + c.x;
                 acc.y = acc.y + c.y;
                 acc.z = acc.z + c.z;
@@ -395,23 +431,29 @@ __device__ __forceinline__ void fold_pixel(const FoldArgs &a, const float *sampl
         // the sources reach colors[p] in the order of their (key, pixel) (finish_step),
         // so each sample's sources are added in that order.  No source: 0 samples, and
         // 0 * (1.f / 0) is NaN, as in the reference.
-        const uint32_t W = map.width, H = npix / W;
+        const uint32_t H = rows;
         const uint32_t dy_lo = p >= W ? (p - W + H) / H : 0u;
         const uint32_t dy_hi = min(H - 1u, p / H);
-        const float4 *s = (const float4 *)samples;
-        for (uint32_t k = 0; k < a.spp_batch; ++k) {
-            const float4 *sk = s + (size_t)k * npix;
+        const uint2 *s2 = (const uint2 *)samples;
+        for (uint32_t k = 0; k < S; ++k) {
             uint64_t prev = 0;  // (key << 32 | pixel) of the last source added
             for (uint32_t t = dy_lo; t <= dy_hi; ++t) {
                 uint64_t best = ~0ull;
+                uint32_t best_slot = 0;
                 for (uint32_t dy = dy_lo; dy <= dy_hi; ++dy) {
-                    const uint32_t src = dy * W + (p - dy * H);
-                    const uint32_t key = __float_as_uint(sk[src].w);
-                    const uint64_t kp = ((uint64_t)key << 32) | src;
-                    if (key != 0u && kp > prev && kp < best) best = kp;
+                    const uint32_t dx = p - dy * H;  // source pixel (dx, dy)
+                    uint32_t sq0, sst;
+                    ts_slot_base(dy, dx, W, rows, S, sq0, sst);
+                    const uint32_t q = sq0 + k * sst;
+                    const uint32_t key = s2[q].y;
+                    const uint64_t kp = ((uint64_t)key << 32) | (dy * W + dx);
+                    if (key != 0u && kp > prev && kp < best) {
+                        best = kp;
+                        best_slot = q;
+                    }
                 }
                 if (best == ~0ull) break;
-                const float4 c = sk[(uint32_t)best];
+                const f3 c = decode_sample(a, s2[best_slot].x);
                 acc.x = acc.x + c.x;
                 acc.y = acc.y + c.y;
                 acc.z = acc.z + c.z;
@@ -431,8 +473,7 @@ __device__ __forceinline__ void fold_pixel(const FoldArgs &a, const float *sampl
     const float r = acc.x * scale, g = acc.y * scale, b = acc.z * scale;
     if (out_rgba) out_rgba[p] = make_float4(r, g, b, 0.f);
     if (out_rgb8) {
-        const uint32_t lr = p / map.width;
-        const uint32_t x = map.x0 + (p - lr * map.width);
+        const uint32_t x = map.x0 + col;
         const uint32_t y = row_of(map, lr);
         const size_t gi = (size_t)3 * ((size_t)(a.height - 1u - y) * a.width + x);
         out_rgb8[gi + 0] = gamma_byte(r);
@@ -441,27 +482,58 @@ __device__ __forceinline__ void fold_pixel(const FoldArgs &a, const float *sampl
     }
 }
 
+// Threads take the region's pixels in 8x8-tile order (tile_pixel), so the 64 lanes of
+// a wave read 64 consecutive slots per sample.
 __global__ __launch_bounds__(256) void fold_kernel(FoldArgs a)
 {
-    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= a.npix) return;
-    fold_pixel(a, a.samples, a.map, a.npix, a.alias, p, a.out_rgba, a.out_rgb8);
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.npix) return;
+    const uint32_t rows = a.npix / a.map.width;
+    uint32_t lr, col;
+    tile_pixel(i, a.map.width, rows, lr, col);
+    fold_pixel(a, a.samples, a.map, rows, a.alias, lr, col, a.out_rgba, a.out_rgb8);
 }
 
-// Batched fold (FoldArgs::rects): pixel p of the batch's concatenated rectangles.
-__global__ __launch_bounds__(256) void fold_kernel_batch(FoldArgs a)
+// The rectangle of pixel i of a batched fold (FoldArgs::rects).
+__device__ __forceinline__ uint32_t fold_rect(const FoldArgs &a, uint32_t i)
 {
-    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= a.npix) return;
     uint32_t lo = 0, hi = a.n_rects;
     while (hi - lo > 1u) {
         const uint32_t mid = (lo + hi) >> 1;
-        if (a.rects[mid].pix_off <= p) lo = mid; else hi = mid;
+        if (a.rects[mid].pix_off <= i) lo = mid; else hi = mid;
     }
-    const BatchRect &r = a.rects[lo];
+    return lo;
+}
+
+// Batched fold (FoldArgs::rects): pixel i of the batch's concatenated rectangles.
+__global__ __launch_bounds__(256) void fold_kernel_batch(FoldArgs a)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.npix) return;
+    const BatchRect &r = a.rects[fold_rect(a, i)];
     const RowMap map{r.y0, r.y0 + r.rows, 1u, 1u, 0u, r.x0, r.w};
-    fold_pixel(a, a.samples + (size_t)a.slot_floats * r.slot_off, map, r.npix, (int)r.alias, p - r.pix_off,
+    uint32_t lr, col;
+    tile_pixel(i - r.pix_off, r.w, r.rows, lr, col);
+    fold_pixel(a, a.samples + (size_t)a.slot_words * r.slot_off, map, r.rows, (int)r.alias, lr, col,
                a.out_rgba ? a.out_rgba + r.pix_off : nullptr, r.rgb8);
+}
+
+// Per-sample colours of a single-batch region (spt_render_samples, a debug path):
+// out[p * spp + s] = {r, g, b, counted}, p the local row-major pixel.
+__global__ __launch_bounds__(256) void expand_kernel(FoldArgs a, float4 *out)
+{
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= a.npix) return;
+    const uint32_t W = a.map.width, rows = a.npix / W, lr = p / W, col = p - lr * W;
+    uint32_t q0, step;
+    ts_slot_base(lr, col, W, rows, a.spp_batch, q0, step);
+    for (uint32_t k = 0; k < a.spp_batch; ++k) {
+        const uint32_t q = q0 + k * step;
+        const uint32_t w = a.slot_words == 1u ? a.samples[q] : a.samples[2u * q];
+        const bool counted = a.slot_words == 1u || a.samples[2u * q + 1u] != 0u;
+        const f3 c = decode_sample(a, w);
+        out[(size_t)p * a.spp_batch + k] = make_float4(c.x, c.y, c.z, counted ? 1.f : 0.f);
+    }
 }
 
 __global__ __launch_bounds__(256) void assemble_kernel(const float4 *tiles, uint32_t max_rows, RowMap base,
@@ -590,6 +662,13 @@ hipError_t launch_fold(const FoldArgs &a, hipStream_t s)
         hipLaunchKernelGGL(fold_kernel_batch, dim3((a.npix + 255) / 256), dim3(256), 0, s, a);
     else
         hipLaunchKernelGGL(fold_kernel, dim3((a.npix + 255) / 256), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_expand(const FoldArgs &a, float4 *out, hipStream_t s)
+{
+    if (a.npix == 0) return hipSuccess;
+    hipLaunchKernelGGL(expand_kernel, dim3((a.npix + 255) / 256), dim3(256), 0, s, a, out);
     return hipGetLastError();
 }
 

@@ -687,11 +687,15 @@ __device__ __forceinline__ Hit find_closest_lane(const AccelView &ac, const f3 &
     return h;
 }
 
-// Per-lane path state of the flattened recursion.
+// Per-lane path state of the flattened recursion.  The diffuse loop's colour is not
+// carried: it is the first diffuse hit's albedo halved once per bounce, so the path
+// keeps that hit's slot and the sample code records it with the bounce count (the fold
+// rebuilds the colour, code_word in spt_internal.h).
 struct Path {
     uint32_t phase, item, bounce, spec;
     uint64_t st;  // keyed splitmix stream of this (pixel, sample)
-    f3 o, d, c;
+    f3 o, d;
+    uint32_t slot;  // slot of the first diffuse hit (PH_DLOOP)
 };
 
 // GenerateUniformDistInsideSphereVector (Random.hpp:115-127) for every lane with
@@ -813,8 +817,8 @@ __device__ __forceinline__ void refract_event(const float4 *__restrict__ slots, 
 // its own queue order; so two paths of a sample reach `colors` in the order of
 // (key, pixel) -- which only matters where colorIndex aliases pixels (non-square
 // tiles, lines 103 and 186; fold_kernel).
-__device__ __forceinline__ void finish_step(uint32_t mode, float *samples, Path &ps, bool fin, bool spec_event,
-                                            bool refr_event, bool sky, f3 col, unsigned long long &done,
+__device__ __forceinline__ void finish_step(uint32_t mode, uint32_t *samples, Path &ps, bool fin, bool spec_event,
+                                            bool refr_event, bool sky, uint32_t word, unsigned long long &done,
                                             unsigned long long &dropped)
 {
     bool counted = true;
@@ -826,24 +830,21 @@ __device__ __forceinline__ void finish_step(uint32_t mode, float *samples, Path 
             // RenderSegmentTask: this path would be processed in pass 10, which never runs
             fin = true;
             counted = false;
-            col = mk(0.f, 0.f, 0.f);
+            word = kZeroWord;
             ++dropped;
         } else if (k + 1u > kSpecularCap) {
             fin = true;
-            col = mk(0.f, 0.f, 0.f);
+            word = kZeroWord;
         }
     }
     if (fin) {
         if (mode == 0u) {
-            // RenderSegment counts every sample: 12-byte slots
-            float *o3 = samples + (size_t)3 * ps.item;
-            o3[0] = col.x;
-            o3[1] = col.y;
-            o3[2] = col.z;
+            // RenderSegment counts every sample: one word per slot
+            samples[ps.item] = word;
         } else {
             const uint32_t key =
                 counted ? 1u + (((ps.spec & 0xFFFFu) << 11) | (sky ? 1u << 10 : 0u) | ((ps.spec >> 16) & 0x3FFu)) : 0u;
-            *(float4 *)(samples + (size_t)4 * ps.item) = make_float4(col.x, col.y, col.z, __uint_as_float(key));
+            *(uint2 *)(samples + (size_t)2 * ps.item) = make_uint2(word, key);
         }
         ps.phase = PH_IDLE;
         ps.d = mk(0.f, 0.f, 0.f);
@@ -864,9 +865,9 @@ __device__ __forceinline__ void shade_step(const RenderArgs &a, Path &ps, const 
     const float4 *__restrict__ hit = a.scene.accel.slots;
     const float4 *__restrict__ shade = a.scene.shade;
     const uint32_t *__restrict__ mat = a.scene.mat;
-    float *samples = a.samples;
+    uint32_t *samples = a.samples;
     uint32_t mode = a.mode;
-    float sky0 = a.cam.sky[0], sky1 = a.cam.sky[1], sky2 = a.cam.sky[2];
+    uint32_t bounces = a.bounces, code_shift = a.scene.code_shift;
 #if defined(__HIP_DEVICE_COMPILE__)
     if constexpr (KARG) {
         // render kernels: read at the point of use from the kernarg segment (scalar
@@ -877,14 +878,13 @@ __device__ __forceinline__ void shade_step(const RenderArgs &a, Path &ps, const 
         mat = k.scene.mat;
         samples = k.samples;
         mode = k.mode;
-        sky0 = k.cam.sky[0];
-        sky1 = k.cam.sky[1];
-        sky2 = k.cam.sky[2];
+        bounces = k.bounces;
+        code_shift = k.scene.code_shift;
     }
 #endif
     const uint32_t idx = h.idx;
     bool fin = false;
-    f3 col = mk(0.f, 0.f, 0.f);
+    uint32_t word = kZeroWord;  // the sample's code (spt_internal.h code_word)
     const bool dl = ps.phase == PH_DLOOP;
     uint32_t m = SPT_SKYBOX_ID;
     if (act && idx != kMiss) m = mat[idx];
@@ -895,7 +895,10 @@ __device__ __forceinline__ void shade_step(const RenderArgs &a, Path &ps, const 
         --ps.bounce;
         const bool end = ps.bounce == 0u || idx == kMiss;
         if (end) {
-            col = ps.c;
+            // the albedo of the first diffuse hit halved 1 + j times: once at that hit
+            // (line 24) and once per further bounce (line 31), j = bounces - bounce - 1
+            const uint32_t j = min(bounces - ps.bounce - 1u, kCodeSat);
+            word = code_word(2u + ((j << code_shift) | ps.slot));
             fin = true;
         }
         scatter = !end;
@@ -905,9 +908,9 @@ __device__ __forceinline__ void shade_step(const RenderArgs &a, Path &ps, const 
         scatter = m == SPT_DIFFUSE_ID || m == SPT_REFLECTIVE_ID;
         refr = m == SPT_REFRACTIVE_ID;
         if (!scatter && !refr) {
-            // SampleColorSkybox, lines 11-14
-            const float k = ps.d.y + 1.f;
-            col = mul(mk(sky0 * k, sky1 * k, sky2 * k), 0.5f);
+            // SampleColorSkybox, lines 11-14: initColor * (d.y + 1) * 0.5, rebuilt by the
+            // fold from k = d.y + 1
+            word = __float_as_uint(ps.d.y + 1.f);
             fin = true;
         }
     }
@@ -923,11 +926,9 @@ __device__ __forceinline__ void shade_step(const RenderArgs &a, Path &ps, const 
         f3 rv = rv_coop;
         f3 base;
         if (dl) {
-            ps.c = mul(ps.c, 0.5f);
-            base = add(ps.o, nrm);  // origin + normal (+ rv), line 32
+            base = add(ps.o, nrm);  // origin + normal (+ rv), line 32; colour *= 0.5 (line 31) in the code
         } else if (m == SPT_DIFFUSE_ID) {
-            const float4 sh = shade[idx];
-            ps.c = mk(sh.x * 0.5f, sh.y * 0.5f, sh.z * 0.5f);
+            ps.slot = idx;  // colour = albedo * 0.5 (line 24), in the code
             base = nrm;
             ps.phase = PH_DLOOP;
         } else {
@@ -942,7 +943,7 @@ __device__ __forceinline__ void shade_step(const RenderArgs &a, Path &ps, const 
         refract_event(hit, ps, idx);
         spec_event = true;
     }
-    finish_step(mode, samples, ps, fin, spec_event, refr, !dl, col, done, dropped);
+    finish_step(mode, samples, ps, fin, spec_event, refr, !dl, word, done, dropped);
 }
 
 
@@ -958,7 +959,7 @@ __device__ __forceinline__ void start_path(const RenderArgs &a, uint32_t mine, u
     uint32_t sl, lr, cx;
     ts_item(mine, a.map.width, rows, a.spp_batch, a.div_band, a.div_tile, sl, lr, cx);
     const uint32_t s = a.s0 + sl;
-    ps.item = sl * a.npix + lr * a.map.width + cx;  // slot: [sample][row-major pixel]
+    ps.item = mine;  // slots in item order (ts_slot_base)
     const uint32_t x = a.map.x0 + cx;
     const uint32_t y = a.map.parts == 1u ? a.map.y0 + lr : row_of_fast(a.map, lr, a.div_strip);
     ps.st = fmix64(a.seed_key ^ (((uint64_t)(y * a.width + x) << 32) | (uint64_t)s));

@@ -36,8 +36,8 @@ namespace spt {
 
 namespace {
 
-// Ray queue entry (SoA of 16-byte records, coalesced): o + c.x, d + c.y,
-// {c.z, item, bounce, phase | spec << 2}, RNG state.
+// Ray queue entry (SoA of 16-byte records, coalesced): o + first diffuse slot, d,
+// {-, item, bounce, phase | spec << 2}, RNG state.
 struct WfRay {
     float4 *o, *d, *m;
     uint2 *st;
@@ -61,7 +61,7 @@ __device__ __forceinline__ Path load_ray(const WfRay &q, uint32_t i)
     Path ps;
     ps.o = mk(o.x, o.y, o.z);
     ps.d = mk(d.x, d.y, d.z);
-    ps.c = mk(o.w, d.w, m.x);
+    ps.slot = __float_as_uint(o.w);
     ps.item = __float_as_uint(m.y);
     ps.bounce = __float_as_uint(m.z);
     const uint32_t ps_bits = __float_as_uint(m.w);
@@ -73,9 +73,9 @@ __device__ __forceinline__ Path load_ray(const WfRay &q, uint32_t i)
 
 __device__ __forceinline__ void store_ray(const WfRay &q, uint32_t i, const Path &ps)
 {
-    q.o[i] = make_float4(ps.o.x, ps.o.y, ps.o.z, ps.c.x);
-    q.d[i] = make_float4(ps.d.x, ps.d.y, ps.d.z, ps.c.y);
-    q.m[i] = make_float4(ps.c.z, __uint_as_float(ps.item), __uint_as_float(ps.bounce),
+    q.o[i] = make_float4(ps.o.x, ps.o.y, ps.o.z, __uint_as_float(ps.slot));
+    q.d[i] = make_float4(ps.d.x, ps.d.y, ps.d.z, 0.f);
+    q.m[i] = make_float4(0.f, __uint_as_float(ps.item), __uint_as_float(ps.bounce),
                          __uint_as_float(ps.phase | (ps.spec << 2)));
     q.st[i] = make_uint2((uint32_t)ps.st, (uint32_t)(ps.st >> 32));
 }
@@ -88,7 +88,7 @@ __global__ __launch_bounds__(256) void wf_generate(WfArgs w, uint32_t base_item,
     const uint32_t rows = a.npix / a.map.width;
     const Recip rw = recip((float)a.width), rh = recip((float)a.height);
     Path ps;
-    ps.c = mk(0.f, 0.f, 0.f);
+    ps.slot = 0;
     start_path(a, base_item + i, rows, rw, rh, mk(a.cam.eye[0], a.cam.eye[1], a.cam.eye[2]), ps);
     store_ray(w.cur, dst0 + i, ps);
 }

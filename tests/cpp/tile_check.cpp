@@ -1,9 +1,13 @@
 // Host check of the kernel's item orders (spt_internal.h): spt::tile_pixel
 // ([sample][tile][pixel]) and spt::ts_item ([band][tile][sample][pixel]) are
 // bijections onto the region (x samples) for every shape in a range plus the
-// config sizes, and full 8x8 tiles are contiguous runs of 64 items.  Exit 0 = pass.
+// config sizes, full 8x8 tiles are contiguous runs of 64 items, and
+// spt::ts_slot_base inverts ts_item (the fold's slot of (pixel, sample)).  The
+// sample codes: code_word / word_code round trip, and no sky word k = fl(y + 1.f)
+// (any float y) falls in the code range.  Exit 0 = pass.
 #include <algorithm>
 #include <cstdio>
+#include <cstring>
 #include <vector>
 
 #include "spt_internal.h"
@@ -57,6 +61,12 @@ int main()
                         std::printf("FAIL ts rows=%u width=%u S=%u q=%u -> (%u, %u, %u)\n", rows, width, S, q, sl, lr, col);
                         return 1;
                     }
+                    uint32_t q0, step;
+                    spt::ts_slot_base(lr, col, width, rows, S, q0, step);
+                    if (q0 + sl * step != q) {
+                        std::printf("FAIL slot rows=%u width=%u S=%u q=%u -> %u + %u * %u\n", rows, width, S, q, q0, sl, step);
+                        return 1;
+                    }
                     // full tiles: 64 consecutive items are the 64 pixels of one tile and sample
                     if (rows % 8 == 0 && width % 8 == 0) {
                         uint32_t s0, l0, c0;
@@ -79,6 +89,12 @@ int main()
                 spt::ts_item(q, width, rows, S, fb, ft, sl, lr, col);
                 if (sl >= S || lr >= rows || col >= width || seen[((size_t)sl * rows + lr) * width + col]++) {
                     std::printf("FAIL ts rows=%u width=%u S=%u q=%u\n", rows, width, S, q);
+                    return 1;
+                }
+                uint32_t q0, step;
+                spt::ts_slot_base(lr, col, width, rows, S, q0, step);
+                if (q0 + sl * step != q) {
+                    std::printf("FAIL slot rows=%u width=%u S=%u q=%u\n", rows, width, S, q);
                     return 1;
                 }
             }
@@ -108,6 +124,39 @@ int main()
                 return 1;
             }
         }
+    }
+    // sample codes: every code round-trips (edges + a stride), the colour-0 word, and
+    // no k = fl(y + 1.f) of any float y is a code word (so sky words and codes never mix)
+    {
+        const uint32_t cmax = 2u * (spt::kCodeSmall - 1u);
+        if (((spt::kCodeSat + 1ull) << spt::kCodeMaxShift) + 1ull > cmax) {
+            std::printf("FAIL code capacity\n");
+            return 1;
+        }
+        for (uint64_t c = 1; c <= cmax; c += (c < 64 || cmax - c < 64 || (c > spt::kCodeSmall - 64 && c < spt::kCodeSmall + 64)) ? 1 : 9973) {
+            const uint32_t w = spt::code_word((uint32_t)c);
+            if (spt::word_code(w) != c) {
+                std::printf("FAIL code %llu -> %08x -> %u\n", (unsigned long long)c, w, spt::word_code(w));
+                return 1;
+            }
+        }
+        if (spt::code_word(1) != spt::kZeroWord || spt::word_code(spt::kZeroWord) != 1) {
+            std::printf("FAIL zero word\n");
+            return 1;
+        }
+        volatile float one = 1.0f;
+        uint32_t bits = 0;
+        do {
+            float y, k;
+            std::memcpy(&y, &bits, 4);
+            k = y + one;
+            uint32_t kw;
+            std::memcpy(&kw, &k, 4);
+            if (spt::word_code(kw) != 0) {
+                std::printf("FAIL sky word y=%08x k=%08x is a code\n", bits, kw);
+                return 1;
+            }
+        } while (++bits != 0);
     }
     std::printf("ok\n");
     return 0;

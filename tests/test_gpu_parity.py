@@ -347,7 +347,7 @@ def test_workspace_batches_fold_in_order(spt, ctx, golden_scenes, task):
 
     setup(ctx, scene_from(spt, golden_scenes, "random"), 1200, 800, 10, 50, seed=4)
     a = render(200, 264, 100, 228)
-    ctx.set_workspace(64 * 128 * 12 * 3)  # 4 (segment) / 5 (task) batches
+    ctx.set_workspace(64 * 128 * (8 if task else 4) * 3)  # 3 samples per batch: 4 batches (4- / 8-byte slots)
     b = render(200, 264, 100, 228)
     ctx.reset_stats()
     st = torch.cuda.Stream()
@@ -359,7 +359,7 @@ def test_workspace_batches_fold_in_order(spt, ctx, golden_scenes, task):
     ctx.set_workspace(4 << 30)
     assert_bitwise(b, a, "batched vs single-batch")
     assert_bitwise(out.cpu().numpy(), a, "batched on a caller stream vs single-batch")
-    assert launches == (5 if task else 4)
+    assert launches == 4
 
 
 def test_row_split_and_assemble_equals_full_frame(spt, ctx, golden_scenes):
@@ -472,7 +472,10 @@ def test_cpp_dropin_shim_renders_like_the_context(spt, golden_scenes, tmp_path, 
         for i in range(tc):
             c.render_segment(sh * j, sh * j + sh, sw * i, sw * i + sw, want, task=bool(task))
     c.close()
-    assert np.array_equal(got, want)
+    bad = np.nonzero(got != want)[0]
+    px = bad // 3
+    tiles = sorted(set(zip(((h - 1 - px // w) // sh).tolist(), ((px % w) // sw).tolist())))
+    assert bad.size == 0, f"{bad.size} bytes differ in tiles (row, col) {tiles[:24]} (of {len(tiles)})"
 
 
 def test_bench_two_ranks_on_one_gpu_matches_one_rank(spt, tmp_path):

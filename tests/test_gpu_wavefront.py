@@ -111,7 +111,7 @@ def test_small_queue_and_sample_batches(spt, mctx, golden_scenes):
         c.set_engine(spt._native.ENGINE_WAVEFRONT)
         scene = scene_from(spt, golden_scenes, "random")
         setup(c, scene, 96, 64, 12, 50)
-        c.set_workspace(96 * 64 * 5 * 12)  # 5 samples per batch (12-byte slots)
+        c.set_workspace(96 * 64 * 5 * 4)  # 5 samples per batch (4-byte slots)
         got = c.render_segment(0, 64, 0, 96)
         setup(mctx, scene, 96, 64, 12, 50)
         assert_bitwise(got, mctx.render_segment(0, 64, 0, 96), "small queue + batches")

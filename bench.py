@@ -4,7 +4,8 @@
 One step = one frame of BASELINE.json config 2 (GenerateSpheres seed 1,
 1200x800, 100 spp, depth 50): every (pixel, sample) path traced by the gfx950
 megakernel, folded in sample order, written as float RGBA + RGB8 g_data.
-With N GPUs (torchrun, one process per GPU) the frame is split into interleaved
+With N GPUs (one process per GPU: `--gpus N` starts the N ranks itself when no
+launcher did, or torchrun starts them) the frame is split into interleaved
 row strips (8 rows, or fewer so the strips deal evenly: 4 at N = 8), rank r renders
 strips r, r+N, ...; the float tiles are gathered to rank 0 over RCCL
 (one gather: send/recv pairs over xGMI) and assembled there (strong scaling: the frame is fixed,
@@ -275,7 +276,7 @@ def main():
 
     from simplepathtracer_amd.distributed import FrameSplit, even_strip, render_frame
     split = FrameSplit(W, H, world, args.strip or even_strip(H, world))
-    slot_bytes = 12 if args.mode == "segment" else 16
+    slot_bytes = 4 if args.mode == "segment" else 8  # sample words (+ the order key in task mode)
     one_batch = W * H * spp * slot_bytes <= (16 << 30)  # the context's default workspace
     nst = args.streams
     if nst <= 0:
@@ -369,10 +370,12 @@ def main():
         px_per_launch = samples_per_launch / spp  # every launch renders its pixels at full spp
         # SURVEY §8(d) algorithmic bytes: 19 B per pixel (float RGBA + RGB8) + 48 B per sphere
         algo_bytes = ALGO_BYTES_PER_PIXEL * px_per_launch + ALGO_BYTES_PER_SPHERE * scene.n
-        slot_bytes = (12.0 if args.mode == "segment" else 16.0) * samples_per_launch  # the design's sample slots
+        slot_bytes = (4.0 if args.mode == "segment" else 8.0) * samples_per_launch  # the design's sample slots
         prof = profile_record(args.config) if world == 1 and args.engine == "megakernel" else None
         rk = (prof or {}).get("render_kernel", {})
+        fk = (prof or {}).get("fold_kernel", {})
         traffic = (rk["fetch_bytes"] + rk["write_bytes"]) if "fetch_bytes" in rk else None
+        frame_traffic = traffic + fk["fetch_bytes"] + fk["write_bytes"] if traffic and "fetch_bytes" in fk else None
         out = {
             "metric": "Msamples/s (pixels×spp/s), RTIOW random-sphere scene, 1/2/4/8 MI355X",
             "value": round(value, 3),
@@ -401,9 +404,16 @@ def main():
                          "algorithmic_bytes": algo_bytes,
                          "algorithmic_def": "19 B x pixels + 48 B x spheres per launch (SURVEY §8d)",
                          "traffic_over_algorithmic": round(traffic / algo_bytes, 1) if traffic else None,
+                         "render_write_over_slots": round(rk["write_bytes"] / slot_bytes, 3) if traffic else None,
+                         "frame_traffic": frame_traffic,
+                         "frame_traffic_def": "render FETCH x2 + WRITE plus the fold's FETCH x2 + WRITE per launch "
+                                              "(PMC, profiles/counters.json)",
+                         "frame_traffic_over_algorithmic": round(frame_traffic / algo_bytes, 1) if frame_traffic
+                                                           else None,
                          "slot_bytes": slot_bytes,
-                         "slot_def": "the design's per-sample slots written by the render kernel (12 B/sample "
-                                     "segment mode) and read back once by the fold: the traffic above",
+                         "slot_def": "the design's per-sample slots (a 4-byte sample word in segment mode, word + "
+                                     "order key in task mode) written once by the render kernel and read back "
+                                     "once by the fold",
                          "kernel": "render_kernel", "avg_launch_ms": round(avg_ms, 4),
                          "avg_launch_ms_def": "union of the render launches' HIP-event intervals (launch stream) "
                                               "/ launches",

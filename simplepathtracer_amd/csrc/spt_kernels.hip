@@ -120,14 +120,7 @@ template <bool TREE, int LEAF, bool LDSN, uint32_t BLOCK, bool BATCH = false, bo
 __device__ __forceinline__ void render_body(const RenderArgs &a)
 {
     const uint32_t lane = __lane_id();
-    const f3 eye = mk(a.cam.eye[0], a.cam.eye[1], a.cam.eye[2]);
     const uint32_t rows = a.npix / a.map.width;  // region rows (uniform)
-    // shared reciprocals of the primary-ray divisors (div_core range: 1 <= W, H <= 2^32)
-    const Recip rw = recip((float)a.width), rh = recip((float)a.height);
-    (void)rows;
-    (void)rw;
-    (void)rh;
-    (void)eye;
 
     __shared__ uint32_t s_lds[BLOCK];  // wave-private scratch of the cooperative sampler
     __shared__ uint4 s_nodes[LDSN ? 2 * kLdsNodeRecords : 1];
@@ -150,7 +143,6 @@ __device__ __forceinline__ void render_body(const RenderArgs &a)
     uint32_t blk_cur = 0, blk_end = 0;
     uint32_t pend = 0;
     uint32_t rect = 0;  // BATCH: rectangle of the current claim
-    (void)rect;
     const uint32_t home = blockIdx.x % a.n_queues;
     uint32_t qi = 0;  // queues tried after the home queue ran dry (lane 0)
     if (lane == 0) pend = claim_next(a, home, qi);
@@ -166,10 +158,6 @@ __device__ __forceinline__ void render_body(const RenderArgs &a)
     hres.t = 0.f;
     uint32_t li = 0, lleaf = kNoSlot, lleaf2 = kNoSlot;
     bool fresh = true;
-    (void)li;
-    (void)lleaf;
-    (void)lleaf2;
-    (void)fresh;
 #if SPT_DIAG
     unsigned long long d_t0 = __builtin_amdgcn_s_memtime();
 #define SPT_STAMP(acc)                                              \
@@ -201,20 +189,15 @@ __device__ __forceinline__ void render_body(const RenderArgs &a)
                 } else {
                     blk_cur = nb;
                     blk_end = min(nb + a.claim, a.n_items);
-#if defined(__HIP_DEVICE_COMPILE__)
                     rect = find_rect(nb);
-#endif
                 }
             }
             if (!exhausted) {
                 const uint32_t take = min((uint32_t)__popcll(need), blk_end - blk_cur);
                 const uint32_t rank = lane_rank(need);
                 const uint32_t mine = blk_cur + rank;
-                (void)mine;
                 blk_cur += take;
-#if defined(__HIP_DEVICE_COMPILE__)
                 if (ps.phase == PH_IDLE && rank < take) start_path_rect(mine, rect, ps);
-#endif
             }
         } else if (!BATCH && need != 0ull && !exhausted) {
             const uint32_t cnt = (uint32_t)__popcll(need);
@@ -239,13 +222,7 @@ __device__ __forceinline__ void render_body(const RenderArgs &a)
                     blk_end = ne;
                 }
             }
-            if (ps.phase == PH_IDLE && mine != 0xFFFFFFFFu) {
-#if defined(__HIP_DEVICE_COMPILE__)
-                start_path_kernarg(mine, rows, ps);
-#else
-                start_path(a, mine, rows, rw, rh, eye, ps);
-#endif
-            }
+            if (ps.phase == PH_IDLE && mine != 0xFFFFFFFFu) start_path_kernarg(mine, rows, ps);
         }
         const unsigned long long live = __ballot(ps.phase != PH_IDLE);
         if (live == 0ull) {
@@ -314,10 +291,6 @@ __device__ __forceinline__ void render_body(const RenderArgs &a)
         atomicAdd(&a.counters[17], dg.lane_pretests);
     }
 #endif
-    (void)d_iters;
-    (void)d_cyc_cast;
-    (void)d_cyc_shade;
-    (void)d_cyc_refill;
 #undef SPT_STAMP
 }
 

@@ -754,7 +754,6 @@ __device__ __forceinline__ f3 coop_ball_vector(uint64_t &st, bool need, uint32_t
     return r;
 }
 
-#if defined(__HIP_DEVICE_COMPILE__)
 // The kernel's RenderArgs in the kernarg segment, behind an opaque zero offset: the
 // refill-only fields read through it are loaded (scalar cache) where they are used
 // instead of being hoisted into SGPRs for the kernel's lifetime.  Only valid in a
@@ -767,7 +766,6 @@ __device__ __forceinline__ kargs_t *kernarg_args()
     typedef __attribute__((address_space(4))) const char kchar;
     return (kargs_t *)((kchar *)__builtin_amdgcn_kernarg_segment_ptr() + z);
 }
-#endif
 
 // SampleColorRefractive (SingleThreadPathTracer.hpp:48-92) for a lane whose ray hit
 // the glass slot idx at the contact point ps.o: new ps.o (exit point) and ps.d.
@@ -868,7 +866,6 @@ __device__ __forceinline__ void shade_step(const RenderArgs &a, Path &ps, const 
     uint32_t *samples = a.samples;
     uint32_t mode = a.mode;
     uint32_t bounces = a.bounces, code_shift = a.scene.code_shift;
-#if defined(__HIP_DEVICE_COMPILE__)
     if constexpr (KARG) {
         // render kernels: read at the point of use from the kernarg segment (scalar
         // loads) instead of holding them in SGPRs across the loop
@@ -881,7 +878,6 @@ __device__ __forceinline__ void shade_step(const RenderArgs &a, Path &ps, const 
         bounces = k.bounces;
         code_shift = k.scene.code_shift;
     }
-#endif
     const uint32_t idx = h.idx;
     bool fin = false;
     uint32_t word = kZeroWord;  // the sample's code (spt_internal.h code_word)
@@ -981,7 +977,6 @@ __device__ __forceinline__ void start_path(const RenderArgs &a, uint32_t mine, u
     ps.spec = 0;
 }
 
-#if defined(__HIP_DEVICE_COMPILE__)
 // start_path with the refill parameters copied out of the kernarg segment at the
 // point of use (scalar loads); render_kernel only.
 __device__ __forceinline__ void start_path_kernarg(uint32_t mine, uint32_t rows, Path &ps)
@@ -1048,7 +1043,6 @@ __device__ __forceinline__ void start_path_rect(uint32_t mine, uint32_t ri, Path
                mk(k.cam.eye[0], k.cam.eye[1], k.cam.eye[2]), ps);
     ps.item += r.slot_off;
 }
-#endif
 
 }  // namespace
 }  // namespace spt

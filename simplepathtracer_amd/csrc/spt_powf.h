@@ -23,6 +23,17 @@
 // exp2 table: tab[i] = bits(2^(i/32) rounded to double) - (i << 47), derived
 // exactly (tools/derive_exp2_table.py); log2 table and the polynomials are the
 // published constants of the algorithm.
+//
+// Provenance and license: the algorithm, its log2 table (powf_log2_data.c) and
+// polynomial coefficients come from ARM's Optimized Routines
+// (github.com/ARM-software/optimized-routines, math/powf.c, Szabolcs Nagy, 2017-2018),
+// contributed to glibc 2.28 as sysdeps/ieee754/flt-32/e_powf.c and e_powf_data.c.
+// Optimized Routines is released under "MIT OR Apache-2.0 WITH LLVM-exception"
+// (SPDX), glibc under LGPL-2.1-or-later; this restatement follows the MIT-licensed
+// upstream: Copyright (c) 2017-2018 Arm Limited.  Permission is hereby granted, free
+// of charge, to any person obtaining a copy of this software to deal in it without
+// restriction, subject to including this notice; the software is provided "as is",
+// without warranty of any kind.
 #pragma once
 #include <stdint.h>
 #include <string.h>

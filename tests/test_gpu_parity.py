@@ -427,9 +427,7 @@ def test_config2_full_frame_properties(spt, ctx, oracle, golden_scenes):
         x, y = int(rng.integers(0, 1200)), int(rng.integers(0, 800))
         want, _ = oracle.render_segment(sc, fr, y, y + 1, x, x + 1)
         assert_bitwise(a[y * 1200 + x, :3], want[0, :3], f"pixel {(x, y)}")
-    gw = np.zeros_like(g1)
     assert np.isfinite(a[:, :3]).all()
-    _ = gw
 
 
 def test_concurrent_render_jobs_share_a_context(spt, golden_scenes):
@@ -634,9 +632,8 @@ def test_progressive_passes_equal_lower_spp_renders(spt, ctx, golden_scenes, tas
     for m in (7, 14):
         setup(ctx, scene, W, H, m, 50)
         gm = np.zeros_like(g)
-        ref = ctx.render_segment(*region, gm, task=task)
+        ctx.render_segment(*region, gm, task=task)
         assert np.array_equal(snaps[m], gm), f"preview after {m} samples"
-        _ = ref
     setup(ctx, scene, W, H, 20, 50)
     g2 = np.zeros_like(g)
     assert_bitwise(full, ctx.render_segment(*region, g2, task=task), "final pass vs one-shot render")

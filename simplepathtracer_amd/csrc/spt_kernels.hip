@@ -148,7 +148,9 @@ __device__ __forceinline__ void render_body(const RenderArgs &a)
     if (lane == 0) pend = claim_next(a, home, qi);
     bool exhausted = false;
     unsigned long long casts = 0, done = 0, dropped = 0;
-    unsigned long long d_iters = 0, d_cyc_cast = 0, d_cyc_shade = 0, d_cyc_refill = 0;
+    struct {
+        unsigned long long iters = 0, cast = 0, shade = 0, refill = 0;  // SPT_DIAG counts and s_memtime split
+    } dc;
     CastDiag dg;
     // resumable lane walk (SPT_LANE_BUDGET): the cast state of lanes whose walk ran
     // out of its iteration budget, continued on the next iteration
@@ -229,14 +231,14 @@ __device__ __forceinline__ void render_body(const RenderArgs &a)
             if (exhausted) break;
             continue;
         }
-        SPT_STAMP(d_cyc_refill);
+        SPT_STAMP(dc.refill);
         // the lane walks are resumable: a lane still walking after SPT_LANE_BUDGET walk
         // iterations and leaf passes keeps its cast state (winner, node, parked leaves)
         // and continues it next iteration while the other lanes shade and refill, so a
         // few long walks (grazing rays) do not hold the wave (config 5: 97.5 -> 90 ms)
         constexpr bool RES = SPT_LANE_BUDGET > 0 && (LDSN || GLANE);
         if (!RES) casts += (unsigned long long)__popcll(live);
-        ++d_iters;
+        ++dc.iters;
         // ---- one cast + one shading step ----
         const bool act = ps.phase != PH_IDLE;
         // GLANE: the lane walk over layout 0 in global memory (trees too large for LDS)
@@ -255,10 +257,10 @@ __device__ __forceinline__ void render_body(const RenderArgs &a)
                     ? find_closest_lane<LEAF>(a.scene.accel, ps.o, ps.d, act, dg, (const uint32_t *)a.scene.accel.nodes)
                     : find_closest<TREE, LEAF, LDSN>(a.scene.accel, ps.o, ps.d, act, dg, (const uint32_t *)s_nodes);
         }
-        SPT_STAMP(d_cyc_cast);
+        SPT_STAMP(dc.cast);
         shade_step<true>(a, ps, h, act && cdone, done, dropped, s_lds + (threadIdx.x & ~63u));
         fresh = cdone;
-        SPT_STAMP(d_cyc_shade);
+        SPT_STAMP(dc.shade);
     }
 
     // per-lane done/dropped -> wave sums (butterfly), one atomic per counter and wave
@@ -275,12 +277,12 @@ __device__ __forceinline__ void render_body(const RenderArgs &a)
     }
 #if SPT_DIAG
     if (lane == 0) {
-        atomicAdd(&a.counters[4], d_iters);
+        atomicAdd(&a.counters[4], dc.iters);
         atomicAdd(&a.counters[5], dg.leaves);
         atomicAdd(&a.counters[6], dg.nodes);
-        atomicAdd(&a.counters[7], d_cyc_cast);
-        atomicAdd(&a.counters[8], d_cyc_shade);
-        atomicAdd(&a.counters[9], d_cyc_refill);
+        atomicAdd(&a.counters[7], dc.cast);
+        atomicAdd(&a.counters[8], dc.shade);
+        atomicAdd(&a.counters[9], dc.refill);
         atomicAdd(&a.counters[10], dg.pairs);
         atomicAdd(&a.counters[11], dg.live);
         atomicAdd(&a.counters[12], dg.spheres);

@@ -116,10 +116,11 @@ inline void sync_globals()
     check(ctx, spt_set_camera(ctx, view, eye, sky), "spt_set_camera");
     check(ctx, spt_set_params(ctx, g_width, g_height, g_samples, g_bounces, seed), "spt_set_params");
     last.swap(key);
-    // page-lock g_data once (best effort): batched calls then write their tiles' bytes
-    // into it in place (no copy-back)
+    // page-lock g_data once (best effort; SPT_PIN=0 leaves it pageable): batched calls
+    // then write their tiles' bytes into it in place (no copy-back)
     static const void *pinned = nullptr;
-    if (g_data && pinned != g_data && spt_pin_host(ctx, g_data, (size_t)g_width * g_height * 3) == SPT_OK)
+    static const bool pin = !std::getenv("SPT_PIN") || std::atoi(std::getenv("SPT_PIN")) != 0;
+    if (pin && g_data && pinned != g_data && spt_pin_host(ctx, g_data, (size_t)g_width * g_height * 3) == SPT_OK)
         pinned = g_data;
 }
 

@@ -166,6 +166,7 @@ struct spt_ctx {
     bool batch_leader = false;  // a caller is assembling the next batch
     BatchSet bsets[kMaxBatchSets];
     uint32_t batch_sets = 2;  // batches in flight at once (SPT_BATCH_SETS)
+    uint32_t batch_grid_div = 1;  // each batch launch takes 1/div of the grid (SPT_BATCH_GRID_DIV)
     std::condition_variable batch_cv;
     uint64_t batches = 0, batched_calls = 0;
 
@@ -843,7 +844,7 @@ int launch_batch(spt_ctx *ctx, BatchSet *bs, const std::vector<BatchReq *> &batc
     }
     EventPair ev = get_pair(ctx);
     HIP_TRY(ctx, hipEventRecord(ev.a, s));
-    spt::LaunchShape sh{render_grid(ctx, ra.n_items, claim, 1u), ctx->block, 1u, 0, 0};
+    spt::LaunchShape sh{render_grid(ctx, ra.n_items, claim, ctx->batch_grid_div), ctx->block, ctx->batch_grid_div, 0, 0};
     HIP_TRY(ctx, spt::launch_render(ra, sh, s));
     ctx->last_grid = sh.ran_grid;
     ctx->last_block = sh.ran_block;
@@ -1251,6 +1252,7 @@ int spt_ctx_create(int device, spt_ctx **out)
     if (const char *e = std::getenv("SPT_HOST_GRID_DIV")) ctx->host_grid_div = (uint32_t)std::max(0, std::atoi(e));
     if (const char *e = std::getenv("SPT_BATCH")) ctx->batching = std::atoi(e) != 0;
     if (const char *e = std::getenv("SPT_BATCH_DBUF")) ctx->batch_dbuf = std::atoi(e) != 0;
+    if (const char *e = std::getenv("SPT_BATCH_GRID_DIV")) ctx->batch_grid_div = (uint32_t)std::max(1, std::atoi(e));
     if (const char *e = std::getenv("SPT_BATCH_SETS"))
         ctx->batch_sets = (uint32_t)std::min<int>((int)kMaxBatchSets, std::max(1, std::atoi(e)));
     if (const char *e = std::getenv("SPT_HOST_SLOTS"))

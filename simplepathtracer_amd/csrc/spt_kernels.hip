@@ -409,31 +409,70 @@ __device__ __forceinline__ void fold_pixel(const FoldArgs &a, const uint32_t *sa
         const uint32_t H = rows;
         const uint32_t dy_lo = p >= W ? (p - W + H) / H : 0u;
         const uint32_t dy_hi = min(H - 1u, p / H);
+        const uint32_t ns = dy_hi + 1u - dy_lo;  // sources: pixels (p - dy H, dy)
         const uint2 *s2 = (const uint2 *)samples;
-        for (uint32_t k = 0; k < S; ++k) {
-            uint64_t prev = 0;  // (key << 32 | pixel) of the last source added
-            for (uint32_t t = dy_lo; t <= dy_hi; ++t) {
-                uint64_t best = ~0ull;
-                uint32_t best_slot = 0;
-                for (uint32_t dy = dy_lo; dy <= dy_hi; ++dy) {
-                    const uint32_t dx = p - dy * H;  // source pixel (dx, dy)
-                    uint32_t sq0, sst;
-                    ts_slot_base(dy, dx, W, rows, S, sq0, sst);
-                    const uint32_t q = sq0 + k * sst;
-                    const uint32_t key = s2[q].y;
-                    const uint64_t kp = ((uint64_t)key << 32) | (dy * W + dx);
-                    if (key != 0u && kp > prev && kp < best) {
-                        best = kp;
-                        best_slot = q;
+        auto add = [&](uint32_t w) {
+            const f3 c = decode_sample(a, w);
+            acc.x = acc.x + c.x;
+            acc.y = acc.y + c.y;
+            acc.z = acc.z + c.z;
+            acc.w = acc.w + 1.f;
+        };
+        constexpr uint32_t kSrc = 4;  // sources kept in registers (config 2's tiles: <= 2)
+        if (ns <= kSrc) {
+            // the sources' slot bases once; per sample their keys, added in (key, pixel)
+            // order (pixel order = dy order when W > H, reversed when W < H)
+            uint32_t sq[kSrc], sst[kSrc];
+#pragma unroll
+            for (uint32_t j = 0; j < kSrc; ++j) {
+                const uint32_t dy = j < ns ? dy_lo + j : dy_lo;
+                ts_slot_base(dy, p - dy * H, W, rows, S, sq[j], sst[j]);
+            }
+            const bool rev = W < H;
+            for (uint32_t k = 0; k < S; ++k) {
+                uint2 v[kSrc];
+#pragma unroll
+                for (uint32_t j = 0; j < kSrc; ++j) v[j] = j < ns ? s2[sq[j] + k * sst[j]] : make_uint2(0u, 0u);
+                uint32_t done = 0;  // sources already added (bit j)
+                for (uint32_t t = 0; t < ns; ++t) {
+                    uint32_t bj = kSrc, bk = 0, bw = 0;  // the next source: index, key, word
+#pragma unroll
+                    for (uint32_t j = 0; j < kSrc; ++j) {
+                        const bool cand = j < ns && v[j].y != 0u && !((done >> j) & 1u);
+                        const bool before = bj == kSrc || v[j].y < bk || (v[j].y == bk && rev);
+                        if (cand && before) {
+                            bj = j;
+                            bk = v[j].y;
+                            bw = v[j].x;
+                        }
                     }
+                    if (bj == kSrc) break;
+                    done |= 1u << bj;
+                    add(bw);
                 }
-                if (best == ~0ull) break;
-                const f3 c = decode_sample(a, s2[best_slot].x);
-                acc.x = acc.x + c.x;
-                acc.y = acc.y + c.y;
-                acc.z = acc.z + c.z;
-                acc.w = acc.w + 1.f;
-                prev = best;
+            }
+        } else {
+            for (uint32_t k = 0; k < S; ++k) {
+                uint64_t prev = 0;  // (key << 32 | pixel) of the last source added
+                for (uint32_t t = dy_lo; t <= dy_hi; ++t) {
+                    uint64_t best = ~0ull;
+                    uint32_t best_slot = 0;
+                    for (uint32_t dy = dy_lo; dy <= dy_hi; ++dy) {
+                        const uint32_t dx = p - dy * H;  // source pixel (dx, dy)
+                        uint32_t sq0, sst;
+                        ts_slot_base(dy, dx, W, rows, S, sq0, sst);
+                        const uint32_t q = sq0 + k * sst;
+                        const uint32_t key = s2[q].y;
+                        const uint64_t kp = ((uint64_t)key << 32) | (dy * W + dx);
+                        if (key != 0u && kp > prev && kp < best) {
+                            best = kp;
+                            best_slot = q;
+                        }
+                    }
+                    if (best == ~0ull) break;
+                    add(s2[best_slot].x);
+                    prev = best;
+                }
             }
         }
     }

@@ -560,6 +560,9 @@ __device__ __forceinline__ void update_member_lane(float tc, float hh, const uin
 #ifndef SPT_LANE_GROUP
 #define SPT_LANE_GROUP 2
 #endif
+#ifndef SPT_LANE_STEPS
+#define SPT_LANE_STEPS 1
+#endif
 // The lane walk as a resumable cast: `fresh` lanes start (winner none, node 0); the
 // others continue from their saved node, parked leaves and winner.  The always-list is
 // re-tested for every lane (idempotent: a sphere tested twice cannot replace itself --
@@ -650,8 +653,10 @@ __device__ __forceinline__ bool lane_cast(const AccelView &ac, const f3 &o, cons
             dg.nodes += (unsigned long long)__popcll(mt);
             dg.live += 1;
         }
-        if (tr) {
+        // one node step of the lane's own walk (lanes with a second parked leaf wait)
+        auto visit = [&]() {
             const uint4 ra = ln[2 * i], rb = ln[2 * i + 1];
+            const uint32_t nskip = rb.x, nslot = rb.y;
             const float ax = __builtin_fmaf(__uint_as_float(ra.x), irx, qlx);
             const float bx = __builtin_fmaf(__uint_as_float(ra.w), irx, qhx);
             const float ay = __builtin_fmaf(__uint_as_float(ra.y), iry, qly);
@@ -663,14 +668,22 @@ __device__ __forceinline__ bool lane_cast(const AccelView &ac, const f3 &o, cons
             const float tf = min3_raw(__builtin_fmaxf(ax, bx), __builtin_fmaxf(ay, by),
                                       min_raw(__builtin_fmaxf(az, bz), sbl));
             const bool hit = tn <= tf || nocull;
-            const bool is_leaf = rb.y != kNoSlot;
+            const bool is_leaf = nslot != kNoSlot;
             if (hit && is_leaf) {
                 if (leaf != kNoSlot)
-                    leaf2 = rb.y;
+                    leaf2 = nslot;
                 else
-                    leaf = rb.y;
+                    leaf = nslot;
             }
-            i = (hit && !is_leaf) ? i + 1 : rb.x;
+            i = (hit && !is_leaf) ? i + 1 : nskip;
+        };
+        if (tr) {
+            visit();
+            // SPT_LANE_STEPS node steps per walk iteration: the iteration's ballots,
+            // budget check and leaf-pass test are paid once per that many steps
+#pragma unroll
+            for (int k = 1; k < SPT_LANE_STEPS; ++k)
+                if (i < n && leaf2 == kNoSlot) visit();
         }
     }
     return !(i < n || leaf != kNoSlot);

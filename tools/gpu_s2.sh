@@ -16,5 +16,4 @@ for k in 2 3 4; do
   done
 done
 echo dropin-done
-[ -n "$PCS" ] && bash tools/pcsample.sh
 exit 0

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define SPT_ABI_VERSION 4
+#define SPT_ABI_VERSION 5
 
 /* Only the functions below are exported from libspt_hip.so (built with
  * -fvisibility=hidden), so several builds can be loaded side by side. */
@@ -260,8 +260,10 @@ SPT_API int spt_save_bmp(const char *path, uint32_t width, uint32_t height, uint
  * glibc's powf(a, 5) and powf(c, 5) restated, powf(a, 2), the refraction scalar
  * r*a - sqrt(1 - r*r*(1 - a*a)) (r = 1/1.5; -1e30 under total reflection), uniform(-1,1)
  * of bits, u8 of a, Normalize({a, b, c}) (3 floats), c/a, uniform(-0.5,0.5) and
- * uniform(0,1) of bits, with c the float whose bit pattern is bits. */
-#define SPT_SELFTEST_COLS 14
+ * uniform(0,1) of bits, with c the float whose bit pattern is bits; then c and a
+ * halved j times as the fold rebuilds a diffuse sample (j = (bits * 2654435761) >> 23
+ * mod 301; spt_kernels.hip halve_n). */
+#define SPT_SELFTEST_COLS 16
 SPT_API int spt_selftest_numerics(spt_ctx *ctx, const float *a, const float *b, const uint32_t *bits, uint32_t n,
                           float *out);
 

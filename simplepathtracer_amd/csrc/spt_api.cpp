@@ -167,6 +167,7 @@ struct spt_ctx {
     BatchSet bsets[kMaxBatchSets];
     uint32_t batch_sets = 2;  // batches in flight at once (SPT_BATCH_SETS)
     uint32_t batch_grid_div = 1;  // each batch launch takes 1/div of the grid (SPT_BATCH_GRID_DIV)
+    bool fold_to_host = true;     // batched folds write page-locked g_data in place (SPT_FOLD_HOST)
     std::condition_variable batch_cv;
     uint64_t batches = 0, batched_calls = 0;
 
@@ -787,7 +788,7 @@ int launch_batch(spt_ctx *ctx, BatchSet *bs, const std::vector<BatchReq *> &batc
         if (r->g_data) {
             b.rgb8 = ctx->d_frame8;
             const size_t fb = (size_t)W * H * 3;
-            for (const spt_ctx::Pinned &p : ctx->pinned) {
+            for (const spt_ctx::Pinned &p : ctx->fold_to_host ? ctx->pinned : std::vector<spt_ctx::Pinned>{}) {
                 const uint8_t *base = (const uint8_t *)p.ptr;
                 if (p.dev && r->g_data >= base && r->g_data + fb <= base + p.bytes) {
                     b.rgb8 = p.dev + (r->g_data - base);
@@ -1252,6 +1253,7 @@ int spt_ctx_create(int device, spt_ctx **out)
     if (const char *e = std::getenv("SPT_HOST_GRID_DIV")) ctx->host_grid_div = (uint32_t)std::max(0, std::atoi(e));
     if (const char *e = std::getenv("SPT_BATCH")) ctx->batching = std::atoi(e) != 0;
     if (const char *e = std::getenv("SPT_BATCH_DBUF")) ctx->batch_dbuf = std::atoi(e) != 0;
+    if (const char *e = std::getenv("SPT_FOLD_HOST")) ctx->fold_to_host = std::atoi(e) != 0;
     if (const char *e = std::getenv("SPT_BATCH_GRID_DIV")) ctx->batch_grid_div = (uint32_t)std::max(1, std::atoi(e));
     if (const char *e = std::getenv("SPT_BATCH_SETS"))
         ctx->batch_sets = (uint32_t)std::min<int>((int)kMaxBatchSets, std::max(1, std::atoi(e)));

@@ -593,6 +593,9 @@ __global__ void selftest_kernel(const float *a, const float *b, const uint32_t *
     o[11] = div_rn(c, x);
     o[12] = uniform_bits(bits[i], -0.5f, 0.5f);
     o[13] = uniform_bits(bits[i], 0.f, 1.f);
+    const uint32_t j = ((bits[i] * 2654435761u) >> 23) % 301u;  // halvings of a diffuse sample word
+    o[14] = halve_n(c, j);
+    o[15] = halve_n(x, j);
 }
 
 // Blocks per CU of the LDS tree variant and CUs of a device, queried once per device

@@ -115,6 +115,17 @@ def test_device_numerics_match_host(ctx, oracle):
         q = c / a
     same_or_nan(out[:, 8:11], want, "Normalize")
     same_or_nan(out[:, 11], q, "division over the full float range")
+    # the fold's rebuild of a diffuse sample: j halvings one by one (a denormal result
+    # rounds at every step), as the render loop applied them (SingleThreadPathTracer.hpp:31)
+    j = ((u.astype(np.uint64) * 2654435761) & 0xFFFFFFFF) >> 23
+    j = (j % 301).astype(np.int64)
+    hc, ha = c.copy(), a.copy()
+    with np.errstate(all="ignore"):
+        for k in range(301):
+            hc = np.where(k < j, hc * np.float32(0.5), hc).astype(np.float32)
+            ha = np.where(k < j, ha * np.float32(0.5), ha).astype(np.float32)
+    same_or_nan(out[:, 14], hc, "halvings over the full float range")
+    same_or_nan(out[:, 15], ha, "halvings")
 
 
 def same_or_nan(got, want, what):

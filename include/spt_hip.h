@@ -176,9 +176,10 @@ SPT_API int spt_render_segment(spt_ctx *ctx, uint32_t yBegin, uint32_t yEnd, uin
  * member 0 pulls the tiles over xGMI (peer copies), scatters them into the frame and
  * writes rgba_out (nullable, width*height float4, row-major) and g_data (nullable,
  * the reference layout).  Pixels are keyed per (pixel, sample), so the frame is
- * bit-identical for any member count.  Exception: in task mode a non-square frame
+ * bit-identical for any member count.  In task mode a non-square frame
  * (RenderImage's RenderSegmentTask({0, H, 0, W}) aliases pixels across rows,
- * TaskBasedPathTracer.hpp:103,186) renders on member 0 alone.  Blocking. */
+ * TaskBasedPathTracer.hpp:103,186) is split by ranges of its colorIndex instead: member
+ * r folds outputs [r L, (r + 1) L) from the rows holding their sources.  Blocking. */
 SPT_API int spt_render_frame(spt_ctx *ctx, int mode, float *rgba_out, uint8_t *g_data);
 /* Progressive RenderSegment / RenderSegmentTask (the preview of RenderImageParallelMain,
  * Renderer.hpp:257-302): the region is rendered in passes of pass_spp samples; after

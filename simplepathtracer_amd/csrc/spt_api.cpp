@@ -166,7 +166,10 @@ struct spt_ctx {
     bool batch_leader = false;  // a caller is assembling the next batch
     BatchSet bsets[kMaxBatchSets];
     uint32_t batch_sets = 2;  // batches in flight at once (SPT_BATCH_SETS)
-    uint32_t batch_grid_div = 1;  // each batch launch takes 1/div of the grid (SPT_BATCH_GRID_DIV)
+    // each batch launch takes 1/div of the grid (SPT_BATCH_GRID_DIV): two batches in flight
+    // then run side by side and each one's tail drains beside the other's blocks (config 2
+    // through the C++ shim at tc = 4: 7.93 -> 7.64 ms per frame, its folds 2x shorter)
+    uint32_t batch_grid_div = 2;
     bool fold_to_host = true;     // batched folds write page-locked g_data in place (SPT_FOLD_HOST)
     std::condition_variable batch_cv;
     uint64_t batches = 0, batched_calls = 0;
@@ -457,12 +460,38 @@ struct Progress {
     std::function<int(uint32_t)> after_pass;
 };
 
+// A range of RenderSegmentTask's colorIndex (spt_render_frame's split of a non-square
+// frame): outputs [i0, i0 + n) of a call of map.width x alias_h pixels, folded from the
+// rows the launch renders (FoldArgs::range_alias); d_rgba then holds n outputs.
+struct AliasRange {
+    uint32_t i0, n, alias_h;
+};
+
 // grid_div: concurrent host calls on this context share the GPU (render_grid)
 int render_impl(spt_ctx *ctx, int mode, const spt::RowMap &map, float4 *d_rgba, uint8_t *d_rgb8, hipStream_t s,
-                bool keep_samples, const Progress *pg = nullptr, uint32_t grid_div = 1)
+                bool keep_samples, const Progress *pg = nullptr, uint32_t grid_div = 1, const AliasRange *ar = nullptr)
 {
     const uint32_t rows = spt::rows_owned(map);
     const uint64_t npix64 = (uint64_t)rows * map.width;
+    if (npix64 == 0 && ar && ar->n) {
+        // a colorIndex range no pixel maps into: its outputs are 0 * (1.f / 0) = NaN
+        // (TaskBasedPathTracer.hpp:196-205); the fold writes them without sources
+        spt::FoldArgs fa = fold_args(ctx, nullptr, 2u);
+        fa.out_rgba = d_rgba;
+        fa.map = map;
+        fa.width = ctx->W;
+        fa.height = ctx->H;
+        fa.npix = ar->n;
+        fa.spp_batch = fa.spp_total = fa.s_done = ctx->spp;
+        fa.first = fa.last = 1;
+        fa.mode = mode;
+        fa.range_alias = 1;
+        fa.out_i0 = ar->i0;
+        fa.alias_h = ar->alias_h;
+        fa.src_rows = 0;
+        HIP_TRY(ctx, spt::launch_fold(fa, s));
+        return SPT_OK;
+    }
     if (npix64 == 0) return SPT_OK;
     if (npix64 > 0x7FFFFFFFull) return fail(ctx, SPT_ERR_ARG, "region too large (%llu pixels)", (unsigned long long)npix64);
     const uint32_t npix = (uint32_t)npix64;
@@ -480,7 +509,7 @@ int render_impl(spt_ctx *ctx, int mode, const spt::RowMap &map, float4 *d_rgba, 
     int rc = ensure(ctx, &w->d_samples, &w->samples_cap, items_max * slot_words);
     if (rc) return rc;
     if (spp_batch < ctx->spp) {
-        rc = ensure(ctx, &w->d_acc, &w->acc_cap, npix);
+        rc = ensure(ctx, &w->d_acc, &w->acc_cap, ar ? std::max(npix, ar->n) : npix);
         if (rc) return rc;
     }
     // several batches: odd batches render on the companion stream into its own
@@ -532,6 +561,15 @@ int render_impl(spt_ctx *ctx, int mode, const spt::RowMap &map, float4 *d_rgba, 
     fa.preview = pg ? 1 : 0;
     // one rectangle in task mode = one RenderSegmentTask call: its colorIndex aliasing
     fa.alias = mode == SPT_MODE_TASK && map.parts == 1u && rows != map.width ? 1 : 0;
+    if (ar) {
+        fa.range_alias = 1;
+        fa.alias = 0;
+        fa.npix = ar->n;
+        fa.out_i0 = ar->i0;
+        fa.alias_h = ar->alias_h;
+        fa.src_rows = rows;
+        fa.out_rgb8 = nullptr;
+    }
 
     uint32_t j = 0;
     for (uint32_t s0 = 0; s0 < ctx->spp; s0 += spp_batch, ++j) {
@@ -1243,7 +1281,7 @@ int spt_ctx_create(int device, spt_ctx **out)
     // kernels (MI355X_MICROARCH.md, Residency): the kernel needs no co-residency, so
     // extra blocks only queue.  SPT_BLOCKS_PER_CU overrides for tuning.
     if (const char *e = std::getenv("SPT_BLOCKS_PER_CU")) per_cu = std::max(1, std::atoi(e));
-    if (const char *e = std::getenv("SPT_CLAIM")) ctx->claim = (uint32_t)std::max(1, std::atoi(e));
+    if (const char *e = std::getenv("SPT_CLAIM")) ctx->claim = (uint32_t)std::max(0, std::atoi(e));  // 0 = per launch
     if (const char *e = std::getenv("SPT_CLUSTER_K")) ctx->cluster_k = (uint32_t)std::max(0, std::atoi(e));
     if (const char *e = std::getenv("SPT_TREE_B")) ctx->tree_branching = (uint32_t)std::max(0, std::atoi(e));
     if (const char *e = std::getenv("SPT_CLAIMS_PER_WAVE")) ctx->claims_per_wave = (uint32_t)std::max(1, std::atoi(e));
@@ -1506,17 +1544,20 @@ int spt_render_frame(spt_ctx *ctx, int mode, float *rgba_out, uint8_t *g_data)
         int rc = check_ready(ctx);
         if (rc) return rc;
         const uint32_t W = ctx->W, H = ctx->H;
-        // RenderImage's RenderSegmentTask({0, H, 0, W}) on a non-square frame aliases
-        // pixels across rows (colorIndex, TaskBasedPathTracer.hpp:103,186), which a
-        // row-strip split cannot resolve locally: that frame renders on member 0 alone
-        if (ctx->peers.empty() || (mode == SPT_MODE_TASK && W != H)) {
+        if (ctx->peers.empty()) {
             lk.unlock();
             return render_segment_host(ctx, mode, 0, H, 0, W, rgba_out, g_data, 0, nullptr, nullptr, false);
         }
     }
     // every member renders its interleaved row strips into a compact tile; member 0
     // pulls the tiles over xGMI (peer copies ordered after each member's render by an
-    // event), scatters them into the frame (assemble_kernel) and copies the frame back
+    // event), scatters them into the frame (assemble_kernel) and copies the frame back.
+    // RenderImage's RenderSegmentTask({0, H, 0, W}) on a non-square frame aliases pixels
+    // across rows (colorIndex = dx + dy * H, TaskBasedPathTracer.hpp:103,186,196-205), so
+    // a strip split cannot resolve it locally: there member r owns the colorIndex range
+    // [r L, (r + 1) L), renders the rows holding its sources (every row whose pixels map
+    // into the range: about L / W + W / H rows) and folds the range; the ranges are the
+    // frame's pixels in row-major order, so member 0 places them end to end.
     std::vector<spt_ctx *> m{ctx};
     m.insert(m.end(), ctx->peers.begin(), ctx->peers.end());
     const uint32_t parts = (uint32_t)m.size();
@@ -1529,9 +1570,16 @@ int spt_render_frame(spt_ctx *ctx, int mode, float *rgba_out, uint8_t *g_data)
     }
     const uint32_t W = ctx->W, H = ctx->H;
     const uint32_t strip = even_strip(H, parts);
+    const bool alias = mode == SPT_MODE_TASK && W != H;
+    const uint64_t total = (uint64_t)W * H;
+    const uint32_t L = (uint32_t)((total + parts - 1) / parts);  // colorIndex range per member (alias)
     uint32_t max_rows = 0;
     for (uint32_t r = 0; r < parts; ++r) max_rows = std::max(max_rows, spt::rows_owned(spt::RowMap{0, H, strip, parts, r, 0, W}));
-    const size_t tile = (size_t)max_rows * W;
+    const size_t tile = alias ? (size_t)L : (size_t)max_rows * W;
+    auto range_of = [&](uint32_t r) {
+        const uint64_t i0 = std::min<uint64_t>((uint64_t)r * L, total), i1 = std::min<uint64_t>(i0 + L, total);
+        return std::make_pair((uint32_t)i0, (uint32_t)i1);
+    };
     // member 0's buffers live on member 0's device: the setters (for_members) and the
     // previous frame leave another member's device current
     HIP_TRY(ctx, hipSetDevice(ctx->device));
@@ -1543,19 +1591,34 @@ int spt_render_frame(spt_ctx *ctx, int mode, float *rgba_out, uint8_t *g_data)
         HIP_TRY(ctx, hipSetDevice(c->device));
         if (r > 0 && (rc = ensure(c, &c->d_tile, &c->tile_cap, tile)))
             return fail(ctx, rc, "member device %d: %s", c->device, c->err.c_str());
-        spt::RowMap map{0, H, strip, parts, r, 0, W};
         float4 *dst = r == 0 ? ctx->d_tile : c->d_tile;
-        if ((rc = render_impl(c, mode, map, dst, nullptr, c->stream, false)))
-            return r == 0 ? rc : fail(ctx, rc, "member device %d: %s", c->device, c->err.c_str());
+        if (alias) {
+            const auto [i0, i1] = range_of(r);
+            if (i1 > i0) {
+                // the rows holding the range's sources: dx + dy H in [i0, i1), 0 <= dx < W
+                // (none when i0 >= (W - 1) + (H - 1) H + 1: an empty map, NaN outputs)
+                const uint32_t dy_lo = i0 >= W ? (i0 - W + H) / H : 0u, dy_hi = std::min(H - 1u, (i1 - 1u) / H);
+                const spt::RowMap map{std::min(dy_lo, H), std::max(std::min(dy_lo, H), dy_hi + 1u), 1u, 1u, 0u, 0u, W};
+                const AliasRange ar{i0, i1 - i0, H};
+                if ((rc = render_impl(c, mode, map, dst, nullptr, c->stream, false, nullptr, 1, &ar)))
+                    return r == 0 ? rc : fail(ctx, rc, "member device %d: %s", c->device, c->err.c_str());
+            }
+        } else {
+            spt::RowMap map{0, H, strip, parts, r, 0, W};
+            if ((rc = render_impl(c, mode, map, dst, nullptr, c->stream, false)))
+                return r == 0 ? rc : fail(ctx, rc, "member device %d: %s", c->device, c->err.c_str());
+        }
         if (r > 0) HIP_TRY(ctx, hipEventRecord(c->frame_ev, c->stream));
     }
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     for (uint32_t r = 1; r < parts; ++r) {
         spt_ctx *c = m[r];
-        const size_t rows_r = spt::rows_owned(spt::RowMap{0, H, strip, parts, r, 0, W});
+        const size_t n_r = alias ? (size_t)(range_of(r).second - range_of(r).first)
+                                 : (size_t)spt::rows_owned(spt::RowMap{0, H, strip, parts, r, 0, W}) * W;
         HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, c->frame_ev, 0));
-        HIP_TRY(ctx, hipMemcpyPeerAsync(ctx->d_tile + r * tile, ctx->device, c->d_tile, c->device,
-                                        rows_r * W * sizeof(float4), ctx->stream));
+        if (n_r)
+            HIP_TRY(ctx, hipMemcpyPeerAsync(ctx->d_tile + r * tile, ctx->device, c->d_tile, c->device,
+                                            n_r * sizeof(float4), ctx->stream));
     }
     float4 *dframe = nullptr;
     if (rgba_out) {
@@ -1569,8 +1632,13 @@ int spt_render_frame(spt_ctx *ctx, int mode, float *rgba_out, uint8_t *g_data)
         if ((rc = check_on_device(ctx, ctx->d_frame8, "g_data's device copy"))) return rc;
         d8 = ctx->d_frame8;
     }
-    HIP_TRY(ctx, spt::launch_assemble(ctx->d_tile, max_rows, spt::RowMap{0, H, strip, parts, 0u, 0, W}, W, H, dframe,
-                                      d8, ctx->stream));
+    // alias: the stack is the frame in row-major order (one part of H rows)
+    if (alias)
+        HIP_TRY(ctx, spt::launch_assemble(ctx->d_tile, H, spt::RowMap{0, H, 1u, 1u, 0u, 0, W}, W, H, dframe, d8,
+                                          ctx->stream));
+    else
+        HIP_TRY(ctx, spt::launch_assemble(ctx->d_tile, max_rows, spt::RowMap{0, H, strip, parts, 0u, 0, W}, W, H,
+                                          dframe, d8, ctx->stream));
     if (rgba_out)
         HIP_TRY(ctx, hipMemcpyAsync(rgba_out, dframe, (size_t)W * H * sizeof(float4), hipMemcpyDeviceToHost, ctx->stream));
     if (g_data) HIP_TRY(ctx, hipMemcpyAsync(g_data, d8, (size_t)W * H * 3, hipMemcpyDeviceToHost, ctx->stream));

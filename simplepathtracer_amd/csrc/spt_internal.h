@@ -303,6 +303,11 @@ struct FoldArgs {
                          // (dx + dy * segmentHeight, TaskBasedPathTracer.hpp:103,186) aliases pixels
     const BatchRect *rects;  // batched fold: n_rects rectangles over npix = their total pixels
     uint32_t n_rects;        // (map and alias per rectangle; spp_batch = spp_total, first = last = 1)
+    // range alias fold (spt_render_frame: RenderSegmentTask over a non-square frame split
+    // over several devices by ranges of its colorIndex): the npix outputs are the alias
+    // indices [out_i0, out_i0 + npix) of a call of map.width x alias_h pixels, whose source
+    // pixels' slots are those of the launch's rows (map: rows [map.y0, map.y0 + src_rows))
+    uint32_t range_alias, out_i0, alias_h, src_rows;
 };
 
 // Launch geometry of one render launch: the context's persistent grid for the

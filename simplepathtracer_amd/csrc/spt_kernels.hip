@@ -364,6 +364,86 @@ __device__ __forceinline__ f3 decode_sample(const FoldArgs &a, uint32_t w)
     return mk(halve_n(sh.x * 0.5f, j), halve_n(sh.y * 0.5f, j), halve_n(sh.z * 0.5f, j));
 }
 
+// RenderSegmentTask's colorIndex aliasing (TaskBasedPathTracer.hpp:103,186,196-205) for
+// output index p of a W x H call: colors[p] collects every pixel (dx, dy) of the call with
+// dx + dy * H == p, and the resolve writes colors[p] to pixel (p % W, p / W).  Within a
+// sample the sources reach colors[p] in the order of their (key, pixel) (finish_step), so
+// each sample's sources are added in that order.  No source: 0 samples, and 0 * (1.f / 0)
+// is NaN, as in the reference.  The sources' slots are those of rows [row0, row0 + rows)
+// of the launch (the call's own rows, or a range of them: spt_render_frame).
+__device__ __forceinline__ void alias_accumulate(const FoldArgs &a, const uint32_t *samples, uint32_t p, uint32_t W,
+                                                 uint32_t H, uint32_t row0, uint32_t rows, uint32_t S, float4 &acc)
+{
+    const uint32_t dy_lo = p >= W ? (p - W + H) / H : 0u;
+    const uint32_t dy_hi = min(H - 1u, p / H);
+    const uint32_t ns = dy_hi + 1u - dy_lo;  // sources: pixels (p - dy H, dy)
+    const uint2 *s2 = (const uint2 *)samples;
+    auto add = [&](uint32_t w) {
+        const f3 c = decode_sample(a, w);
+        acc.x = acc.x + c.x;
+        acc.y = acc.y + c.y;
+        acc.z = acc.z + c.z;
+        acc.w = acc.w + 1.f;
+    };
+    constexpr uint32_t kSrc = 4;  // sources kept in registers (config 2's tiles: <= 2)
+    if (ns <= kSrc) {
+        // the sources' slot bases once; per sample their keys, added in (key, pixel)
+        // order (pixel order = dy order when W > H, reversed when W < H)
+        uint32_t sq[kSrc], sst[kSrc];
+#pragma unroll
+        for (uint32_t j = 0; j < kSrc; ++j) {
+            const uint32_t dy = j < ns ? dy_lo + j : dy_lo;
+            ts_slot_base(dy - row0, p - dy * H, W, rows, S, sq[j], sst[j]);
+        }
+        const bool rev = W < H;
+        for (uint32_t k = 0; k < S; ++k) {
+            uint2 v[kSrc];
+#pragma unroll
+            for (uint32_t j = 0; j < kSrc; ++j) v[j] = j < ns ? s2[sq[j] + k * sst[j]] : make_uint2(0u, 0u);
+            uint32_t done = 0;  // sources already added (bit j)
+            for (uint32_t t = 0; t < ns; ++t) {
+                uint32_t bj = kSrc, bk = 0, bw = 0;  // the next source: index, key, word
+#pragma unroll
+                for (uint32_t j = 0; j < kSrc; ++j) {
+                    const bool cand = j < ns && v[j].y != 0u && !((done >> j) & 1u);
+                    const bool before = bj == kSrc || v[j].y < bk || (v[j].y == bk && rev);
+                    if (cand && before) {
+                        bj = j;
+                        bk = v[j].y;
+                        bw = v[j].x;
+                    }
+                }
+                if (bj == kSrc) break;
+                done |= 1u << bj;
+                add(bw);
+            }
+        }
+    } else {
+        for (uint32_t k = 0; k < S; ++k) {
+            uint64_t prev = 0;  // (key << 32 | pixel) of the last source added
+            for (uint32_t t = dy_lo; t <= dy_hi; ++t) {
+                uint64_t best = ~0ull;
+                uint32_t best_slot = 0;
+                for (uint32_t dy = dy_lo; dy <= dy_hi; ++dy) {
+                    const uint32_t dx = p - dy * H;  // source pixel (dx, dy)
+                    uint32_t sq0, sst;
+                    ts_slot_base(dy - row0, dx, W, rows, S, sq0, sst);
+                    const uint32_t q = sq0 + k * sst;
+                    const uint32_t key = s2[q].y;
+                    const uint64_t kp = ((uint64_t)key << 32) | (dy * W + dx);
+                    if (key != 0u && kp > prev && kp < best) {
+                        best = kp;
+                        best_slot = q;
+                    }
+                }
+                if (best == ~0ull) break;
+                add(s2[best_slot].x);
+                prev = best;
+            }
+        }
+    }
+}
+
 // RenderSegment's / RenderSegmentTask's resolve of local pixel (lr, col) of a region
 // (map, `rows` rows, alias: task mode on a non-square tile) whose slots start at
 // `samples` (item order of a batch of a.spp_batch samples: ts_slot_base); local float4
@@ -400,81 +480,7 @@ __device__ __forceinline__ void fold_pixel(const FoldArgs &a, const uint32_t *sa
             }
         }
     } else {
-        // Non-square tile: colors[p] collects every pixel (dx, dy) of the tile with
-        // dx + dy * H == p (TaskBasedPathTracer.hpp:103,186; H = segmentHeight), and the
-        // resolve (196-205) writes colors[p] to pixel (p % W, p / W).  Within a sample
-        // the sources reach colors[p] in the order of their (key, pixel) (finish_step),
-        // so each sample's sources are added in that order.  No source: 0 samples, and
-        // 0 * (1.f / 0) is NaN, as in the reference.
-        const uint32_t H = rows;
-        const uint32_t dy_lo = p >= W ? (p - W + H) / H : 0u;
-        const uint32_t dy_hi = min(H - 1u, p / H);
-        const uint32_t ns = dy_hi + 1u - dy_lo;  // sources: pixels (p - dy H, dy)
-        const uint2 *s2 = (const uint2 *)samples;
-        auto add = [&](uint32_t w) {
-            const f3 c = decode_sample(a, w);
-            acc.x = acc.x + c.x;
-            acc.y = acc.y + c.y;
-            acc.z = acc.z + c.z;
-            acc.w = acc.w + 1.f;
-        };
-        constexpr uint32_t kSrc = 4;  // sources kept in registers (config 2's tiles: <= 2)
-        if (ns <= kSrc) {
-            // the sources' slot bases once; per sample their keys, added in (key, pixel)
-            // order (pixel order = dy order when W > H, reversed when W < H)
-            uint32_t sq[kSrc], sst[kSrc];
-#pragma unroll
-            for (uint32_t j = 0; j < kSrc; ++j) {
-                const uint32_t dy = j < ns ? dy_lo + j : dy_lo;
-                ts_slot_base(dy, p - dy * H, W, rows, S, sq[j], sst[j]);
-            }
-            const bool rev = W < H;
-            for (uint32_t k = 0; k < S; ++k) {
-                uint2 v[kSrc];
-#pragma unroll
-                for (uint32_t j = 0; j < kSrc; ++j) v[j] = j < ns ? s2[sq[j] + k * sst[j]] : make_uint2(0u, 0u);
-                uint32_t done = 0;  // sources already added (bit j)
-                for (uint32_t t = 0; t < ns; ++t) {
-                    uint32_t bj = kSrc, bk = 0, bw = 0;  // the next source: index, key, word
-#pragma unroll
-                    for (uint32_t j = 0; j < kSrc; ++j) {
-                        const bool cand = j < ns && v[j].y != 0u && !((done >> j) & 1u);
-                        const bool before = bj == kSrc || v[j].y < bk || (v[j].y == bk && rev);
-                        if (cand && before) {
-                            bj = j;
-                            bk = v[j].y;
-                            bw = v[j].x;
-                        }
-                    }
-                    if (bj == kSrc) break;
-                    done |= 1u << bj;
-                    add(bw);
-                }
-            }
-        } else {
-            for (uint32_t k = 0; k < S; ++k) {
-                uint64_t prev = 0;  // (key << 32 | pixel) of the last source added
-                for (uint32_t t = dy_lo; t <= dy_hi; ++t) {
-                    uint64_t best = ~0ull;
-                    uint32_t best_slot = 0;
-                    for (uint32_t dy = dy_lo; dy <= dy_hi; ++dy) {
-                        const uint32_t dx = p - dy * H;  // source pixel (dx, dy)
-                        uint32_t sq0, sst;
-                        ts_slot_base(dy, dx, W, rows, S, sq0, sst);
-                        const uint32_t q = sq0 + k * sst;
-                        const uint32_t key = s2[q].y;
-                        const uint64_t kp = ((uint64_t)key << 32) | (dy * W + dx);
-                        if (key != 0u && kp > prev && kp < best) {
-                            best = kp;
-                            best_slot = q;
-                        }
-                    }
-                    if (best == ~0ull) break;
-                    add(s2[best_slot].x);
-                    prev = best;
-                }
-            }
-        }
+        alias_accumulate(a, samples, p, W, rows, 0u, rows, S, acc);
     }
     if (!a.last) {
         a.acc[p] = acc;
@@ -506,6 +512,22 @@ __global__ __launch_bounds__(256) void fold_kernel(FoldArgs a)
     uint32_t lr, col;
     tile_pixel(i, a.map.width, rows, lr, col);
     fold_pixel(a, a.samples, a.map, rows, a.alias, lr, col, a.out_rgba, a.out_rgb8);
+}
+
+// Range alias fold (FoldArgs::range_alias): output t is alias index out_i0 + t, local
+// float4 output at out_rgba[t] (g_data is written by the assemble step).
+__global__ __launch_bounds__(256) void fold_alias_range_kernel(FoldArgs a)
+{
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= a.npix) return;
+    float4 acc = a.first ? make_float4(0.f, 0.f, 0.f, 0.f) : a.acc[t];
+    alias_accumulate(a, a.samples, a.out_i0 + t, a.map.width, a.alias_h, a.map.y0, a.src_rows, a.spp_batch, acc);
+    if (!a.last) {
+        a.acc[t] = acc;
+        if (!a.preview) return;
+    }
+    const float scale = 1.f / acc.w;
+    if (a.out_rgba) a.out_rgba[t] = make_float4(acc.x * scale, acc.y * scale, acc.z * scale, 0.f);
 }
 
 // The rectangle of pixel i of a batched fold (FoldArgs::rects).
@@ -675,7 +697,9 @@ hipError_t launch_render(const RenderArgs &a, LaunchShape &sh, hipStream_t s)
 hipError_t launch_fold(const FoldArgs &a, hipStream_t s)
 {
     if (a.npix == 0) return hipSuccess;
-    if (a.rects)
+    if (a.range_alias)
+        hipLaunchKernelGGL(fold_alias_range_kernel, dim3((a.npix + 255) / 256), dim3(256), 0, s, a);
+    else if (a.rects)
         hipLaunchKernelGGL(fold_kernel_batch, dim3((a.npix + 255) / 256), dim3(256), 0, s, a);
     else
         hipLaunchKernelGGL(fold_kernel, dim3((a.npix + 255) / 256), dim3(256), 0, s, a);

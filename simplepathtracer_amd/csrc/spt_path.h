@@ -555,7 +555,7 @@ __device__ __forceinline__ void update_member_lane(float tc, float hh, const uin
 // SPT_DIAG counters here: nodes = lane node visits, live = walk iterations, leaves =
 // leaf passes, pairs = (lane, leaf) tests.
 #ifndef SPT_LANE_LEAF_T
-#define SPT_LANE_LEAF_T 64
+#define SPT_LANE_LEAF_T 24
 #endif
 #ifndef SPT_LANE_GROUP
 #define SPT_LANE_GROUP 2

@@ -750,12 +750,16 @@ def test_config3_full_frame_batches_vs_oracle(spt, ctx, oracle, golden_scenes):
 
 # ---------------------------------------------------------------- multi-device context
 
-@pytest.mark.parametrize("devices,task", [([0, 0], False), ([0, 0, 0], False), ([0, 0], True)])
-def test_multi_device_frame_equals_one_device(spt, golden_scenes, devices, task):
+@pytest.mark.parametrize("devices,task,W,H", [([0, 0], False, 360, 200), ([0, 0, 0], False, 360, 200),
+                                             ([0, 0], True, 360, 200), ([0, 0, 0], True, 360, 200),
+                                             ([0, 0, 0], True, 96, 250), ([0, 0], True, 64, 64)])
+def test_multi_device_frame_equals_one_device(spt, golden_scenes, devices, task, W, H):
     """spt_render_frame over a device list (one process driving
     several GPUs; here device 0 listed several times): interleaved strips per member,
-    peer-copy gather to member 0, assemble -- bit-identical to a one-device frame."""
-    W, H, spp = 360, 200, 6
+    peer-copy gather to member 0, assemble -- bit-identical to a one-device frame.  Task
+    mode on a non-square frame (RenderImage's aliased RenderSegmentTask) is split by
+    colorIndex ranges instead (wide and tall frames; NaN pixels where no source maps)."""
+    spp = 6
     one = spt.Context(0)
     setup(one, scene_from(spt, golden_scenes, "random"), W, H, spp, 50)
     g1 = np.zeros(W * H * 3, np.uint8)
@@ -772,8 +776,14 @@ def test_multi_device_frame_equals_one_device(spt, golden_scenes, devices, task)
     multi.close()
     same_bits_or_nan(got[:, :3], want[:, :3], f"{len(devices)} members")
     assert np.array_equal(gm, g1)
-    # task mode on a non-square frame aliases across rows: member 0 renders it alone
-    assert st["samples"] == W * H * spp and st["launches"] == (1 if task else len(devices))
+    if task and W != H:
+        # a member whose colorIndex range no pixel maps into only writes NaN (no render)
+        assert 1 <= st["launches"] <= len(devices)
+        # each member renders the rows holding its colorIndex range's sources (a tall
+        # frame's rows dy >= W hold none: dx + dy H >= W H is never resolved)
+        assert 0 < st["samples"] <= 2 * W * H * spp
+    else:
+        assert st["launches"] == len(devices) and st["samples"] == W * H * spp
 
 
 def test_multi_device_context_serves_render_jobs(spt, golden_scenes):

@@ -17,6 +17,9 @@
 #ifndef SPT_DIAG
 #define SPT_DIAG 0
 #endif
+#ifndef SPT_LEAF_SPLIT
+#define SPT_LEAF_SPLIT 0
+#endif
 
 // 1: the megakernel's start_path reads its parameters from the kernarg segment
 // where used instead of holding them in SGPRs (with the SGPR cap of
@@ -277,10 +280,21 @@ __device__ __forceinline__ void test_leaf(cfloat *slots, const uint32_t *__restr
                                           const f3 &o, const f3 &d, float dod, Hit &h, CastDiag &dg)
 {
     cfloat *cs = slots + 4 * leaf_slot;
+#if SPT_LEAF_SPLIT
+    // SPT_LEAF_SPLIT: the members in groups of four (16 SGPRs at a time instead of 32)
+#pragma unroll
+    for (int g = 0; g < S; g += 4) {
+        float4 ms[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) ms[k] = ld_uniform(cs, g + k);
+        test_group<4>(ms, orig, leaf_slot + g, o, d, dod, h, dg);
+    }
+#else
     float4 ms[S];
 #pragma unroll
     for (int k = 0; k < S; ++k) ms[k] = ld_uniform(cs, k);
     test_group<S>(ms, orig, leaf_slot, o, d, dod, h, dg);
+#endif
 }
 
 // Leaf test behind the member pretest: the S slots plus their S pretest constants.

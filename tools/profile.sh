@@ -37,6 +37,7 @@ for group in "SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES SQ_INSTS_SMEM" \
   i=$((i + 1))
   step pmc$i 0 120 rocprofv3 --pmc $group --output-format csv -d "$OUT/pmc$i" -o run -- python3 "$R/bench.py" $ARGS
 done
-make -s -C "$R/simplepathtracer_amd/csrc" diag > "$OUT/diag_build.log" 2>&1 || exit 3
+# the SPT_DIAG library is built beforehand on the build host (make -C simplepathtracer_amd/csrc diag)
+[ -f "$R/simplepathtracer_amd/lib/libspt_hip_diag.so" ] || { echo "missing libspt_hip_diag.so"; exit 3; }
 SPT_LIB=libspt_hip_diag.so step diag 1 300 python3 "$R/tools/diag.py" "$CFG" --json "$OUT/diag.json"
 find "$OUT" -name "*.csv" | head -40

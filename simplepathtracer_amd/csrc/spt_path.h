@@ -18,7 +18,7 @@
 #define SPT_DIAG 0
 #endif
 #ifndef SPT_LEAF_SPLIT
-#define SPT_LEAF_SPLIT 0
+#define SPT_LEAF_SPLIT 1
 #endif
 
 // 1: the megakernel's start_path reads its parameters from the kernarg segment
@@ -281,7 +281,8 @@ __device__ __forceinline__ void test_leaf(cfloat *slots, const uint32_t *__restr
 {
     cfloat *cs = slots + 4 * leaf_slot;
 #if SPT_LEAF_SPLIT
-    // SPT_LEAF_SPLIT: the members in groups of four (16 SGPRs at a time instead of 32)
+    // SPT_LEAF_SPLIT: the members in groups of four (16 SGPRs at a time instead of 32;
+    // SGPR spills 22 -> 13; config 2 5.61 -> 5.57 ms, a config-3 sample 7.20 -> 7.05 ms)
 #pragma unroll
     for (int g = 0; g < S; g += 4) {
         float4 ms[4];

@@ -89,6 +89,49 @@ constexpr uint32_t kGlaneMaxNodes = SPT_GLANE_MAX_NODES;
 #ifndef SPT_LANE_WALK
 #define SPT_LANE_WALK 1
 #endif
+// 1: the wave-walk kernels start paths in primary batches (render_body, PRIM): 64 new
+// paths at a time, all 64 lanes, cast and shaded once together, the survivors parked
+// in a per-wave LDS queue that refills idle lanes
+#ifndef SPT_PRIM
+#define SPT_PRIM 1
+#endif
+// idle lanes needed before a refill from the primary queue (the queue's pops are cheap;
+// SPT_REFILL_MIN rules the kernels without it)
+#ifndef SPT_PRIM_REFILL_MIN
+#define SPT_PRIM_REFILL_MIN 8
+#endif
+
+// A path parked in LDS (the primary queue of render_body): 12 words, structure of arrays
+// over the wave's 64 rows (conflict-free b32 accesses).  Fields: item, st (2), o (3), d (3),
+// slot, bounce, phase | spec << 2.
+constexpr uint32_t kParkWords = 12;
+__device__ __forceinline__ void park_path(uint32_t *q, uint32_t row, const Path &ps)
+{
+    q[0 * 64 + row] = ps.item;
+    q[1 * 64 + row] = (uint32_t)ps.st;
+    q[2 * 64 + row] = (uint32_t)(ps.st >> 32);
+    q[3 * 64 + row] = __float_as_uint(ps.o.x);
+    q[4 * 64 + row] = __float_as_uint(ps.o.y);
+    q[5 * 64 + row] = __float_as_uint(ps.o.z);
+    q[6 * 64 + row] = __float_as_uint(ps.d.x);
+    q[7 * 64 + row] = __float_as_uint(ps.d.y);
+    q[8 * 64 + row] = __float_as_uint(ps.d.z);
+    q[9 * 64 + row] = ps.slot;
+    q[10 * 64 + row] = ps.bounce;
+    q[11 * 64 + row] = ps.phase | (ps.spec << 2);
+}
+__device__ __forceinline__ void unpark_path(const uint32_t *q, uint32_t row, Path &ps)
+{
+    ps.item = q[0 * 64 + row];
+    ps.st = (uint64_t)q[1 * 64 + row] | ((uint64_t)q[2 * 64 + row] << 32);
+    ps.o = mk(__uint_as_float(q[3 * 64 + row]), __uint_as_float(q[4 * 64 + row]), __uint_as_float(q[5 * 64 + row]));
+    ps.d = mk(__uint_as_float(q[6 * 64 + row]), __uint_as_float(q[7 * 64 + row]), __uint_as_float(q[8 * 64 + row]));
+    ps.slot = q[9 * 64 + row];
+    ps.bounce = q[10 * 64 + row];
+    const uint32_t w = q[11 * 64 + row];
+    ps.phase = w & 3u;
+    ps.spec = w >> 2;
+}
 
 // One kernel per traversal shape (flat list of 4- or 8-slot leaves, tree of
 // 8-slot leaves), each with its own register allocation; launch_render picks.
@@ -124,6 +167,19 @@ __device__ __forceinline__ void render_body(const RenderArgs &a)
 
     __shared__ uint32_t s_lds[BLOCK];  // wave-private scratch of the cooperative sampler
     __shared__ uint4 s_nodes[LDSN ? 2 * kLdsNodeRecords : 1];
+    // Primary batches (SPT_PRIM; the wave walk of a single launch): when idle lanes want
+    // more paths than the wave's queue holds, every lane parks its own path in the queue
+    // rows, takes a NEW item (64 consecutive items: one sample of one 8x8 tile) and the
+    // wave runs one ordinary iteration -- cast + shading step -- over those 64 primary
+    // rays; then each lane takes its own path back and the survivors (paths not finished
+    // by their first shading step) fill the queue, from which idle lanes are refilled.
+    // The primary cast is one coherent bundle from the eye (the wave walk's union of
+    // leaves is about a single ray's), and every path enters the main loop one cast in.
+    // Per path the arithmetic and its order are unchanged: bit-identical frames.
+    constexpr bool PRIM = SPT_PRIM && !BATCH && !LDSN && !GLANE;
+    __shared__ uint32_t s_park[PRIM ? (BLOCK / 64u) * kParkWords * 64u : 1];
+    uint32_t *const park = s_park + (PRIM ? (threadIdx.x >> 6) * kParkWords * 64u : 0u);
+    uint32_t q_n = 0, q_pos = 0;  // the wave's queue: rows [q_pos, q_n) hold parked paths
     if (LDSN) {
         // the host launches this variant only when n_nodes + 1 <= kLdsNodeRecords
         const uint4 *src = (const uint4 *)a.scene.accel.nodes;
@@ -174,14 +230,62 @@ __device__ __forceinline__ void render_body(const RenderArgs &a)
     } while (0)
 #endif
 
+    // items of the launch for the lanes of `need` (ballot + prefix rank over the current
+    // claim, then the claim in flight); 0xFFFFFFFF for lanes that get none
+    auto take_items = [&](unsigned long long need) -> uint32_t {
+        const uint32_t cnt = (uint32_t)__popcll(need);
+        const uint32_t rank = lane_rank(need);
+        const uint32_t avail = blk_end - blk_cur;
+        uint32_t mine = 0xFFFFFFFFu;
+        if (rank < avail) mine = blk_cur + rank;
+        if (avail >= cnt) {
+            blk_cur += cnt;
+        } else {
+            // switch to the claim in flight and put the next one in flight
+            const uint32_t nb = __builtin_amdgcn_readfirstlane(pend);
+            if (nb < a.n_items && lane == 0) pend = claim_next(a, home, qi);
+            if (nb >= a.n_items) {
+                exhausted = true;
+                blk_cur = blk_end = 0;
+            } else {
+                const uint32_t ne = min(nb + a.claim, a.n_items);
+                const uint32_t r2 = rank - avail;
+                if (rank >= avail && r2 < ne - nb) mine = nb + r2;
+                blk_cur = nb + min(cnt - avail, ne - nb);
+                blk_end = ne;
+            }
+        }
+        return ((need >> lane) & 1ull) ? mine : 0xFFFFFFFFu;
+    };
+
     for (;;) {
         // ---- refill: hand out (pixel, sample) items to idle lanes (ballot + prefix)
         // idle lanes wait until SPT_REFILL_MIN of them (or the whole wave) can be
         // refilled together: the refill's primary-ray code then runs a quarter as
         // often for ~4 more idle lanes per iteration (config 2 -2%, config 5 -1.5%)
         unsigned long long need = __ballot(ps.phase == PH_IDLE);
-        if (__popcll(need) < SPT_REFILL_MIN && need != ~0ull) need = 0ull;
-        if (BATCH && need != 0ull && !exhausted) {
+        if (__popcll(need) < (PRIM ? SPT_PRIM_REFILL_MIN : SPT_REFILL_MIN) && need != ~0ull) need = 0ull;
+        bool prim_iter = false;  // PRIM: this iteration runs a primary batch
+        if (PRIM) {
+            if (need != 0ull) {
+                const uint32_t cnt = (uint32_t)__popcll(need);
+                const uint32_t rank = lane_rank(need);
+                const uint32_t take = min(cnt, q_n - q_pos);
+                if (ps.phase == PH_IDLE && rank < take) unpark_path(park, q_pos + rank, ps);
+                q_pos += take;
+                if (cnt > take && !exhausted) {
+                    // the queue is empty: park every lane's own path in its own row and
+                    // start 64 new paths (wave-uniform)
+                    park_path(park, lane, ps);
+                    // the own path lives in LDS across the batch, not in registers
+                    asm volatile("" ::: "memory");
+                    const uint32_t mine = take_items(~0ull);
+                    ps.phase = PH_IDLE;
+                    if (mine != 0xFFFFFFFFu) start_path_kernarg(mine, rows, ps);
+                    prim_iter = true;
+                }
+            }
+        } else if (BATCH && need != 0ull && !exhausted) {
             if (blk_cur == blk_end) {
                 // the claim in flight becomes current, the next one goes in flight
                 const uint32_t nb = __builtin_amdgcn_readfirstlane(pend);
@@ -202,33 +306,18 @@ __device__ __forceinline__ void render_body(const RenderArgs &a)
                 if (ps.phase == PH_IDLE && rank < take) start_path_rect(mine, rect, ps);
             }
         } else if (!BATCH && need != 0ull && !exhausted) {
-            const uint32_t cnt = (uint32_t)__popcll(need);
-            const uint32_t rank = lane_rank(need);
-            const uint32_t avail = blk_end - blk_cur;
-            uint32_t mine = 0xFFFFFFFFu;
-            if (rank < avail) mine = blk_cur + rank;
-            if (avail >= cnt) {
-                blk_cur += cnt;
-            } else {
-                // switch to the claim in flight and put the next one in flight
-                const uint32_t nb = __builtin_amdgcn_readfirstlane(pend);
-                if (nb < a.n_items && lane == 0) pend = claim_next(a, home, qi);
-                if (nb >= a.n_items) {
-                    exhausted = true;
-                    blk_cur = blk_end = 0;
-                } else {
-                    const uint32_t ne = min(nb + a.claim, a.n_items);
-                    const uint32_t r2 = rank - avail;
-                    if (rank >= avail && r2 < ne - nb) mine = nb + r2;
-                    blk_cur = nb + min(cnt - avail, ne - nb);
-                    blk_end = ne;
-                }
-            }
-            if (ps.phase == PH_IDLE && mine != 0xFFFFFFFFu) start_path_kernarg(mine, rows, ps);
+            const uint32_t mine = take_items(need);
+            if (mine != 0xFFFFFFFFu) start_path_kernarg(mine, rows, ps);
         }
         const unsigned long long live = __ballot(ps.phase != PH_IDLE);
         if (live == 0ull) {
-            if (exhausted) break;
+            if (PRIM && prim_iter) {
+                // no item was left for the batch: the lanes' own paths back
+                unpark_path(park, lane, ps);
+                q_n = q_pos = 0;
+                continue;
+            }
+            if (exhausted && q_pos == q_n) break;
             continue;
         }
         SPT_STAMP(dc.refill);
@@ -260,6 +349,19 @@ __device__ __forceinline__ void render_body(const RenderArgs &a)
         SPT_STAMP(dc.cast);
         shade_step<true>(a, ps, h, act && cdone, done, dropped, s_lds + (threadIdx.x & ~63u));
         fresh = cdone;
+        if (PRIM && prim_iter) {
+            // the lane's own path back from its row, then the batch's survivors into
+            // rows [0, n) of the queue (a lane writes row rank <= lane, after the whole
+            // wave has read its own row: LDS operations of a wave complete in order)
+            Path own;
+            unpark_path(park, lane, own);
+            __builtin_amdgcn_wave_barrier();
+            const unsigned long long lv = __ballot(ps.phase != PH_IDLE);
+            if (ps.phase != PH_IDLE) park_path(park, lane_rank(lv), ps);
+            ps = own;
+            q_n = (uint32_t)__popcll(lv);
+            q_pos = 0;
+        }
         SPT_STAMP(dc.shade);
     }
 
@@ -364,6 +466,30 @@ __device__ __forceinline__ f3 decode_sample(const FoldArgs &a, uint32_t w)
     return mk(halve_n(sh.x * 0.5f, j), halve_n(sh.y * 0.5f, j), halve_n(sh.z * 0.5f, j));
 }
 
+// decode_sample for a run of words without branches around the loads: the shading-table
+// reads of all N words are issued together (slot 0 stands in for sky and zero words), the
+// colours selected afterwards; only denormal halvings (halve_n's slow path) branch.
+template <int N>
+__device__ __forceinline__ void decode_run(const FoldArgs &a, const uint32_t (&w)[N], f3 (&col)[N])
+{
+    uint32_t c[N], j[N];
+    float4 sh[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        c[i] = word_code(w[i]);
+        const uint32_t v = c[i] >= 2u ? c[i] - 2u : 0u;
+        j[i] = v >> a.code_shift;
+        sh[i] = a.shade[v & ((1u << a.code_shift) - 1u)];
+    }
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        const float k = __uint_as_float(w[i]);
+        const f3 s = mul(mk(a.sky[0] * k, a.sky[1] * k, a.sky[2] * k), 0.5f);
+        const f3 d = mk(halve_n(sh[i].x * 0.5f, j[i]), halve_n(sh[i].y * 0.5f, j[i]), halve_n(sh[i].z * 0.5f, j[i]));
+        col[i] = c[i] == 0u ? s : c[i] == 1u ? mk(0.f, 0.f, 0.f) : d;
+    }
+}
+
 // RenderSegmentTask's colorIndex aliasing (TaskBasedPathTracer.hpp:103,186,196-205) for
 // output index p of a W x H call: colors[p] collects every pixel (dx, dy) of the call with
 // dx + dy * H == p, and the resolve writes colors[p] to pixel (p % W, p / W).  Within a
@@ -458,8 +584,25 @@ __device__ __forceinline__ void fold_pixel(const FoldArgs &a, const uint32_t *sa
     uint32_t q0, step;
     ts_slot_base(lr, col, W, rows, S, q0, step);
     if (a.mode == 0) {
-        // RenderSegment: one word per slot, every sample counts
-        for (uint32_t k = 0; k < S; ++k) {
+        // RenderSegment: one word per slot, every sample counts.  Runs of kFoldRun words
+        // are loaded before any is decoded (the loads of a run are in flight together)
+        constexpr int kFoldRun = 8;
+        uint32_t k = 0;
+        for (; k + kFoldRun <= S; k += kFoldRun) {
+            uint32_t w[kFoldRun];
+#pragma unroll
+            for (int i = 0; i < kFoldRun; ++i) w[i] = samples[q0 + (k + i) * step];
+            f3 c[kFoldRun];
+            decode_run<kFoldRun>(a, w, c);
+#pragma unroll
+            for (int i = 0; i < kFoldRun; ++i) {
+                acc.x = acc.x + c[i].x;
+                acc.y = acc.y + c[i].y;
+                acc.z = acc.z + c[i].z;
+                acc.w = acc.w + 1.f;
+            }
+        }
+        for (; k < S; ++k) {
             const f3 c = decode_sample(a, samples[q0 + k * step]);
             acc.x = acc.x + c.x;
             acc.y = acc.y + c.y;

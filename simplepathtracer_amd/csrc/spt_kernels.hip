@@ -167,7 +167,7 @@ __device__ __forceinline__ void render_body(const RenderArgs &a)
 
     __shared__ uint32_t s_lds[BLOCK];  // wave-private scratch of the cooperative sampler
     __shared__ uint4 s_nodes[LDSN ? 2 * kLdsNodeRecords : 1];
-    // Primary batches (SPT_PRIM; the wave walk of a single launch): when idle lanes want
+    // Primary batches (SPT_PRIM; the wave-walk kernels): when idle lanes want
     // more paths than the wave's queue holds, every lane parks its own path in the queue
     // rows, takes a NEW item (64 consecutive items: one sample of one 8x8 tile) and the
     // wave runs one ordinary iteration -- cast + shading step -- over those 64 primary
@@ -176,7 +176,7 @@ __device__ __forceinline__ void render_body(const RenderArgs &a)
     // The primary cast is one coherent bundle from the eye (the wave walk's union of
     // leaves is about a single ray's), and every path enters the main loop one cast in.
     // Per path the arithmetic and its order are unchanged: bit-identical frames.
-    constexpr bool PRIM = SPT_PRIM && !BATCH && !LDSN && !GLANE;
+    constexpr bool PRIM = SPT_PRIM && !LDSN && !GLANE;
     __shared__ uint32_t s_park[PRIM ? (BLOCK / 64u) * kParkWords * 64u : 1];
     uint32_t *const park = s_park + (PRIM ? (threadIdx.x >> 6) * kParkWords * 64u : 0u);
     uint32_t q_n = 0, q_pos = 0;  // the wave's queue: rows [q_pos, q_n) hold parked paths
@@ -258,6 +258,20 @@ __device__ __forceinline__ void render_body(const RenderArgs &a)
         return ((need >> lane) & 1ull) ? mine : 0xFFFFFFFFu;
     };
 
+    // BATCH: the claim in flight becomes current (with its rectangle), the next one goes
+    // in flight
+    auto next_claim = [&]() {
+        const uint32_t nb = __builtin_amdgcn_readfirstlane(pend);
+        if (nb < a.n_items && lane == 0) pend = claim_next(a, home, qi);
+        if (nb >= a.n_items) {
+            exhausted = true;
+        } else {
+            blk_cur = nb;
+            blk_end = min(nb + a.claim, a.n_items);
+            rect = find_rect(nb);
+        }
+    };
+
     for (;;) {
         // ---- refill: hand out (pixel, sample) items to idle lanes (ballot + prefix)
         // idle lanes wait until SPT_REFILL_MIN of them (or the whole wave) can be
@@ -279,25 +293,26 @@ __device__ __forceinline__ void render_body(const RenderArgs &a)
                     park_path(park, lane, ps);
                     // the own path lives in LDS across the batch, not in registers
                     asm volatile("" ::: "memory");
-                    const uint32_t mine = take_items(~0ull);
                     ps.phase = PH_IDLE;
-                    if (mine != 0xFFFFFFFFu) start_path_kernarg(mine, rows, ps);
+                    if (BATCH) {
+                        // claims are multiples of 64 items and never span two rectangles:
+                        // a batch is 64 items of one claim (fewer at the launch's end)
+                        if (blk_cur == blk_end) next_claim();
+                        if (!exhausted) {
+                            const uint32_t n = min(64u, blk_end - blk_cur);
+                            const uint32_t mine = blk_cur + lane;
+                            blk_cur += n;
+                            if (lane < n) start_path_rect(mine, rect, ps);
+                        }
+                    } else {
+                        const uint32_t mine = take_items(~0ull);
+                        if (mine != 0xFFFFFFFFu) start_path_kernarg(mine, rows, ps);
+                    }
                     prim_iter = true;
                 }
             }
         } else if (BATCH && need != 0ull && !exhausted) {
-            if (blk_cur == blk_end) {
-                // the claim in flight becomes current, the next one goes in flight
-                const uint32_t nb = __builtin_amdgcn_readfirstlane(pend);
-                if (nb < a.n_items && lane == 0) pend = claim_next(a, home, qi);
-                if (nb >= a.n_items) {
-                    exhausted = true;
-                } else {
-                    blk_cur = nb;
-                    blk_end = min(nb + a.claim, a.n_items);
-                    rect = find_rect(nb);
-                }
-            }
+            if (blk_cur == blk_end) next_claim();
             if (!exhausted) {
                 const uint32_t take = min((uint32_t)__popcll(need), blk_end - blk_cur);
                 const uint32_t rank = lane_rank(need);

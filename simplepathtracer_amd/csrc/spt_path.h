@@ -576,7 +576,7 @@ __device__ __forceinline__ void update_member_lane(float tc, float hh, const uin
 #define SPT_LANE_GROUP 2
 #endif
 #ifndef SPT_LANE_STEPS
-#define SPT_LANE_STEPS 6
+#define SPT_LANE_STEPS 8
 #endif
 // The lane walk as a resumable cast: `fresh` lanes start (winner none, node 0); the
 // others continue from their saved node, parked leaves and winner.  The always-list is
@@ -691,7 +691,9 @@ __device__ __forceinline__ bool lane_cast(const AccelView &ac, const f3 &o, cons
         };
         // SPT_LANE_STEPS node steps per walk iteration: the iteration's ballots, budget
         // check and leaf-pass test are paid once per that many steps (config 5: 1 / 3 / 4 /
-        // 6 steps at budgets 40 / 16 / 12 / 8 iterations: 90.4 / 80.5 / 79.5 / 78.2 ms)
+        // 6 steps at budgets 40 / 16 / 12 / 8 iterations: 90.4 / 80.5 / 79.5 / 78.2 ms; with
+        // leaf passes at 24 lanes, steps x budget 6x8 / 7x7 / 7x6 / 8x6 / 8x5 / 6x6 / 5x8:
+        // 77.1 / 75.5 / 75.6 / 75.3 / 75.8 / 78.4 / 77.0 ms)
 #pragma unroll
         for (int k = 0; k < SPT_LANE_STEPS; ++k) {
             const bool w = i < n && leaf2 == kNoSlot;

@@ -21,6 +21,7 @@
 #include <cstring>
 #include <functional>
 #include <mutex>
+#include <thread>
 #include <string>
 #include <utility>
 #include <vector>
@@ -85,6 +86,7 @@ struct Workspace {
     float4 *d_acc = nullptr;       // ordered partial sums when a frame is batched
     size_t acc_cap = 0;
     uint32_t *d_head = nullptr;    // claim counter
+    bool head_clean = false;       // d_head zeroed by the last batched fold (launch_batch)
     spt::WavefrontBuffers wf{};    // queues of the wavefront engine (allocated on first use)
     uint32_t *h_count = nullptr;   // pinned host word: queue length read back per pass
 };
@@ -171,6 +173,10 @@ struct spt_ctx {
     // through the C++ shim at tc = 4: 7.93 -> 7.64 ms per frame, its folds 2x shorter)
     uint32_t batch_grid_div = 2;
     bool fold_to_host = true;     // batched folds write page-locked g_data in place (SPT_FOLD_HOST)
+    // per-batch launch latency (launch_batch): rectangles in the kernel arguments
+    // (SPT_INLINE_RECTS), claim counters zeroed by the previous fold (SPT_FOLD_HEAD); the
+    // leader polls its batch's stream instead of a blocking wait (SPT_SPIN_SYNC)
+    bool inline_rects = true, fold_resets_head = true, spin_sync = false;
     std::condition_variable batch_cv;
     uint64_t batches = 0, batched_calls = 0;
 
@@ -845,7 +851,10 @@ int launch_batch(spt_ctx *ctx, BatchSet *bs, const std::vector<BatchReq *> &batc
     if ((rc = ensure(ctx, &w->d_samples, &w->samples_cap, (size_t)slot * slot_words))) return rc;
     if (any_rgba && (rc = ensure(ctx, &bs->d_stage, &bs->stage_cap, (size_t)pix))) return rc;
     const hipStream_t s = bs->stream;
-    HIP_TRY(ctx, hipMemcpyAsync(bs->d_rects, bs->h_rects, n * sizeof(spt::BatchRect), hipMemcpyHostToDevice, s));
+    // up to kInlineRects rectangles travel in the kernel arguments; more in the table
+    const bool inl = ctx->inline_rects && n <= spt::kInlineRects;
+    if (!inl)
+        HIP_TRY(ctx, hipMemcpyAsync(bs->d_rects, bs->h_rects, n * sizeof(spt::BatchRect), hipMemcpyHostToDevice, s));
 
     spt::RenderArgs ra{};
     ra.scene = spt::DeviceScene{ctx->d_shade, ctx->d_mat, ctx->n, ctx->code_shift, ctx->accel};
@@ -875,8 +884,15 @@ int launch_batch(spt_ctx *ctx, BatchSet *bs, const std::vector<BatchReq *> &batc
     ra.counters = ctx->d_counters;
     ra.rects = bs->d_rects;
     ra.n_rects = (uint32_t)n;
+    ra.inline_rects = inl ? 1u : 0u;
+    if (inl)
+        for (size_t i = 0; i < n; ++i) ra.rects_inline[i] = bs->h_rects[i];
 
-    HIP_TRY(ctx, hipMemsetAsync(w->d_head, 0, sizeof(uint32_t) * spt::kQueueStride * ra.n_queues, s));
+    // the claim counters are zeroed by the previous batch's fold on this workspace
+    // (FoldArgs::head_reset), or here when that fold did not run
+    if (!w->head_clean || !ctx->fold_resets_head)
+        HIP_TRY(ctx, hipMemsetAsync(w->d_head, 0, sizeof(uint32_t) * spt::kQueueStride * ra.n_queues, s));
+    w->head_clean = false;
     if (!ctx->ref_recorded) {
         HIP_TRY(ctx, hipEventRecord(ctx->ref_ev, s));
         ctx->ref_recorded = true;
@@ -904,9 +920,15 @@ int launch_batch(spt_ctx *ctx, BatchSet *bs, const std::vector<BatchReq *> &batc
     fa.mode = mode;
     fa.rects = bs->d_rects;
     fa.n_rects = (uint32_t)n;
+    fa.inline_rects = inl ? 1u : 0u;
+    if (inl)
+        for (size_t i = 0; i < n; ++i) fa.rects_inline[i] = bs->h_rects[i];
+    fa.head_reset = ctx->fold_resets_head ? w->d_head : nullptr;
+    fa.head_queues = ra.n_queues;
     EventPair ef = get_pair(ctx);
     HIP_TRY(ctx, hipEventRecord(ef.a, s));
     HIP_TRY(ctx, spt::launch_fold(fa, s));
+    w->head_clean = true;
     HIP_TRY(ctx, hipEventRecord(ef.b, s));
     ctx->pending_fold.push_back(ef);
 
@@ -990,7 +1012,12 @@ int render_batched(spt_ctx *ctx, std::unique_lock<std::mutex> &lk, int mode, uin
         int rc = bs->stream ? launch_batch(ctx, bs, batch) : fail(ctx, SPT_ERR_HIP, "stream creation failed");
         if (rc == SPT_OK) {
             lk.unlock();
-            const hipError_t e = hipStreamSynchronize(bs->stream);
+            hipError_t e;
+            if (ctx->spin_sync) {
+                while ((e = hipStreamQuery(bs->stream)) == hipErrorNotReady) std::this_thread::yield();
+            } else {
+                e = hipStreamSynchronize(bs->stream);
+            }
             lk.lock();
             if (e != hipSuccess) rc = fail(ctx, SPT_ERR_HIP, "hipStreamSynchronize failed: %s", hipGetErrorString(e));
         } else if (bs->stream) {
@@ -1293,6 +1320,9 @@ int spt_ctx_create(int device, spt_ctx **out)
     if (const char *e = std::getenv("SPT_BATCH_DBUF")) ctx->batch_dbuf = std::atoi(e) != 0;
     if (const char *e = std::getenv("SPT_FOLD_HOST")) ctx->fold_to_host = std::atoi(e) != 0;
     if (const char *e = std::getenv("SPT_BATCH_GRID_DIV")) ctx->batch_grid_div = (uint32_t)std::max(1, std::atoi(e));
+    if (const char *e = std::getenv("SPT_INLINE_RECTS")) ctx->inline_rects = std::atoi(e) != 0;
+    if (const char *e = std::getenv("SPT_FOLD_HEAD")) ctx->fold_resets_head = std::atoi(e) != 0;
+    if (const char *e = std::getenv("SPT_SPIN_SYNC")) ctx->spin_sync = std::atoi(e) != 0;
     if (const char *e = std::getenv("SPT_BATCH_SETS"))
         ctx->batch_sets = (uint32_t)std::min<int>((int)kMaxBatchSets, std::max(1, std::atoi(e)));
     if (const char *e = std::getenv("SPT_HOST_SLOTS"))

@@ -256,6 +256,7 @@ struct BatchRect {
     FastDiv div_band, div_tile;  // ts_item divisors 8*w*spp and 64*spp
 };
 static_assert(sizeof(BatchRect) == 72, "BatchRect layout");
+constexpr uint32_t kInlineRects = 4;  // rectangles carried in the kernel arguments
 
 struct RenderArgs {
     DeviceScene scene;
@@ -280,6 +281,10 @@ struct RenderArgs {
     // claims come from n_queues counters head[k * kQueueStride], queue k
     // handing out items [k * queue_items, (k + 1) * queue_items) (claim multiples)
     uint32_t n_queues, queue_items;
+    // batched launches of at most kInlineRects rectangles may carry them here, in the
+    // kernel arguments (inline_rects = 1: no table upload before the launch)
+    uint32_t inline_rects;
+    BatchRect rects_inline[kInlineRects];
 };
 
 // claim counters: at most one per XCD, 256 bytes apart (separate cache lines)
@@ -308,6 +313,12 @@ struct FoldArgs {
     // indices [out_i0, out_i0 + npix) of a call of map.width x alias_h pixels, whose source
     // pixels' slots are those of the launch's rows (map: rows [map.y0, map.y0 + src_rows))
     uint32_t range_alias, out_i0, alias_h, src_rows;
+    // batched fold: the render's claim counters (head[k * kQueueStride], k < head_queues),
+    // zeroed for the workspace's next launch (no memset before it); null = leave them
+    uint32_t *head_reset;
+    uint32_t head_queues;
+    uint32_t inline_rects;                 // as RenderArgs::inline_rects / rects_inline
+    BatchRect rects_inline[kInlineRects];
 };
 
 // Launch geometry of one render launch: the context's persistent grid for the

@@ -505,6 +505,13 @@ __device__ __forceinline__ void decode_run(const FoldArgs &a, const uint32_t (&w
     }
 }
 
+// words loaded ahead per thread in the fold (a multiple of 8): small folds (the drop-in's
+// batches of one or two tiles) have few threads, and each is bound by its loads' latency
+#ifndef SPT_FOLD_RUN
+#define SPT_FOLD_RUN 8
+#endif
+static_assert(SPT_FOLD_RUN % 8 == 0, "fold runs are decoded eight words at a time");
+
 // RenderSegmentTask's colorIndex aliasing (TaskBasedPathTracer.hpp:103,186,196-205) for
 // output index p of a W x H call: colors[p] collects every pixel (dx, dy) of the call with
 // dx + dy * H == p, and the resolve writes colors[p] to pixel (p % W, p / W).  Within a
@@ -600,21 +607,28 @@ __device__ __forceinline__ void fold_pixel(const FoldArgs &a, const uint32_t *sa
     ts_slot_base(lr, col, W, rows, S, q0, step);
     if (a.mode == 0) {
         // RenderSegment: one word per slot, every sample counts.  Runs of kFoldRun words
-        // are loaded before any is decoded (the loads of a run are in flight together)
-        constexpr int kFoldRun = 8;
+        // are loaded before any is decoded (the loads of a run are in flight together),
+        // then decoded eight at a time
+        constexpr int kFoldRun = SPT_FOLD_RUN;
         uint32_t k = 0;
         for (; k + kFoldRun <= S; k += kFoldRun) {
             uint32_t w[kFoldRun];
 #pragma unroll
             for (int i = 0; i < kFoldRun; ++i) w[i] = samples[q0 + (k + i) * step];
-            f3 c[kFoldRun];
-            decode_run<kFoldRun>(a, w, c);
 #pragma unroll
-            for (int i = 0; i < kFoldRun; ++i) {
-                acc.x = acc.x + c[i].x;
-                acc.y = acc.y + c[i].y;
-                acc.z = acc.z + c[i].z;
-                acc.w = acc.w + 1.f;
+            for (int g = 0; g < kFoldRun; g += 8) {
+                uint32_t w8[8];
+#pragma unroll
+                for (int i = 0; i < 8; ++i) w8[i] = w[g + i];
+                f3 c[8];
+                decode_run<8>(a, w8, c);
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    acc.x = acc.x + c[i].x;
+                    acc.y = acc.y + c[i].y;
+                    acc.z = acc.z + c[i].z;
+                    acc.w = acc.w + 1.f;
+                }
             }
         }
         for (; k < S; ++k) {
@@ -689,22 +703,30 @@ __global__ __launch_bounds__(256) void fold_alias_range_kernel(FoldArgs a)
 }
 
 // The rectangle of pixel i of a batched fold (FoldArgs::rects).
-__device__ __forceinline__ uint32_t fold_rect(const FoldArgs &a, uint32_t i)
+typedef __attribute__((address_space(4))) const BatchRect crect_k;
+__device__ __forceinline__ uint32_t fold_rect(crect_k *rs, uint32_t n, uint32_t i)
 {
-    uint32_t lo = 0, hi = a.n_rects;
+    uint32_t lo = 0, hi = n;
     while (hi - lo > 1u) {
         const uint32_t mid = (lo + hi) >> 1;
-        if (a.rects[mid].pix_off <= i) lo = mid; else hi = mid;
+        if (rs[mid].pix_off <= i) lo = mid; else hi = mid;
     }
     return lo;
 }
 
-// Batched fold (FoldArgs::rects): pixel i of the batch's concatenated rectangles.
+// Batched fold (FoldArgs::rects): pixel i of the batch's concatenated rectangles.  Block
+// 0 also zeroes the render's claim counters for the workspace's next batch.
 __global__ __launch_bounds__(256) void fold_kernel_batch(FoldArgs a)
 {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (blockIdx.x == 0 && a.head_reset && threadIdx.x < a.head_queues) a.head_reset[threadIdx.x * kQueueStride] = 0u;
     if (i >= a.npix) return;
-    const BatchRect &r = a.rects[fold_rect(a, i)];
+    // the rectangles from the kernel arguments (this kernel's first argument is `a`)
+    typedef __attribute__((address_space(4))) const FoldArgs cfold_t;
+    typedef __attribute__((address_space(4))) const char kchar;
+    cfold_t *ka = (cfold_t *)(kchar *)__builtin_amdgcn_kernarg_segment_ptr();
+    crect_k *rs = a.inline_rects ? (crect_k *)ka->rects_inline : (crect_k *)a.rects;
+    crect_k &r = rs[fold_rect(rs, a.n_rects, i)];
     const RowMap map{r.y0, r.y0 + r.rows, 1u, 1u, 0u, r.x0, r.w};
     uint32_t lr, col;
     tile_pixel(i - r.pix_off, r.w, r.rows, lr, col);

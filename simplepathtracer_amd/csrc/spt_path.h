@@ -1036,7 +1036,7 @@ typedef __attribute__((address_space(4))) const BatchRect crect_t;
 __device__ __forceinline__ uint32_t find_rect(uint32_t nb)
 {
     kargs_t &k = *kernarg_args();
-    crect_t *r = (crect_t *)k.rects;
+    crect_t *r = k.inline_rects ? (crect_t *)k.rects_inline : (crect_t *)k.rects;
     uint32_t lo = 0, hi = k.n_rects;
     while (hi - lo > 1u) {
         const uint32_t mid = (lo + hi) >> 1;
@@ -1051,7 +1051,7 @@ __device__ __forceinline__ uint32_t find_rect(uint32_t nb)
 __device__ __forceinline__ void start_path_rect(uint32_t mine, uint32_t ri, Path &ps)
 {
     kargs_t &k = *kernarg_args();
-    crect_t &r = ((crect_t *)k.rects)[ri];
+    crect_t &r = (k.inline_rects ? (crect_t *)k.rects_inline : (crect_t *)k.rects)[ri];
     if (mine >= r.item_end) return;
     RenderArgs a;
     a.map = RowMap{r.y0, r.y0 + r.rows, 1u, 1u, 0u, r.x0, r.w};

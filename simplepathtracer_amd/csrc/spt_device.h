@@ -162,11 +162,7 @@ __device__ __forceinline__ float uniform(uint64_t &st, float a, float b) { retur
 // glibc's powf restated bit for bit (spt_powf.h, exhaustively pinned) and the
 // correctly rounded sqrtf.
 // ---------------------------------------------------------------------------
-// SPT_POW5_FAST 0: always glibc's full algorithm (spt_pow5f equals it bit for bit)
-#ifndef SPT_POW5_FAST
-#define SPT_POW5_FAST 1
-#endif
-__device__ __forceinline__ float pow5f(float x) { return SPT_POW5_FAST ? spt_pow5f(x) : spt_glibc_powf(x, 5.f); }
+__device__ __forceinline__ float pow5f(float x) { return spt_glibc_powf(x, 5.f); }
 
 // rSq + (1 - rSq) * pow(1 - c, 5)  (lines 58-59, 75-76)
 __device__ __forceinline__ float schlick(float rsq, float c) { return rsq + (1.f - rsq) * pow5f(1.f - c); }

@@ -186,35 +186,3 @@ SPT_POWF_HD inline float spt_glibc_powf(float x, float y)
     e = e * s;
     return (float)e;
 }
-
-// powf(x, 5.f) with a short exact path (Schlick's term, SingleThreadPathTracer.hpp:58-59,
-// 75-76): for x in [2^-20, 2], x5 = x^5 in double (x*x exact, two rounded products:
-// |x5 - x^5| <= 2^-51.9 x^5) rounds to the float r; when x5 lies at least 2^(e-29) (e =
-// r's exponent; at least 2^-29 x^5 / 2) inside the rounding interval of r -- the
-// half-ulp on the side x5 lies, halved below a power of two -- r is returned; otherwise
-// (about 3% of inputs, and x outside the range) glibc's algorithm above.  Equal to
-// glibc's powf(x, 5.f) bit for bit for every float x: tests/cpp/kat_powf.cpp checks all
-// 2^32 inputs (the short path alone is not a proof: glibc's core is accurate to ~2^-34,
-// the exhaustive comparison is).
-SPT_POWF_HD inline float spt_pow5f(float x)
-{
-    using namespace spt_powf_detail;
-    if (x >= 0x1p-20f && x <= 2.0f) {
-        const double xd = (double)x;
-        const double x2 = xd * xd;
-        const double x4 = x2 * x2;
-        const double x5 = x4 * xd;
-        const float r = (float)x5;
-        const uint32_t ir = f2u(r);
-        const double rd = (double)r;
-        const int e = (int)(ir >> 23) - 127;
-        // 2^(e-24): half an ulp of r; 2^(e-25) below r when r is a power of two
-        const bool below_pow2 = x5 < rd && (ir & 0x7fffffu) == 0u;
-        const double half = u2d((uint64_t)(e - 24 - (below_pow2 ? 1 : 0) + 1023) << 52);
-        const double slack = u2d((uint64_t)(e - 29 + 1023) << 52);
-        const double dist = x5 >= rd ? x5 - rd : rd - x5;
-        if (dist <= half - slack) return r;
-    }
-    return spt_glibc_powf(x, 5.f);
-}
-

@@ -29,13 +29,6 @@ int main(int argc, char **argv)
                 if (spt_powf_detail::f2u(want) != spt_powf_detail::f2u(got)) {
                     if (b++ < 4) printf("x=%a y=%a glibc=%a restated=%a\n", x, y, want, got);
                 }
-                if (y == 5.f) {
-                    // the kernel's pow5f: the short exact path, else the restatement
-                    const float fast = spt_pow5f(x);
-                    if (spt_powf_detail::f2u(want) != spt_powf_detail::f2u(fast)) {
-                        if (b++ < 4) printf("x=%a y=5 glibc=%a spt_pow5f=%a\n", x, want, fast);
-                    }
-                }
             }
             bad += b;
             n += c;

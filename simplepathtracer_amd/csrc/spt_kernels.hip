@@ -167,6 +167,8 @@ __device__ __forceinline__ void render_body(const RenderArgs &a)
 
     __shared__ uint32_t s_lds[BLOCK];  // wave-private scratch of the cooperative sampler
     __shared__ uint4 s_nodes[LDSN ? 2 * kLdsNodeRecords : 1];
+    // the LDS copy holds byte-offset skip links when only lane_cast walks it
+    constexpr bool LDS_BYTES = LDSN && SPT_LANE_WALK && SPT_LANE_BUDGET > 0;
     // Primary batches (SPT_PRIM; the wave-walk kernels): when idle lanes want
     // more paths than the wave's queue holds, every lane parks its own path in the queue
     // rows, takes a NEW item (64 consecutive items: one sample of one 8x8 tile) and the
@@ -184,7 +186,12 @@ __device__ __forceinline__ void render_body(const RenderArgs &a)
         // the host launches this variant only when n_nodes + 1 <= kLdsNodeRecords
         const uint4 *src = (const uint4 *)a.scene.accel.nodes;
         const uint32_t n4 = 2u * (a.scene.accel.n_nodes + 1u);
-        for (uint32_t k = threadIdx.x; k < n4; k += BLOCK) s_nodes[k] = src[k];
+        for (uint32_t k = threadIdx.x; k < n4; k += BLOCK) {
+            uint4 v = src[k];
+            // the lane walk's copy: skip links as byte offsets (lane_cast BYTES)
+            if (LDS_BYTES && (k & 1u)) v.x <<= 5;
+            s_nodes[k] = v;
+        }
         __syncthreads();
     }
     Path ps;
@@ -349,7 +356,7 @@ __device__ __forceinline__ void render_body(const RenderArgs &a)
         bool cdone = true;
         Hit h;
         if constexpr (RES) {
-            cdone = lane_cast<LEAF>(a.scene.accel, ps.o, ps.d, act, dg,
+            cdone = lane_cast<LEAF, LDS_BYTES>(a.scene.accel, ps.o, ps.d, act, dg,
                                     LDSN ? (const uint32_t *)s_nodes : (const uint32_t *)a.scene.accel.nodes, fresh,
                                     (uint32_t)SPT_LANE_BUDGET, hres, li, lleaf, lleaf2);
             h = hres;

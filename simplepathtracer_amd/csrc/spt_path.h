@@ -583,7 +583,12 @@ __device__ __forceinline__ void update_member_lane(float tc, float hh, const uin
 // re-tested for every lane (idempotent: a sphere tested twice cannot replace itself --
 // equal distance and index).  Runs at most `budget` walk iterations and leaf passes;
 // returns whether the lane's cast is complete (inactive lanes: true).
-template <int LEAF>
+// BYTES: node positions (i, the records' skip links) are byte offsets into `lnodes` (the
+// LDS copy of render_kernel_lds stores them so: no shift per node step); else indices.
+// Parked leaves form a two-entry shift register: a leaf reached goes to `leaf`, the one
+// there moves to `leaf2` (2 VALU per step fewer than filling the first free entry; the
+// pass tests both, in any order: the winner does not depend on it).
+template <int LEAF, bool BYTES = false>
 __device__ __forceinline__ bool lane_cast(const AccelView &ac, const f3 &o, const f3 &d, bool active, CastDiag &dg,
                                           const uint32_t *lnodes, bool fresh, uint32_t budget, Hit &h, uint32_t &i,
                                           uint32_t &leaf, uint32_t &leaf2)
@@ -592,7 +597,7 @@ __device__ __forceinline__ bool lane_cast(const AccelView &ac, const f3 &o, cons
         h.idx = kMiss;
         h.best = FLT_MAX;
         h.t = 0.f;
-        i = active ? 0u : ac.n_nodes;
+        i = active ? 0u : (BYTES ? ac.n_nodes << 5 : ac.n_nodes);
         leaf = leaf2 = kNoSlot;
     }
     const float dod = dot(o, d);
@@ -624,7 +629,7 @@ __device__ __forceinline__ bool lane_cast(const AccelView &ac, const f3 &o, cons
     float sbl = near_bound(h.best);
     const uint4 *ln = (const uint4 *)lnodes;
     const float4 *__restrict__ gs = ac.slots;
-    const uint32_t n = ac.n_nodes;
+    const uint32_t n = BYTES ? ac.n_nodes << 5 : ac.n_nodes;  // end of the walk
     // parked leaves (first slots), kNoSlot = none: a lane keeps walking while one
     // leaf is parked and stops at the second
     uint32_t it = 0;
@@ -667,7 +672,8 @@ __device__ __forceinline__ bool lane_cast(const AccelView &ac, const f3 &o, cons
         if (SPT_DIAG) dg.live += 1;
         // one node step of the lane's own walk (lanes with a second parked leaf wait)
         auto visit = [&]() {
-            const uint4 ra = ln[2 * i], rb = ln[2 * i + 1];
+            const uint4 *rec = BYTES ? (const uint4 *)((const char *)lnodes + i) : ln + 2 * i;
+            const uint4 ra = rec[0], rb = rec[1];
             const uint32_t nskip = rb.x, nslot = rb.y;
             const float ax = __builtin_fmaf(__uint_as_float(ra.x), irx, qlx);
             const float bx = __builtin_fmaf(__uint_as_float(ra.w), irx, qhx);
@@ -679,15 +685,13 @@ __device__ __forceinline__ bool lane_cast(const AccelView &ac, const f3 &o, cons
                                       max_raw(__builtin_fminf(az, bz), neta));
             const float tf = min3_raw(__builtin_fmaxf(ax, bx), __builtin_fmaxf(ay, by),
                                       min_raw(__builtin_fmaxf(az, bz), sbl));
-            const bool hit = tn <= tf || nocull;
+            const bool hit = (tn <= tf) | nocull;
             const bool is_leaf = nslot != kNoSlot;
             if (hit && is_leaf) {
-                if (leaf != kNoSlot)
-                    leaf2 = nslot;
-                else
-                    leaf = nslot;
+                leaf2 = leaf;
+                leaf = nslot;
             }
-            i = (hit && !is_leaf) ? i + 1 : nskip;
+            i = (hit && !is_leaf) ? i + (BYTES ? 32u : 1u) : nskip;
         };
         // SPT_LANE_STEPS node steps per walk iteration: the iteration's ballots, budget
         // check and leaf-pass test are paid once per that many steps (config 5: 1 / 3 / 4 /

@@ -262,7 +262,7 @@ __device__ __forceinline__ void render_body(const RenderArgs &a)
                 blk_end = ne;
             }
         }
-        return ((need >> lane) & 1ull) ? mine : 0xFFFFFFFFu;
+        return __builtin_amdgcn_inverse_ballot_w64(need) ? mine : 0xFFFFFFFFu;
     };
 
     // BATCH: the claim in flight becomes current (with its rectangle), the next one goes

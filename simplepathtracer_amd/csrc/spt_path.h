@@ -754,10 +754,12 @@ __device__ __forceinline__ f3 coop_ball_vector(uint64_t &st, bool need, uint32_t
     const uint32_t s_lo = (uint32_t)st0, s_hi = (uint32_t)(st0 >> 32);
     while (pend != 0ull) {
         const uint32_t np = (uint32_t)__popcll(pend);
-        const uint32_t q64 = 64u / np;
-        uint32_t lg = 31u - (uint32_t)__builtin_clz(q64);
+        // lg = min(floor(log2(64 / np)), 4) = min(6 - ceil(log2 np), 4) on the scalar unit
+        // (64 / np compiled to a float reciprocal sequence on the vector unit)
+        uint32_t lg = np <= 4u ? 4u : (uint32_t)__builtin_clz(np - 1u) - 26u;
         lg = lg > 4u ? 4u : lg;
-        const bool is_p = (pend >> lane) & 1ull;
+        // the lane's bit of a wave mask as a lane predicate without vector instructions
+        const bool is_p = __builtin_amdgcn_inverse_ballot_w64(pend);
         const uint32_t rank = lane_rank(pend);
         if (is_p) lds[rank] = lane;
         const uint32_t pidx = lane >> lg, tt = lane & ((1u << lg) - 1u);

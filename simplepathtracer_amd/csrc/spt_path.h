@@ -211,7 +211,11 @@ __device__ __forceinline__ void test_group(const float4 (&sp)[G], const uint32_t
             dg.branches += __ballot(pass[k]) != 0ull ? 1 : 0;
             dg.passing += (unsigned long long)__popcll(__ballot(pass[k]));
         }
-        if (__ballot(pass[k]) != 0ull) update_member(pass[k], tcv[k], hv[k], orig, slot + k, o, d, dod, h, dg);
+        // the update gets the pass mask back as a lane predicate (inverse ballot): a bool
+        // kept across the branch would be rebuilt from a VGPR copy (2 VALU per update)
+        const unsigned long long pmk = __ballot(pass[k]);
+        if (pmk != 0ull)
+            update_member(__builtin_amdgcn_inverse_ballot_w64(pmk), tcv[k], hv[k], orig, slot + k, o, d, dod, h, dg);
     }
 }
 
@@ -268,7 +272,9 @@ __device__ __forceinline__ void test_group_pre(const float4 (&sp)[G], const floa
             float tc, hh;
             const bool pass = ray_sphere(sp[k], o, d, tc, hh);
             if (SPT_DIAG) dg.lane_tests += dg.live_now;
-            if (__ballot(pass) != 0ull) update_member(pass, tc, hh, orig, slot + k, o, d, dod, h, dg);
+            const unsigned long long pmk = __ballot(pass);
+            if (pmk != 0ull)
+                update_member(__builtin_amdgcn_inverse_ballot_w64(pmk), tc, hh, orig, slot + k, o, d, dod, h, dg);
         }
     }
 }
@@ -443,9 +449,11 @@ __device__ __forceinline__ Hit find_closest(const AccelView &ac, const f3 &o, co
     if (TREE) {
         // the layout of the wave's majority direction octant (siblings front to back)
         const uint32_t nlive = (uint32_t)__popcll(live_mask);
-        const uint32_t oct = (2u * (uint32_t)__popcll(__ballot(active && d.x < 0.f)) > nlive ? 1u : 0u) |
-                             (2u * (uint32_t)__popcll(__ballot(active && d.y < 0.f)) > nlive ? 2u : 0u) |
-                             (2u * (uint32_t)__popcll(__ballot(active && d.z < 0.f)) > nlive ? 4u : 0u);
+        // ballots of the compares themselves, masked with the live lanes (a ballot of
+        // `active && ...` goes through a VGPR bool per term)
+        const uint32_t oct = (2u * (uint32_t)__popcll(__ballot(d.x < 0.f) & live_mask) > nlive ? 1u : 0u) |
+                             (2u * (uint32_t)__popcll(__ballot(d.y < 0.f) & live_mask) > nlive ? 2u : 0u) |
+                             (2u * (uint32_t)__popcll(__ballot(d.z < 0.f) & live_mask) > nlive ? 4u : 0u);
         if (!LDSN) nodes += (size_t)8 * (ac.n_nodes + 1) * oct;
     }
     // Tree nodes are boxes [lo, hi] already expanded by kBoxS Bm.  Per
@@ -473,7 +481,8 @@ __device__ __forceinline__ Hit find_closest(const AccelView &ac, const f3 &o, co
     const float kn = active ? __builtin_fmaf(1e-5f, obs, 1e-6f) : -INFINITY;
     // tree node masks are (ballot(test) & live) | nocull: the ballot of a compare is
     // the compare's own lane mask, with no VALU round trip
-    const unsigned long long tree_nocull = __ballot(no_cull || (active && !(oo <= 1e30f)));
+    const unsigned long long tree_nocull =
+        (__ballot(!(ddev <= 1e-6f && ddev >= -1e-6f)) | __ballot(!(oo <= 1e30f))) & live_mask;
     // near bound of the lane's current winner, refreshed after every leaf test;
     // ~1.8e19 while there is none (best = FLT_MAX: never culls)
     auto near_bound = [&](float best) {

@@ -139,40 +139,40 @@ struct CastDiag {
 };
 
 // The closest-contact / distance update of one member (Collision.hpp:19-27,49-56,
-// 87-109) for the lanes that pass RaySphereIntersection (`pass`, with its tc and
+// 87-109) for the lanes that pass RaySphereIntersection (wave mask `pm`, with their tc and
 // hh); called in wave-uniform control flow when some lane passes.  Slots are
 // visited in traversal order, so the winner is the lexicographic minimum of
 // (distance, original index): identical to the reference's strict-'>' scan in
 // index order (first index wins ties; NaN and FLT_MAX distances never win).
-__device__ __forceinline__ void update_member(bool pass, float tc, float hh, const uint32_t *__restrict__ orig,
-                                              uint32_t s, const f3 &o, const f3 &d, float dod, Hit &h, CastDiag &dg)
+__device__ __forceinline__ void update_member(unsigned long long pm, float tc, float hh,
+                                              const uint32_t *__restrict__ orig, uint32_t s, const f3 &o, const f3 &d,
+                                              float dod, Hit &h, CastDiag &dg)
 {
     // CalculateRaySphereClosestContactPoint, Collision.hpp:19-27,49-56
     const float t = tc - sqrt_pos_normal(hh);
     const f3 p = contact(o, d, t);
-    const bool front = dod < dot(p, d);
-    const bool ok = pass && front;
     const float ds = lensq(sub(o, p));
-    bool better = ok && ds < h.best;
-    // exact tie (rare): the first original index wins.  Behind a wave-uniform
-    // branch, with scalar loads only (one per distinct current winner): a vector
-    // load here made every cast wait on vmcnt(0), i.e. on the previous shading
-    // step's sample stores.
-    const bool tie = ok && ds == h.best && h.idx != kMiss;
-    // the ballot of a compare is its own lane mask; a ballot of the combined bool
-    // would go through a VGPR (v_cndmask + v_cmp) first
-    unsigned long long tm = __ballot(pass) & __ballot(front) & __ballot(ds == h.best) & __ballot(h.idx != kMiss);
+    // wave masks (ballots of the compares themselves; a bool kept across the tie
+    // branch would round-trip through a VGPR): `pm` = the lanes that pass
+    // RaySphereIntersection, ok = those whose contact point lies ahead
+    const unsigned long long ok = pm & __ballot(dod < dot(p, d));
+    unsigned long long bm = ok & __ballot(ds < h.best);
+    // exact tie (rare): the first original index wins.  Scalar loads only (one per
+    // distinct current winner): a vector load here made every cast wait on vmcnt(0),
+    // i.e. on the previous shading step's sample stores.
+    unsigned long long tm = ok & __ballot(ds == h.best) & __ballot(h.idx != kMiss);
     if (__builtin_expect(tm != 0ull, 0)) {
         const uint32_t mo = ((cuint *)orig)[s];
         while (tm != 0ull) {
             const uint32_t wi = __builtin_amdgcn_readlane(h.idx, (int)__builtin_ctzll(tm));
             const uint32_t wo = ((cuint *)orig)[wi];
-            const bool same = tie && h.idx == wi;
-            if (same) better = mo < wo;
-            tm &= ~__ballot(same);
+            const unsigned long long same = tm & __ballot(h.idx == wi);
+            if (mo < wo) bm |= same;
+            tm &= ~same;
         }
     }
-    if (SPT_DIAG) dg.improving += __ballot(better) != 0ull ? 1 : 0;
+    if (SPT_DIAG) dg.improving += bm != 0ull ? 1 : 0;
+    const bool better = __builtin_amdgcn_inverse_ballot_w64(bm);
     h.best = better ? ds : h.best;
     h.idx = better ? s : h.idx;
     h.t = better ? t : h.t;
@@ -211,11 +211,11 @@ __device__ __forceinline__ void test_group(const float4 (&sp)[G], const uint32_t
             dg.branches += __ballot(pass[k]) != 0ull ? 1 : 0;
             dg.passing += (unsigned long long)__popcll(__ballot(pass[k]));
         }
-        // the update gets the pass mask back as a lane predicate (inverse ballot): a bool
-        // kept across the branch would be rebuilt from a VGPR copy (2 VALU per update)
+        // the update takes the pass mask (a bool kept across the branch would be rebuilt
+        // from a VGPR copy: 2 VALU per update)
         const unsigned long long pmk = __ballot(pass[k]);
         if (pmk != 0ull)
-            update_member(__builtin_amdgcn_inverse_ballot_w64(pmk), tcv[k], hv[k], orig, slot + k, o, d, dod, h, dg);
+            update_member(pmk, tcv[k], hv[k], orig, slot + k, o, d, dod, h, dg);
     }
 }
 
@@ -274,7 +274,7 @@ __device__ __forceinline__ void test_group_pre(const float4 (&sp)[G], const floa
             if (SPT_DIAG) dg.lane_tests += dg.live_now;
             const unsigned long long pmk = __ballot(pass);
             if (pmk != 0ull)
-                update_member(__builtin_amdgcn_inverse_ballot_w64(pmk), tc, hh, orig, slot + k, o, d, dod, h, dg);
+                update_member(pmk, tc, hh, orig, slot + k, o, d, dod, h, dg);
         }
     }
 }

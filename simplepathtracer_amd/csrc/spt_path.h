@@ -21,38 +21,7 @@
 #define SPT_LEAF_SPLIT 1
 #endif
 
-// 1: the megakernel's start_path reads its parameters from the kernarg segment
-// where used instead of holding them in SGPRs (with the SGPR cap of
-// spt_kernels.hip: 7-8 resident waves per SIMD instead of 6)
-
-// 1: flat-list cluster members are tested behind the conservative pretest of
-// test_group_pre (10 VALU per member instead of 18)
-
-// 1: tree leaves (config 5) behind the member pretest too (measured 10% slower on
-// config 5: the tree's walk, not its member tests, bounds it)
-// 1: leaf tables addressed by 32-bit byte offsets (SGPR-offset scalar loads)
-// 1: the tie mask of update_member as the AND of compare ballots (no VGPR round trip)
-// 1: flat node records loaded as one s_load_dwordx8 each
-
-// timing experiments only: a second, discarded evaluation of
-// one part of the path, whose cost is the part's marginal cost
-
-// 1: tree walks use the layout of the wave's majority direction octant (0: layout 0
-// for every wave: one eighth of the node table in the scalar cache)
-
-// 1: tree node masks as the AND of the three compare ballots
-// 1: the LDS tree walk issues the successor's reads before the node's tests
-
-// 1: flat node records pinned to SGPRs only when the walk reaches them
-// 1: the LDS tree walk also prefetches each node's skip target
-
-// 1: a leaf's member pretests all run before its first branch
-
-
-// 1: the cube-minus-ball rejection loop runs cooperatively across the wave
-
-// Item order of a batch: SPT_TS_ORDER 1 = [band][8x8 tile][sample][pixel] (ts_item);
-// else SPT_TILE 1 = [sample][8x8 tile][pixel] (tile_pixel), 0 = [sample][row-major pixel]
+// Item order of a batch: [band][8x8 tile][sample][pixel] (ts_item, spt_internal.h)
 
 #pragma clang fp contract(off)
 

@@ -102,6 +102,7 @@ struct spt_ctx {
     uint32_t claims_per_wave = 2;                              // render_grid (config 1: 2 > 1, 4)
     uint32_t queues = spt::kMaxQueues;                         // claim counters (RenderArgs::n_queues)
     uint32_t grid_overlap = 0;  // grid while frames are in flight on several streams
+    uint32_t grid_small = 0;    // grid_overlap for small launches (render_grid), 0 = none
     uint32_t last_grid = 0, last_block = 0;  // shape of the most recent render launch
 
     // scene (Globals.hpp:31-37)
@@ -337,6 +338,9 @@ uint64_t fmix64(uint64_t z)
 // (frames in flight), one block slot per CU is left free so the next frame's
 // blocks start while this frame's tail drains: config 2 two-stream frame 8.57 ->
 // 8.41 ms; single-stream launches keep the full grid (1-3% faster there).
+// items per wave below which a launch with frames in flight takes grid_small
+constexpr uint64_t kSmallGridItems = 3072;
+
 uint32_t full_grid(const spt_ctx *ctx)
 {
     return ctx->ws.size() > 1 ? ctx->grid_overlap : ctx->grid;
@@ -373,7 +377,15 @@ uint32_t render_grid(const spt_ctx *ctx, uint64_t items, uint32_t claim, uint32_
 {
     const uint64_t claims = (items + claim - 1) / claim;
     const uint64_t per_block = (uint64_t)(ctx->block / 64) * ctx->claims_per_wave;
-    const uint64_t full = (full_grid(ctx) + div - 1) / div;
+    uint64_t full = (full_grid(ctx) + div - 1) / div;
+    // frames in flight, a launch of under 3 Ki items per wave (config 2's 1/8 rank share):
+    // one more block slot per CU left free, so fewer of the launch's paths are still in
+    // flight when its claims run out and the other stream's launch takes the CUs sooner
+    // (the 1/8 share 0.755-0.762 -> 0.725 ms per frame; the 1/4 share, 3.9 Ki items per
+    // wave, would lose 0.5%: tools/scaling_probe.py)
+    if (div == 1 && ctx->ws.size() > 1 && ctx->grid_small &&
+        items < (uint64_t)full_grid(ctx) * (ctx->block / 64) * kSmallGridItems)
+        full = ctx->grid_small;
     return (uint32_t)std::min<uint64_t>(full, std::max<uint64_t>(1, (claims + per_block - 1) / per_block));
 }
 
@@ -1329,6 +1341,8 @@ int spt_ctx_create(int device, spt_ctx **out)
         ctx->host_slots = (uint32_t)std::min<int>((int)kMaxHostSlots, std::max(1, std::atoi(e)));
     ctx->grid = (uint32_t)(per_cu * ctx->num_cu);
     ctx->grid_overlap = std::getenv("SPT_BLOCKS_PER_CU") || per_cu < 2 ? ctx->grid : (uint32_t)((per_cu - 1) * ctx->num_cu);
+    ctx->grid_small = std::getenv("SPT_BLOCKS_PER_CU") || per_cu < 3 ? 0u : (uint32_t)((per_cu - 2) * ctx->num_cu);
+    if (const char *e = std::getenv("SPT_SMALL_GRID")) ctx->grid_small = std::atoi(e) != 0 ? ctx->grid_small : 0u;
     if (hipEventCreate(&ctx->ref_ev) != hipSuccess || hipEventCreateWithFlags(&ctx->frame_ev, hipEventDisableTiming) != hipSuccess ||
         hipMalloc((void **)&ctx->d_counters, kCounters * sizeof(unsigned long long)) != hipSuccess ||
         hipMemset(ctx->d_counters, 0, kCounters * sizeof(unsigned long long)) != hipSuccess) {

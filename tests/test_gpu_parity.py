@@ -1041,3 +1041,33 @@ def test_claim_queues_render_the_same(spt, golden_scenes, monkeypatch, task):
     for q in ("3", "8"):
         for k, (a, b) in enumerate(zip(out[q], out["1"])):
             assert_bitwise(a, b, f"queues {q} vs 1, part {k}")
+
+
+def test_small_launches_on_two_streams_render_the_same(spt, ctx, golden_scenes):
+    """Frames in flight on two streams (the bench's rank shares): a launch of under 3 Ki
+    items per wave takes the smaller grid (spt_api.cpp render_grid, grid_small).  The
+    strips of an 8-way split rendered alternately on two streams, the same strips on the
+    caller's stream alone, and the whole frame assembled from either, are bit-identical."""
+    import torch
+    setup(ctx, scene_from(spt, golden_scenes, "random"), 1200, 800, 4, 50, seed=5)
+    parts, strip = 8, 4
+    rows = [spt.rows_count(0, 800, strip, parts, p) for p in range(parts)]
+    mr = max(rows)
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    two = torch.zeros((parts, mr * 1200, 4), dtype=torch.float32, device="cuda")
+    for p in range(parts):
+        ctx.render_rows_async(0, 0, 800, strip, parts, p, 0, 1200, two[p].data_ptr(), 0, streams[p % 2].cuda_stream)
+    torch.cuda.synchronize()
+    ncu = torch.cuda.get_device_properties(0).multi_processor_count
+    assert ctx.stats()["grid_blocks"] <= 5 * ncu, "the small-launch grid was not taken"
+    one = torch.zeros_like(two)
+    for p in range(parts):
+        ctx.render_rows_async(0, 0, 800, strip, parts, p, 0, 1200, one[p].data_ptr(), 0)
+    ctx.synchronize()
+    assert torch.equal(two.view(torch.int32), one.view(torch.int32))
+    full = torch.zeros((800 * 1200, 4), dtype=torch.float32, device="cuda")
+    ctx.render_rows_async(0, 0, 800, 1, 1, 0, 0, 1200, full.data_ptr(), 0)
+    frame = torch.zeros_like(full)
+    ctx.assemble_rows_async(two.data_ptr(), mr, 0, 800, strip, parts, 0, 1200, frame.data_ptr(), 0)
+    ctx.synchronize()
+    assert torch.equal(frame.view(torch.int32), full.view(torch.int32))

@@ -79,7 +79,7 @@ constexpr uint32_t kLdsMinNodes = SPT_LDS_MIN_NODES;
 #endif
 constexpr uint32_t kGlaneMaxNodes = SPT_GLANE_MAX_NODES;
 #ifndef SPT_LANE_BUDGET
-#define SPT_LANE_BUDGET 6
+#define SPT_LANE_BUDGET 7
 #endif
 #ifndef SPT_REFILL_MIN
 #define SPT_REFILL_MIN 16

@@ -358,7 +358,7 @@ __device__ __forceinline__ void render_body(const RenderArgs &a)
         if constexpr (RES) {
             cdone = lane_cast<LEAF, LDS_BYTES>(a.scene.accel, ps.o, ps.d, act, dg,
                                     LDSN ? (const uint32_t *)s_nodes : (const uint32_t *)a.scene.accel.nodes, fresh,
-                                    (uint32_t)SPT_LANE_BUDGET, hres, li, lleaf, lleaf2, s_lds + (threadIdx.x & ~63u));
+                                    (uint32_t)SPT_LANE_BUDGET, hres, li, lleaf, lleaf2);
             h = hres;
             casts += (unsigned long long)__popcll(__ballot(act && cdone));
         } else {

@@ -538,28 +538,20 @@ __device__ __forceinline__ void update_member_lane(float tc, float hh, const uin
 // lane follows its own preorder/skip path through the node records (two ds_read_b128
 // per lane and node) and tests only the leaves its own ray may need, their member
 // records read by vector loads.  A lane parks the leaves it meets (two at most; it
-// stops walking at the second) and the wave tests the parked leaves once
-// SPT_LANE_LEAF_T lanes hold one or no lane can walk on (Aila & Laine's postponed
-// leaves, while-while): the (lane, leaf) pairs are dealt one per lane, each tested
-// against its owner's ray and its winner merged back (SPT_LANE_PAIRS).  The wave walk (find_closest) pays for the union of its lanes'
+// stops walking at the second) and the wave tests the parked leaves -- each lane its
+// newest one -- once SPT_LANE_LEAF_T lanes hold one or no lane can walk on (Aila &
+// Laine's postponed leaves, while-while).  The wave walk (find_closest) pays for the union of its lanes'
 // leaves -- on config 5 a lane needs ~10% of the members the wave tests.  Node test,
 // margins and near bound are find_closest's, per lane; leaves are
 // tested in a lane-dependent order, and the winner is still the lexicographic minimum
 // of (distance, original index), which does not depend on the order.
 // SPT_DIAG counters here: nodes = lane node visits, live = walk iterations, leaves =
 // leaf passes, pairs = (lane, leaf) tests.
-// leaf pass threshold (lanes holding a parked leaf); with the pair passes 16 (config 5:
-// 8 / 12 / 16 / 20 lanes 72.89 / 71.15 / 70.71 / 70.64 ms), before them 24
 #ifndef SPT_LANE_LEAF_T
-#define SPT_LANE_LEAF_T 16
+#define SPT_LANE_LEAF_T 24
 #endif
 #ifndef SPT_LANE_GROUP
 #define SPT_LANE_GROUP 2
-#endif
-// 1: a leaf pass deals the wave's (lane, leaf) pairs one per lane (lane_cast, `pairs`:
-// 64 words of wave-private LDS)
-#ifndef SPT_LANE_PAIRS
-#define SPT_LANE_PAIRS 1
 #endif
 #ifndef SPT_LANE_STEPS
 #define SPT_LANE_STEPS 8
@@ -577,7 +569,7 @@ __device__ __forceinline__ void update_member_lane(float tc, float hh, const uin
 template <int LEAF, bool BYTES = false>
 __device__ __forceinline__ bool lane_cast(const AccelView &ac, const f3 &o, const f3 &d, bool active, CastDiag &dg,
                                           const uint32_t *lnodes, bool fresh, uint32_t budget, Hit &h, uint32_t &i,
-                                          uint32_t &leaf, uint32_t &leaf2, uint32_t *pairs = nullptr)
+                                          uint32_t &leaf, uint32_t &leaf2)
 {
     if (fresh) {
         h.idx = kMiss;
@@ -598,16 +590,18 @@ __device__ __forceinline__ bool lane_cast(const AccelView &ac, const f3 &o, cons
         for (int k = 0; k < SPT_GROUP; ++k) g4[k] = ld_uniform(slots, g * SPT_GROUP + k);
         test_group<SPT_GROUP>(g4, ac.orig, g * SPT_GROUP, o, d, dod, h, dg);
     }
-    const float olen = __builtin_amdgcn_sqrtf(oo) * 1.000001f;
     auto rcp_dir = [](float x) {
         const float m = __builtin_fmaxf(__builtin_fabsf(x), kBoxMinDir);
         return __builtin_amdgcn_rcpf(__builtin_copysignf(m, x));
     };
-    // the node test's per-lane slab terms; SPT_LANE_PAIRS recomputes them after a pair
-    // pass (from o, d) rather than keeping nine VGPRs live through it
-    float irx, iry, irz, qlx, qly, qlz, qhx, qhy, qhz;
-    auto slab_terms = [&]() {
-        const float el = __builtin_fmaf((float)kBoxS, __builtin_amdgcn_sqrtf(oo) * 1.000001f, 1e-6f);
+    const bool nocull = no_cull || (active && !(oo <= 1e30f));
+    // the node test's per-lane terms (slabs, front slack, near bound), formed from o, d and
+    // the winner
+    float irx, iry, irz, qlx, qly, qlz, qhx, qhy, qhz, neta, kn, sbl;
+    auto near_bound = [&](float best) { return __builtin_fmaf(__builtin_amdgcn_sqrtf(best), 1.00001f, kn); };
+    auto walk_terms = [&]() {
+        const float olen = __builtin_amdgcn_sqrtf(lensq(o)) * 1.000001f;
+        const float el = __builtin_fmaf((float)kBoxS, olen, 1e-6f);
         irx = rcp_dir(d.x);
         iry = rcp_dir(d.y);
         irz = rcp_dir(d.z);
@@ -617,14 +611,12 @@ __device__ __forceinline__ bool lane_cast(const AccelView &ac, const f3 &o, cons
         qhx = (el - o.x) * irx;
         qhy = (el - o.y) * iry;
         qhz = (el - o.z) * irz;
+        const float obs = olen + ac.pre_cm;
+        neta = -__builtin_fmaf(1e-6f, obs, 1e-6f);
+        kn = __builtin_fmaf(1e-5f, obs, 1e-6f);
+        sbl = near_bound(h.best);
     };
-    slab_terms();
-    const float obs = olen + ac.pre_cm;
-    const float neta = -__builtin_fmaf(1e-6f, obs, 1e-6f);
-    const float kn = __builtin_fmaf(1e-5f, obs, 1e-6f);
-    const bool nocull = no_cull || (active && !(oo <= 1e30f));
-    auto near_bound = [&](float best) { return __builtin_fmaf(__builtin_amdgcn_sqrtf(best), 1.00001f, kn); };
-    float sbl = near_bound(h.best);
+    walk_terms();
     const uint4 *ln = (const uint4 *)lnodes;
     const float4 *__restrict__ gs = ac.slots;
     const uint32_t n = BYTES ? ac.n_nodes << 5 : ac.n_nodes;  // end of the walk
@@ -639,95 +631,32 @@ __device__ __forceinline__ bool lane_cast(const AccelView &ac, const f3 &o, cons
         if ((mt | mp) == 0ull) break;
         if (mp != 0ull && (mt == 0ull || __popcll(mp) >= SPT_LANE_LEAF_T)) {
             if (SPT_DIAG) {
-                const unsigned long long nl = (unsigned long long)(__popcll(mp) + __popcll(__ballot(leaf2 != kNoSlot)));
+                const unsigned long long nl = (unsigned long long)__popcll(mp);
                 dg.leaves += 1;
                 dg.pairs += nl;
                 dg.lane_tests += (unsigned long long)LEAF * nl;
             }
-#if SPT_LANE_PAIRS
-            if (pairs) {
-                // the wave's (lane, leaf) pairs dealt one per lane: lane j tests pair j's
-                // LEAF members against its owner's ray (pulled by lane shuffles) and hands
-                // the pair's winner back; the owner merges it by the same (distance,
-                // original index) rule, so the result equals testing its leaves itself.
-                // A pass then costs LEAF member tests, not 2 LEAF with most lanes idle.
-                const unsigned long long m2 = __ballot(leaf2 != kNoSlot);
-                const uint32_t n1 = (uint32_t)__popcll(mp), np = n1 + (uint32_t)__popcll(m2);
-                const uint32_t ja = lane_rank(mp), jb = n1 + lane_rank(m2);
-                for (uint32_t b0 = 0; b0 < np; b0 += 64u) {
-                    // owners publish this round's pairs (leaf slot << 6 | owner lane); a
-                    // wave's LDS operations complete in order
-                    if (leaf != kNoSlot && ja - b0 < 64u) pairs[ja - b0] = (leaf << 6) | __lane_id();
-                    if (leaf2 != kNoSlot && jb - b0 < 64u) pairs[jb - b0] = (leaf2 << 6) | __lane_id();
-                    __builtin_amdgcn_wave_barrier();
-                    const bool has = b0 + __lane_id() < np;
-                    const uint32_t e = has ? pairs[__lane_id()] : 0u;
-                    __builtin_amdgcn_wave_barrier();
-                    const int ow = (int)(e & 63u);
-                    const uint32_t pl = e >> 6;
-                    const f3 po = mk(__shfl(o.x, ow), __shfl(o.y, ow), __shfl(o.z, ow));
-                    const f3 pd = mk(__shfl(d.x, ow), __shfl(d.y, ow), __shfl(d.z, ow));
-                    const float pdod = __shfl(dod, ow);
-                    Hit loc;
-                    loc.idx = kMiss;
-                    loc.best = FLT_MAX;
-                    loc.t = 0.f;
-                    if (has) {
-#pragma unroll 1
-                        for (int k0 = 0; k0 < LEAF; k0 += SPT_LANE_GROUP) {
-                            float4 m[SPT_LANE_GROUP];
-#pragma unroll
-                            for (int k = 0; k < SPT_LANE_GROUP; ++k) m[k] = gs[pl + k0 + k];
-#pragma unroll
-                            for (int k = 0; k < SPT_LANE_GROUP; ++k) {
-                                float tc, hh;
-                                if (ray_sphere(m[k], po, pd, tc, hh))
-                                    update_member_lane(tc, hh, ac.orig, pl + k0 + k, po, pd, pdod, loc);
-                            }
-                        }
-                    }
-                    // the pairs' winners back to their owners, merged in (distance, index)
-                    auto merge = [&](uint32_t j, bool mine) {
-                        const int src = (int)(j & 63u);
-                        const float bd = __shfl(loc.best, src), bt = __shfl(loc.t, src);
-                        const uint32_t bs = (uint32_t)__shfl((int)loc.idx, src);
-                        if (mine && bs != kMiss) {
-                            bool better = bd < h.best;
-                            if (__builtin_expect(bd == h.best && h.idx != kMiss, 0)) better = ac.orig[bs] < ac.orig[h.idx];
-                            h.best = better ? bd : h.best;
-                            h.idx = better ? bs : h.idx;
-                            h.t = better ? bt : h.t;
-                        }
-                    };
-                    merge(ja - b0, leaf != kNoSlot && ja - b0 < 64u);
-                    merge(jb - b0, leaf2 != kNoSlot && jb - b0 < 64u);
-                }
-                sbl = near_bound(h.best);
-                leaf = leaf2 = kNoSlot;
-                slab_terms();
-                continue;
-            }
-#endif
             if (leaf != kNoSlot) {
-                // the lane's parked leaves (one or two) as one run of members, taken
-                // SPT_LANE_GROUP at a time (8 waves/SIMD: 64 VGPRs; loading a whole
-                // leaf at once spills)
-                const int lim = leaf2 != kNoSlot ? 2 * LEAF : LEAF;
+                // the lane's newest parked leaf, its members SPT_LANE_GROUP at a time (8
+                // waves/SIMD: 64 VGPRs; loading a whole leaf at once spills).  A second
+                // leaf stays parked for a later pass and the lane walks on, so a pass is
+                // LEAF member tests (testing both kept the whole wave at 2 LEAF whenever
+                // one lane held two: config 5 71.8 -> 70.8 ms)
 #pragma unroll 1
-                for (int k0 = 0; k0 < lim; k0 += SPT_LANE_GROUP) {
-                    const uint32_t base = k0 < LEAF ? leaf + k0 : leaf2 + (k0 - LEAF);
+                for (int k0 = 0; k0 < LEAF; k0 += SPT_LANE_GROUP) {
                     float4 m[SPT_LANE_GROUP];
 #pragma unroll
-                    for (int k = 0; k < SPT_LANE_GROUP; ++k) m[k] = gs[base + k];
+                    for (int k = 0; k < SPT_LANE_GROUP; ++k) m[k] = gs[leaf + k0 + k];
 #pragma unroll
                     for (int k = 0; k < SPT_LANE_GROUP; ++k) {
                         float tc, hh;
                         if (ray_sphere(m[k], o, d, tc, hh))
-                            update_member_lane(tc, hh, ac.orig, base + k, o, d, dod, h);
+                            update_member_lane(tc, hh, ac.orig, leaf + k0 + k, o, d, dod, h);
                     }
                 }
                 sbl = near_bound(h.best);
-                leaf = leaf2 = kNoSlot;
+                leaf = leaf2;
+                leaf2 = kNoSlot;
             }
             continue;
         }

@@ -355,16 +355,23 @@ uint32_t full_grid(const spt_ctx *ctx)
 // (RenderArgs::n_queues), where small claims cost little and even out the tail: config 2
 // at 128 / 192 / 256 / 384 / 512 items 5.43 / 5.32 / 5.29 / 5.28 / 5.32 ms, its 1/8
 // rank share 0.78 / 0.78 / 0.80 / 0.91 / 1.03 ms (tools/scaling_probe.py), config 5
-// (lane walk) 89.1 / 88.8 / 89.3 / - / 91.8 ms.
-constexpr uint32_t kSmallClaim = 192, kClaim = 256, kBigClaim = 512;
+// (lane walk) 89.1 / 88.8 / 89.3 / - / 91.8 ms.  With primary
+// batches and the max-ILP build, launches of 12-64 Ki items per wave (config 2's full
+// frame) prefer 448: bench 20 533-20 561 (256) / 20 677-20 697 (384) / 20 727-20 731 (448)
+// / 20 699-20 707 (512) Msamples/s, while its rank shares still prefer 256 (384: the 1/2
+// share 2.414 -> 2.447 ms); trees walked lane by lane keep 256.
+constexpr uint32_t kSmallClaim = 192, kClaim = 256, kMidClaim = 448, kBigClaim = 512;
 uint32_t claim_size(const spt_ctx *ctx, uint64_t items)
 {
     if (ctx->claim) return ctx->claim;
     const uint64_t waves = std::max<uint64_t>((uint64_t)full_grid(ctx) * (ctx->block / 64), 1);
     const uint64_t fair = items / (waves * 4);
     const uint64_t per_wave = items / waves;
+    const bool lane = spt::lane_walk_tree(ctx->accel);
     const uint32_t cap = per_wave < 4096u ? kSmallClaim
-                       : (per_wave >= 65536u && !spt::lane_walk_tree(ctx->accel)) ? kBigClaim : kClaim;
+                       : lane ? kClaim
+                       : per_wave >= 65536u ? kBigClaim
+                       : per_wave >= 12288u ? kMidClaim : kClaim;
     return (uint32_t)std::min<uint64_t>(cap, std::max<uint64_t>(64, fair / 64 * 64));
 }
 

@@ -86,6 +86,14 @@ def cpu_model():
     return "unknown"
 
 
+def tiled_pixels(w, h, tc):
+    """Pixels RenderImageParallelMain actually renders: MakeRenderSegmentData tiles W / tc
+    columns and H / tc rows per tile (integer division, Renderer.hpp:264-265), so the
+    remainder columns / rows of the frame are never rendered (tc = 32 on 1200 x 800: 1 184
+    x 800 pixels)."""
+    return (w // tc) * tc * (h // tc) * tc
+
+
 def cpu_baseline(scene, view, w, h, spp_sample, bounces):
     """The CPU restatement (oracle/, "port", gcc -O2 -msse4.1) timed with the
     reference's RenderImageParallelMain tiling (Renderer.hpp:257-302: tc x tc tiles,
@@ -108,7 +116,7 @@ def cpu_baseline(scene, view, w, h, spp_sample, bounces):
             pyoracle.render_image_parallel(osc, fr, threads, mode=mode, want_rgba=False)
             dt = time.perf_counter() - t0
             wall += dt
-            res[(name, threads)] = round(w * h * spp_sample / dt / 1e6, 4)
+            res[(name, threads)] = round(tiled_pixels(w, h, threads) * spp_sample / dt / 1e6, 4)
     return {"value": res[("task", tc)], "unit": "Msamples/s", "cores": cores, "kind": "port",
             "segment_value": res[("segment", tc)], "threads": tc,
             "shipped_tc4": {"task": res[("task", 4)], "segment": res[("segment", 4)],
@@ -117,7 +125,8 @@ def cpu_baseline(scene, view, w, h, spp_sample, bounces):
             "sample": f"RenderSegmentTask (value) and RenderSegment (segment_value) of the oracle C restatement "
                       f"(gcc -O2 -msse4.1), RenderImageParallelMain tiling {tc}x{tc} with <= {tc} in flight on "
                       f"{cores} cores, and the shipped tc = 4; same scene/camera at {w}x{h}, {spp_sample} spp, "
-                      f"depth {bounces}; {wall:.1f} s wall for the four runs"}
+                      f"depth {bounces}; {wall:.1f} s wall for the four runs; rates count the pixels the tiling "
+                      f"renders ((W/tc)*tc x (H/tc)*tc, Renderer.hpp:264-265)"}
 
 
 def dropin_bench(w, h, spp, bounces, frames, tcs):
@@ -137,7 +146,7 @@ def dropin_bench(w, h, spp, bounces, frames, tcs):
                 raise RuntimeError(f"dropin harness failed: {r.stderr[-400:]}")
             sec = float(r.stdout.split("seconds=")[1].split()[0])
             key = f"{'task' if task else 'segment'}_tc{tc}"
-            out[key] = round(w * h * spp * frames / sec / 1e6, 3)
+            out[key] = round(tiled_pixels(w, h, tc) * spp * frames / sec / 1e6, 3)
             if "batches=" in r.stdout:  # calls per batched launch, over all frames run
                 calls = int(r.stdout.split("calls=")[1].split()[0])
                 batches = int(r.stdout.split("batches=")[1].split()[0])
@@ -223,6 +232,9 @@ def main():
                          "the previous one's last paths drain; each stream has its own workspace); 0 = auto: "
                          "2 when a frame is one workspace batch, else 1 (long multi-batch frames gain nothing "
                          "and would double the workspace)")
+    ap.add_argument("--service", type=int, default=1,
+                    help="1: frames are jobs of the resident render service (spt_service_start: one persistent "
+                         "launch per timed region, no launch ramp and tail per frame); 0: one launch per frame")
     ap.add_argument("--cpu-spp", type=int, default=0,
                     help="spp of the CPU-baseline sample (0: the config's own spp on config 2, scaled down on others)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -317,16 +329,27 @@ def main():
             render_frame(ctx, split, rank, mode, b["local"], b["gathered"], b["frame"], b["g_data"],
                          streams[k].cuda_stream, gather_events=ev)
 
+    # the render service (--service 1) is started around each timed region and stopped
+    # (drained) inside it: a device-wide synchronisation must not wait for its resident kernel
+    use_svc = args.service and args.engine == "megakernel"
+    if use_svc:
+        ctx.service_start()
     for _ in range(args.warmup):
         step()
+    if use_svc:
+        ctx.service_stop()
     torch.cuda.synchronize(dev)
     ctx.reset_stats()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
+    if use_svc:
+        ctx.service_start()
     for _ in range(args.steps):
         step(timed=True)
+    if use_svc:
+        ctx.service_stop()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -471,7 +494,8 @@ def main():
             if d:
                 out["dropin"] = {"unit": "Msamples/s", **d,
                                  "def": "C++ shim under RenderImageParallelMain tiling (tools/dropin_harness.cpp), "
-                                        "host g_data, tc=4 (shipped g_maxThreads) and tc=2*cores; "
+                                        "host g_data, tc=4 (shipped g_maxThreads) and tc=2*cores; rates count the "
+                                        "pixels the tiling renders ((W/tc)*tc x (H/tc)*tc, Renderer.hpp:264-265); "
                                         f"{args.dropin_frames} timed frames each"}
         print(json.dumps(out), flush=True)
         if args.dump:

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define SPT_ABI_VERSION 5
+#define SPT_ABI_VERSION 6
 
 /* Only the functions below are exported from libspt_hip.so (built with
  * -fvisibility=hidden), so several builds can be loaded side by side. */
@@ -89,6 +89,14 @@ typedef struct spt_stats {
                               for live lanes (lane-pretests) */
     uint64_t batches;       /* batched launches of concurrent spt_render_segment[_task] calls */
     uint64_t batched_calls; /* calls rendered in them */
+    /* render service (spt_service_start); the device counters above include a session's
+       waves once the session has ended (spt_service_stop, spt_synchronize) */
+    uint64_t svc_sessions;       /* service sessions (resident launches) started */
+    uint64_t svc_jobs;           /* jobs published to them */
+    uint64_t svc_watchdog_exits; /* sessions whose waves left after 100 ms without work */
+    double svc_kernel_ms;        /* summed device time of the ended sessions' launches */
+    uint32_t svc_running;        /* a session is resident now */
+    uint32_t svc_grid_blocks;    /* the service's grid (one block slot per CU left free) */
 } spt_stats;
 
 SPT_API int spt_abi_version(void);
@@ -216,6 +224,23 @@ SPT_API int spt_render_segment_task(spt_ctx *ctx, uint32_t yBegin, uint32_t yEnd
  * while the previous frame's last paths drain. */
 SPT_API int spt_render_rows_async(spt_ctx *ctx, int mode, uint32_t yBegin, uint32_t yEnd, uint32_t strip, uint32_t parts,
                           uint32_t part, uint32_t xBegin, uint32_t xEnd, void *d_rgba, void *d_rgb8, void *stream);
+/* ---- render service ----------------------------------------------------------------
+ * spt_service_start: from now on the renders of spt_render_rows_async, spt_render_frame
+ * and the unbatched host calls are jobs of a resident render service instead of launches
+ * of their own.  One launch of the service kernel (a "session") stays on the device and
+ * renders the jobs in the order they are published: claims of the next job fill the CUs
+ * while the last paths of the previous one drain, so consecutive frames, rank shares and
+ * sample batches pay no launch ramp and tail each.  A job's fold waits for its completion
+ * counter on the caller's stream (hipStreamWaitValue32); results are bit-identical to the
+ * launched renders.  Sessions start on the first job and end on spt_service_stop,
+ * spt_synchronize, a setter, a render the service does not take (lane-walk trees,
+ * spt_render_samples, the wavefront engine, jobs over half the 4 GiB slot ring) or a
+ * pause of 40 ms without jobs; a session's waves leave after 100 ms without work, so
+ * a device-wide synchronisation (hipDeviceSynchronize, torch.cuda.synchronize) waits at
+ * most that long.  spt_service_stop drains and ends the session and turns the service off. */
+SPT_API int spt_service_start(spt_ctx *ctx);
+SPT_API int spt_service_stop(spt_ctx *ctx);
+
 /* Number of rows the (yBegin, yEnd, strip, parts, part) map owns. */
 SPT_API int spt_rows_count(uint32_t yBegin, uint32_t yEnd, uint32_t strip, uint32_t parts, uint32_t part, uint32_t *rows);
 /* Scatter a gathered, rank-major stack of local float4 tiles (parts tiles of

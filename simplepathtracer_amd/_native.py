@@ -15,7 +15,7 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG_DIR, "lib", os.environ.get("SPT_LIB", "libspt_hip.so"))
 HEADER_PATH = os.path.join(os.path.dirname(PKG_DIR), "include", "spt_hip.h")
 
-ABI_VERSION = 5  # SPT_ABI_VERSION of include/spt_hip.h
+ABI_VERSION = 6  # SPT_ABI_VERSION of include/spt_hip.h
 SPT_OK = 0
 STATUS_NAMES = {0: "SPT_OK", 1: "SPT_ERR_ARG", 2: "SPT_ERR_STATE", 3: "SPT_ERR_HIP", 4: "SPT_ERR_NOMEM",
                 5: "SPT_ERR_NODEVICE"}
@@ -47,6 +47,12 @@ class Stats(ctypes.Structure):
         ("diag", ctypes.c_uint64 * 14),
         ("batches", ctypes.c_uint64),
         ("batched_calls", ctypes.c_uint64),
+        ("svc_sessions", ctypes.c_uint64),
+        ("svc_jobs", ctypes.c_uint64),
+        ("svc_watchdog_exits", ctypes.c_uint64),
+        ("svc_kernel_ms", ctypes.c_double),
+        ("svc_running", ctypes.c_uint32),
+        ("svc_grid_blocks", ctypes.c_uint32),
     ]
 
 
@@ -112,6 +118,8 @@ def lib() -> ctypes.CDLL:
         "spt_pin_host": ([P, P, ctypes.c_size_t], I),
         "spt_unpin_host": ([P, P], I),
         "spt_selftest_numerics": ([P, P, P, P, u32, P], I),
+        "spt_service_start": ([P], I),
+        "spt_service_stop": ([P], I),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

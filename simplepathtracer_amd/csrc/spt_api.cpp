@@ -14,6 +14,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cmath>
+#include <chrono>
 #include <condition_variable>
 #include <cstdarg>
 #include <cstdio>
@@ -90,6 +91,42 @@ struct Workspace {
     spt::WavefrontBuffers wf{};    // queues of the wavefront engine (allocated on first use)
     uint32_t *h_count = nullptr;   // pinned host word: queue length read back per pass
 };
+
+// The render service: one resident launch of render_kernel_svc per session
+// renders the jobs published to it -- every render of render_impl while the service is on
+// (frames, rank shares, sample batches, host-slot calls) -- so consecutive jobs follow each
+// other without a launch ramp and tail between them.  A job's sample words live in a ring
+// in HBM; its fold waits (hipStreamWaitValue32) on its completion counter.
+struct SvcInflight {
+    uint64_t w0, w1;    // ring words of its slots
+    uint32_t done_idx;  // its completion counter
+    hipEvent_t ev;      // recorded after its fold
+};
+struct Service {
+    bool enabled = false;  // spt_service_start: renders go through the service
+    bool running = false;  // a session's kernel is resident
+    hipStream_t stream = nullptr;  // the session kernel
+    hipStream_t pub = nullptr;     // publish and stop launches
+    uint32_t *d_ctl = nullptr;
+    spt::SvcJob *d_jobs = nullptr;
+    uint32_t *d_job_claim = nullptr, *d_done = nullptr, *d_ring = nullptr;
+    uint64_t ring_words = 0;
+    uint64_t ring_bytes = 4ull << 30;  // SPT_SVC_RING_MB
+    uint32_t job_cap = 1u << 16, done_cap = 4096;
+    uint32_t claim = 448, queues = spt::kMaxQueues;  // SPT_SVC_CLAIM, SPT_SVC_QUEUES
+    // session
+    int mode = 0;
+    uint32_t n_jobs = 0;
+    uint64_t claims = 0;  // published
+    uint64_t ring_head = 0;
+    uint32_t next_done = 0;
+    std::vector<SvcInflight> inflight;
+    std::vector<hipEvent_t> ev_pool;
+    hipEvent_t ev_start = nullptr, ev_end = nullptr, ev_ctl = nullptr;
+    std::chrono::steady_clock::time_point last_pub;
+    uint64_t sessions = 0, jobs = 0, watchdog_exits = 0;
+    double kernel_ms = 0;  // summed session spans
+};
 }  // namespace
 
 struct spt_ctx {
@@ -103,6 +140,9 @@ struct spt_ctx {
     uint32_t queues = spt::kMaxQueues;                         // claim counters (RenderArgs::n_queues)
     uint32_t grid_overlap = 0;  // grid while frames are in flight on several streams
     uint32_t grid_small = 0;    // grid_overlap for small launches (render_grid), 0 = none
+    // the render service's grid: the occupancy's blocks per CU minus one, always (its
+    // folds, publish launches and other streams' kernels need the free slot)
+    uint32_t svc_grid = 0;
     uint32_t last_grid = 0, last_block = 0;  // shape of the most recent render launch
 
     // scene (Globals.hpp:31-37)
@@ -113,7 +153,9 @@ struct spt_ctx {
     size_t shade_cap = 0, mat_cap = 0, slots_cap = 0, orig_cap = 0, nodes_cap = 0, kpre_cap = 0;
     spt::AccelTables tables;
     uint32_t n = 0;
-    uint32_t code_shift = 0;  // slot bits of a diffuse sample code (spt_internal.h code_word)
+    // diffuse sample codes (spt_internal.h diffuse_code): the slot count, and the halvings
+    // after which every finite albedo of the scene is 0 (j saturates at min(bounces - 1, jz))
+    uint32_t code_stride = 1, code_jz = 0;
     bool scene_set = false;
     // host copy of the hit geometry, to rebuild the traversal tables
     std::vector<float> h_centers, h_radii;
@@ -156,6 +198,9 @@ struct spt_ctx {
         bool owner;    // registered by this context (member 0 of a multi-device context)
     };
     std::vector<Pinned> pinned;
+    // serialises spt_pin_host / spt_unpin_host as a whole: they drop ctx->mu while they
+    // visit the member devices, and a concurrent pair must not both find and erase an entry
+    std::mutex pin_mu;
 
     // host-call slots (render_segment_host), created on demand up to host_slots
     std::vector<HostSlot *> slots;
@@ -199,6 +244,8 @@ struct spt_ctx {
     bool ref_recorded = false;
     std::vector<std::pair<double, double>> spans;
     uint64_t launches = 0;
+
+    Service svc;
 };
 
 namespace {
@@ -222,11 +269,15 @@ int fail(spt_ctx *ctx, int code, const char *fmt, ...)
             return fail((ctx), SPT_ERR_HIP, "%s failed: %s", #expr, hipGetErrorString(e_));        \
     } while (0)
 
+int svc_end(spt_ctx *ctx);
+
 template <class T>
 int ensure(spt_ctx *ctx, T **p, size_t *cap, size_t count)
 {
     if (*cap >= count && *p) return SPT_OK;
     if (*p) {
+        // a resident service session would hold the device synchronisation until it idles out
+        if (int rc = svc_end(ctx)) return rc;
         HIP_TRY(ctx, hipDeviceSynchronize());  // launches on caller streams may still read it
         HIP_TRY(ctx, hipFree(*p));
         *p = nullptr;
@@ -319,11 +370,46 @@ double busy_ms(const spt_ctx *ctx)
     return total;
 }
 
+// Halvings after which every finite albedo component a of the scene, as the diffuse code
+// rebuilds it (a * 0.5f, then * 0.5f per further bounce: spt_kernels.hip halve_n), is 0;
+// at most kCodeSat.  Saturating j there changes no colour (diffuse_code).
+uint32_t halvings_to_zero(const std::vector<float4> &shade)
+{
+    uint32_t jz = 0;
+    for (const float4 &s : shade)
+        for (float a : {s.x, s.y, s.z}) {
+            if (!std::isfinite(a)) continue;  // inf and NaN stay themselves
+            volatile float x = a * 0.5f;
+            uint32_t j = 0;
+            while (x != 0.f && j < spt::kCodeSat) {
+                x = x * 0.5f;
+                ++j;
+            }
+            jz = std::max(jz, j);
+        }
+    return jz;
+}
+
+// j's saturation of the diffuse codes at the context's depth: j <= bounces - 1 always
+uint32_t code_jmax(const spt_ctx *ctx)
+{
+    return std::min(ctx->bounces > 0 ? ctx->bounces - 1u : 0u, ctx->code_jz);
+}
+
+spt::DeviceScene device_scene(const spt_ctx *ctx)
+{
+    return spt::DeviceScene{ctx->d_shade, ctx->d_mat, ctx->n, ctx->code_stride, code_jmax(ctx), ctx->accel};
+}
+
 int check_ready(spt_ctx *ctx)
 {
     if (!ctx->scene_set) return fail(ctx, SPT_ERR_STATE, "scene not set (spt_set_scene)");
     if (!ctx->cam_set) return fail(ctx, SPT_ERR_STATE, "camera not set (spt_set_camera)");
     if (!ctx->params_set) return fail(ctx, SPT_ERR_STATE, "params not set (spt_set_params)");
+    if (!spt::code_layout_fits(ctx->code_stride, code_jmax(ctx)))
+        return fail(ctx, SPT_ERR_ARG,
+                    "%u sphere slots at depth %u exceed the sample code space ((jmax + 1) * slots + 1 <= %u, jmax = %u)",
+                    ctx->code_stride, ctx->bounces, spt::kCodeMax, code_jmax(ctx));
     return SPT_OK;
 }
 
@@ -462,8 +548,222 @@ int ensure_wavefront(spt_ctx *ctx, Workspace *w, uint32_t cap)
     return SPT_OK;
 }
 
+// ---- render service (DESIGN.md §5 "Render service") -----------------------------------
+// The host publishes to a session only while it has published within kSvcHostIdleMs;
+// after a longer pause it ends the session and starts a new one.  The session's waves
+// leave after spt::kSvcIdleTicks (100 ms) without work, more than twice that, so a job is
+// never published to a session that may have left.
+constexpr double kSvcHostIdleMs = 40.0;
+
+hipEvent_t svc_event(spt_ctx *ctx)
+{
+    Service &v = ctx->svc;
+    if (!v.ev_pool.empty()) {
+        hipEvent_t e = v.ev_pool.back();
+        v.ev_pool.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
+    return e;
+}
+
+// End the session: publish the stop flag after every job, wait for the kernel to drain
+// them and leave.  No-op without a session.
+int svc_end(spt_ctx *ctx)
+{
+    Service &v = ctx->svc;
+    if (!v.running) return SPT_OK;
+    v.running = false;
+    HIP_TRY(ctx, spt::launch_svc_stop(v.d_ctl, v.pub));
+    HIP_TRY(ctx, hipStreamSynchronize(v.stream));
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, v.ev_start, v.ev_end) == hipSuccess) v.kernel_ms += ms;
+    uint32_t wd = 0;
+    HIP_TRY(ctx, hipMemcpy(&wd, v.d_ctl + spt::kSvcWatchdog, sizeof wd, hipMemcpyDeviceToHost));
+    if (wd) v.watchdog_exits++;
+    return SPT_OK;
+}
+
+// Start a session for `mode` (the session's kernel arguments hold the scene, camera,
+// frame and mode of the context as they are now; the setters end the session).
+int svc_begin(spt_ctx *ctx, int mode)
+{
+    Service &v = ctx->svc;
+    if (!v.stream) {
+        HIP_TRY(ctx, hipStreamCreateWithFlags(&v.stream, hipStreamNonBlocking));
+        HIP_TRY(ctx, hipStreamCreateWithFlags(&v.pub, hipStreamNonBlocking));
+        HIP_TRY(ctx, hipEventCreate(&v.ev_start));
+        HIP_TRY(ctx, hipEventCreate(&v.ev_end));
+        HIP_TRY(ctx, hipEventCreateWithFlags(&v.ev_ctl, hipEventDisableTiming));
+        v.ring_words = v.ring_bytes / sizeof(uint32_t) / 2 * 2;
+        const bool ok = hipMalloc((void **)&v.d_ctl, spt::kSvcCtlWords * sizeof(uint32_t)) == hipSuccess &&
+                        hipMalloc((void **)&v.d_jobs, (size_t)v.job_cap * sizeof(spt::SvcJob)) == hipSuccess &&
+                        hipMalloc((void **)&v.d_job_claim, (size_t)v.job_cap * sizeof(uint32_t)) == hipSuccess &&
+                        hipMalloc((void **)&v.d_done, (size_t)v.done_cap * sizeof(uint32_t)) == hipSuccess &&
+                        hipMalloc((void **)&v.d_ring, (size_t)v.ring_words * sizeof(uint32_t)) == hipSuccess;
+        if (!ok) return fail(ctx, SPT_ERR_NOMEM, "render service buffers (%llu MiB ring) allocation failed",
+                             (unsigned long long)(v.ring_bytes >> 20));
+    }
+    spt::RenderArgs ra{};
+    ra.scene = device_scene(ctx);
+    ra.cam = ctx->cam;
+    ra.width = ctx->W;
+    ra.height = ctx->H;
+    ra.bounces = ctx->bounces;
+    ra.mode = (uint32_t)mode;
+    ra.seed_key = fmix64(ctx->seed);
+    ra.samples = v.d_ring;
+    ra.slot_words = mode == SPT_MODE_SEGMENT ? 1u : 2u;
+    ra.claim = v.claim;
+    ra.n_queues = v.queues;
+    ra.counters = ctx->d_counters;
+    ra.svc_ctl = v.d_ctl;
+    ra.svc_jobs = v.d_jobs;
+    ra.svc_job_claim = v.d_job_claim;
+    ra.svc_done = v.d_done;
+    // control words zeroed before the kernel and before any publish of the session
+    HIP_TRY(ctx, hipMemsetAsync(v.d_ctl, 0, spt::kSvcCtlWords * sizeof(uint32_t), v.stream));
+    HIP_TRY(ctx, hipEventRecord(v.ev_ctl, v.stream));
+    HIP_TRY(ctx, hipStreamWaitEvent(v.pub, v.ev_ctl, 0));
+    HIP_TRY(ctx, hipEventRecord(v.ev_start, v.stream));
+    HIP_TRY(ctx, spt::launch_render_svc(ra, ctx->svc_grid, v.stream));
+    HIP_TRY(ctx, hipEventRecord(v.ev_end, v.stream));
+    v.running = true;
+    v.mode = mode;
+    v.n_jobs = 0;
+    v.claims = 0;
+    v.sessions++;
+    v.last_pub = std::chrono::steady_clock::now();
+    return SPT_OK;
+}
+
+// Can render_impl hand a launch of `words` sample words to the service?
+bool svc_eligible(const spt_ctx *ctx, uint64_t words, bool keep_samples)
+{
+    const Service &v = ctx->svc;
+    return v.enabled && !keep_samples && ctx->engine == SPT_ENGINE_MEGAKERNEL && spt::svc_supported(ctx->accel) &&
+           words <= v.ring_bytes / sizeof(uint32_t) / 2;
+}
+
+// One job of a publication: a region (rows or interleaved strips, columns) at spp_batch
+// samples from sample s0, its slots at slot_local of the publication's ring region.
+struct SvcJobSpec {
+    spt::RowMap map;
+    uint32_t rows, spp_batch, s0;
+    spt::FastDiv div_band, div_tile, div_strip;
+    uint64_t slot_local;
+};
+
+// Publish jobs sharing one completion counter (a render_impl batch: one job; a batched
+// drop-in launch: one job per call) whose slots take total_slots consecutive ring slots,
+// and make stream s wait for all their samples.  Out: the ring word of the publication's
+// first slot and its counter (svc_retire after the folds).
+int svc_submit_jobs(spt_ctx *ctx, int mode, const SvcJobSpec *jobs, size_t n, uint64_t total_slots, hipStream_t s,
+                    uint64_t *w0_out, uint32_t *idx_out)
+{
+    Service &v = ctx->svc;
+    const uint32_t slot_words = mode == SPT_MODE_SEGMENT ? 1u : 2u;
+    uint64_t items = 0, nclaims = 0;
+    for (size_t i = 0; i < n; ++i) {
+        const uint64_t it = (uint64_t)spt::rows_owned(jobs[i].map) * jobs[i].map.width * jobs[i].spp_batch;
+        items += it;
+        nclaims += (it + v.claim - 1) / v.claim;
+    }
+    if (items > 0xFFFFFFFFull) return fail(ctx, SPT_ERR_ARG, "render service: %llu samples in one publication",
+                                           (unsigned long long)items);
+    const uint64_t words = total_slots * slot_words;
+    const auto now = std::chrono::steady_clock::now();
+    const double idle_ms = std::chrono::duration<double, std::milli>(now - v.last_pub).count();
+    // a new session: none yet, another mode, a pause (the kernel may idle out), a kernel
+    // that left already, or the session's job table / claim range full
+    if (!v.running || v.mode != mode || idle_ms >= kSvcHostIdleMs || hipEventQuery(v.ev_end) != hipErrorNotReady ||
+        v.n_jobs + n > v.job_cap || (v.claims + nclaims) * v.claim > 0x7FFFFFFFull) {
+        int rc = svc_end(ctx);
+        if (!rc) rc = svc_begin(ctx, mode);
+        if (rc) return rc;
+    }
+    if (v.ring_head + words > v.ring_words) v.ring_head = 0;
+    const uint64_t w0 = v.ring_head, w1 = w0 + words;
+    v.ring_head = w1;
+    const uint32_t idx = v.next_done;
+    v.next_done = (v.next_done + 1u) % v.done_cap;
+    // flow control on the publish stream: folds still reading the ring words, or jobs
+    // whose fold still waits on the counter, finish first (at most 1024 jobs in flight)
+    for (size_t i = 0; i < v.inflight.size();) {
+        SvcInflight &e = v.inflight[i];
+        const bool busy = (e.w0 < w1 && w0 < e.w1) || e.done_idx == idx || (i == 0 && v.inflight.size() >= 1024);
+        if (busy) {
+            HIP_TRY(ctx, hipStreamWaitEvent(v.pub, e.ev, 0));
+            v.ev_pool.push_back(e.ev);
+            v.inflight.erase(v.inflight.begin() + (std::ptrdiff_t)i);
+        } else {
+            ++i;
+        }
+    }
+    // the records, kSvcPubMax per publish launch; the first zeroes the counter
+    for (size_t i0 = 0; i0 < n; i0 += spt::kSvcPubMax) {
+        spt::SvcPublish p{};
+        p.ctl = v.d_ctl;
+        p.jobs = v.d_jobs;
+        p.job_claim = v.d_job_claim;
+        p.done = v.d_done;
+        p.first_job = v.n_jobs;
+        p.n_jobs = (uint32_t)std::min<size_t>(spt::kSvcPubMax, n - i0);
+        p.n_zero = i0 == 0 ? 1u : 0u;
+        p.zero_idx[0] = idx;
+        for (uint32_t k = 0; k < p.n_jobs; ++k) {
+            const SvcJobSpec &js = jobs[i0 + k];
+            const uint64_t it = (uint64_t)spt::rows_owned(js.map) * js.map.width * js.spp_batch;
+            const uint64_t nc = (it + v.claim - 1) / v.claim;
+            spt::SvcJob &j = p.rec[k];
+            j.item_off = (uint32_t)(v.claims * v.claim);
+            j.item_end = (uint32_t)(j.item_off + it);
+            j.slot_off = (uint32_t)(w0 / slot_words + js.slot_local);
+            j.done_idx = idx;
+            j.rows = js.rows;
+            j.spp_batch = js.spp_batch;
+            j.s0 = js.s0;
+            j.claim_end = (uint32_t)(v.claims + nc);
+            j.map = js.map;
+            j.div_band = js.div_band;
+            j.div_tile = js.div_tile;
+            j.div_strip = js.div_strip;
+            j.claim_first = (uint32_t)v.claims;
+            v.claims += nc;
+            v.n_jobs++;
+            v.jobs++;
+        }
+        p.pub_claims = (uint32_t)v.claims;
+        HIP_TRY(ctx, spt::launch_svc_publish(p, v.pub));
+    }
+    v.last_pub = now;
+    HIP_TRY(ctx, hipStreamWaitValue32(s, v.d_done + idx, (uint32_t)items, hipStreamWaitValueGte, 0xFFFFFFFFu));
+    *w0_out = w0;
+    *idx_out = idx;
+    return SPT_OK;
+}
+
+// One render_impl launch (`ra`: map, npix, spp_batch, s0, divisors) as one job.
+int svc_submit(spt_ctx *ctx, const spt::RenderArgs &ra, int mode, hipStream_t s, uint64_t *w0_out, uint32_t *idx_out)
+{
+    SvcJobSpec js{ra.map, ra.npix / ra.map.width, ra.spp_batch, ra.s0, ra.div_band, ra.div_tile, ra.div_strip, 0};
+    return svc_submit_jobs(ctx, mode, &js, 1, (uint64_t)ra.n_items, s, w0_out, idx_out);
+}
+
+// After the job's fold was enqueued on s: its ring words and counter are free once the
+// fold has run.
+int svc_retire(spt_ctx *ctx, hipStream_t s, uint64_t w0, uint64_t words, uint32_t idx)
+{
+    hipEvent_t e = svc_event(ctx);
+    if (!e) return fail(ctx, SPT_ERR_HIP, "event creation failed");
+    HIP_TRY(ctx, hipEventRecord(e, s));
+    ctx->svc.inflight.push_back(SvcInflight{w0, w0 + words, idx, e});
+    return SPT_OK;
+}
+
 // Fold arguments shared by every fold of ctx: the slots and the decode tables of the
-// sample words (shading table, sky colour, slot bits).
+// sample words (shading table, sky colour, code stride).
 spt::FoldArgs fold_args(const spt_ctx *ctx, const uint32_t *samples, uint32_t slot_words)
 {
     spt::FoldArgs fa{};
@@ -471,7 +771,7 @@ spt::FoldArgs fold_args(const spt_ctx *ctx, const uint32_t *samples, uint32_t sl
     fa.slot_words = slot_words;
     fa.shade = ctx->d_shade;
     for (int j = 0; j < 3; ++j) fa.sky[j] = ctx->cam.sky[j];
-    fa.code_shift = ctx->code_shift;
+    fa.code_div = spt::make_fastdiv(ctx->code_stride);
     return fa;
 }
 
@@ -529,10 +829,14 @@ int render_impl(spt_ctx *ctx, int mode, const spt::RowMap &map, float4 *d_rgba, 
     if (keep_samples && spp_batch != ctx->spp)
         return fail(ctx, SPT_ERR_ARG, "region * spp exceeds the workspace for spt_render_samples");
     const uint64_t items_max = (uint64_t)npix * spp_batch;
+    // the resident render service takes the launch when it is on and can (svc_eligible);
+    // a launch it cannot take ends the session first, so that launch has the whole GPU
+    const bool use_svc = svc_eligible(ctx, items_max * slot_words, keep_samples);
+    int rc = SPT_OK;
+    if (!use_svc && (rc = svc_end(ctx))) return rc;
     Workspace *w = workspace_for(ctx, s);
     if (!w) return SPT_ERR_STATE;
-    int rc = ensure(ctx, &w->d_samples, &w->samples_cap, items_max * slot_words);
-    if (rc) return rc;
+    if (!use_svc && (rc = ensure(ctx, &w->d_samples, &w->samples_cap, items_max * slot_words))) return rc;
     if (spp_batch < ctx->spp) {
         rc = ensure(ctx, &w->d_acc, &w->acc_cap, ar ? std::max(npix, ar->n) : npix);
         if (rc) return rc;
@@ -543,7 +847,7 @@ int render_impl(spt_ctx *ctx, int mode, const spt::RowMap &map, float4 *d_rgba, 
     // batch order (each waits for the previous one): the sums are unchanged.
     hipStream_t s2 = nullptr;
     Workspace *w2 = nullptr;
-    if (spp_batch < ctx->spp && !pg && !keep_samples && ctx->batch_dbuf && ctx->engine == SPT_ENGINE_MEGAKERNEL &&
+    if (!use_svc && spp_batch < ctx->spp && !pg && !keep_samples && ctx->batch_dbuf && ctx->engine == SPT_ENGINE_MEGAKERNEL &&
         (s2 = companion_for(ctx, s)) != nullptr && (w2 = workspace_for(ctx, s2)) != nullptr) {
         if ((rc = ensure(ctx, &w2->d_samples, &w2->samples_cap, items_max * slot_words))) return rc;
         // the companion starts after the work already queued on the caller's stream
@@ -557,7 +861,7 @@ int render_impl(spt_ctx *ctx, int mode, const spt::RowMap &map, float4 *d_rgba, 
     Workspace *const w_caller = w;
 
     spt::RenderArgs ra{};
-    ra.scene = spt::DeviceScene{ctx->d_shade, ctx->d_mat, ctx->n, ctx->code_shift, ctx->accel};
+    ra.scene = device_scene(ctx);
     ra.cam = ctx->cam;
     ra.width = ctx->W;
     ra.height = ctx->H;
@@ -617,7 +921,20 @@ int render_impl(spt_ctx *ctx, int mode, const spt::RowMap &map, float4 *d_rgba, 
         ra.div_band = spt::make_fastdiv(rows >= 8 ? 8u * map.width * b : 1u);
         ra.div_tile = spt::make_fastdiv(64u * b);
         EventPair ev = get_pair(ctx);
-        if (ctx->engine == SPT_ENGINE_WAVEFRONT) {
+        uint64_t svc_w0 = 0;
+        uint32_t svc_idx = 0;
+        if (use_svc) {
+            // published to the service; the stream waits for the job's completion counter
+            // (the events bracket that wait: the job's span as the stream sees it)
+            if (!ctx->ref_recorded) {
+                HIP_TRY(ctx, hipEventRecord(ctx->ref_ev, s));
+                ctx->ref_recorded = true;
+            }
+            HIP_TRY(ctx, hipEventRecord(ev.a, s));
+            if ((rc = svc_submit(ctx, ra, mode, s, &svc_w0, &svc_idx))) return rc;
+            HIP_TRY(ctx, hipEventRecord(ev.b, s));
+            fa.samples = ctx->svc.d_ring + svc_w0;
+        } else if (ctx->engine == SPT_ENGINE_WAVEFRONT) {
             // queue passes until every item is issued and the queue has drained; the
             // host reads the queue length back after each pass (4 bytes, pinned)
             const uint32_t cap = (uint32_t)std::min<uint64_t>(ctx->wf_cap, std::max<uint32_t>(ra.n_items, 1024u));
@@ -667,6 +984,7 @@ int render_impl(spt_ctx *ctx, int mode, const spt::RowMap &map, float4 *d_rgba, 
         HIP_TRY(ctx, hipEventRecord(ef.b, s));
         if (s2) HIP_TRY(ctx, hipEventRecord(ctx->dbuf_fold, s));
         ctx->pending_fold.push_back(ef);
+        if (use_svc && (rc = svc_retire(ctx, s, svc_w0, (uint64_t)npix * b * slot_words, svc_idx))) return rc;
         if (pg && pg->after_pass) {
             const int r = pg->after_pass(s0 + b);
             if (r < 0) return r;
@@ -717,12 +1035,11 @@ int rebuild_accel(spt_ctx *ctx)
                                           sh.leaf_slots);
     const std::string bad = spt::validate_accel(t, ctx->h_centers.data(), ctx->h_radii.data(), ctx->n);
     if (!bad.empty()) return fail(ctx, SPT_ERR_STATE, "traversal tables invalid: %s", bad.c_str());
-    // a diffuse sample's code holds its slot in code_shift bits (code_word)
-    uint32_t shift = 0;
-    while (shift < 32 && (1ull << shift) < t.slots.size()) ++shift;
-    if (shift > spt::kCodeMaxShift)
-        return fail(ctx, SPT_ERR_ARG, "%zu sphere slots exceed the sample code's %u slot bits", t.slots.size(),
-                    spt::kCodeMaxShift);
+    // a diffuse sample's code is 2 + j * slots + slot (diffuse_code); check_ready checks
+    // that the scene's codes fit at the frame's depth
+    const uint32_t jz = halvings_to_zero(ctx->h_shade);
+    if (!spt::code_layout_fits(t.slots.size(), 0))
+        return fail(ctx, SPT_ERR_ARG, "%zu sphere slots exceed the sample code space", t.slots.size());
     // shading tables in slot order: the kernel keeps the winner's slot, not its index
     std::vector<float4> shade(t.slots.size(), make_float4(0.f, 0.f, 0.f, 0.f));
     std::vector<uint32_t> mat(t.slots.size(), SPT_SKYBOX);
@@ -742,8 +1059,9 @@ int rebuild_accel(spt_ctx *ctx)
     if (rc) return rc;
     ctx->accel = spt::AccelView{ctx->d_slots, ctx->d_orig, ctx->d_nodes, t.always_groups, t.n_nodes,
                                 t.n_nodes > t.leaves ? 1u : 0u, t.leaf_slots, ctx->d_kpre, t.pre_cm};
+    ctx->code_stride = (uint32_t)std::max<size_t>(t.slots.size(), 1);
+    ctx->code_jz = jz;
     ctx->tables = std::move(t);
-    ctx->code_shift = shift;
     return SPT_OK;
 }
 
@@ -865,18 +1183,43 @@ int launch_batch(spt_ctx *ctx, BatchSet *bs, const std::vector<BatchReq *> &batc
         slot += (uint64_t)np * spp;
         px += np;
     }
+    // the render service takes the batch when it is on: one job per call, one counter
+    const bool use_svc = svc_eligible(ctx, slot * slot_words, false);
+    if (!use_svc && (rc = svc_end(ctx))) return rc;
     Workspace *w = workspace_for(ctx, bs->stream);
     if (!w) return SPT_ERR_STATE;
-    if ((rc = ensure(ctx, &w->d_samples, &w->samples_cap, (size_t)slot * slot_words))) return rc;
+    if (!use_svc && (rc = ensure(ctx, &w->d_samples, &w->samples_cap, (size_t)slot * slot_words))) return rc;
     if (any_rgba && (rc = ensure(ctx, &bs->d_stage, &bs->stage_cap, (size_t)pix))) return rc;
     const hipStream_t s = bs->stream;
+    uint64_t svc_w0 = 0;
+    uint32_t svc_idx = 0;
+    EventPair ev = get_pair(ctx);
+    if (use_svc) {
+        std::vector<SvcJobSpec> specs(n);
+        for (size_t i = 0; i < n; ++i) {
+            const spt::BatchRect &b = bs->h_rects[i];
+            specs[i] = SvcJobSpec{spt::RowMap{b.y0, b.y0 + b.rows, 1u, 1u, 0u, b.x0, b.w}, b.rows, spp, 0u, b.div_band,
+                                  b.div_tile, spt::make_fastdiv(1u), b.slot_off};
+        }
+        if (!ctx->ref_recorded) {
+            HIP_TRY(ctx, hipEventRecord(ctx->ref_ev, s));
+            ctx->ref_recorded = true;
+        }
+        HIP_TRY(ctx, hipEventRecord(ev.a, s));
+        if ((rc = svc_submit_jobs(ctx, mode, specs.data(), n, slot, s, &svc_w0, &svc_idx))) return rc;
+        HIP_TRY(ctx, hipEventRecord(ev.b, s));
+        // the fold reads each call's slots in the ring
+        for (size_t i = 0; i < n; ++i) bs->h_rects[i].slot_off += (uint32_t)(svc_w0 / slot_words);
+        ctx->pending_render.push_back(ev);
+        ctx->launches++;
+    }
     // up to kInlineRects rectangles travel in the kernel arguments; more in the table
     const bool inl = ctx->inline_rects && n <= spt::kInlineRects;
     if (!inl)
         HIP_TRY(ctx, hipMemcpyAsync(bs->d_rects, bs->h_rects, n * sizeof(spt::BatchRect), hipMemcpyHostToDevice, s));
 
     spt::RenderArgs ra{};
-    ra.scene = spt::DeviceScene{ctx->d_shade, ctx->d_mat, ctx->n, ctx->code_shift, ctx->accel};
+    ra.scene = device_scene(ctx);
     ra.cam = ctx->cam;
     ra.width = W;
     ra.height = H;
@@ -909,24 +1252,26 @@ int launch_batch(spt_ctx *ctx, BatchSet *bs, const std::vector<BatchReq *> &batc
 
     // the claim counters are zeroed by the previous batch's fold on this workspace
     // (FoldArgs::head_reset), or here when that fold did not run
-    if (!w->head_clean || !ctx->fold_resets_head)
-        HIP_TRY(ctx, hipMemsetAsync(w->d_head, 0, sizeof(uint32_t) * spt::kQueueStride * ra.n_queues, s));
-    w->head_clean = false;
-    if (!ctx->ref_recorded) {
-        HIP_TRY(ctx, hipEventRecord(ctx->ref_ev, s));
-        ctx->ref_recorded = true;
+    if (!use_svc) {
+        if (!w->head_clean || !ctx->fold_resets_head)
+            HIP_TRY(ctx, hipMemsetAsync(w->d_head, 0, sizeof(uint32_t) * spt::kQueueStride * ra.n_queues, s));
+        w->head_clean = false;
+        if (!ctx->ref_recorded) {
+            HIP_TRY(ctx, hipEventRecord(ctx->ref_ev, s));
+            ctx->ref_recorded = true;
+        }
+        HIP_TRY(ctx, hipEventRecord(ev.a, s));
+        spt::LaunchShape sh{render_grid(ctx, ra.n_items, claim, ctx->batch_grid_div), ctx->block, ctx->batch_grid_div,
+                            0, 0};
+        HIP_TRY(ctx, spt::launch_render(ra, sh, s));
+        ctx->last_grid = sh.ran_grid;
+        ctx->last_block = sh.ran_block;
+        HIP_TRY(ctx, hipEventRecord(ev.b, s));
+        ctx->pending_render.push_back(ev);
+        ctx->launches++;
     }
-    EventPair ev = get_pair(ctx);
-    HIP_TRY(ctx, hipEventRecord(ev.a, s));
-    spt::LaunchShape sh{render_grid(ctx, ra.n_items, claim, ctx->batch_grid_div), ctx->block, ctx->batch_grid_div, 0, 0};
-    HIP_TRY(ctx, spt::launch_render(ra, sh, s));
-    ctx->last_grid = sh.ran_grid;
-    ctx->last_block = sh.ran_block;
-    HIP_TRY(ctx, hipEventRecord(ev.b, s));
-    ctx->pending_render.push_back(ev);
-    ctx->launches++;
 
-    spt::FoldArgs fa = fold_args(ctx, w->d_samples, slot_words);
+    spt::FoldArgs fa = fold_args(ctx, use_svc ? ctx->svc.d_ring : w->d_samples, slot_words);
     fa.out_rgba = any_rgba ? bs->d_stage : nullptr;
     fa.out_rgb8 = any_g ? ctx->d_frame8 : nullptr;
     fa.width = W;
@@ -942,12 +1287,12 @@ int launch_batch(spt_ctx *ctx, BatchSet *bs, const std::vector<BatchReq *> &batc
     fa.inline_rects = inl ? 1u : 0u;
     if (inl)
         for (size_t i = 0; i < n; ++i) fa.rects_inline[i] = bs->h_rects[i];
-    fa.head_reset = ctx->fold_resets_head ? w->d_head : nullptr;
+    fa.head_reset = ctx->fold_resets_head && !use_svc ? w->d_head : nullptr;
     fa.head_queues = ra.n_queues;
     EventPair ef = get_pair(ctx);
     HIP_TRY(ctx, hipEventRecord(ef.a, s));
     HIP_TRY(ctx, spt::launch_fold(fa, s));
-    w->head_clean = true;
+    w->head_clean = !use_svc;
     HIP_TRY(ctx, hipEventRecord(ef.b, s));
     ctx->pending_fold.push_back(ef);
 
@@ -965,6 +1310,7 @@ int launch_batch(spt_ctx *ctx, BatchSet *bs, const std::vector<BatchReq *> &batc
                                           hipMemcpyDeviceToHost, s));
         }
     }
+    if (use_svc && (rc = svc_retire(ctx, s, svc_w0, slot * slot_words, svc_idx))) return rc;
     return SPT_OK;
 }
 
@@ -1185,6 +1531,7 @@ int spt_set_scene_one(spt_ctx *ctx, const float *centers4, const float *radii, c
 {
     if (!ctx) return fail(nullptr, SPT_ERR_ARG, "null context");
     std::lock_guard<std::mutex> lk(ctx->mu);
+    if (int rc_ = svc_end(ctx)) return rc_;  // the session holds the state this setter changes
     if (n > 0 && (!centers4 || !radii || !colors4 || !materials || !fuzz))
         return fail(ctx, SPT_ERR_ARG, "null scene array");
     HIP_TRY(ctx, hipSetDevice(ctx->device));
@@ -1209,6 +1556,7 @@ int spt_set_camera_one(spt_ctx *ctx, const float view[16], const float eye[4], c
 {
     if (!ctx) return fail(nullptr, SPT_ERR_ARG, "null context");
     std::lock_guard<std::mutex> lk(ctx->mu);
+    if (int rc_ = svc_end(ctx)) return rc_;  // the session holds the state this setter changes
     if (!view || !eye || !sky) return fail(ctx, SPT_ERR_ARG, "null camera array");
     for (int j = 12; j < 16; ++j)
         if (view[j] != 0.0f)
@@ -1226,6 +1574,7 @@ int spt_set_params_one(spt_ctx *ctx, uint32_t width, uint32_t height, uint32_t s
 {
     if (!ctx) return fail(nullptr, SPT_ERR_ARG, "null context");
     std::lock_guard<std::mutex> lk(ctx->mu);
+    if (int rc_ = svc_end(ctx)) return rc_;  // the session holds the state this setter changes
     if (width == 0 || height == 0) return fail(ctx, SPT_ERR_ARG, "empty frame %ux%u", width, height);
     if ((uint64_t)width * height * 3 > 0xFFFFFFFFull)
         return fail(ctx, SPT_ERR_ARG, "frame %ux%u overflows the reference's uint32 g_size", width, height);
@@ -1244,6 +1593,7 @@ int spt_set_cluster_size_one(spt_ctx *ctx, uint32_t k)
 {
     if (!ctx) return fail(nullptr, SPT_ERR_ARG, "null context");
     std::lock_guard<std::mutex> lk(ctx->mu);
+    if (int rc_ = svc_end(ctx)) return rc_;  // the session holds the state this setter changes
     if (k > spt::kClusterSlots && k != SPT_CLUSTER_AUTO)
         return fail(ctx, SPT_ERR_ARG, "cluster size %u > %u", k, spt::kClusterSlots);
     ctx->cluster_k = k;
@@ -1256,6 +1606,7 @@ int spt_set_cluster_tree_one(spt_ctx *ctx, uint32_t branching)
 {
     if (!ctx) return fail(nullptr, SPT_ERR_ARG, "null context");
     std::lock_guard<std::mutex> lk(ctx->mu);
+    if (int rc_ = svc_end(ctx)) return rc_;  // the session holds the state this setter changes
     if (branching == 1 || (branching > 64 && branching != SPT_TREE_AUTO))
         return fail(ctx, SPT_ERR_ARG, "tree branching %u not in {0, 2..64, SPT_TREE_AUTO}", branching);
     ctx->tree_branching = branching;
@@ -1268,6 +1619,7 @@ int spt_set_engine_one(spt_ctx *ctx, int engine)
 {
     if (!ctx) return fail(nullptr, SPT_ERR_ARG, "null context");
     std::lock_guard<std::mutex> lk(ctx->mu);
+    if (int rc_ = svc_end(ctx)) return rc_;  // the session holds the state this setter changes
     if (engine != SPT_ENGINE_MEGAKERNEL && engine != SPT_ENGINE_WAVEFRONT)
         return fail(ctx, SPT_ERR_ARG, "unknown engine %d", engine);
     ctx->engine = engine;
@@ -1278,6 +1630,7 @@ int spt_set_workspace_one(spt_ctx *ctx, uint64_t bytes)
 {
     if (!ctx) return fail(nullptr, SPT_ERR_ARG, "null context");
     std::lock_guard<std::mutex> lk(ctx->mu);
+    if (int rc_ = svc_end(ctx)) return rc_;  // the session holds the state this setter changes
     if (bytes < sizeof(float4)) return fail(ctx, SPT_ERR_ARG, "workspace too small");
     ctx->ws_bytes = bytes;
     return SPT_OK;
@@ -1323,6 +1676,7 @@ int spt_ctx_create(int device, spt_ctx **out)
     }
     int per_cu = 0;
     if (spt::render_occupancy(ctx->block, &per_cu) != hipSuccess || per_cu <= 0) per_cu = 1;
+    ctx->svc_grid = (uint32_t)(std::max(1, per_cu - 1) * ctx->num_cu);
     // launch_bounds / occupancy API may over-report by one block per CU for SGPR-heavy
     // kernels (MI355X_MICROARCH.md, Residency): the kernel needs no co-residency, so
     // extra blocks only queue.  SPT_BLOCKS_PER_CU overrides for tuning.
@@ -1346,6 +1700,13 @@ int spt_ctx_create(int device, spt_ctx **out)
         ctx->batch_sets = (uint32_t)std::min<int>((int)kMaxBatchSets, std::max(1, std::atoi(e)));
     if (const char *e = std::getenv("SPT_HOST_SLOTS"))
         ctx->host_slots = (uint32_t)std::min<int>((int)kMaxHostSlots, std::max(1, std::atoi(e)));
+    // SPT_SERVICE=1: the context starts with the render service on (spt_service_start)
+    if (const char *e = std::getenv("SPT_SERVICE")) ctx->svc.enabled = std::atoi(e) != 0;
+    if (const char *e = std::getenv("SPT_SVC_CLAIM")) ctx->svc.claim = (uint32_t)std::max(64, std::atoi(e) / 64 * 64);
+    if (const char *e = std::getenv("SPT_SVC_QUEUES"))
+        ctx->svc.queues = (uint32_t)std::min<int>((int)spt::kMaxQueues, std::max(1, std::atoi(e)));
+    if (const char *e = std::getenv("SPT_SVC_RING_MB"))
+        ctx->svc.ring_bytes = (uint64_t)std::max(64, std::atoi(e)) << 20;
     ctx->grid = (uint32_t)(per_cu * ctx->num_cu);
     ctx->grid_overlap = std::getenv("SPT_BLOCKS_PER_CU") || per_cu < 2 ? ctx->grid : (uint32_t)((per_cu - 1) * ctx->num_cu);
     ctx->grid_small = std::getenv("SPT_BLOCKS_PER_CU") || per_cu < 3 ? 0u : (uint32_t)((per_cu - 2) * ctx->num_cu);
@@ -1411,6 +1772,7 @@ void spt_ctx_destroy(spt_ctx *ctx)
 {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
+    (void)svc_end(ctx);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     for (auto *vec : {&ctx->pending_render, &ctx->pending_fold, &ctx->pool})
         for (EventPair &p : *vec) {
@@ -1452,6 +1814,17 @@ void spt_ctx_destroy(spt_ctx *ctx)
     for (hipEvent_t e : {ctx->dbuf_start, ctx->dbuf_fold})
         if (e) (void)hipEventDestroy(e);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    {
+        Service &v = ctx->svc;
+        for (void *b : {(void *)v.d_ctl, (void *)v.d_jobs, (void *)v.d_job_claim, (void *)v.d_done, (void *)v.d_ring})
+            if (b) (void)hipFree(b);
+        for (const SvcInflight &e : v.inflight) (void)hipEventDestroy(e.ev);
+        for (hipEvent_t e : v.ev_pool) (void)hipEventDestroy(e);
+        for (hipEvent_t e : {v.ev_start, v.ev_end, v.ev_ctl})
+            if (e) (void)hipEventDestroy(e);
+        for (hipStream_t st : {v.stream, v.pub})
+            if (st) (void)hipStreamDestroy(st);
+    }
     for (spt_ctx *p : ctx->peers) spt_ctx_destroy(p);
     delete ctx;
 }
@@ -1528,6 +1901,7 @@ int spt_pin_host(spt_ctx *ctx, void *ptr, size_t bytes)
 {
     if (!ctx) return fail(nullptr, SPT_ERR_ARG, "null context");
     if (!ptr || bytes == 0) return fail(ctx, SPT_ERR_ARG, "null or empty host buffer");
+    std::lock_guard<std::mutex> plk(ctx->pin_mu);
     {
         std::lock_guard<std::mutex> lk(ctx->mu);
         for (const spt_ctx::Pinned &p : ctx->pinned)
@@ -1557,6 +1931,7 @@ int spt_unpin_host(spt_ctx *ctx, void *ptr)
     auto find = [&](spt_ctx *c) {
         return std::find_if(c->pinned.begin(), c->pinned.end(), [&](const spt_ctx::Pinned &p) { return p.ptr == ptr; });
     };
+    std::lock_guard<std::mutex> plk(ctx->pin_mu);
     {
         std::lock_guard<std::mutex> lk(ctx->mu);
         if (find(ctx) == ctx->pinned.end() || !find(ctx)->owner)
@@ -1566,15 +1941,19 @@ int spt_unpin_host(spt_ctx *ctx, void *ptr)
     for (spt_ctx *m : ctx->peers) {
         std::lock_guard<std::mutex> lk(m->mu);
         HIP_TRY(ctx, hipSetDevice(m->device));
+        if (svc_end(m)) return fail(ctx, SPT_ERR_HIP, "member device %d: %s", m->device, m->err.c_str());
         HIP_TRY(ctx, hipDeviceSynchronize());
         auto it = find(m);
         if (it != m->pinned.end()) m->pinned.erase(it);
     }
     std::lock_guard<std::mutex> lk(ctx->mu);
     HIP_TRY(ctx, hipSetDevice(ctx->device));
+    if (int rc = svc_end(ctx)) return rc;
     HIP_TRY(ctx, hipDeviceSynchronize());
+    const auto it = find(ctx);
+    if (it == ctx->pinned.end() || !it->owner) return fail(ctx, SPT_ERR_ARG, "buffer %p was not pinned", ptr);
     HIP_TRY(ctx, hipHostUnregister(ptr));
-    ctx->pinned.erase(find(ctx));
+    ctx->pinned.erase(it);
     return SPT_OK;
 }
 
@@ -1605,10 +1984,15 @@ int spt_render_frame(spt_ctx *ctx, int mode, float *rgba_out, uint8_t *g_data)
     // event), scatters them into the frame (assemble_kernel) and copies the frame back.
     // RenderImage's RenderSegmentTask({0, H, 0, W}) on a non-square frame aliases pixels
     // across rows (colorIndex = dx + dy * H, TaskBasedPathTracer.hpp:103,186,196-205), so
-    // a strip split cannot resolve it locally: there member r owns the colorIndex range
-    // [r L, (r + 1) L), renders the rows holding its sources (every row whose pixels map
-    // into the range: about L / W + W / H rows) and folds the range; the ranges are the
-    // frame's pixels in row-major order, so member 0 places them end to end.
+    // a strip split cannot resolve it locally: there member r owns a colorIndex range
+    // [i0_r, i1_r), renders the rows holding its sources (every row whose pixels map into
+    // the range: about (i1_r - i0_r) / H + W / H rows) and folds the range; the ranges are
+    // the frame's pixels in row-major order, so member 0 places them end to end.  Only
+    // outputs up to p_max = (W - 1) + (H - 1) H have sources (the rest resolve to NaN
+    // without any render), so the source-holding outputs are dealt evenly and the
+    // last member also takes the source-less tail: every member renders about the same
+    // number of rows (an even split of all W H outputs left members idle: 2 of 8 on a
+    // 1200 x 800 frame, all but member 0 when W is about 10 H).
     std::vector<spt_ctx *> m{ctx};
     m.insert(m.end(), ctx->peers.begin(), ctx->peers.end());
     const uint32_t parts = (uint32_t)m.size();
@@ -1623,18 +2007,28 @@ int spt_render_frame(spt_ctx *ctx, int mode, float *rgba_out, uint8_t *g_data)
     const uint32_t strip = even_strip(H, parts);
     const bool alias = mode == SPT_MODE_TASK && W != H;
     const uint64_t total = (uint64_t)W * H;
-    const uint32_t L = (uint32_t)((total + parts - 1) / parts);  // colorIndex range per member (alias)
+    // alias: outputs [0, n_src) have sources (p_max + 1 = W + (H - 1) H, at most W H)
+    const uint64_t n_src = std::min<uint64_t>(total, (uint64_t)W + (uint64_t)(H - 1u) * H);
+    const uint64_t L = (n_src + parts - 1) / parts;  // source-holding outputs per member (alias)
     uint32_t max_rows = 0;
     for (uint32_t r = 0; r < parts; ++r) max_rows = std::max(max_rows, spt::rows_owned(spt::RowMap{0, H, strip, parts, r, 0, W}));
-    const size_t tile = alias ? (size_t)L : (size_t)max_rows * W;
     auto range_of = [&](uint32_t r) {
-        const uint64_t i0 = std::min<uint64_t>((uint64_t)r * L, total), i1 = std::min<uint64_t>(i0 + L, total);
+        const uint64_t i0 = std::min<uint64_t>((uint64_t)r * L, n_src);
+        const uint64_t i1 = r + 1 == parts ? total : std::min<uint64_t>(i0 + L, n_src);
         return std::make_pair((uint32_t)i0, (uint32_t)i1);
     };
+    // a member's tile: its strips, or its colorIndex range (the largest: the last member's,
+    // with the source-less tail); member 0 stacks the tiles (alias: the whole frame)
+    size_t tile = (size_t)max_rows * W;
+    if (alias) {
+        tile = 0;
+        for (uint32_t r = 0; r < parts; ++r) tile = std::max<size_t>(tile, range_of(r).second - range_of(r).first);
+    }
+    const size_t stack = alias ? (size_t)total : tile * parts;
     // member 0's buffers live on member 0's device: the setters (for_members) and the
     // previous frame leave another member's device current
     HIP_TRY(ctx, hipSetDevice(ctx->device));
-    int rc = ensure(ctx, &ctx->d_tile, &ctx->tile_cap, tile * parts);  // member 0: the gathered stack
+    int rc = ensure(ctx, &ctx->d_tile, &ctx->tile_cap, std::max(stack, tile));  // member 0: the gathered stack
     if (rc) return rc;
     if ((rc = check_on_device(ctx, ctx->d_tile, "the gathered tile stack"))) return rc;
     for (uint32_t r = 0; r < parts; ++r) {
@@ -1667,8 +2061,10 @@ int spt_render_frame(spt_ctx *ctx, int mode, float *rgba_out, uint8_t *g_data)
         const size_t n_r = alias ? (size_t)(range_of(r).second - range_of(r).first)
                                  : (size_t)spt::rows_owned(spt::RowMap{0, H, strip, parts, r, 0, W}) * W;
         HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, c->frame_ev, 0));
+        // alias: member r's range lands at its first output, so the stack is the frame
+        const size_t at = alias ? (size_t)range_of(r).first : (size_t)r * tile;
         if (n_r)
-            HIP_TRY(ctx, hipMemcpyPeerAsync(ctx->d_tile + r * tile, ctx->device, c->d_tile, c->device,
+            HIP_TRY(ctx, hipMemcpyPeerAsync(ctx->d_tile + at, ctx->device, c->d_tile, c->device,
                                             n_r * sizeof(float4), ctx->stream));
     }
     float4 *dframe = nullptr;
@@ -1700,6 +2096,25 @@ int spt_render_frame(spt_ctx *ctx, int mode, float *rgba_out, uint8_t *g_data)
     }
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     return SPT_OK;
+}
+
+int spt_service_start(spt_ctx *ctx)
+{
+    return for_members(ctx, [](spt_ctx *c) {
+        std::lock_guard<std::mutex> lk(c->mu);
+        c->svc.enabled = true;
+        return SPT_OK;
+    });
+}
+
+int spt_service_stop(spt_ctx *ctx)
+{
+    return for_members(ctx, [](spt_ctx *c) {
+        std::lock_guard<std::mutex> lk(c->mu);
+        HIP_TRY(c, hipSetDevice(c->device));
+        c->svc.enabled = false;
+        return svc_end(c);
+    });
 }
 
 int spt_rows_count(uint32_t yB, uint32_t yE, uint32_t strip, uint32_t parts, uint32_t part, uint32_t *rows)
@@ -1751,14 +2166,18 @@ int spt_assemble_rows_async(spt_ctx *ctx, const void *d_tiles, uint32_t max_rows
 int spt_synchronize(spt_ctx *ctx)
 {
     if (!ctx) return fail(nullptr, SPT_ERR_ARG, "null context");
+    // a resident service session ends first (its kernel would keep the device busy until it
+    // idles out); the next render starts a new one
     for (spt_ctx *c : ctx->peers) {
         std::lock_guard<std::mutex> lk(c->mu);
         HIP_TRY(ctx, hipSetDevice(c->device));
+        if (svc_end(c)) return fail(ctx, SPT_ERR_HIP, "member device %d: %s", c->device, c->err.c_str());
         HIP_TRY(ctx, hipDeviceSynchronize());
         if (collect_timings(c)) return fail(ctx, SPT_ERR_HIP, "member device %d: %s", c->device, c->err.c_str());
     }
     std::lock_guard<std::mutex> lk(ctx->mu);
     HIP_TRY(ctx, hipSetDevice(ctx->device));
+    if (int rc = svc_end(ctx)) return rc;
     HIP_TRY(ctx, hipDeviceSynchronize());
     return collect_timings(ctx);
 }
@@ -1774,18 +2193,31 @@ int spt_render_samples(spt_ctx *ctx, int mode, uint32_t yB, uint32_t yE, uint32_
     if (yB >= yE || xB >= xE) return SPT_OK;
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     spt::RowMap map{yB, yE, 1u, 1u, 0u, xB, xE - xB};
-    if ((rc = render_impl(ctx, mode, map, nullptr, nullptr, ctx->stream, true))) return rc;
-    // decode the sample words on the device: out[p * spp + s] = {r, g, b, counted}
+    // the sample words are decoded on the device, out[p * spp + s] = {r, g, b, counted},
+    // in chunks of pixels through one staging buffer of at most 256 MiB, allocated before
+    // the render (a failed allocation leaves nothing rendered)
     const size_t npix = (size_t)(xE - xB) * (yE - yB);
+    const size_t per_px = (size_t)ctx->spp * sizeof(float4);
+    const size_t chunk = std::max<size_t>(1, std::min(npix, ((size_t)256 << 20) / per_px));
     float4 *d_out = nullptr;
-    HIP_TRY(ctx, hipMalloc((void **)&d_out, npix * ctx->spp * sizeof(float4)));
+    if (hipMalloc((void **)&d_out, chunk * per_px) != hipSuccess)
+        return fail(ctx, SPT_ERR_NOMEM, "spt_render_samples: %zu bytes of staging", chunk * per_px);
+    if ((rc = render_impl(ctx, mode, map, nullptr, nullptr, ctx->stream, true))) {
+        (void)hipFree(d_out);
+        return rc;
+    }
     spt::FoldArgs fa = fold_args(ctx, workspace_for(ctx, ctx->stream)->d_samples, mode == SPT_MODE_SEGMENT ? 1u : 2u);
     fa.map = map;
     fa.npix = (uint32_t)npix;
     fa.spp_batch = ctx->spp;
-    hipError_t e = spt::launch_expand(fa, d_out, ctx->stream);
-    if (e == hipSuccess) e = hipMemcpyAsync(out, d_out, npix * ctx->spp * sizeof(float4), hipMemcpyDeviceToHost, ctx->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    hipError_t e = hipSuccess;
+    for (size_t p0 = 0; p0 < npix && e == hipSuccess; p0 += chunk) {
+        const size_t n = std::min(chunk, npix - p0);
+        e = spt::launch_expand(fa, d_out, (uint32_t)p0, (uint32_t)n, ctx->stream);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(out + p0 * ctx->spp * 4, d_out, n * per_px, hipMemcpyDeviceToHost, ctx->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    }
     (void)hipFree(d_out);
     if (e != hipSuccess) return fail(ctx, SPT_ERR_HIP, "spt_render_samples: %s", hipGetErrorString(e));
     return collect_timings(ctx);
@@ -1813,6 +2245,12 @@ int stats_one(spt_ctx *ctx, spt_stats *out)
     out->block_threads = ctx->last_block ? ctx->last_block : ctx->block;
     out->batches = ctx->batches;
     out->batched_calls = ctx->batched_calls;
+    out->svc_sessions = ctx->svc.sessions;
+    out->svc_jobs = ctx->svc.jobs;
+    out->svc_watchdog_exits = ctx->svc.watchdog_exits;
+    out->svc_kernel_ms = ctx->svc.kernel_ms;
+    out->svc_running = ctx->svc.running ? 1u : 0u;
+    out->svc_grid_blocks = ctx->svc_grid;
     return SPT_OK;
 }
 
@@ -1820,12 +2258,15 @@ int reset_one(spt_ctx *ctx)
 {
     std::lock_guard<std::mutex> lk(ctx->mu);
     HIP_TRY(ctx, hipSetDevice(ctx->device));
-    int rc = collect_timings(ctx);
+    int rc = svc_end(ctx);  // its waves add their counts when they leave
+    if (!rc) rc = collect_timings(ctx);
     if (rc) return rc;
     HIP_TRY(ctx, hipMemset(ctx->d_counters, 0, kCounters * sizeof(unsigned long long)));
     ctx->render_ms = ctx->fold_ms = ctx->last_render_ms = 0;
     ctx->launches = 0;
     ctx->batches = ctx->batched_calls = 0;
+    ctx->svc.sessions = ctx->svc.jobs = ctx->svc.watchdog_exits = 0;
+    ctx->svc.kernel_ms = 0;
     ctx->spans.clear();
     ctx->ref_recorded = false;
     return SPT_OK;

@@ -173,14 +173,33 @@ __host__ __device__ inline void ts_slot_base(uint32_t lr, uint32_t col, uint32_t
 //   * 0 (the specular-event cap; RenderSegmentTask's dropped paths).
 // A finite k is 0 or at least 2^-24 in magnitude (fl(y + 1) for float y: only y = -1
 // lies within 2^-24 of -1), so the words whose magnitude as a float is below 2^-24 and
-// nonzero never hold a k: they carry the codes c in [1, 2 (kCodeSmall - 1)], positive
-// words first, then the same magnitudes with the sign bit.  c = 1 is the colour 0,
-// c = 2 + (j << shift | slot) a diffuse sample; after kCodeSat halvings every finite
-// albedo is 0 (and inf / NaN stay themselves), so j saturates there.  The fold rebuilds
-// the colour with the render kernel's own operations: bit-identical.
-constexpr uint32_t kCodeSmall = 0x33800000u;  // bits of 2^-24
-constexpr uint32_t kCodeSat = 280;            // 2^-280 * FLT_MAX rounds to 0
-constexpr uint32_t kCodeMaxShift = 22;        // (kCodeSat + 1) << 22 codes fit
+// nonzero never hold a k: they carry the codes c in [1, kCodeMax], positive words
+// first, then the same magnitudes with the sign bit.  c = 1 is the colour 0,
+// c = 2 + j * stride + slot a diffuse sample (stride = the scene's slot count).  j is
+// saturated at jmax = min(bounces - 1, jz): j <= bounces - 1 always, and after jz
+// halvings every finite albedo of the scene is 0 (inf / NaN stay themselves; jz <=
+// kCodeSat, since 2^-280 * FLT_MAX rounds to 0), so saturating there changes no colour.
+// A scene fits when (jmax + 1) * stride + 1 <= kCodeMax: ~34 M slots at depth 50, ~11 M
+// for deep paths over albedos up to 255 (jz = 157).  The fold rebuilds the colour with
+// the render kernel's own operations: bit-identical.
+constexpr uint32_t kCodeSmall = 0x33800000u;        // bits of 2^-24
+constexpr uint32_t kCodeMax = 2u * (kCodeSmall - 1u);  // the largest code
+constexpr uint32_t kCodeSat = 280;                  // 2^-280 * FLT_MAX rounds to 0
+__host__ __device__ inline bool code_layout_fits(uint64_t stride, uint32_t jmax)
+{
+    return (jmax + 1ull) * stride + 1ull <= kCodeMax;
+}
+// diffuse code of (j, slot) and back (div = FastDiv(stride), defined below)
+__host__ __device__ inline uint32_t diffuse_code(uint32_t j, uint32_t slot, uint32_t stride)
+{
+    return 2u + j * stride + slot;
+}
+__host__ __device__ inline void diffuse_decode(uint32_t c, const FastDiv &div, uint32_t &j, uint32_t &slot)
+{
+    const uint32_t v = c - 2u;  // < kCodeMax < 2^31 (fast_div's range)
+    j = fast_div(v, div);
+    slot = v - j * div.d;
+}
 __host__ __device__ inline uint32_t code_word(uint32_t c)
 {
     return c < kCodeSmall ? c : 0x80000000u | (c - kCodeSmall + 1u);
@@ -229,7 +248,7 @@ struct DeviceScene {
     const float4 *shade;    // {red, green, blue, fuzz} per slot (hit geometry: accel.slots)
     const uint32_t *mat;    // material id per slot
     uint32_t n;
-    uint32_t code_shift;    // slot bits of a diffuse sample code (code_word)
+    uint32_t code_stride, code_jmax;  // diffuse sample codes (diffuse_code)
     AccelView accel;
 };
 
@@ -285,17 +304,78 @@ struct RenderArgs {
     // kernel arguments (inline_rects = 1: no table upload before the launch)
     uint32_t inline_rects;
     BatchRect rects_inline[kInlineRects];
+    // render service (render_kernel_svc): the session's control words
+    // (SvcCtl), job table, first claim of every job and completion counters; the fields
+    // above then hold the session's constants only (scene, camera, frame, mode, ring of
+    // sample slots in `samples`, claim size, n_queues)
+    uint32_t *svc_ctl;
+    const struct SvcJob *svc_jobs;
+    const uint32_t *svc_job_claim;
+    uint32_t *svc_done;
 };
 
 // claim counters: at most one per XCD, 256 bytes apart (separate cache lines)
 constexpr uint32_t kMaxQueues = 8, kQueueStride = 64;
+
+// ---- render service (DESIGN.md §5 "Render service") --------------------------------
+// One resident launch of render_kernel_svc renders a stream of jobs (a frame, a rank's
+// strips, a sample batch, a drop-in tile), published while it runs.  A session's claims
+// form one sequence: job j owns claims [job_claim[j], job_claim[j] + n) of `claim` items,
+// its items [item_off, item_end) (item_off = its first claim * claim, the rest of its last
+// claim is padding).  Queue q of n_queues reserves claims q, q + n_queues, ... from its
+// counter; a wave keeps one reserved claim and takes it once the publish kernel has
+// published it.  Finished samples are counted per completion counter (several jobs may
+// share one); hipStreamWaitValue32 on the counter gates the job's fold.
+struct SvcJob {
+    uint32_t item_off, item_end;  // session items of the job
+    uint32_t slot_off;            // slot of its item 0 in the ring (samples, item order)
+    uint32_t done_idx;            // its completion counter
+    uint32_t rows, spp_batch, s0; // region rows; samples of the batch and the first one
+    uint32_t claim_end;           // first claim after the job
+    RowMap map;                   // region (rows or interleaved strips, columns)
+    FastDiv div_band, div_tile, div_strip;  // ts_item / row_of_fast divisors
+    uint32_t claim_first;         // its first claim (item_off / claim)
+    uint32_t pad[7];
+};
+static_assert(sizeof(SvcJob) == 128, "SvcJob: 32 words, one per lane of the loading wave");
+constexpr uint32_t kSvcJobWords = 32;
+// SvcCtl words (svc_ctl): claim counters head[q * kQueueStride] (q < kMaxQueues), then on
+// lines of their own the published pair {claims, jobs} (one 64-bit word, stored and
+// loaded as one), the stop flag, and the watchdog word (nonzero: the session ended
+// after kSvcIdleTicks without work; the host restarts it).
+constexpr uint32_t kSvcPub = kMaxQueues * kQueueStride;  // uint64_t: claims | jobs << 32
+constexpr uint32_t kSvcStop = kSvcPub + 64;
+constexpr uint32_t kSvcWatchdog = kSvcStop + 64;
+constexpr uint32_t kSvcCtlWords = kSvcWatchdog + 64;
+// a wave with no work for 2 s (s_memrealtime, 100 MHz) leaves; the host never lets a
+// session idle 1 s before publishing to it (it restarts it), so no job is ever lost
+constexpr unsigned long long kSvcIdleTicks = 200000000ull;
+// jobs published by one publish launch (their records travel in its kernel arguments)
+constexpr uint32_t kSvcPubMax = 16;
+struct SvcPublish {
+    uint32_t *ctl;
+    SvcJob *jobs;
+    uint32_t *job_claim;
+    uint32_t *done;
+    uint32_t first_job, n_jobs;  // records [first_job, first_job + n_jobs)
+    uint32_t pub_claims;         // claims published after them
+    uint32_t n_zero;             // completion counters zeroed before the jobs are published
+    uint32_t zero_idx[kSvcPubMax];
+    SvcJob rec[kSvcPubMax];
+};
+hipError_t launch_render_svc(const RenderArgs &a, uint32_t grid, hipStream_t s);
+hipError_t launch_svc_publish(const SvcPublish &p, hipStream_t s);
+hipError_t launch_svc_stop(uint32_t *ctl, hipStream_t s);
+// the service covers the wave-walk kernels (render_kernel's shapes); the lane-walk
+// trees (LDS / global-memory node tables) keep their own launches
+bool svc_supported(const AccelView &ac);
 
 struct FoldArgs {
     const uint32_t *samples;  // slot_words per slot, in item order (ts_slot_base)
     uint32_t slot_words;
     const float4 *shade;      // the scene's shading table (diffuse codes name its slots)
     float sky[3];             // initColor (sky words)
-    uint32_t code_shift;
+    FastDiv code_div;         // FastDiv(code stride): diffuse_decode
     float4 *acc;         // persistent accumulator (w = sample count)
     float4 *out_rgba;    // nullable, local pixel order
     uint8_t *out_rgb8;   // nullable, full frame (g_data layout)
@@ -354,7 +434,8 @@ size_t wavefront_scan_bytes(uint32_t cap);
 hipError_t launch_wavefront_pass(const WavefrontBuffers &b, const RenderArgs &a, uint32_t cur, uint32_t n_cur,
                                  uint32_t gen_base, uint32_t gen_n, hipStream_t s);
 hipError_t launch_fold(const FoldArgs &a, hipStream_t s);
-hipError_t launch_expand(const FoldArgs &a, float4 *out, hipStream_t s);  // spt_render_samples
+// spt_render_samples: pixels [p0, p0 + n) of the region, out[(p - p0) * spp + s]
+hipError_t launch_expand(const FoldArgs &a, float4 *out, uint32_t p0, uint32_t n, hipStream_t s);
 hipError_t launch_assemble(const float4 *tiles, uint32_t max_rows, RowMap base, uint32_t width, uint32_t height,
                            float4 *frame, uint8_t *rgb8, hipStream_t s);
 hipError_t launch_selftest(const float *a, const float *b, const uint32_t *bits, uint32_t n, float *out,

@@ -103,10 +103,12 @@ constexpr uint32_t kGlaneMaxNodes = SPT_GLANE_MAX_NODES;
 
 // A path parked in LDS (the primary queue of render_body): 12 words, structure of arrays
 // over the wave's 64 rows (conflict-free b32 accesses).  Fields: item, st (2), o (3), d (3),
-// slot, bounce, phase | spec << 2.
+// slot, bounce, phase | spec << 2; the render service adds its job's counter (word 12).
 constexpr uint32_t kParkWords = 12;
+template <bool JOB = false>
 __device__ __forceinline__ void park_path(uint32_t *q, uint32_t row, const Path &ps)
 {
+    if (JOB) q[12 * 64 + row] = ps.job;
     q[0 * 64 + row] = ps.item;
     q[1 * 64 + row] = (uint32_t)ps.st;
     q[2 * 64 + row] = (uint32_t)(ps.st >> 32);
@@ -120,8 +122,10 @@ __device__ __forceinline__ void park_path(uint32_t *q, uint32_t row, const Path 
     q[10 * 64 + row] = ps.bounce;
     q[11 * 64 + row] = ps.phase | (ps.spec << 2);
 }
+template <bool JOB = false>
 __device__ __forceinline__ void unpark_path(const uint32_t *q, uint32_t row, Path &ps)
 {
+    if (JOB) ps.job = q[12 * 64 + row];
     ps.item = q[0 * 64 + row];
     ps.st = (uint64_t)q[1 * 64 + row] | ((uint64_t)q[2 * 64 + row] << 32);
     ps.o = mk(__uint_as_float(q[3 * 64 + row]), __uint_as_float(q[4 * 64 + row]), __uint_as_float(q[5 * 64 + row]));
@@ -159,11 +163,82 @@ __device__ __forceinline__ uint32_t claim_next(const RenderArgs &a, uint32_t hom
     return a.n_items;
 }
 
-template <bool TREE, int LEAF, bool LDSN, uint32_t BLOCK, bool BATCH = false, bool GLANE = false>
+// ---- render service (SVC): claims, publication, jobs, completion ----------------------
+typedef __attribute__((address_space(1))) uint32_t gu32;
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+
+// Reserve queue q's next claim: lane 0 issues the add and keeps its result (the claim
+// is value * n_queues + q, published or not yet) in flight until the claim is taken.
+// The address is formed in uniform code (scalar loads of the kernel arguments).
+__device__ __forceinline__ uint32_t svc_reserve(uint32_t q, uint32_t lane, uint32_t old)
+{
+    kargs_t &k = *kernarg_args();
+    uint32_t *const h = k.svc_ctl + q * kQueueStride;
+    return lane == 0 ? atomicAdd(h, 1u) : old;
+}
+// the wave's LDS words after its job record: published claims and jobs as last seen, the
+// current job and the first claim after it
+constexpr uint32_t kSvcSt = 28;
+
+// The published pair {claims, jobs} (one 64-bit sc1 load: the publish kernel stores it
+// after its records, sc1, with its stores drained -- MI355X_MICROARCH.md, hand-off table)
+__device__ __forceinline__ unsigned long long svc_pub()
+{
+    kargs_t &k = *kernarg_args();
+    return __hip_atomic_load((gu64 *)(k.svc_ctl + kSvcPub), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ bool svc_stopped()
+{
+    kargs_t &k = *kernarg_args();
+    return __hip_atomic_load((gu32 *)(k.svc_ctl + kSvcStop), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+}
+
+// The job holding published claim nb, searched forward from job `cur` (a wave's claims
+// only grow) over the first claims of the njobs published jobs, 64 per step (ballot of
+// job_claim <= nb: a prefix, job_claim is increasing); its record is copied into the
+// wave's LDS record `rec`, one word per lane.  Wave-uniform.
+__device__ __forceinline__ uint32_t svc_find_job(uint32_t nb, uint32_t cur, uint32_t njobs, uint32_t *rec,
+                                                 uint32_t lane)
+{
+    kargs_t &k = *kernarg_args();
+    const gu32 *jc = (const gu32 *)k.svc_job_claim;
+    for (;;) {
+        const uint32_t j = cur + lane;
+        const uint32_t v = j < njobs ? __hip_atomic_load(jc + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0xFFFFFFFFu;
+        const unsigned long long le = __ballot(v <= nb);
+        if (le != ~0ull || cur + 64u >= njobs) {
+            cur += 63u - (uint32_t)__builtin_clzll(le);
+            break;
+        }
+        cur += 64u;
+    }
+    // words 0-23 (the fields start_path_svc reads); kSvcSt.. hold the wave's claim state
+    const gu32 *src = (const gu32 *)(k.svc_jobs + cur);
+    const uint32_t w = lane < 24u ? __hip_atomic_load(src + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+    if (lane < 24u) rec[lane] = w;
+    return __builtin_amdgcn_readfirstlane(cur);
+}
+
+// Publish `cnt` finished samples of completion counter `idx`: every sample word the wave
+// stored is drained and written back to memory (agent release: the fold runs on any XCD)
+// before the add (MI355X_MICROARCH.md, Compiler hazard: the asm wait after the fence).
+__device__ __forceinline__ void svc_flush(uint32_t idx, uint32_t cnt, uint32_t lane)
+{
+    if (cnt == 0u) return;
+    kargs_t &k = *kernarg_args();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0) __hip_atomic_fetch_add((gu32 *)(k.svc_done + idx), cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <bool TREE, int LEAF, bool LDSN, uint32_t BLOCK, bool BATCH = false, bool GLANE = false, bool SVC = false>
 __device__ __forceinline__ void render_body(const RenderArgs &a)
 {
+    static_assert(!SVC || (SPT_PRIM && !LDSN && !GLANE && !BATCH), "the render service runs the wave-walk kernel");
     const uint32_t lane = __lane_id();
-    const uint32_t rows = a.npix / a.map.width;  // region rows (uniform)
+    const uint32_t rows = SVC ? 0u : a.npix / a.map.width;  // region rows (uniform; SVC: per job)
 
     __shared__ uint32_t s_lds[BLOCK];  // wave-private scratch of the cooperative sampler
     __shared__ uint4 s_nodes[LDSN ? 2 * kLdsNodeRecords : 1];
@@ -179,8 +254,14 @@ __device__ __forceinline__ void render_body(const RenderArgs &a)
     // leaves is about a single ray's), and every path enters the main loop one cast in.
     // Per path the arithmetic and its order are unchanged: bit-identical frames.
     constexpr bool PRIM = SPT_PRIM && !LDSN && !GLANE;
-    __shared__ uint32_t s_park[PRIM ? (BLOCK / 64u) * kParkWords * 64u : 1];
-    uint32_t *const park = s_park + (PRIM ? (threadIdx.x >> 6) * kParkWords * 64u : 0u);
+    constexpr uint32_t PW = kParkWords + (SVC ? 1u : 0u);  // parked words per path
+    __shared__ uint32_t s_park[PRIM ? (BLOCK / 64u) * PW * 64u : 1];
+    uint32_t *const park = s_park + (PRIM ? (threadIdx.x >> 6) * PW * 64u : 0u);
+    // SVC: the wave's copy of its current job's record (svc_find_job, words 0-23) and its
+    // claim state (words kSvcSt..31: kept in LDS, not SGPRs, since only claims read them)
+    __shared__ uint32_t s_rec[SVC ? (BLOCK / 64u) * kSvcJobWords : 1];
+    uint32_t *const rec = s_rec + (SVC ? (threadIdx.x >> 6) * kSvcJobWords : 0u);
+    if (SVC && lane < 4u) rec[kSvcSt + lane] = 0u;
     uint32_t q_n = 0, q_pos = 0;  // the wave's queue: rows [q_pos, q_n) hold parked paths
     if (LDSN) {
         // the host launches this variant only when n_nodes + 1 <= kLdsNodeRecords
@@ -200,6 +281,7 @@ __device__ __forceinline__ void render_body(const RenderArgs &a)
     ps.st = 0;
     ps.o = ps.d = mk(0.f, 0.f, 0.f);
     ps.slot = 0;
+    ps.job = 0;
 
     // Items are handed out in claims of a.claim from one global counter; each wave
     // keeps the next claim in flight (lane 0) so the atomic's latency is hidden.
@@ -208,8 +290,13 @@ __device__ __forceinline__ void render_body(const RenderArgs &a)
     uint32_t rect = 0;  // BATCH: rectangle of the current claim
     const uint32_t home = blockIdx.x % a.n_queues;
     uint32_t qi = 0;  // queues tried after the home queue ran dry (lane 0)
-    if (lane == 0) pend = claim_next(a, home, qi);
-    bool exhausted = false;
+    if (SVC)
+        pend = svc_reserve(home, lane, 0u);
+    else if (lane == 0)
+        pend = claim_next(a, home, qi);
+    bool exhausted = false;  // SVC: no published claim right now (the reservation waits)
+    // SVC: the wave's finished samples not yet added to completion counter acc_idx
+    uint32_t acc_idx = 0, acc_cnt = 0;
     unsigned long long casts = 0, done = 0, dropped = 0;
     struct {
         unsigned long long iters = 0, cast = 0, shade = 0, refill = 0;  // SPT_DIAG counts and s_memtime split
@@ -279,6 +366,38 @@ __device__ __forceinline__ void render_body(const RenderArgs &a)
         }
     };
 
+    // SVC: the reserved claim becomes current once published (re-reading the published
+    // pair when it is beyond the last one seen), the next one is reserved, and the job
+    // record of a claim past the current job is looked up; else exhausted (waiting)
+    auto next_claim_svc = [&]() {
+        uint32_t *const st = rec + kSvcSt;
+        const uint32_t nb = __builtin_amdgcn_readfirstlane(pend) * a.n_queues + home;
+        uint32_t pc = __builtin_amdgcn_readfirstlane(st[0]);
+        if (nb >= pc) {
+            const unsigned long long p = svc_pub();
+            pc = __builtin_amdgcn_readfirstlane((uint32_t)p);
+            const uint32_t pj = __builtin_amdgcn_readfirstlane((uint32_t)(p >> 32));
+            if (lane == 0) {
+                st[0] = pc;
+                st[1] = pj;
+            }
+        }
+        exhausted = nb >= pc;
+        if (exhausted) return;
+        pend = svc_reserve(home, lane, pend);
+        if (nb >= __builtin_amdgcn_readfirstlane(st[3])) {
+            const uint32_t cur = svc_find_job(nb, __builtin_amdgcn_readfirstlane(st[2]),
+                                              __builtin_amdgcn_readfirstlane(st[1]), rec, lane);
+            const uint32_t ce = __builtin_amdgcn_readfirstlane(rec[7]);
+            if (lane == 0) {
+                st[2] = cur;
+                st[3] = ce;
+            }
+        }
+        blk_cur = nb * a.claim;
+        blk_end = min(blk_cur + a.claim, __builtin_amdgcn_readfirstlane(rec[1]));
+    };
+
     for (;;) {
         // ---- refill: hand out (pixel, sample) items to idle lanes (ballot + prefix)
         // idle lanes wait until SPT_REFILL_MIN of them (or the whole wave) can be
@@ -292,16 +411,28 @@ __device__ __forceinline__ void render_body(const RenderArgs &a)
                 const uint32_t cnt = (uint32_t)__popcll(need);
                 const uint32_t rank = lane_rank(need);
                 const uint32_t take = min(cnt, q_n - q_pos);
-                if (ps.phase == PH_IDLE && rank < take) unpark_path(park, q_pos + rank, ps);
+                if (ps.phase == PH_IDLE && rank < take) unpark_path<SVC>(park, q_pos + rank, ps);
                 q_pos += take;
-                if (cnt > take && !exhausted) {
+                bool more = !exhausted;
+                if (SVC && cnt > take) {
+                    if (blk_cur == blk_end) next_claim_svc();
+                    more = blk_cur < blk_end;
+                }
+                if (cnt > take && more) {
                     // the queue is empty: park every lane's own path in its own row and
                     // start 64 new paths (wave-uniform)
-                    park_path(park, lane, ps);
+                    park_path<SVC>(park, lane, ps);
                     // the own path lives in LDS across the batch, not in registers
                     asm volatile("" ::: "memory");
                     ps.phase = PH_IDLE;
-                    if (BATCH) {
+                    if (SVC) {
+                        // claims are multiples of 64 items and never span two jobs: a batch
+                        // is 64 items of one claim (fewer at a job's end)
+                        const uint32_t n = min(64u, blk_end - blk_cur);
+                        const uint32_t mine = blk_cur + lane;
+                        blk_cur += n;
+                        if (lane < n) start_path_svc(mine, rec, ps);
+                    } else if (BATCH) {
                         // claims are multiples of 64 items and never span two rectangles:
                         // a batch is 64 items of one claim (fewer at the launch's end)
                         if (blk_cur == blk_end) next_claim();
@@ -335,8 +466,38 @@ __device__ __forceinline__ void render_body(const RenderArgs &a)
         if (live == 0ull) {
             if (PRIM && prim_iter) {
                 // no item was left for the batch: the lanes' own paths back
-                unpark_path(park, lane, ps);
+                unpark_path<SVC>(park, lane, ps);
                 q_n = q_pos = 0;
+                continue;
+            }
+            if (SVC && q_pos == q_n) {
+                // no path and no published claim: publish the finished samples, then wait
+                // for a publication or the stop flag (read before the last look at the
+                // published pair: jobs are published before the stop), at most
+                // kSvcIdleTicks (then the watchdog word tells the host)
+                svc_flush(acc_idx, acc_cnt, lane);
+                acc_cnt = 0;
+                const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+                bool leave = false;
+                for (;;) {
+                    const bool stop = svc_stopped();
+                    next_claim_svc();
+                    if (!exhausted) break;
+                    if (stop) {
+                        leave = true;
+                        break;
+                    }
+                    if (__builtin_amdgcn_s_memrealtime() - t0 > kSvcIdleTicks) {
+                        kargs_t &k = *kernarg_args();
+                        if (lane == 0)
+                            __hip_atomic_store((gu32 *)(k.svc_ctl + kSvcWatchdog), 1u, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+                        leave = true;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(8);
+                }
+                if (leave) break;
                 continue;
             }
             if (exhausted && q_pos == q_n) break;
@@ -371,15 +532,32 @@ __device__ __forceinline__ void render_body(const RenderArgs &a)
         SPT_STAMP(dc.cast);
         shade_step<true>(a, ps, h, act && cdone, done, dropped, s_lds + (threadIdx.x & ~63u));
         fresh = cdone;
+        if (SVC) {
+            // finished samples per completion counter, summed in the wave (acc) and added
+            // to the counter when the wave moves on to another one (svc_flush)
+            const bool fin = act && ps.phase == PH_IDLE;
+            unsigned long long fm = __ballot(fin);
+            while (fm != 0ull) {
+                const uint32_t j = __builtin_amdgcn_readlane(ps.job, (int)__builtin_ctzll(fm));
+                const unsigned long long m = __ballot(fin && ps.job == j);
+                if (j != acc_idx) {
+                    svc_flush(acc_idx, acc_cnt, lane);
+                    acc_idx = j;
+                    acc_cnt = 0;
+                }
+                acc_cnt += (uint32_t)__popcll(m);
+                fm &= ~m;
+            }
+        }
         if (PRIM && prim_iter) {
             // the lane's own path back from its row, then the batch's survivors into
             // rows [0, n) of the queue (a lane writes row rank <= lane, after the whole
             // wave has read its own row: LDS operations of a wave complete in order)
             Path own;
-            unpark_path(park, lane, own);
+            unpark_path<SVC>(park, lane, own);
             __builtin_amdgcn_wave_barrier();
             const unsigned long long lv = __ballot(ps.phase != PH_IDLE);
-            if (ps.phase != PH_IDLE) park_path(park, lane_rank(lv), ps);
+            if (ps.phase != PH_IDLE) park_path<SVC>(park, lane_rank(lv), ps);
             ps = own;
             q_n = (uint32_t)__popcll(lv);
             q_pos = 0;
@@ -387,6 +565,7 @@ __device__ __forceinline__ void render_body(const RenderArgs &a)
         SPT_STAMP(dc.shade);
     }
 
+    if (SVC) svc_flush(acc_idx, acc_cnt, lane);
     // per-lane done/dropped -> wave sums (butterfly), one atomic per counter and wave
     // (same-address atomics from every lane cost a launch ~10%; see render_grid)
 #pragma unroll
@@ -431,6 +610,44 @@ template <bool TREE, int LEAF>
 __global__ __launch_bounds__(kRenderBlock) SPT_RENDER_ATTR void render_kernel_batch(RenderArgs a)
 {
     render_body<TREE, LEAF, false, kRenderBlock, true>(a);
+}
+
+// the render service: one resident launch over a stream of published jobs (RenderArgs
+// svc_*)
+template <bool TREE, int LEAF>
+__global__ __launch_bounds__(kRenderBlock) SPT_RENDER_ATTR void render_kernel_svc(RenderArgs a)
+{
+    render_body<TREE, LEAF, false, kRenderBlock, false, false, true>(a);
+}
+
+// The publish launch: one wave stores the job records, their first claims and the zeroed
+// completion counters write-through (sc1), drains its stores, then lane 0 stores the
+// published pair {claims, jobs} (the R1 hand-off of MI355X_MICROARCH.md: the service polls
+// the pair and reads the records with sc1 loads).
+__global__ __launch_bounds__(64) void svc_publish_kernel(SvcPublish p)
+{
+    const uint32_t lane = threadIdx.x;
+    for (uint32_t i = 0; i < p.n_zero; ++i)
+        if (lane == 0) __hip_atomic_store((gu32 *)(p.done + p.zero_idx[i]), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (uint32_t r = 0; r < p.n_jobs; ++r) {
+        const uint32_t *w = (const uint32_t *)&p.rec[r];
+        if (lane < kSvcJobWords)
+            __hip_atomic_store((gu32 *)(p.jobs + p.first_job + r) + lane, w[lane], __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        if (lane == 0)
+            __hip_atomic_store((gu32 *)(p.job_claim + p.first_job + r), p.rec[r].claim_first, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0) {
+        const unsigned long long v = (unsigned long long)p.pub_claims | ((unsigned long long)(p.first_job + p.n_jobs) << 32);
+        __hip_atomic_store((gu64 *)(p.ctl + kSvcPub), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+__global__ __launch_bounds__(64) void svc_stop_kernel(uint32_t *ctl)
+{
+    if (threadIdx.x == 0) __hip_atomic_store((gu32 *)(ctl + kSvcStop), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // trees of kLdsNodeRecords to kGlaneMaxNodes nodes: the lane walk reading layout 0 from
@@ -482,8 +699,8 @@ __device__ __forceinline__ f3 decode_sample(const FoldArgs &a, uint32_t w)
         return mul(mk(a.sky[0] * k, a.sky[1] * k, a.sky[2] * k), 0.5f);
     }
     if (c == 1u) return mk(0.f, 0.f, 0.f);
-    const uint32_t v = c - 2u;
-    const uint32_t slot = v & ((1u << a.code_shift) - 1u), j = v >> a.code_shift;
+    uint32_t j, slot;
+    diffuse_decode(c, a.code_div, j, slot);
     const float4 sh = a.shade[slot];
     return mk(halve_n(sh.x * 0.5f, j), halve_n(sh.y * 0.5f, j), halve_n(sh.z * 0.5f, j));
 }
@@ -499,9 +716,9 @@ __device__ __forceinline__ void decode_run(const FoldArgs &a, const uint32_t (&w
 #pragma unroll
     for (int i = 0; i < N; ++i) {
         c[i] = word_code(w[i]);
-        const uint32_t v = c[i] >= 2u ? c[i] - 2u : 0u;
-        j[i] = v >> a.code_shift;
-        sh[i] = a.shade[v & ((1u << a.code_shift) - 1u)];
+        uint32_t slot;
+        diffuse_decode(c[i] >= 2u ? c[i] : 2u, a.code_div, j[i], slot);
+        sh[i] = a.shade[slot];
     }
 #pragma unroll
     for (int i = 0; i < N; ++i) {
@@ -743,10 +960,11 @@ __global__ __launch_bounds__(256) void fold_kernel_batch(FoldArgs a)
 
 // Per-sample colours of a single-batch region (spt_render_samples, a debug path):
 // out[p * spp + s] = {r, g, b, counted}, p the local row-major pixel.
-__global__ __launch_bounds__(256) void expand_kernel(FoldArgs a, float4 *out)
+__global__ __launch_bounds__(256) void expand_kernel(FoldArgs a, float4 *out, uint32_t p0, uint32_t n)
 {
-    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= a.npix) return;
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t p = p0 + i;
     const uint32_t W = a.map.width, rows = a.npix / W, lr = p / W, col = p - lr * W;
     uint32_t q0, step;
     ts_slot_base(lr, col, W, rows, a.spp_batch, q0, step);
@@ -755,7 +973,7 @@ __global__ __launch_bounds__(256) void expand_kernel(FoldArgs a, float4 *out)
         const uint32_t w = a.slot_words == 1u ? a.samples[q] : a.samples[2u * q];
         const bool counted = a.slot_words == 1u || a.samples[2u * q + 1u] != 0u;
         const f3 c = decode_sample(a, w);
-        out[(size_t)p * a.spp_batch + k] = make_float4(c.x, c.y, c.z, counted ? 1.f : 0.f);
+        out[(size_t)i * a.spp_batch + k] = make_float4(c.x, c.y, c.z, counted ? 1.f : 0.f);
     }
 }
 
@@ -881,6 +1099,36 @@ hipError_t launch_render(const RenderArgs &a, LaunchShape &sh, hipStream_t s)
     return hipGetLastError();
 }
 
+bool svc_supported(const AccelView &ac)
+{
+    return !(ac.tree && ac.n_nodes >= kLdsMinNodes && ac.n_nodes <= kGlaneMaxNodes);
+}
+
+hipError_t launch_render_svc(const RenderArgs &a, uint32_t grid, hipStream_t s)
+{
+    if (!svc_supported(a.scene.accel)) return hipErrorInvalidValue;
+    if (a.scene.accel.tree)
+        hipLaunchKernelGGL((render_kernel_svc<true, (int)kClusterSlots>), dim3(grid), dim3(kRenderBlock), 0, s, a);
+    else if (a.scene.accel.leaf_slots == kFlatLeafSlots)
+        hipLaunchKernelGGL((render_kernel_svc<false, (int)kFlatLeafSlots>), dim3(grid), dim3(kRenderBlock), 0, s, a);
+    else
+        hipLaunchKernelGGL((render_kernel_svc<false, (int)kClusterSlots>), dim3(grid), dim3(kRenderBlock), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_svc_publish(const SvcPublish &p, hipStream_t s)
+{
+    if (p.n_jobs > kSvcPubMax || p.n_zero > kSvcPubMax) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(svc_publish_kernel, dim3(1), dim3(64), 0, s, p);
+    return hipGetLastError();
+}
+
+hipError_t launch_svc_stop(uint32_t *ctl, hipStream_t s)
+{
+    hipLaunchKernelGGL(svc_stop_kernel, dim3(1), dim3(64), 0, s, ctl);
+    return hipGetLastError();
+}
+
 hipError_t launch_fold(const FoldArgs &a, hipStream_t s)
 {
     if (a.npix == 0) return hipSuccess;
@@ -893,10 +1141,10 @@ hipError_t launch_fold(const FoldArgs &a, hipStream_t s)
     return hipGetLastError();
 }
 
-hipError_t launch_expand(const FoldArgs &a, float4 *out, hipStream_t s)
+hipError_t launch_expand(const FoldArgs &a, float4 *out, uint32_t p0, uint32_t n, hipStream_t s)
 {
-    if (a.npix == 0) return hipSuccess;
-    hipLaunchKernelGGL(expand_kernel, dim3((a.npix + 255) / 256), dim3(256), 0, s, a, out);
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(expand_kernel, dim3((n + 255) / 256), dim3(256), 0, s, a, out, p0, n);
     return hipGetLastError();
 }
 

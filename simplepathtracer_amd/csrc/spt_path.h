@@ -719,6 +719,7 @@ struct Path {
     uint64_t st;  // keyed splitmix stream of this (pixel, sample)
     f3 o, d;
     uint32_t slot;  // slot of the first diffuse hit (PH_DLOOP)
+    uint32_t job;   // render service: the completion counter of the path's job (else unused)
 };
 
 // GenerateUniformDistInsideSphereVector (Random.hpp:115-127) for every lane with
@@ -890,7 +891,7 @@ __device__ __forceinline__ void shade_step(const RenderArgs &a, Path &ps, const 
     const uint32_t *__restrict__ mat = a.scene.mat;
     uint32_t *samples = a.samples;
     uint32_t mode = a.mode;
-    uint32_t bounces = a.bounces, code_shift = a.scene.code_shift;
+    uint32_t bounces = a.bounces, code_stride = a.scene.code_stride, code_jmax = a.scene.code_jmax;
     if constexpr (KARG) {
         // render kernels: read at the point of use from the kernarg segment (scalar
         // loads) instead of holding them in SGPRs across the loop
@@ -901,7 +902,8 @@ __device__ __forceinline__ void shade_step(const RenderArgs &a, Path &ps, const 
         samples = k.samples;
         mode = k.mode;
         bounces = k.bounces;
-        code_shift = k.scene.code_shift;
+        code_stride = k.scene.code_stride;
+        code_jmax = k.scene.code_jmax;
     }
     const uint32_t idx = h.idx;
     bool fin = false;
@@ -918,8 +920,9 @@ __device__ __forceinline__ void shade_step(const RenderArgs &a, Path &ps, const 
         if (end) {
             // the albedo of the first diffuse hit halved 1 + j times: once at that hit
             // (line 24) and once per further bounce (line 31), j = bounces - bounce - 1
-            const uint32_t j = min(bounces - ps.bounce - 1u, kCodeSat);
-            word = code_word(2u + ((j << code_shift) | ps.slot));
+            // (saturated where every albedo of the scene is 0: diffuse_code)
+            const uint32_t j = min(bounces - ps.bounce - 1u, code_jmax);
+            word = code_word(diffuse_code(j, ps.slot, code_stride));
             fin = true;
         }
         scatter = !end;
@@ -1067,6 +1070,33 @@ __device__ __forceinline__ void start_path_rect(uint32_t mine, uint32_t ri, Path
     start_path(a, mine - r.item_off, r.rows, recip((float)a.width), recip((float)a.height),
                mk(k.cam.eye[0], k.cam.eye[1], k.cam.eye[2]), ps);
     ps.item += r.slot_off;
+}
+
+// start_path for session item `mine` of the render service: the job's fields from the
+// wave's LDS copy of its record (SvcJob words, wave-uniform), the session's constants
+// from the kernel arguments.  Items past the job's item_end (claim padding) start nothing.
+__device__ __forceinline__ void start_path_svc(uint32_t mine, const uint32_t *rec, Path &ps)
+{
+    auto f = [&](int i) -> uint32_t { return (uint32_t)__builtin_amdgcn_readfirstlane(rec[i]); };
+    if (mine >= f(1)) return;
+    kargs_t &k = *kernarg_args();
+    RenderArgs a;
+    a.map = RowMap{f(8), f(9), f(10), f(11), f(12), f(13), f(14)};
+    a.width = k.width;
+    a.height = k.height;
+    a.bounces = k.bounces;
+    a.spp_batch = f(5);
+    a.s0 = f(6);
+    a.seed_key = k.seed_key;
+    a.div_band = FastDiv{f(15), f(16), f(17)};
+    a.div_tile = FastDiv{f(18), f(19), f(20)};
+    a.div_strip = FastDiv{f(21), f(22), f(23)};
+#pragma unroll
+    for (int q = 0; q < 12; ++q) a.cam.view[q] = k.cam.view[q];
+    start_path(a, mine - f(0), f(4), recip((float)a.width), recip((float)a.height),
+               mk(k.cam.eye[0], k.cam.eye[1], k.cam.eye[2]), ps);
+    ps.item += f(2);
+    ps.job = f(3);
 }
 
 }  // namespace

@@ -191,6 +191,15 @@ class Context:
     def synchronize(self) -> None:
         self._check(_native.lib().spt_synchronize(self._h))
 
+    def service_start(self) -> None:
+        """Render through the resident render service (spt_service_start): consecutive
+        renders run as jobs of one persistent launch, without a ramp and tail each."""
+        self._check(_native.lib().spt_service_start(self._h))
+
+    def service_stop(self) -> None:
+        """Drain and end the service session; renders launch per call again."""
+        self._check(_native.lib().spt_service_stop(self._h))
+
     def stats(self) -> dict:
         s = _native.Stats()
         self._check(_native.lib().spt_get_stats(self._h, ctypes.byref(s)))

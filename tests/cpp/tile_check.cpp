@@ -128,9 +128,33 @@ int main()
     // sample codes: every code round-trips (edges + a stride), the colour-0 word, and
     // no k = fl(y + 1.f) of any float y is a code word (so sky words and codes never mix)
     {
-        const uint32_t cmax = 2u * (spt::kCodeSmall - 1u);
-        if (((spt::kCodeSat + 1ull) << spt::kCodeMaxShift) + 1ull > cmax) {
-            std::printf("FAIL code capacity\n");
+        const uint32_t cmax = spt::kCodeMax;
+        // diffuse codes 2 + j * stride + slot: every (j, slot) of a fitting layout stays in
+        // [2, cmax] and decodes back (edges of j and slot, strides up to the largest that fits)
+        const uint32_t strides[] = {1, 2, 3, 149, 164, 10007, 1u << 22, 34500000u, 0x66FFFFFCu};
+        const uint32_t jmaxes[] = {0, 1, 49, 157, 280};
+        for (uint32_t S : strides)
+            for (uint32_t J : jmaxes) {
+                if (!spt::code_layout_fits(S, J)) continue;
+                const spt::FastDiv div = spt::make_fastdiv(S);
+                const uint32_t js[] = {0, 1, J / 2, J > 0 ? J - 1 : 0, J};
+                const uint32_t ss[] = {0, 1, S / 2, S - 1};
+                for (uint32_t j : js)
+                    for (uint32_t sl : ss) {
+                        if (j > J || sl >= S) continue;
+                        const uint32_t c = spt::diffuse_code(j, sl, S);
+                        uint32_t j2, s2;
+                        spt::diffuse_decode(c, div, j2, s2);
+                        if (c < 2 || c > cmax || j2 != j || s2 != sl) {
+                            std::printf("FAIL diffuse code S=%u J=%u j=%u slot=%u -> %u -> (%u, %u)\n", S, J, j, sl, c,
+                                        j2, s2);
+                            return 1;
+                        }
+                    }
+            }
+        if (spt::code_layout_fits(0x66FFFFFEu, 0) || !spt::code_layout_fits(34500000u, 49) ||
+            spt::code_layout_fits(34600000u, 49)) {
+            std::printf("FAIL code capacity bounds\n");
             return 1;
         }
         for (uint64_t c = 1; c <= cmax; c += (c < 64 || cmax - c < 64 || (c > spt::kCodeSmall - 64 && c < spt::kCodeSmall + 64)) ? 1 : 9973) {

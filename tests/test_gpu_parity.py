@@ -323,6 +323,55 @@ def test_more_than_255_spheres(spt, ctx, oracle):
     assert_bitwise(got[:, :3], want[:, :3], "300 spheres")
 
 
+def test_diffuse_codes_saturate_where_albedos_vanish(spt, ctx, oracle, golden_scenes):
+    """Sample codes saturate j at min(bounces - 1, jz), jz = the halvings after which every
+    finite albedo is 0 (spt_internal.h diffuse_code): tiny, denormal and infinite albedos at
+    depth 40, where jz (~30) is below bounces - 1 and halve_n takes its denormal path."""
+    gs = golden_scenes
+    col = gs["reference_colors"].copy()
+    col[:, :3] *= np.float32(1e-37)
+    col[1, :3] = np.float32([1e-44, 3e-42, 7e-40])  # denormal albedos
+    col[3, 1] = np.float32(np.inf)
+    scene = spt.Scene(gs["reference_centers"], gs["reference_radii"], col, gs["reference_materials"],
+                      gs["reference_fuzz"])
+    setup(ctx, scene, 48, 32, 6, 40)
+    got = ctx.render_segment(0, 32, 0, 48)
+    osc = oracle.OracleScene(gs["reference_centers"], gs["reference_radii"], col, gs["reference_materials"],
+                             gs["reference_fuzz"])
+    fr = oracle.make_frame(gs["view"], EYE, SKY, 48, 32, 6, 40, 1)
+    want, _ = oracle.render_segment(osc, fr, 0, 32, 0, 48)
+    same_bits_or_nan(got[:, :3], want[:, :3], "saturated diffuse codes")
+    assert (got[:, :3] != 0).any() and np.isinf(got[:, 1]).any()
+
+
+def test_scene_beyond_four_million_slots(spt, oracle, golden_scenes):
+    """Sample codes are 2 + j * slots + slot (the former 22 slot bits refused
+    scenes over 4 194 304 slots).  4.3 M tiny spheres far behind the camera, then the
+    reference scene's 10, so every hit lands on a slot above 2^22; brute force (cluster
+    size 0) keeps the host build cheap."""
+    gs = golden_scenes
+    n_far = 4_300_000
+    far = np.zeros((n_far, 4), np.float32)
+    far[:, 0] = np.arange(n_far, dtype=np.float32) * np.float32(1e-3)
+    far[:, 2] = np.float32(-500.0)
+    c = np.concatenate([far, gs["reference_centers"]]).astype(np.float32)
+    r = np.concatenate([np.full(n_far, 1e-3, np.float32), gs["reference_radii"]]).astype(np.float32)
+    col = np.concatenate([np.full((n_far, 4), 9, np.float32), gs["reference_colors"]]).astype(np.float32)
+    m = np.concatenate([np.full(n_far, 3, np.uint8), gs["reference_materials"]]).astype(np.uint8)
+    f = np.concatenate([np.zeros(n_far, np.float32), gs["reference_fuzz"]]).astype(np.float32)
+    cx = spt.Context(0)
+    try:
+        cx.set_cluster_size(0)
+        setup(cx, spt.Scene(c, r, col, m, f), 64, 48, 2, 6)
+        got = cx.render_segment(20, 24, 28, 36)
+    finally:
+        cx.close()
+    osc = oracle.OracleScene(c, r, col, m, f)
+    fr = oracle.make_frame(gs["view"], EYE, SKY, 64, 48, 2, 6, 1)
+    want, _ = oracle.render_segment(osc, fr, 20, 24, 28, 36)
+    assert_bitwise(got[:, :3], want[:, :3], "4.3 M sphere slots")
+
+
 def test_nondefault_camera_and_odd_frame(spt, ctx, oracle, golden_scenes):
     view = spt.camera_basis([2, 3, -4, 0], [0, 0.5, 2, 0], UP)
     setup(ctx, scene_from(spt, golden_scenes, "random"), 131, 77, 3, 12, seed=3, view=view)

@@ -1,0 +1,187 @@
+"""GPU tests of the resident render service (spt_service_start, DESIGN.md §5 "Render
+service"): frames, rank shares, sample batches and task-mode jobs rendered as jobs of
+one persistent launch must be bit-identical to the launched renders (and those are
+pinned against the oracle by test_gpu_parity.py), and every session must end cleanly.
+Every device synchronisation here goes through ctx.service_stop()/ctx.synchronize()
+first (a device-wide sync would wait for the resident kernel to idle out)."""
+import time
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+EYE, LOOK, UP, SKY = [0, 1, -3, 0], [0, 1, 0, 0], [0, 1, 0, 0], [137, 207, 240, 0]
+
+
+def bits(a):
+    return np.ascontiguousarray(a, np.float32).view(np.uint32)
+
+
+def assert_bitwise(got, want, what=""):
+    g, w = bits(got), bits(want)
+    bad = np.nonzero(g != w)
+    assert not len(bad[0]), f"{what}: {len(bad[0])} of {g.size} lanes differ"
+
+
+@pytest.fixture(scope="module")
+def spt():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import simplepathtracer_amd as m
+    m.lib()
+    return m
+
+
+def make_ctx(spt, golden_scenes, w, h, spp, bounces, seed=1, name="random"):
+    gs = golden_scenes
+    c = spt.Context(0)
+    c.set_scene(spt.Scene(*(gs[f"{name}_{k}"] for k in ("centers", "radii", "colors", "materials", "fuzz"))))
+    c.set_camera(spt.camera_basis(EYE, LOOK, UP), EYE, SKY)
+    c.set_params(w, h, spp, bounces, seed)
+    return c
+
+
+def render_frames(ctx, jobs, W, H, mode, streams, service):
+    """jobs: list of (yB, yE, strip, parts, part, xB, xE); each rendered into its own
+    device buffers on alternating streams, all enqueued before any synchronisation."""
+    import torch
+    from simplepathtracer_amd.renderer import rows_count
+    outs = []
+    if service:
+        ctx.service_start()
+    for k, (yB, yE, strip, parts, part, xB, xE) in enumerate(jobs):
+        n = rows_count(yB, yE, strip, parts, part) * (xE - xB)
+        rgba = torch.zeros((max(n, 1), 4), dtype=torch.float32, device="cuda")
+        g8 = torch.zeros(W * H * 3, dtype=torch.uint8, device="cuda")
+        st = streams[k % len(streams)]
+        ctx.render_rows_async(mode, yB, yE, strip, parts, part, xB, xE, rgba.data_ptr(), g8.data_ptr(), st.cuda_stream)
+        outs.append((rgba, g8))
+    if service:
+        ctx.service_stop()
+    ctx.synchronize()
+    torch.cuda.synchronize()
+    return [(a.cpu().numpy(), b.cpu().numpy()) for a, b in outs]
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_service_frames_equal_launched_frames(spt, golden_scenes, mode):
+    """K consecutive frames through the queue, each compared with a one-shot render."""
+    import torch
+    W, H = 320, 200
+    ctx = make_ctx(spt, golden_scenes, W, H, 16, 50, seed=3)
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    jobs = [(0, H, 1, 1, 0, 0, W)] * 5
+    ref = render_frames(ctx, jobs[:1], W, H, mode, streams, service=False)[0]
+    ctx.reset_stats()
+    got = render_frames(ctx, jobs, W, H, mode, streams, service=True)
+    st = ctx.stats()
+    ctx.close()
+    for k, (a, b) in enumerate(got):
+        assert_bitwise(a[:, :3], ref[0][:, :3], f"frame {k} rgba")
+        assert np.array_equal(b, ref[1]), f"frame {k} g_data"
+    assert st["svc_jobs"] == len(jobs) and st["svc_sessions"] >= 1 and st["svc_running"] == 0
+    assert st["samples"] == len(jobs) * W * H * 16
+    assert st["launches"] == len(jobs)
+
+
+def test_service_rank_shares_and_regions(spt, golden_scenes):
+    """Interleaved strips (the bench's rank shares), odd rectangles and tiny regions, many
+    jobs in flight at once (more than 64 of them: the job search's second step)."""
+    import torch
+    W, H = 240, 160
+    ctx = make_ctx(spt, golden_scenes, W, H, 8, 50, seed=7)
+    streams = [torch.cuda.Stream(), torch.cuda.Stream(), torch.cuda.Stream()]
+    jobs = [(0, H, 4, 8, p, 0, W) for p in range(8)] + [(0, H, 8, 3, p, 17, 201) for p in range(3)]
+    jobs += [(y, y + 3, 1, 1, 0, x, x + 5) for y in range(0, 150, 13) for x in range(0, 230, 37)]
+    jobs += [(11, 12, 1, 1, 0, 23, 24)] * 3
+    assert len(jobs) > 64
+    ref = render_frames(ctx, jobs, W, H, 0, streams, service=False)
+    got = render_frames(ctx, jobs, W, H, 0, streams, service=True)
+    st = ctx.stats()
+    ctx.close()
+    for k, ((a, b), (ra, rb)) in enumerate(zip(got, ref)):
+        assert_bitwise(a[:, :3], ra[:, :3], f"job {k} {jobs[k]} rgba")
+        assert np.array_equal(b, rb), f"job {k} g_data"
+    assert st["svc_watchdog_exits"] == 0
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_service_sample_batches_fold_in_order(spt, golden_scenes, mode):
+    """A workspace smaller than the frame's sample words: each frame is several jobs (one
+    per sample batch), folded in order into the accumulator."""
+    import torch
+    W, H = 200, 120
+    ctx = make_ctx(spt, golden_scenes, W, H, 24, 50, seed=2)
+    streams = [torch.cuda.Stream()]
+    jobs = [(0, H, 1, 1, 0, 0, W)] * 2
+    ref = render_frames(ctx, jobs[:1], W, H, mode, streams, service=False)[0]
+    ctx.set_workspace(W * H * 5 * 4 * (2 if mode else 1))  # 5 samples per batch: 5 batches
+    got = render_frames(ctx, jobs, W, H, mode, streams, service=True)
+    st = ctx.stats()
+    ctx.close()
+    for k, (a, b) in enumerate(got):
+        assert_bitwise(a[:, :3], ref[0][:, :3], f"frame {k}")
+        assert np.array_equal(b, ref[1])
+    assert st["svc_jobs"] >= 2 * 5
+
+
+def test_service_restarts_after_a_pause_and_a_setter(spt, golden_scenes):
+    """A pause longer than the session's idle limit (its waves leave; the host starts a
+    new session), a camera change between frames (the session ends), then more frames."""
+    import torch
+    W, H = 160, 96
+    ctx = make_ctx(spt, golden_scenes, W, H, 8, 50, seed=4)
+    st0 = torch.cuda.Stream()
+    job = [(0, H, 1, 1, 0, 0, W)]
+    ref = render_frames(ctx, job, W, H, 0, [st0], service=False)[0]
+    ctx.service_start()
+    outs = []
+    for k in range(3):
+        rgba = torch.zeros((W * H, 4), dtype=torch.float32, device="cuda")
+        ctx.render_rows_async(0, 0, H, 1, 1, 0, 0, W, rgba.data_ptr(), 0, st0.cuda_stream)
+        st0.synchronize()  # the stream only: the session stays resident
+        outs.append(rgba.cpu().numpy())
+        time.sleep(0.3)  # > 100 ms: the session's waves leave
+    view2 = spt.camera_basis([0.5, 1.2, -3, 0], LOOK, UP)
+    ctx.set_camera(view2, EYE, SKY)
+    rgba2 = torch.zeros((W * H, 4), dtype=torch.float32, device="cuda")
+    ctx.render_rows_async(0, 0, H, 1, 1, 0, 0, W, rgba2.data_ptr(), 0, st0.cuda_stream)
+    ctx.service_stop()
+    st = ctx.stats()
+    ctx.synchronize()
+    torch.cuda.synchronize()
+    got2 = rgba2.cpu().numpy()
+    ctx.set_camera(view2, EYE, SKY)
+    want2 = render_frames(ctx, job, W, H, 0, [st0], service=False)[0]
+    ctx.close()
+    for k, a in enumerate(outs):
+        assert_bitwise(a[:, :3], ref[0][:, :3], f"frame {k} after a pause")
+    assert_bitwise(got2[:, :3], want2[0][:, :3], "frame after set_camera")
+    assert st["svc_sessions"] >= 4 and st["svc_watchdog_exits"] >= 2
+
+
+def test_service_host_slot_calls(spt, golden_scenes, monkeypatch):
+    """Unbatched host calls (SPT_BATCH=0: one host slot and stream per call, from several
+    threads) go through the service too."""
+    import threading
+    monkeypatch.setenv("SPT_BATCH", "0")
+    W, H = 200, 120
+    ctx = make_ctx(spt, golden_scenes, W, H, 6, 50, seed=9)
+    tiles = [(y, y + 40, x, x + 50) for y in range(0, H, 40) for x in range(0, W, 50)]
+    want = np.zeros(W * H * 3, np.uint8)
+    for t in tiles:
+        ctx.render_segment(*t, want)
+    ctx.service_start()
+    got = np.zeros(W * H * 3, np.uint8)
+    th = [threading.Thread(target=ctx.render_segment, args=(*t, got)) for t in tiles]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    st = ctx.stats()
+    ctx.service_stop()
+    ctx.close()
+    assert np.array_equal(got, want)
+    assert st["svc_jobs"] == len(tiles)

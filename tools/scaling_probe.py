@@ -1,22 +1,30 @@
-"""Strong-scaling probe on ONE GPU: device time of the render kernel for the rows
-one rank of an N-rank job owns (interleaved 8-row strips), vs the full frame.
-Usage (GPU box): python tools/scaling_probe.py [--config c2] [--reps 3]"""
+"""Strong-scaling probe on ONE GPU: wall time per frame of the rows one rank of an N-rank
+job owns (interleaved strips, the bench's split) against the full frame, with frames in
+flight on alternating streams, through the render service (--service 1) or one launch
+per frame (--service 0).  Per-rank efficiency = (full-frame time / N) / share time.
+--record FILE writes the table with its settings and the build it ran (one record per
+build and setting: profiles/scaling_<round>.txt keeps them).
+Usage (GPU box): python tools/scaling_probe.py [--config c2] [--reps 5] [--streams 2] [--service 1]"""
 import argparse
+import datetime
 import os
+import subprocess
 import sys
+import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import simplepathtracer_amd as spt  # noqa: E402
 from simplepathtracer_amd.distributed import FrameSplit, even_strip  # noqa: E402
-import time  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--config", default="c2")
 ap.add_argument("--reps", type=int, default=3)
 ap.add_argument("--streams", type=int, default=1, help="frames in flight on alternating streams (wall time)")
-ap.add_argument("--frames", type=int, default=8)
+ap.add_argument("--frames", type=int, default=20)
+ap.add_argument("--service", type=int, default=1)
+ap.add_argument("--record", default="")
 args = ap.parse_args()
 W, H, SPP, B = {"c2": (1200, 800, 100, 50), "c3": (3840, 2160, 1024, 50)}[args.config]
 ctx = spt.Context(0)
@@ -25,6 +33,7 @@ ctx.set_camera(spt.camera_basis(), spt.scene.DEFAULT_EYE, spt.INIT_COLOR)
 ctx.set_params(W, H, SPP, B, 1)
 base = None
 streams = [torch.cuda.Stream() for _ in range(args.streams)]
+lines = []
 for n in (1, 2, 4, 8):
     split = FrameSplit(W, H, n, even_strip(H, n))
     tiles = [torch.zeros((split.tile_pixels(), 4), dtype=torch.float32, device="cuda") for _ in streams]
@@ -35,14 +44,39 @@ for n in (1, 2, 4, 8):
 
     ts = []
     for r in range(args.reps + 1):
+        ctx.synchronize()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
+        if args.service:
+            ctx.service_start()
         for k in range(args.frames):
             frame(k)
+        if args.service:
+            ctx.service_stop()
         torch.cuda.synchronize()
         if r:
             ts.append((time.perf_counter() - t0) * 1e3 / args.frames)
     t = float(np.median(ts))
     base = base or t
-    print(f"N={n}: rank-0 share {split.rows[0]} rows (strip {split.strip}), wall per frame {t:8.3f} ms "
-          f"({args.streams} stream(s)), ideal {base / n:8.3f} ms, efficiency {base / n / t:6.3f}", flush=True)
+    line = (f"N={n}: rank-0 share {split.rows[0]} rows (strip {split.strip}), wall per frame {t:8.3f} ms "
+            f"({args.streams} stream(s)), ideal {base / n:8.3f} ms, efficiency {base / n / t:6.3f}")
+    print(line, flush=True)
+    lines.append(line)
+if args.record:
+    try:
+        head = subprocess.run(["git", "rev-parse", "--short", "HEAD"], capture_output=True, text=True,
+                              cwd=os.path.dirname(os.path.abspath(__file__))).stdout.strip() or "unknown"
+    except OSError:
+        head = "unknown"
+    so = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "simplepathtracer_amd", "lib",
+                      "libspt_hip.so")
+    with open(args.record, "w") as f:
+        f.write(f"# tools/scaling_probe.py --config {args.config} --streams {args.streams} --frames {args.frames} "
+                f"--reps {args.reps} --service {args.service}\n")
+        f.write(f"# {datetime.datetime.now().isoformat(timespec='seconds')}, git {head}, libspt_hip.so mtime "
+                f"{datetime.datetime.fromtimestamp(os.path.getmtime(so)).isoformat(timespec='seconds')}, "
+                f"env SPT_*: {' '.join(f'{k}={v}' for k, v in sorted(os.environ.items()) if k.startswith('SPT_')) or '-'}\n")
+        f.write("# wall time per frame over the frames of one timed region (median of reps); the frame's "
+                "rows as one rank of N owns them, on one GPU\n")
+        f.write("\n".join(lines) + "\n")
+ctx.close()

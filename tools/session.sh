@@ -1,0 +1,57 @@
+#!/bin/bash
+# GPU-box session runner: named steps, each under its own time limit, logs under
+# gpurun_out/<tag>_<step>.log.  A timeout, abort, segfault or kill ends the session (no
+# further GPU step runs after a possible fault); a step that merely fails (tests red,
+# nonzero exit) is reported and the next step runs.
+# Usage: tools/session.sh <tag> <step> [<step> ...]
+#   steps: svc          pytest tests/test_gpu_service.py
+#          gpu          pytest -m gpu (the whole GPU suite)
+#          smoke        __graft_entry__.smoke()
+#          bench        python bench.py (default arguments: config 2, service on)
+#          bench0       python bench.py --service 0 (one launch per frame)
+#          benchq       bench.py without the CPU baseline and drop-in legs (quick)
+#          bench0q      the same with --service 0
+#          c5 / c3      bench.py --config c5 / c3 (quick legs)
+#          scaling      tools/scaling_probe.py --streams 2 (service on and off)
+#          dropin       the C++ drop-in harness at tc = 4 and tc = 32 (bench.py's legs)
+#          profile      tools/profile.sh <tag>_c2 c2 (kernel trace + PMC passes + SPT_DIAG)
+#          profile5     tools/profile.sh <tag>_c5 c5 --config c5 --steps 2 --warmup 1 ...
+#          ab:<args>    tools/ab.py <args>
+set -o pipefail
+R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
+cd "$R" || exit 2
+mkdir -p gpurun_out
+TAG=${1:?tag}
+shift
+run() {  # name seconds cmd...
+  local name=$1 t=$2; shift 2
+  local log="gpurun_out/${TAG}_${name}.log"
+  echo "== $name ($(date +%T))"
+  timeout -k 10 "$t" "$@" > "$log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc"
+  tail -n 6 "$log"
+  case $rc in 124|134|137|139) echo "stopping after $name (rc=$rc)"; exit $rc ;; esac
+  return 0
+}
+PYT="python -u -m pytest -x -q --timeout 120 --timeout-method thread"
+for step in "$@"; do
+  case $step in
+    svc) run svc 300 $PYT -v tests/test_gpu_service.py ;;
+    gpu) run gpu 600 $PYT -m gpu tests ;;
+    smoke) run smoke 120 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) run bench 400 python bench.py ;;
+    bench0) run bench0 400 python bench.py --service 0 ;;
+    benchq) run benchq 120 python bench.py --no-cpu-baseline --no-dropin ;;
+    bench0q) run bench0q 120 python bench.py --no-cpu-baseline --no-dropin --service 0 ;;
+    c5) run c5 300 python bench.py --config c5 --steps 4 --warmup 1 --no-cpu-baseline ;;
+    c3) run c3 300 python bench.py --config c3 --steps 2 --warmup 1 --no-cpu-baseline ;;
+    scaling) run scaling 300 python tools/scaling_probe.py --streams 2 --reps 5 --service 1 --record "gpurun_out/${TAG}_scaling.txt"
+             run scaling0 300 python tools/scaling_probe.py --streams 2 --reps 5 --service 0 --record "gpurun_out/${TAG}_scaling0.txt" ;;
+    dropin) run dropin 300 python -c "import bench; print(bench.dropin_bench(1200, 800, 100, 50, 5, (4, 32)))" ;;
+    profile) run profile 900 bash tools/profile.sh "${TAG}_c2" c2 ;;
+    profile5) run profile5 900 bash tools/profile.sh "${TAG}_c5" c5 --config c5 --steps 2 --warmup 1 --no-cpu-baseline ;;
+    ab:*) run ab 600 python tools/ab.py ${step#ab:} ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done

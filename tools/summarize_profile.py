@@ -64,10 +64,11 @@ out += ["", f"## PMC counters (average per dispatch over the last {timed} dispat
 for (k, c), v in sorted(agg.items()):
     val = sum(v) / len(v)
     note = ""
+    # rocprofv3 reports both in KiB (1024 bytes); printed in decimal megabytes (1e6 bytes)
     if c == "FETCH_SIZE":
-        note = f" (KB; x2 gfx950 correction = {2*val/1024:.1f} MB)"
+        note = f" (KiB; x2 gfx950 correction = {2*val*1024/1e6:,.1f} MB, decimal)"
     elif c == "WRITE_SIZE":
-        note = f" (KB = {val/1024:.1f} MB)"
+        note = f" (KiB = {val*1024/1e6:,.1f} MB, decimal)"
     out.append(f"| `{k}` | {c} | {val:,.0f}{note} |")
 open(dst, "w").write("\n".join(out) + "\n")
 # profiles/counters.json[config]: per-launch PMC values of the render and fold kernels

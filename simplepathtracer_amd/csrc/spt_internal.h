@@ -347,9 +347,9 @@ constexpr uint32_t kSvcPub = kMaxQueues * kQueueStride;  // uint64_t: claims | j
 constexpr uint32_t kSvcStop = kSvcPub + 64;
 constexpr uint32_t kSvcWatchdog = kSvcStop + 64;
 constexpr uint32_t kSvcCtlWords = kSvcWatchdog + 64;
-// a wave with no work for 2 s (s_memrealtime, 100 MHz) leaves; the host never lets a
-// session idle 1 s before publishing to it (it restarts it), so no job is ever lost
-constexpr unsigned long long kSvcIdleTicks = 200000000ull;
+// a wave with no work for 0.5 s (s_memrealtime, 100 MHz) leaves; the host never publishes
+// to a session it has not published to for 40 ms (it restarts it), so no job is ever lost
+constexpr unsigned long long kSvcIdleTicks = 50000000ull;
 // jobs published by one publish launch (their records travel in its kernel arguments)
 constexpr uint32_t kSvcPubMax = 16;
 struct SvcPublish {

@@ -208,7 +208,7 @@ __device__ __forceinline__ uint32_t svc_find_job(uint32_t nb, uint32_t cur, uint
         const uint32_t v = j < njobs ? __hip_atomic_load(jc + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0xFFFFFFFFu;
         const unsigned long long le = __ballot(v <= nb);
         if (le != ~0ull || cur + 64u >= njobs) {
-            cur += 63u - (uint32_t)__builtin_clzll(le);
+            if (le != 0ull) cur += 63u - (uint32_t)__builtin_clzll(le);  // (never 0: job_claim[cur] <= nb)
             break;
         }
         cur += 64u;
@@ -220,16 +220,27 @@ __device__ __forceinline__ uint32_t svc_find_job(uint32_t nb, uint32_t cur, uint
     return __builtin_amdgcn_readfirstlane(cur);
 }
 
+// 1 (default): the service stores sample words write-through (sc1), and a completion
+// count needs only the wave's own drain; 0: plain stores and an agent release (buffer_wbl2,
+// a write-back of the XCD's whole L2) before every count
+#ifndef SPT_SVC_WT
+#define SPT_SVC_WT 1
+#endif
+
 // Publish `cnt` finished samples of completion counter `idx`: every sample word the wave
-// stored is drained and written back to memory (agent release: the fold runs on any XCD)
-// before the add (MI355X_MICROARCH.md, Compiler hazard: the asm wait after the fence).
+// stored is drained (write-through stores: in memory once drained; else written back by
+// an agent release: the fold runs on any XCD) before the add (MI355X_MICROARCH.md
+// hand-off table, each storing wave signalling for itself; Compiler hazard: the asm wait
+// after the fence).
 __device__ __forceinline__ void svc_flush(uint32_t idx, uint32_t cnt, uint32_t lane)
 {
     if (cnt == 0u) return;
     kargs_t &k = *kernarg_args();
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (!SPT_SVC_WT) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     if (lane == 0) __hip_atomic_fetch_add((gu32 *)(k.svc_done + idx), cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
@@ -480,7 +491,15 @@ __device__ __forceinline__ void render_body(const RenderArgs &a)
                 const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
                 bool leave = false;
                 for (;;) {
+                    // the stop flag is stored after every publication: once it is seen, the
+                    // published pair must be read after it (the two loads would otherwise be
+                    // in flight together, and the pair's could return a value older than the
+                    // flag's, leaving a published reservation behind)
                     const bool stop = svc_stopped();
+                    if (stop) {
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                    }
                     next_claim_svc();
                     if (!exhausted) break;
                     if (stop) {
@@ -530,7 +549,7 @@ __device__ __forceinline__ void render_body(const RenderArgs &a)
                     : find_closest<TREE, LEAF, LDSN>(a.scene.accel, ps.o, ps.d, act, dg, (const uint32_t *)s_nodes);
         }
         SPT_STAMP(dc.cast);
-        shade_step<true>(a, ps, h, act && cdone, done, dropped, s_lds + (threadIdx.x & ~63u));
+        shade_step<true, SVC && SPT_SVC_WT>(a, ps, h, act && cdone, done, dropped, s_lds + (threadIdx.x & ~63u));
         fresh = cdone;
         if (SVC) {
             // finished samples per completion counter, summed in the wave (acc) and added

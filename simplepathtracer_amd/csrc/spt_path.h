@@ -841,6 +841,10 @@ __device__ __forceinline__ void refract_event(const float4 *__restrict__ slots, 
 // its own queue order; so two paths of a sample reach `colors` in the order of
 // (key, pixel) -- which only matters where colorIndex aliases pixels (non-square
 // tiles, lines 103 and 186; fold_kernel).
+// WT (the render service): the sample word is stored write-through (sc1: it leaves the
+// XCD's L2 at once), so the completion count that follows needs only the wave's own
+// s_waitcnt, not an L2 write-back (spt_kernels.hip svc_flush).
+template <bool WT = false>
 __device__ __forceinline__ void finish_step(uint32_t mode, uint32_t *samples, Path &ps, bool fin, bool spec_event,
                                             bool refr_event, bool sky, uint32_t word, unsigned long long &done,
                                             unsigned long long &dropped)
@@ -862,13 +866,22 @@ __device__ __forceinline__ void finish_step(uint32_t mode, uint32_t *samples, Pa
         }
     }
     if (fin) {
+        typedef __attribute__((address_space(1))) uint32_t gu32_t;
+        typedef __attribute__((address_space(1))) unsigned long long gu64_t;
         if (mode == 0u) {
             // RenderSegment counts every sample: one word per slot
-            samples[ps.item] = word;
+            if (WT)
+                __hip_atomic_store((gu32_t *)(samples + ps.item), word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            else
+                samples[ps.item] = word;
         } else {
             const uint32_t key =
                 counted ? 1u + (((ps.spec & 0xFFFFu) << 11) | (sky ? 1u << 10 : 0u) | ((ps.spec >> 16) & 0x3FFu)) : 0u;
-            *(uint2 *)(samples + (size_t)2 * ps.item) = make_uint2(word, key);
+            if (WT)
+                __hip_atomic_store((gu64_t *)(samples + (size_t)2 * ps.item), (unsigned long long)word | ((unsigned long long)key << 32),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            else
+                *(uint2 *)(samples + (size_t)2 * ps.item) = make_uint2(word, key);
         }
         ps.phase = PH_IDLE;
         ps.d = mk(0.f, 0.f, 0.f);
@@ -881,7 +894,7 @@ __device__ __forceinline__ void finish_step(uint32_t mode, uint32_t *samples, Pa
 // bounce loop (21-37) in PH_DLOOP.  Finishing paths write their sample slot.
 // Called by every lane of the wave (`act` = the lane holds a path), so the
 // cooperative cube-minus-ball sampler runs in uniform control flow.
-template <bool KARG = false>
+template <bool KARG = false, bool WT = false>
 __device__ __forceinline__ void shade_step(const RenderArgs &a, Path &ps, const Hit &h, bool act,
                                            unsigned long long &done, unsigned long long &dropped, uint32_t *lds)
 {
@@ -967,7 +980,7 @@ __device__ __forceinline__ void shade_step(const RenderArgs &a, Path &ps, const 
         refract_event(hit, ps, idx);
         spec_event = true;
     }
-    finish_step(mode, samples, ps, fin, spec_event, refr, !dl, word, done, dropped);
+    finish_step<WT>(mode, samples, ps, fin, spec_event, refr, !dl, word, done, dropped);
 }
 
 

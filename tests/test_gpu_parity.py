@@ -982,6 +982,47 @@ def test_config4_eight_way_strip_split_equals_one_part(spt, ctx, golden_scenes):
     assert np.array_equal(gm, g_full.cpu().numpy())
 
 
+def test_config4_full_spp_split_equals_config3_frame(spt, ctx, oracle, golden_scenes):
+    """BASELINE config 4 at its own size and depth (3840x2160, 1024 spp, depth 50): the 8
+    rank shares of the interleaved 2-row strips (what each of 8 bench ranks renders; one
+    launch each, 1.06 G samples), assembled as rank 0 does after the gather, equal the
+    one-GPU config-3 frame bit for bit, and sampled pixels equal the oracle.  The RCCL
+    gather itself needs 8 GPUs (tests/test_multirank.py covers its logic over gloo)."""
+    import torch
+    from simplepathtracer_amd.distributed import even_strip
+    W, H, spp, parts = 3840, 2160, 1024, 8
+    strip = even_strip(H, parts)
+    setup(ctx, scene_from(spt, golden_scenes, "random"), W, H, spp, 50)
+    full = torch.zeros((W * H, 4), dtype=torch.float32, device="cuda")
+    g_full = torch.zeros(W * H * 3, dtype=torch.uint8, device="cuda")
+    ctx.render_rows_async(0, 0, H, 1, 1, 0, 0, W, full.data_ptr(), g_full.data_ptr())
+    rows = spt.rows_count(0, H, strip, parts, 0)
+    tiles = torch.zeros((parts, rows * W, 4), dtype=torch.float32, device="cuda")
+    ctx.reset_stats()
+    for p in range(parts):
+        ctx.render_rows_async(0, 0, H, strip, parts, p, 0, W, tiles[p].data_ptr(), 0)
+    frame = torch.zeros_like(full)
+    g = torch.zeros_like(g_full)
+    ctx.assemble_rows_async(tiles.data_ptr(), rows, 0, H, strip, parts, 0, W, frame.data_ptr(), g.data_ptr())
+    ctx.synchronize()
+    st = ctx.stats()
+    assert st["samples"] == W * H * spp
+    assert torch.equal(frame.view(torch.int32), full.view(torch.int32))
+    assert torch.equal(g, g_full)
+    a = frame.cpu().numpy()
+    g8 = g.cpu().numpy()
+    sc = oscene_from(oracle, golden_scenes, "random")
+    fr = oracle.make_frame(golden_scenes["view"], EYE, SKY, W, H, spp, 50, 1)
+    rng = np.random.default_rng(11)
+    for _ in range(4):
+        x, y = int(rng.integers(0, W)), int(rng.integers(0, H))
+        gw = np.zeros(W * H * 3, np.uint8)
+        want, _ = oracle.render_segment(sc, fr, y, y + 1, x, x + 1, rgb8=gw)
+        assert_bitwise(a[y * W + x, :3], want[0, :3], f"C4 pixel {(x, y)}")
+        i = 3 * ((H - 1 - y) * W + x)
+        assert np.array_equal(g8[i:i + 3], gw[i:i + 3])
+
+
 def test_culling_is_exact_with_exact_distance_ties(spt, ctx, golden_scenes):
     """Every small sphere of the config-2 scene duplicated (same centre and radius,
     another colour and material, a higher index): each hit is an exact distance tie,

@@ -19,7 +19,10 @@ for r in csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv"))
     out.append(f"| `{r['Name'][:60]}` | {r['Calls']} | {float(r['AverageNs'])/1e6:.4f} | "
                f"{float(r['MinNs'])/1e6:.4f} | {float(r['MaxNs'])/1e6:.4f} | {float(r['Percentage']):.2f} |")
 # the timed launches only (the last `timed` of each spt kernel): clocks ramp over the
-# warmup launches, and bench.py's HIP-event average covers the timed ones
+# warmup launches, and bench.py's HIP-event average covers the timed ones.  The render
+# service's kernel (render_kernel_svc) is one dispatch per session: its timed session is
+# its last dispatch, which renders all `timed` frames (per-frame figures = / timed).
+SVC = "render_kernel_svc"
 trace = os.path.join(src, "trace", "run_kernel_trace.csv")
 if os.path.exists(trace):
     per = collections.defaultdict(list)
@@ -33,7 +36,7 @@ if os.path.exists(trace):
             "time per launch that bench.py's roofline uses (from its HIP events).\n",
             "| kernel | launches | avg span ms | min ms | max ms | union/launch ms |", "|---|---|---|---|---|---|"]
     for k, v in sorted(per.items()):
-        iv = sorted((x[0], x[0] + x[1]) for x in v)[-timed:]
+        iv = sorted((x[0], x[0] + x[1]) for x in v)[-(1 if SVC in k else timed):]
         d = [(b - a) / 1e6 for a, b in iv]
         tot, cs, ce = 0, None, None
         for a, b in iv:
@@ -46,6 +49,9 @@ if os.path.exists(trace):
         tot += ce - cs
         out.append(f"| `{k[:60]}` | {len(d)} | {sum(d)/len(d):.4f} | {min(d):.4f} | {max(d):.4f} | "
                    f"{tot/1e6/len(d):.4f} |")
+        if SVC in k:
+            out.append(f"| `{k[:60]}` per frame | {timed} frames in the last session | "
+                       f"{sum(d)/timed:.4f} | | | {tot/1e6/timed:.4f} |")
 agg = collections.defaultdict(list)
 for d in sorted(x for x in os.listdir(src) if x.startswith("pmc")):
     p = os.path.join(src, d, "run_counter_collection.csv")
@@ -57,9 +63,16 @@ for d in sorted(x for x in os.listdir(src) if x.startswith("pmc")):
                 (int(r["Dispatch_Id"]), float(r["Counter_Value"])))
 # the timed dispatches only (the last `timed` of each kernel, as in the trace section): the
 # bench's probe render (one row) and warmup frames would otherwise pull the average down
+# the service's last session renders `timed` frames: per-frame values of the extensive
+# counters (instructions, cycles, bytes); ratios and means stay as measured
+INTENSIVE = ("VALUUtilization", "VALUBusy", "MeanOccupancyPerCU")
 for key, v in agg.items():
-    agg[key] = [x for _, x in sorted(v)[-timed:]]
-out += ["", f"## PMC counters (average per dispatch over the last {timed} dispatches of each kernel, separate passes)\n",
+    if SVC in key[0]:
+        agg[key] = [x if key[1] in INTENSIVE else x / timed for _, x in sorted(v)[-1:]]
+    else:
+        agg[key] = [x for _, x in sorted(v)[-timed:]]
+out += ["", f"## PMC counters (average per dispatch over the last {timed} dispatches of each kernel; for "
+        f"{SVC}: its last dispatch / {timed} frames, i.e. per frame; separate passes)\n",
         "| kernel | counter | value |", "|---|---|---|"]
 for (k, c), v in sorted(agg.items()):
     val = sum(v) / len(v)
@@ -83,7 +96,12 @@ if ccfg:
     rel = os.path.relpath(os.path.abspath(dst), os.path.dirname(os.path.dirname(os.path.abspath(cp))))
     entry = {}
     for short in ("render_kernel", "fold_kernel"):
-        vals = {c: sum(v) / len(v) for (k, c), v in agg.items() if short in k}
+        # the render kernel of the timed frames: the service's when it ran (the bench's
+        # one-row probe launch is a plain render_kernel dispatch)
+        names = {k for (k, c) in agg if short in k}
+        if short == "render_kernel" and any(SVC in k for k in names):
+            names = {k for k in names if SVC in k}
+        vals = {c: sum(v) / len(v) for (k, c), v in agg.items() if k in names}
         if not vals:
             continue
         e = {"source": rel}

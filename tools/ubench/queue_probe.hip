@@ -201,6 +201,48 @@ int main()
         CK(hipStreamDestroy(a));
         CK(hipStreamDestroy(c));
     }
+    // T6: a long kernel on one stream, short kernels on 7 other streams: which of them run
+    // while it runs (streams sharing a hardware queue with it would wait for it)
+    {
+        const int ns = 8;
+        hipStream_t st[ns];
+        for (int i = 0; i < ns; ++i) CK(hipStreamCreateWithFlags(&st[i], hipStreamNonBlocking));
+        unsigned long long *d_ts = nullptr;
+        CK(hipMalloc(&d_ts, 64 * sizeof(unsigned long long)));
+        CK(hipMemset(d_ts, 0, 64 * sizeof(unsigned long long)));
+        CK(hipDeviceSynchronize());
+        hipLaunchKernelGGL(producer, dim3(1), dim3(64), 0, st[0], ctr, d_ts, 30000u);  // 30 ms
+        std::this_thread::sleep_for(std::chrono::milliseconds(2));
+        for (int i = 1; i < ns; ++i) hipLaunchKernelGGL(consumer, dim3(1), dim3(64), 0, st[i], ctr, d_ts + 2 * i, seen);
+        CK(hipDeviceSynchronize());
+        unsigned long long t[64];
+        CK(hipMemcpy(t, d_ts, sizeof t, hipMemcpyDeviceToHost));
+        const char *env = getenv("GPU_MAX_HW_QUEUES");
+        printf("T6 GPU_MAX_HW_QUEUES=%s: long kernel ends at t=0; short kernels start at", env ? env : "(unset)");
+        for (int i = 1; i < ns; ++i) printf(" %+.1f", ((double)(long long)(t[2 * i + 1] - t[0])) / 100.0);
+        printf(" us\n");
+        for (int i = 0; i < ns; ++i) CK(hipStreamDestroy(st[i]));
+        // T7: the same with the long kernel on a high-priority stream, 12 short streams
+        int lo = 0, hi = 0;
+        CK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+        hipStream_t hs;
+        CK(hipStreamCreateWithPriority(&hs, hipStreamNonBlocking, hi));
+        const int nl = 12;
+        hipStream_t ls[nl];
+        for (int i = 0; i < nl; ++i) CK(hipStreamCreateWithFlags(&ls[i], hipStreamNonBlocking));
+        CK(hipMemset(d_ts, 0, 64 * sizeof(unsigned long long)));
+        CK(hipDeviceSynchronize());
+        hipLaunchKernelGGL(producer, dim3(1), dim3(64), 0, hs, ctr, d_ts, 30000u);
+        std::this_thread::sleep_for(std::chrono::milliseconds(2));
+        for (int i = 0; i < nl; ++i) hipLaunchKernelGGL(consumer, dim3(1), dim3(64), 0, ls[i], ctr, d_ts + 2 * (i + 1), seen);
+        CK(hipDeviceSynchronize());
+        CK(hipMemcpy(t, d_ts, sizeof t, hipMemcpyDeviceToHost));
+        printf("T7 priority range [%d, %d], long kernel on priority %d: short kernels (12 streams) start at", lo, hi, hi);
+        for (int i = 0; i < nl; ++i) printf(" %+.1f", ((double)(long long)(t[2 * (i + 1) + 1] - t[0])) / 100.0);
+        printf(" us\n");
+        CK(hipStreamDestroy(hs));
+        for (int i = 0; i < nl; ++i) CK(hipStreamDestroy(ls[i]));
+    }
     printf("done\n");
     return 0;
 }

@@ -129,19 +129,28 @@ def cpu_baseline(scene, view, w, h, spp_sample, bounces):
                       f"renders ((W/tc)*tc x (H/tc)*tc, Renderer.hpp:264-265)"}
 
 
-def dropin_bench(w, h, spp, bounces, frames, tcs):
+def dropin_bench(w, h, spp, bounces, frames, tcs, env=None):
     """The C++ drop-in (include/spt/RenderSegmentShim.hpp) driven exactly like
     RenderImageParallelMain (tools/dropin_harness.cpp): tc x tc RenderJob tiles, <= tc
-    threads in flight, host g_data, per tc the Msamples/s of `frames` timed frames."""
+    threads in flight, host g_data, per tc the Msamples/s of `frames` timed frames; and
+    the calling pattern's own ceiling: the same frames with RenderJob doing nothing
+    (SPT_HARNESS_NOOP), as ms per frame and the rate it would allow."""
     import subprocess
     exe = os.path.join(ROOT, "simplepathtracer_amd", "lib", "spt_dropin_harness")
     if not os.path.exists(exe):
         return None
     out = {}
+    run_env = dict(os.environ, **(env or {}))
     for tc in tcs:
+        r = subprocess.run([exe, "/dev/null", str(w), str(h), str(spp), str(bounces), str(tc), "0", str(frames)],
+                           capture_output=True, text=True, timeout=600, env=dict(run_env, SPT_HARNESS_NOOP="1"))
+        if r.returncode == 0:
+            sec = float(r.stdout.split("seconds=")[1].split()[0])
+            out[f"noop_tc{tc}_ms_per_frame"] = round(sec / frames * 1e3, 3)
+            out[f"noop_tc{tc}_ceiling"] = round(tiled_pixels(w, h, tc) * spp * frames / sec / 1e6, 1)
         for task in (0, 1):
             r = subprocess.run([exe, "/dev/null", str(w), str(h), str(spp), str(bounces), str(tc), str(task),
-                                str(frames)], capture_output=True, text=True, timeout=600)
+                                str(frames)], capture_output=True, text=True, timeout=600, env=run_env)
             if r.returncode != 0:
                 raise RuntimeError(f"dropin harness failed: {r.stderr[-400:]}")
             sec = float(r.stdout.split("seconds=")[1].split()[0])
@@ -232,7 +241,7 @@ def main():
                          "the previous one's last paths drain; each stream has its own workspace); 0 = auto: "
                          "2 when a frame is one workspace batch, else 1 (long multi-batch frames gain nothing "
                          "and would double the workspace)")
-    ap.add_argument("--service", type=int, default=1,
+    ap.add_argument("--service", type=int, default=0,
                     help="1: frames are jobs of the resident render service (spt_service_start: one persistent "
                          "launch per timed region, no launch ramp and tail per frame); 0: one launch per frame")
     ap.add_argument("--cpu-spp", type=int, default=0,

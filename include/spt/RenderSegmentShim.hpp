@@ -65,10 +65,10 @@ inline spt_ctx *context()
             const char *dev = std::getenv("SPT_DEVICE");
             check(nullptr, spt_ctx_create(dev ? std::atoi(dev) : 0, &c), "spt_ctx_create");
         }
-        // RenderJob tiles are jobs of the resident render service (SPT_SERVICE=0: one
+        // SPT_SERVICE=1: RenderJob tiles are jobs of the resident render service (else one
         // launch per batch of tiles); its session idles out by itself between frames
         const char *svc = std::getenv("SPT_SERVICE");
-        if (!svc || std::atoi(svc) != 0) check(c, spt_service_start(c), "spt_service_start");
+        if (svc && std::atoi(svc) != 0) check(c, spt_service_start(c), "spt_service_start");
         return c;
     }();
     return ctx;

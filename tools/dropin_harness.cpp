@@ -62,35 +62,50 @@ int main(int argc, char **argv)
         g_materials.push_back(static_cast<Material>(m[i]));
     }
     if (spt_camera_basis(eyePos.xyzw, lookAt.xyzw, upDir.xyzw, viewMatrix.array)) return 4;
-    // RenderImageParallelMain: tc x tc tiles, at most tc in flight
+    // SPT_HARNESS_NOOP=1: the same threads and tiles with RenderJob doing nothing -- the
+    // calling pattern's own cost (thread spawn, condition variable, join) per frame, the
+    // ceiling any RenderSegment implementation can reach under it
+    const bool noop = std::getenv("SPT_HARNESS_NOOP") && std::atoi(std::getenv("SPT_HARNESS_NOOP")) != 0;
+    // RenderImageParallelMain (Renderer.hpp:257-302) as written: per tile a thread running
+    // RenderJob (242-255: it takes a free slot when it starts and returns it when its tile
+    // is done, then notifies) is spawned and detached, and the main thread waits for a free
+    // slot before the next; at the end it waits until all tc slots are free.  Two changes
+    // keep the harness itself defined: the count, condition variable and mutex outlive the
+    // frame (the reference's are locals while detached threads may still notify them),
+    // and the slot is returned under the mutex (the reference's unlocked fetch_add +
+    // notify can be lost and leave the final wait asleep).  `alive` lets main return only
+    // after every detached thread has finished touching them.
+    static std::atomic<int> free_threads, alive{0};
+    static std::condition_variable cv;
+    static std::mutex mu;
     auto frame_once = [&]() {
         const uint32_t sw = g_width / tc, sh = g_height / tc;
-        std::atomic<int> free_threads((int)tc);
-        std::condition_variable cv;
-        std::mutex mu;
-        std::vector<std::thread> threads;
+        free_threads = (int)tc;
+        std::unique_lock<std::mutex> lk(mu);
         for (uint32_t j = 0; j < tc; ++j)
             for (uint32_t i = 0; i < tc; ++i) {
                 RenderSegmentData seg{sh * j, sh * j + sh > g_height ? g_height : sh * j + sh, sw * i,
                                       sw * i + sw > g_width ? g_width : sw * i + sw};
-                {
-                    std::unique_lock<std::mutex> lk(mu);
-                    cv.wait(lk, [&] { return free_threads.load() > 0; });
+                alive.fetch_add(1);
+                std::thread thread([seg, task, noop] {
                     free_threads.fetch_sub(1);
-                }
-                threads.emplace_back([seg, task, &free_threads, &cv, &mu] {
-                    if (task)
+                    if (noop) {
+                    } else if (task) {
                         RenderSegmentTask(seg);
-                    else
+                    } else {
                         RenderSegment(seg);
+                    }
                     {
-                        std::lock_guard<std::mutex> lk(mu);
+                        std::lock_guard<std::mutex> g(mu);
                         free_threads.fetch_add(1);
                     }
                     cv.notify_one();
+                    alive.fetch_sub(1);
                 });
+                thread.detach();
+                cv.wait(lk, [] { return free_threads.load() > 0; });
             }
-        for (auto &t : threads) t.join();
+        cv.wait(lk, [&] { return free_threads.load() == (int)tc; });
     };
     frame_once();
     const int frames = argc > 8 ? atoi(argv[8]) : 0;
@@ -99,11 +114,12 @@ int main(int argc, char **argv)
         for (int k = 0; k < frames; ++k) frame_once();
         const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         spt_stats st{};
-        spt_get_stats(spt_shim::context(), &st);  // since the context's creation (no reset)
+        if (!noop) spt_get_stats(spt_shim::context(), &st);  // since the context's creation (no reset)
         printf("frames=%d seconds=%.6f calls=%llu batches=%llu render_ms=%.3f busy_ms=%.3f fold_ms=%.3f\n", frames, sec,
                (unsigned long long)st.batched_calls, (unsigned long long)st.batches, st.render_ms, st.render_busy_ms,
                st.fold_ms);
     }
+    while (alive.load() != 0) std::this_thread::yield();
     FILE *f = fopen(argv[1], "wb");
     if (!f) return 5;
     fwrite(frame.data(), 1, frame.size(), f);

@@ -41,6 +41,7 @@ for step in "$@"; do
     gpu) run gpu 600 $PYT -m gpu tests ;;
     smoke) run smoke 120 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 400 python bench.py ;;
+    bench1q) run bench1q 120 python bench.py --no-cpu-baseline --no-dropin --service 1 ;;
     bench0) run bench0 400 python bench.py --service 0 ;;
     benchq) run benchq 120 python bench.py --no-cpu-baseline --no-dropin ;;
     bench0q) run bench0q 120 python bench.py --no-cpu-baseline --no-dropin --service 0 ;;

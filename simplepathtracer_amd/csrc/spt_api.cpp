@@ -120,6 +120,12 @@ struct Service {
     uint64_t claims = 0;  // published
     uint64_t ring_head = 0;
     uint32_t next_done = 0;
+    // completion counters only grow (zeroed once at allocation): a job waits for its
+    // counter to reach the host's running total of the counter's samples, so no wait can
+    // see a count left over from an earlier job (a zeroing launch on the publish stream
+    // is not ordered before the caller's wait); a total that would pass 2^32 restarts at
+    // zero, with the caller's stream ordered after that publish
+    std::vector<uint64_t> done_cum;
     std::vector<SvcInflight> inflight;
     std::vector<hipEvent_t> ev_pool;
     hipEvent_t ev_start = nullptr, ev_end = nullptr, ev_ctl = nullptr;
@@ -551,7 +557,7 @@ int ensure_wavefront(spt_ctx *ctx, Workspace *w, uint32_t cap)
 // ---- render service (DESIGN.md §5 "Render service") -----------------------------------
 // The host publishes to a session only while it has published within kSvcHostIdleMs;
 // after a longer pause it ends the session and starts a new one.  The session's waves
-// leave after spt::kSvcIdleTicks (100 ms) without work, more than twice that, so a job is
+// leave after spt::kSvcIdleTicks (0.5 s) without work, far longer than that, so a job is
 // never published to a session that may have left.
 constexpr double kSvcHostIdleMs = 40.0;
 
@@ -591,7 +597,18 @@ int svc_begin(spt_ctx *ctx, int mode)
 {
     Service &v = ctx->svc;
     if (!v.stream) {
-        HIP_TRY(ctx, hipStreamCreateWithFlags(&v.stream, hipStreamNonBlocking));
+        // The resident kernel never ends while the session runs, so nothing may queue
+        // behind it: HIP maps a process's streams of one priority round-robin onto
+        // GPU_MAX_HW_QUEUES hardware queues (4 on the box), and a stream sharing the
+        // kernel's queue would wait for the session's end (a publish stuck there: a hang
+        // until the waves idle out).  A stream of another priority gets a queue of its own
+        // (tools/ubench/queue_probe T6/T7, profiles/queue_probe_r04.txt); SPT_SVC_PRIO
+        // picks it (default: the greatest priority).
+        int lo = 0, hi = 0;
+        HIP_TRY(ctx, hipDeviceGetStreamPriorityRange(&lo, &hi));
+        int prio = hi;
+        if (const char *e = std::getenv("SPT_SVC_PRIO")) prio = std::atoi(e);
+        HIP_TRY(ctx, hipStreamCreateWithPriority(&v.stream, hipStreamNonBlocking, prio));
         HIP_TRY(ctx, hipStreamCreateWithFlags(&v.pub, hipStreamNonBlocking));
         HIP_TRY(ctx, hipEventCreate(&v.ev_start));
         HIP_TRY(ctx, hipEventCreate(&v.ev_end));
@@ -604,6 +621,8 @@ int svc_begin(spt_ctx *ctx, int mode)
                         hipMalloc((void **)&v.d_ring, (size_t)v.ring_words * sizeof(uint32_t)) == hipSuccess;
         if (!ok) return fail(ctx, SPT_ERR_NOMEM, "render service buffers (%llu MiB ring) allocation failed",
                              (unsigned long long)(v.ring_bytes >> 20));
+        HIP_TRY(ctx, hipMemset(v.d_done, 0, (size_t)v.done_cap * sizeof(uint32_t)));
+        v.done_cum.assign(v.done_cap, 0);
     }
     spt::RenderArgs ra{};
     ra.scene = device_scene(ctx);
@@ -688,6 +707,10 @@ int svc_submit_jobs(spt_ctx *ctx, int mode, const SvcJobSpec *jobs, size_t n, ui
     v.ring_head = w1;
     const uint32_t idx = v.next_done;
     v.next_done = (v.next_done + 1u) % v.done_cap;
+    uint64_t target = v.done_cum[idx] + items;
+    const bool reset = target > 0xFFFFFFFFull;
+    if (reset) target = items;
+    v.done_cum[idx] = target;
     // flow control on the publish stream: folds still reading the ring words, or jobs
     // whose fold still waits on the counter, finish first (at most 1024 jobs in flight)
     for (size_t i = 0; i < v.inflight.size();) {
@@ -701,7 +724,7 @@ int svc_submit_jobs(spt_ctx *ctx, int mode, const SvcJobSpec *jobs, size_t n, ui
             ++i;
         }
     }
-    // the records, kSvcPubMax per publish launch; the first zeroes the counter
+    // the records, kSvcPubMax per publish launch; the first zeroes the counter on a reset
     for (size_t i0 = 0; i0 < n; i0 += spt::kSvcPubMax) {
         spt::SvcPublish p{};
         p.ctl = v.d_ctl;
@@ -710,7 +733,7 @@ int svc_submit_jobs(spt_ctx *ctx, int mode, const SvcJobSpec *jobs, size_t n, ui
         p.done = v.d_done;
         p.first_job = v.n_jobs;
         p.n_jobs = (uint32_t)std::min<size_t>(spt::kSvcPubMax, n - i0);
-        p.n_zero = i0 == 0 ? 1u : 0u;
+        p.n_zero = i0 == 0 && reset ? 1u : 0u;
         p.zero_idx[0] = idx;
         for (uint32_t k = 0; k < p.n_jobs; ++k) {
             const SvcJobSpec &js = jobs[i0 + k];
@@ -738,7 +761,14 @@ int svc_submit_jobs(spt_ctx *ctx, int mode, const SvcJobSpec *jobs, size_t n, ui
         HIP_TRY(ctx, spt::launch_svc_publish(p, v.pub));
     }
     v.last_pub = now;
-    HIP_TRY(ctx, hipStreamWaitValue32(s, v.d_done + idx, (uint32_t)items, hipStreamWaitValueGte, 0xFFFFFFFFu));
+    if (reset) {
+        hipEvent_t e = svc_event(ctx);
+        if (!e) return fail(ctx, SPT_ERR_HIP, "event creation failed");
+        HIP_TRY(ctx, hipEventRecord(e, v.pub));
+        HIP_TRY(ctx, hipStreamWaitEvent(s, e, 0));
+        v.ev_pool.push_back(e);
+    }
+    HIP_TRY(ctx, hipStreamWaitValue32(s, v.d_done + idx, (uint32_t)target, hipStreamWaitValueGte, 0xFFFFFFFFu));
     *w0_out = w0;
     *idx_out = idx;
     return SPT_OK;

@@ -359,7 +359,7 @@ struct SvcPublish {
     uint32_t *done;
     uint32_t first_job, n_jobs;  // records [first_job, first_job + n_jobs)
     uint32_t pub_claims;         // claims published after them
-    uint32_t n_zero;             // completion counters zeroed before the jobs are published
+    uint32_t n_zero;             // completion counters zeroed before the jobs are published (total restarts)
     uint32_t zero_idx[kSvcPubMax];
     SvcJob rec[kSvcPubMax];
 };

@@ -639,8 +639,9 @@ __global__ __launch_bounds__(kRenderBlock) SPT_RENDER_ATTR void render_kernel_sv
     render_body<TREE, LEAF, false, kRenderBlock, false, false, true>(a);
 }
 
-// The publish launch: one wave stores the job records, their first claims and the zeroed
-// completion counters write-through (sc1), drains its stores, then lane 0 stores the
+// The publish launch: one wave stores the job records, their first claims and (when the
+// host restarts a counter's running total) the zeroed completion counter write-through
+// (sc1), drains its stores, then lane 0 stores the
 // published pair {claims, jobs} (the R1 hand-off of MI355X_MICROARCH.md: the service polls
 // the pair and reads the records with sc1 loads).
 __global__ __launch_bounds__(64) void svc_publish_kernel(SvcPublish p)

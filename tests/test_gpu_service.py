@@ -143,7 +143,7 @@ def test_service_restarts_after_a_pause_and_a_setter(spt, golden_scenes):
         ctx.render_rows_async(0, 0, H, 1, 1, 0, 0, W, rgba.data_ptr(), 0, st0.cuda_stream)
         st0.synchronize()  # the stream only: the session stays resident
         outs.append(rgba.cpu().numpy())
-        time.sleep(0.3)  # > 100 ms: the session's waves leave
+        time.sleep(0.7)  # > kSvcIdleTicks (0.5 s): the session's waves leave
     view2 = spt.camera_basis([0.5, 1.2, -3, 0], LOOK, UP)
     ctx.set_camera(view2, EYE, SKY)
     rgba2 = torch.zeros((W * H, 4), dtype=torch.float32, device="cuda")

@@ -25,6 +25,8 @@ ap.add_argument("--streams", type=int, default=1, help="frames in flight on alte
 ap.add_argument("--frames", type=int, default=20)
 ap.add_argument("--service", type=int, default=1)
 ap.add_argument("--record", default="")
+ap.add_argument("--ns", default="1,2,4,8", help="rank counts to probe")
+ap.add_argument("--stats", type=int, default=0, help="print the context's service counters per N")
 args = ap.parse_args()
 W, H, SPP, B = {"c2": (1200, 800, 100, 50), "c3": (3840, 2160, 1024, 50)}[args.config]
 ctx = spt.Context(0)
@@ -34,7 +36,7 @@ ctx.set_params(W, H, SPP, B, 1)
 base = None
 streams = [torch.cuda.Stream() for _ in range(args.streams)]
 lines = []
-for n in (1, 2, 4, 8):
+for n in [int(x) for x in args.ns.split(",")]:
     split = FrameSplit(W, H, n, even_strip(H, n))
     tiles = [torch.zeros((split.tile_pixels(), 4), dtype=torch.float32, device="cuda") for _ in streams]
 
@@ -43,6 +45,7 @@ for n in (1, 2, 4, 8):
                               tiles[k % len(streams)].data_ptr(), 0, streams[k % len(streams)].cuda_stream)
 
     ts = []
+    ctx.reset_stats()
     for r in range(args.reps + 1):
         ctx.synchronize()
         torch.cuda.synchronize()
@@ -62,6 +65,11 @@ for n in (1, 2, 4, 8):
             f"({args.streams} stream(s)), ideal {base / n:8.3f} ms, efficiency {base / n / t:6.3f}")
     print(line, flush=True)
     lines.append(line)
+    if args.stats:
+        st = ctx.stats()
+        print("   stats: " + " ".join(f"{k}={st[k]}" for k in ("launches", "svc_sessions", "svc_jobs", "svc_watchdog_exits",
+                                                               "svc_kernel_ms", "svc_grid_blocks", "render_busy_ms")),
+              flush=True)
 if args.record:
     try:
         head = subprocess.run(["git", "rev-parse", "--short", "HEAD"], capture_output=True, text=True,

@@ -14,6 +14,7 @@
 #          c5 / c3      bench.py --config c5 / c3 (quick legs)
 #          scaling      tools/scaling_probe.py --streams 2 (service on and off)
 #          dropin       the C++ drop-in harness at tc = 4 and tc = 32 (bench.py's legs)
+#          dropin1      the same with SPT_SERVICE=1 (the shim's calls through the render service)
 #          profile      tools/profile.sh <tag>_c2 c2 (kernel trace + PMC passes + SPT_DIAG)
 #          profile5     tools/profile.sh <tag>_c5 c5 --config c5 --steps 2 --warmup 1 ...
 #          ab:<args>    tools/ab.py <args>
@@ -50,6 +51,7 @@ for step in "$@"; do
     scaling) run scaling 300 python tools/scaling_probe.py --streams 2 --reps 5 --service 1 --record "gpurun_out/${TAG}_scaling.txt"
              run scaling0 300 python tools/scaling_probe.py --streams 2 --reps 5 --service 0 --record "gpurun_out/${TAG}_scaling0.txt" ;;
     dropin) run dropin 300 python -c "import bench; print(bench.dropin_bench(1200, 800, 100, 50, 5, (4, 32)))" ;;
+    dropin1) run dropin1 300 python -c "import bench; print(bench.dropin_bench(1200, 800, 100, 50, 5, (4, 32), {'SPT_SERVICE': '1'}))" ;;
     profile) run profile 900 bash tools/profile.sh "${TAG}_c2" c2 ;;
     profile5) run profile5 900 bash tools/profile.sh "${TAG}_c5" c5 --config c5 --steps 2 --warmup 1 --no-cpu-baseline ;;
     ab:*) run ab 600 python tools/ab.py ${step#ab:} ;;

@@ -604,12 +604,17 @@ int svc_begin(spt_ctx *ctx, int mode)
         // until the waves idle out).  A stream of another priority gets a queue of its own
         // (tools/ubench/queue_probe T6/T7, profiles/queue_probe_r04.txt); SPT_SVC_PRIO
         // picks it (default: the greatest priority).
+        // The publish stream must not share a queue with the callers' streams either: a
+        // caller's counter wait would hold every later publish behind it, so jobs would be
+        // published one fold at a time (SPT_SVC_PUB_PRIO; default: the least priority;
+        // T9).
         int lo = 0, hi = 0;
         HIP_TRY(ctx, hipDeviceGetStreamPriorityRange(&lo, &hi));
-        int prio = hi;
+        int prio = hi, pub_prio = lo;
         if (const char *e = std::getenv("SPT_SVC_PRIO")) prio = std::atoi(e);
+        if (const char *e = std::getenv("SPT_SVC_PUB_PRIO")) pub_prio = std::atoi(e);
         HIP_TRY(ctx, hipStreamCreateWithPriority(&v.stream, hipStreamNonBlocking, prio));
-        HIP_TRY(ctx, hipStreamCreateWithFlags(&v.pub, hipStreamNonBlocking));
+        HIP_TRY(ctx, hipStreamCreateWithPriority(&v.pub, hipStreamNonBlocking, pub_prio));
         HIP_TRY(ctx, hipEventCreate(&v.ev_start));
         HIP_TRY(ctx, hipEventCreate(&v.ev_end));
         HIP_TRY(ctx, hipEventCreateWithFlags(&v.ev_ctl, hipEventDisableTiming));
@@ -1169,11 +1174,15 @@ int launch_batch(spt_ctx *ctx, BatchSet *bs, const std::vector<BatchReq *> &batc
     const size_t n = batch.size();
     int rc = SPT_OK;
     if (bs->h_rects_cap < n) {
+        // hipHostFree synchronises the device, which a resident service kernel would hold
+        // until its waves idle out (0.5 s): end the session first; grow geometrically
+        if ((rc = svc_end(ctx))) return rc;
+        const size_t cap = std::max<size_t>({n, 2 * bs->h_rects_cap, 64});
         if (bs->h_rects) HIP_TRY(ctx, hipHostFree(bs->h_rects));
         bs->h_rects = nullptr;
         bs->h_rects_cap = 0;
-        HIP_TRY(ctx, hipHostMalloc((void **)&bs->h_rects, n * sizeof(spt::BatchRect)));
-        bs->h_rects_cap = n;
+        HIP_TRY(ctx, hipHostMalloc((void **)&bs->h_rects, cap * sizeof(spt::BatchRect)));
+        bs->h_rects_cap = cap;
     }
     if ((rc = ensure(ctx, &bs->d_rects, &bs->rects_cap, n))) return rc;
     if (any_g && (rc = ensure(ctx, &ctx->d_frame8, &ctx->frame8_cap, (size_t)W * H * 3))) return rc;

@@ -412,6 +412,7 @@ def test_workspace_batches_fold_in_order(spt, ctx, golden_scenes, task):
     ctx.reset_stats()
     st = torch.cuda.Stream()
     out = torch.zeros((64 * 128, 4), dtype=torch.float32, device="cuda")
+    torch.cuda.synchronize()  # the fill runs on the current stream, the render on st
     ctx.render_rows_async(spt.MODE_TASK if task else spt.MODE_SEGMENT, 200, 264, 1, 1, 0, 100, 228,
                           out.data_ptr(), 0, st.cuda_stream)
     st.synchronize()
@@ -1145,6 +1146,7 @@ def test_small_launches_on_two_streams_render_the_same(spt, ctx, golden_scenes):
     mr = max(rows)
     streams = [torch.cuda.Stream(), torch.cuda.Stream()]
     two = torch.zeros((parts, mr * 1200, 4), dtype=torch.float32, device="cuda")
+    torch.cuda.synchronize()  # the fill runs on the current stream, the renders on others
     for p in range(parts):
         ctx.render_rows_async(0, 0, 800, strip, parts, p, 0, 1200, two[p].data_ptr(), 0, streams[p % 2].cuda_stream)
     torch.cuda.synchronize()

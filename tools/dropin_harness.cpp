@@ -115,9 +115,11 @@ int main(int argc, char **argv)
         const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         spt_stats st{};
         if (!noop) spt_get_stats(spt_shim::context(), &st);  // since the context's creation (no reset)
-        printf("frames=%d seconds=%.6f calls=%llu batches=%llu render_ms=%.3f busy_ms=%.3f fold_ms=%.3f\n", frames, sec,
-               (unsigned long long)st.batched_calls, (unsigned long long)st.batches, st.render_ms, st.render_busy_ms,
-               st.fold_ms);
+        printf("frames=%d seconds=%.6f calls=%llu batches=%llu render_ms=%.3f busy_ms=%.3f fold_ms=%.3f "
+               "svc_sessions=%llu svc_jobs=%llu svc_watchdog_exits=%llu svc_kernel_ms=%.3f\n",
+               frames, sec, (unsigned long long)st.batched_calls, (unsigned long long)st.batches, st.render_ms,
+               st.render_busy_ms, st.fold_ms, (unsigned long long)st.svc_sessions, (unsigned long long)st.svc_jobs,
+               (unsigned long long)st.svc_watchdog_exits, st.svc_kernel_ms);
     }
     while (alive.load() != 0) std::this_thread::yield();
     FILE *f = fopen(argv[1], "wb");

@@ -27,6 +27,7 @@ ap.add_argument("--service", type=int, default=1)
 ap.add_argument("--record", default="")
 ap.add_argument("--ns", default="1,2,4,8", help="rank counts to probe")
 ap.add_argument("--stats", type=int, default=0, help="print the context's service counters per N")
+ap.add_argument("--strip", type=int, default=0, help="rows per interleaved strip (0: even_strip, the bench's)")
 args = ap.parse_args()
 W, H, SPP, B = {"c2": (1200, 800, 100, 50), "c3": (3840, 2160, 1024, 50)}[args.config]
 ctx = spt.Context(0)
@@ -37,7 +38,7 @@ base = None
 streams = [torch.cuda.Stream() for _ in range(args.streams)]
 lines = []
 for n in [int(x) for x in args.ns.split(",")]:
-    split = FrameSplit(W, H, n, even_strip(H, n))
+    split = FrameSplit(W, H, n, args.strip or even_strip(H, n))
     tiles = [torch.zeros((split.tile_pixels(), 4), dtype=torch.float32, device="cuda") for _ in streams]
 
     def frame(k):

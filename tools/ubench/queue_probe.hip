@@ -7,6 +7,8 @@
 //   T4     a one-thread "publish" kernel storing the word instead.
 //   T5     host cost of one job's stream operations (publish kernel + wait value +
 //          gated kernel + event) over 1000 jobs.
+//   T6-T9  which streams share a hardware queue with a long-running kernel (priorities).
+//   T10    a running kernel polling a word of coherent pinned host memory the host stores.
 // Every spin is bounded (s_memrealtime, 100 MHz): a missed signal ends in a timeout
 // code, never a hang.  Build: hipcc --offload-arch=gfx950 -O2 queue_probe.hip
 #include <hip/hip_runtime.h>
@@ -242,6 +244,53 @@ int main()
         printf(" us\n");
         CK(hipStreamDestroy(hs));
         for (int i = 0; i < nl; ++i) CK(hipStreamDestroy(ls[i]));
+        // T8 / T9: the long kernel on a high-priority stream, short kernels on 7 other
+        // streams of the same (high) or the lowest priority
+        for (int variant = 0; variant < 2; ++variant) {
+            const int prio = variant == 0 ? hi : lo;
+            hipStream_t h0, os[7];
+            CK(hipStreamCreateWithPriority(&h0, hipStreamNonBlocking, hi));
+            for (int i = 0; i < 7; ++i) CK(hipStreamCreateWithPriority(&os[i], hipStreamNonBlocking, prio));
+            CK(hipMemset(d_ts, 0, 64 * sizeof(unsigned long long)));
+            CK(hipDeviceSynchronize());
+            hipLaunchKernelGGL(producer, dim3(1), dim3(64), 0, h0, ctr, d_ts, 30000u);
+            std::this_thread::sleep_for(std::chrono::milliseconds(2));
+            for (int i = 0; i < 7; ++i) hipLaunchKernelGGL(consumer, dim3(1), dim3(64), 0, os[i], ctr, d_ts + 2 * (i + 1), seen);
+            CK(hipDeviceSynchronize());
+            CK(hipMemcpy(t, d_ts, sizeof t, hipMemcpyDeviceToHost));
+            printf("T%d long kernel on priority %d, short kernels on 7 streams of priority %d start at", 8 + variant, hi,
+                   prio);
+            for (int i = 0; i < 7; ++i) printf(" %+.1f", ((double)(long long)(t[2 * (i + 1) + 1] - t[0])) / 100.0);
+            printf(" us\n");
+            CK(hipStreamDestroy(h0));
+            for (int i = 0; i < 7; ++i) CK(hipStreamDestroy(os[i]));
+        }
+    }
+    // T10: a running kernel polls a word in coherent pinned host memory that the host
+    // stores (no stream operation): host store -> the kernel's end seen by the host
+    {
+        unsigned *hw = nullptr;
+        CK(hipHostMalloc((void **)&hw, 64, hipHostMallocCoherent));
+        hipStream_t a;
+        CK(hipStreamCreateWithFlags(&a, hipStreamNonBlocking));
+        for (int rep = 0; rep < 3; ++rep) {
+            __atomic_store_n(hw, 0u, __ATOMIC_RELEASE);
+            CK(hipMemset(d_t, 0, 32));
+            CK(hipDeviceSynchronize());
+            hipLaunchKernelGGL(poller, dim3(1), dim3(64), 0, a, hw, 1u, d_t, 200000u);
+            std::this_thread::sleep_for(std::chrono::milliseconds(2));
+            const auto h0 = std::chrono::steady_clock::now();
+            __atomic_store_n(hw, 1u, __ATOMIC_RELEASE);
+            while (hipStreamQuery(a) == hipErrorNotReady) {
+            }
+            const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - h0).count();
+            unsigned long long t2[2];
+            CK(hipMemcpy(t2, d_t, 16, hipMemcpyDeviceToHost));
+            printf("T10 host store rep %d: poller %s, host saw the kernel end %.1f us after its store\n", rep,
+                   t2[1] == ~0ull ? "TIMED OUT" : "saw it", us);
+        }
+        CK(hipStreamDestroy(a));
+        CK(hipHostFree(hw));
     }
     printf("done\n");
     return 0;

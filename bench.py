@@ -241,9 +241,12 @@ def main():
                          "the previous one's last paths drain; each stream has its own workspace); 0 = auto: "
                          "2 when a frame is one workspace batch, else 1 (long multi-batch frames gain nothing "
                          "and would double the workspace)")
-    ap.add_argument("--service", type=int, default=0,
+    ap.add_argument("--service", type=int, default=-1,
                     help="1: frames are jobs of the resident render service (spt_service_start: one persistent "
-                         "launch per timed region, no launch ramp and tail per frame); 0: one launch per frame")
+                         "launch per timed region, no launch ramp and tail per frame); 0: one launch per frame; "
+                         "-1 (default): the service for the rank shares of N > 1 ranks, launches at N = 1 "
+                         "(profiles/svc_timeline_r04.txt: 20 config-2 frames, 1/8 shares 13.4 vs 14.4 ms, "
+                         "whole frames 95.0 vs 92.9 ms)")
     ap.add_argument("--cpu-spp", type=int, default=0,
                     help="spp of the CPU-baseline sample (0: the config's own spp on config 2, scaled down on others)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -340,7 +343,7 @@ def main():
 
     # the render service (--service 1) is started around each timed region and stopped
     # (drained) inside it: a device-wide synchronisation must not wait for its resident kernel
-    use_svc = args.service and args.engine == "megakernel"
+    use_svc = (args.service if args.service >= 0 else world > 1) and args.engine == "megakernel"
     if use_svc:
         ctx.service_start()
     for _ in range(args.warmup):
@@ -425,7 +428,7 @@ def main():
                                    f"{spp} spp, depth {bounces}, {args.mode} mode, {args.engine}",
                        "width": W, "height": H, "spp": spp, "bounces": bounces, "spheres": scene.n,
                        "parallelism": f"row-strips{split.strip}x{world}" if world > 1 else "1 GPU",
-                       "frames_in_flight": nst},
+                       "frames_in_flight": nst, "render_service": bool(use_svc)},
             # contract form: the render kernel against HBM with SURVEY §8(d)'s algorithmic
             # bytes; HBM does not bind this kernel (VALU issue + latency do: roofline_valu)
             "roofline": {"bound": "hbm", "achieved": round(algo_bytes / t_launch / 1e9, 4),

@@ -132,6 +132,7 @@ struct Service {
     std::chrono::steady_clock::time_point last_pub;
     uint64_t sessions = 0, jobs = 0, watchdog_exits = 0;
     double kernel_ms = 0;  // summed session spans
+    unsigned long long *d_trace = nullptr;  // SPT_SVC_TRACE: printed by svc_end
 };
 }  // namespace
 
@@ -588,6 +589,26 @@ int svc_end(spt_ctx *ctx)
     uint32_t wd = 0;
     HIP_TRY(ctx, hipMemcpy(&wd, v.d_ctl + spt::kSvcWatchdog, sizeof wd, hipMemcpyDeviceToHost));
     if (wd) v.watchdog_exits++;
+    if (v.d_trace) {
+        // per counter used this session: first / last claim taken, last count, in us
+        // from the session's first claim (s_memrealtime: 100 MHz)
+        std::vector<unsigned long long> tr((size_t)v.done_cap * 4 + spt::kSvcTraceClaims);
+        HIP_TRY(ctx, hipMemcpy(tr.data(), v.d_trace, tr.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+        unsigned long long t0 = ~0ull;
+        for (uint32_t i = 0; i < v.done_cap; ++i) t0 = std::min(t0, tr[4 * i]);
+        for (uint32_t i = 0; i < v.done_cap; ++i)
+            if (tr[4 * i] != ~0ull)
+                std::fprintf(stderr, "svc trace idx %u: claims %.1f .. %.1f us, last count %.1f us\n", i,
+                             (tr[4 * i] - t0) / 100.0, (tr[4 * i + 1] - t0) / 100.0, (tr[4 * i + 2] - t0) / 100.0);
+        if (const char *path = std::getenv("SPT_SVC_TRACE_FILE")) {
+            // the per-claim take times (block << 40 | 40-bit time), raw
+            if (FILE *f = std::fopen(path, "wb")) {
+                std::fwrite(&t0, sizeof t0, 1, f);
+                std::fwrite(tr.data() + (size_t)v.done_cap * 4, sizeof(unsigned long long), spt::kSvcTraceClaims, f);
+                std::fclose(f);
+            }
+        }
+    }
     return SPT_OK;
 }
 
@@ -646,6 +667,14 @@ int svc_begin(spt_ctx *ctx, int mode)
     ra.svc_jobs = v.d_jobs;
     ra.svc_job_claim = v.d_job_claim;
     ra.svc_done = v.d_done;
+    if (std::getenv("SPT_SVC_TRACE")) {
+        const size_t n = (size_t)v.done_cap * 4 + spt::kSvcTraceClaims;
+        if (!v.d_trace) HIP_TRY(ctx, hipMalloc((void **)&v.d_trace, n * sizeof(unsigned long long)));
+        std::vector<unsigned long long> init(n, 0ull);
+        for (size_t i = 0; i < (size_t)v.done_cap * 4; i += 4) init[i] = ~0ull;
+        HIP_TRY(ctx, hipMemcpy(v.d_trace, init.data(), n * sizeof(unsigned long long), hipMemcpyHostToDevice));
+        ra.svc_trace = v.d_trace;
+    }
     // control words zeroed before the kernel and before any publish of the session
     HIP_TRY(ctx, hipMemsetAsync(v.d_ctl, 0, spt::kSvcCtlWords * sizeof(uint32_t), v.stream));
     HIP_TRY(ctx, hipEventRecord(v.ev_ctl, v.stream));

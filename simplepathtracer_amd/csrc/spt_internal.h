@@ -312,6 +312,9 @@ struct RenderArgs {
     const struct SvcJob *svc_jobs;
     const uint32_t *svc_job_claim;
     uint32_t *svc_done;
+    // SPT_SVC_TRACE (diagnostics, null otherwise): per completion counter, the
+    // s_memrealtime of the first and last claim taken and of the last count added
+    unsigned long long *svc_trace;
 };
 
 // claim counters: at most one per XCD, 256 bytes apart (separate cache lines)
@@ -352,6 +355,7 @@ constexpr uint32_t kSvcCtlWords = kSvcWatchdog + 64;
 constexpr unsigned long long kSvcIdleTicks = 50000000ull;
 // jobs published by one publish launch (their records travel in its kernel arguments)
 constexpr uint32_t kSvcPubMax = 16;
+constexpr uint32_t kSvcTraceClaims = 1u << 21;  // SPT_SVC_TRACE: claims with a take time
 struct SvcPublish {
     uint32_t *ctl;
     SvcJob *jobs;

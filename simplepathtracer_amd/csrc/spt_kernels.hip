@@ -242,6 +242,7 @@ __device__ __forceinline__ void svc_flush(uint32_t idx, uint32_t cnt, uint32_t l
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     if (lane == 0) __hip_atomic_fetch_add((gu32 *)(k.svc_done + idx), cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (k.svc_trace && lane == 0) atomicMax(k.svc_trace + 4u * idx + 2u, __builtin_amdgcn_s_memrealtime());
 }
 
 template <bool TREE, int LEAF, bool LDSN, uint32_t BLOCK, bool BATCH = false, bool GLANE = false, bool SVC = false>
@@ -407,6 +408,16 @@ __device__ __forceinline__ void render_body(const RenderArgs &a)
         }
         blk_cur = nb * a.claim;
         blk_end = min(blk_cur + a.claim, __builtin_amdgcn_readfirstlane(rec[1]));
+        kargs_t &kt = *kernarg_args();
+        if (kt.svc_trace && lane == 0) {
+            const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+            unsigned long long *tr = kt.svc_trace + 4u * rec[3];
+            atomicMin(tr, t);
+            atomicMax(tr + 1, t);
+            // per claim (SPT_SVC_TRACE_FILE): its take time, the taking block in the top bits
+            if (nb < kSvcTraceClaims)
+                kt.svc_trace[4u * 4096u + nb] = (t & 0xFFFFFFFFFFull) | ((unsigned long long)blockIdx.x << 40);
+        }
     };
 
     for (;;) {

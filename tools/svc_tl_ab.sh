@@ -1,8 +1,11 @@
 #!/bin/bash
-# Service timeline A/B (tools/svc_timeline.py, 2 reps each): env variants x N, then launches.
-for v in "SPT_SVC_X=0" "SPT_SVC_TAIL_CLAIM=0" "SPT_SVC_TAIL_DIV=4" "SPT_SVC_TAIL_CLAIM=64" "SPT_SVC_CLAIM=448"; do
+# Service timeline A/B (tools/svc_timeline.py, 2 reps each): "LIB [ENV=VAL...]" variants x N,
+# then launches.
+for v in "libspt_hip.so" "libspt_hip_wave.so SPT_SVC_CLAIM=448" "libspt_hip.so SPT_SVC_CLAIM=896" "libspt_hip.so SPT_SVC_CLAIM=3584"; do
+  set -- $v
+  L=$1; shift
   for n in 8 1; do
-    r=$(env $v timeout -k 10 120 python tools/svc_timeline.py --n $n --reps 2 2>&1 | grep -o "wall [0-9.]* ms\|slope [0-9.]* ms/frame, intercept [0-9.]* ms" | tr '\n' ' ')
+    r=$(env SPT_LIB=$L "$@" timeout -k 10 120 python tools/svc_timeline.py --n $n --reps 2 2>&1 | grep -o "wall [0-9.]* ms\|slope [0-9.]* ms/frame, intercept [0-9.]* ms\|Error.*" | tr '\n' ' ')
     echo "$v n=$n: $r"
   done
 done

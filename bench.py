@@ -343,7 +343,10 @@ def main():
 
     # the render service (--service 1) is started around each timed region and stopped
     # (drained) inside it: a device-wide synchronisation must not wait for its resident kernel
-    use_svc = (args.service if args.service >= 0 else world > 1) and args.engine == "megakernel"
+    # (auto: rank shares of N > 1 ranks, each on a GPU of its own -- ranks rehearsed on a
+    # shared GPU would hold each other's resident kernels off the CUs)
+    auto_svc = world > 1 and world <= torch.cuda.device_count()
+    use_svc = (args.service if args.service >= 0 else auto_svc) and args.engine == "megakernel"
     if use_svc:
         ctx.service_start()
     for _ in range(args.warmup):

@@ -251,7 +251,7 @@ def main():
                     help="spp of the CPU-baseline sample (0: the config's own spp on config 2, scaled down on others)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-dropin", action="store_true", help="skip the C++ drop-in measurement (config 2)")
-    ap.add_argument("--dropin-frames", type=int, default=5)
+    ap.add_argument("--dropin-frames", type=int, default=20)
     ap.add_argument("--dump", default="", help="write rank 0's final g_data bytes to this file")
     ap.add_argument("--launch-check", action="store_true",
                     help="only start the ranks and report the process group (launcher test; no GPU work)")
@@ -511,7 +511,10 @@ def main():
                                  "def": "C++ shim under RenderImageParallelMain tiling (tools/dropin_harness.cpp), "
                                         "host g_data, tc=4 (shipped g_maxThreads) and tc=2*cores; rates count the "
                                         "pixels the tiling renders ((W/tc)*tc x (H/tc)*tc, Renderer.hpp:264-265); "
-                                        f"{args.dropin_frames} timed frames each"}
+                                        f"{args.dropin_frames} timed frames each; every frame's tiles served "
+                                        "from the shim's tiling read-ahead (spt_api.cpp SpecFrame: the whole "
+                                        "tiling rendered once per frame in 4 launches when its first tile is "
+                                        "called; SPT_READAHEAD=0 turns it off)"}
         print(json.dumps(out), flush=True)
         if args.dump:
             torch.cuda.synchronize(dev)

@@ -48,7 +48,7 @@ constexpr uint32_t kMaxBatchSets = 8;  // batches of host calls in flight (Batch
 // + one companion stream per caller stream / host slot for double-buffered sample
 // batches (render_impl)
 constexpr size_t kMaxCompanions = kMaxCallerStreams + kMaxHostSlots;
-constexpr size_t kMaxWorkspaces = kMaxCallerStreams + kMaxHostSlots + kMaxBatchSets + 1 + kMaxCompanions;
+constexpr size_t kMaxWorkspaces = kMaxCallerStreams + kMaxHostSlots + kMaxBatchSets + 1 + kMaxCompanions + 2;
 // One in-flight unbatched host call (spt_render_progressive, or any call with
 // SPT_BATCH=0 or too large for one batch): its own stream (hence its own workspace) and
 // output staging, so such calls run on the GPU together instead of one after another.
@@ -80,6 +80,30 @@ struct BatchReq {
     int rc;
     bool launched, done;
 };
+// Read-ahead of the reference's tiling (render_segment_host, DESIGN.md §5 "Drop-in
+// read-ahead"): RenderImageParallelMain (Renderer.hpp:257-302) calls RenderSegment on the
+// tc x tc tiles of MakeRenderSegmentData in a fixed order, at most tc at a time.  When the
+// first tile of such a tiling arrives, every tile of the frame is rendered at once in
+// `parts` batched launches of consecutive tile rows (SPT_READAHEAD_PARTS, default 4) into
+// a device copy of g_data; each
+// tile's call then waits for its part and copies its own rows to the caller's g_data.
+// Every tile is still rendered once per frame; nothing is written to the caller's buffer
+// before its call.
+struct SpecFrame {
+    bool active = false;
+    int mode = 0;
+    uint32_t tc = 0, sw = 0, sh = 0;
+    uint64_t gen = 0;            // spt_ctx::gen when launched
+    std::vector<uint8_t> served; // per tile (row-major over tile rows j, columns i)
+    static constexpr int kParts = 4;
+    uint32_t parts = 4, rows_per_part = 1;  // tile rows per launch
+    hipEvent_t ev[kParts] = {};
+    bool launched[kParts] = {};
+    BatchSet bs[kParts];
+    uint8_t *d8 = nullptr;  // the frame's RGB8 bytes (g_data layout), device
+    size_t d8_cap = 0;
+};
+
 struct Workspace {
     hipStream_t stream = nullptr;  // key
     uint32_t *d_samples = nullptr; // per-sample slots of the current batch (sample words)
@@ -221,6 +245,10 @@ struct spt_ctx {
     bool batch_leader = false;  // a caller is assembling the next batch
     BatchSet bsets[kMaxBatchSets];
     uint32_t batch_sets = 2;  // batches in flight at once (SPT_BATCH_SETS)
+    // tiling read-ahead (SpecFrame; SPT_READAHEAD=0 turns it off); gen counts the setters
+    bool readahead = true;
+    SpecFrame spec;
+    uint64_t gen = 0;
     // each batch launch takes 1/div of the grid (SPT_BATCH_GRID_DIV): two batches in flight
     // then run side by side and each one's tail drains beside the other's blocks (config 2
     // through the C++ shim at tc = 4: 7.93 -> 7.64 ms per frame, its folds 2x shorter)
@@ -1184,7 +1212,7 @@ uint64_t batch_slot_bytes(const spt_ctx *ctx, int mode, uint64_t npix)
 
 // Enqueue one batch on bs->stream: rectangle table, render, fold, the copy-back of
 // every request's outputs.  Called with ctx->mu held.
-int launch_batch(spt_ctx *ctx, BatchSet *bs, const std::vector<BatchReq *> &batch)
+int launch_batch(spt_ctx *ctx, BatchSet *bs, const std::vector<BatchReq *> &batch, uint8_t *spec_d8 = nullptr)
 {
     const int mode = batch[0]->mode;
     const uint32_t slot_words = mode == SPT_MODE_SEGMENT ? 1u : 2u;
@@ -1214,7 +1242,7 @@ int launch_batch(spt_ctx *ctx, BatchSet *bs, const std::vector<BatchReq *> &batc
         bs->h_rects_cap = cap;
     }
     if ((rc = ensure(ctx, &bs->d_rects, &bs->rects_cap, n))) return rc;
-    if (any_g && (rc = ensure(ctx, &ctx->d_frame8, &ctx->frame8_cap, (size_t)W * H * 3))) return rc;
+    if (any_g && !spec_d8 && (rc = ensure(ctx, &ctx->d_frame8, &ctx->frame8_cap, (size_t)W * H * 3))) return rc;
     uint64_t item = 0, slot = 0, px = 0;
     for (size_t i = 0; i < n; ++i) {
         const BatchReq *r = batch[i];
@@ -1234,7 +1262,9 @@ int launch_batch(spt_ctx *ctx, BatchSet *bs, const std::vector<BatchReq *> &batc
         // g_data inside a page-locked buffer (spt_pin_host; the C++ shim pins it): the
         // fold writes the bytes in place, no copy-back
         b.rgb8 = nullptr;
-        if (r->g_data) {
+        if (r->g_data && spec_d8) {
+            b.rgb8 = spec_d8;  // read-ahead: the frame's device copy, no copy-back here
+        } else if (r->g_data) {
             b.rgb8 = ctx->d_frame8;
             const size_t fb = (size_t)W * H * 3;
             for (const spt_ctx::Pinned &p : ctx->fold_to_host ? ctx->pinned : std::vector<spt_ctx::Pinned>{}) {
@@ -1329,7 +1359,10 @@ int launch_batch(spt_ctx *ctx, BatchSet *bs, const std::vector<BatchReq *> &batc
             ctx->ref_recorded = true;
         }
         HIP_TRY(ctx, hipEventRecord(ev.a, s));
-        spt::LaunchShape sh{render_grid(ctx, ra.n_items, claim, ctx->batch_grid_div), ctx->block, ctx->batch_grid_div,
+        // read-ahead parts take the whole grid: the second part's blocks fill the CUs as the
+        // first part's drain, so the first half of the tiles is served at half the frame
+        const uint32_t gdiv = spec_d8 ? 1u : ctx->batch_grid_div;
+        spt::LaunchShape sh{render_grid(ctx, ra.n_items, claim, gdiv), ctx->block, gdiv,
                             0, 0};
         HIP_TRY(ctx, spt::launch_render(ra, sh, s));
         ctx->last_grid = sh.ran_grid;
@@ -1341,7 +1374,7 @@ int launch_batch(spt_ctx *ctx, BatchSet *bs, const std::vector<BatchReq *> &batc
 
     spt::FoldArgs fa = fold_args(ctx, use_svc ? ctx->svc.d_ring : w->d_samples, slot_words);
     fa.out_rgba = any_rgba ? bs->d_stage : nullptr;
-    fa.out_rgb8 = any_g ? ctx->d_frame8 : nullptr;
+    fa.out_rgb8 = any_g ? (spec_d8 ? spec_d8 : ctx->d_frame8) : nullptr;
     fa.width = W;
     fa.height = H;
     fa.npix = (uint32_t)pix;
@@ -1370,7 +1403,7 @@ int launch_batch(spt_ctx *ctx, BatchSet *bs, const std::vector<BatchReq *> &batc
         if (r->rgba)
             HIP_TRY(ctx, hipMemcpyAsync(r->rgba, bs->d_stage + b.pix_off, (size_t)b.npix * sizeof(float4),
                                         hipMemcpyDeviceToHost, s));
-        if (r->g_data && b.rgb8 == ctx->d_frame8) {
+        if (r->g_data && !spec_d8 && b.rgb8 == ctx->d_frame8) {
             // rows y in [yB, yE) live at g_data rows H-1-y: one band, xB.. per row
             const size_t pitch = (size_t)W * 3;
             const size_t off = (size_t)(H - r->yE) * pitch + (size_t)r->xB * 3;
@@ -1469,6 +1502,106 @@ int render_batched(spt_ctx *ctx, std::unique_lock<std::mutex> &lk, int mode, uin
     return req.rc;
 }
 
+// ---- tiling read-ahead (SpecFrame) ------------------------------------------------------
+constexpr uint32_t kSpecMaxTiles = 64 * 64;
+constexpr int kSpecMiss = 1;  // spec_serve: not a read-ahead tile (render it as usual)
+
+// Wait for a read-ahead frame's launched parts (before its buffers are reused).
+int spec_drain(spt_ctx *ctx)
+{
+    SpecFrame &sp = ctx->spec;
+    for (int p = 0; p < SpecFrame::kParts; ++p)
+        if (sp.launched[p]) {
+            HIP_TRY(ctx, hipEventSynchronize(sp.ev[p]));
+            sp.launched[p] = false;
+        }
+    sp.active = false;
+    return SPT_OK;
+}
+
+// Render every tile of the tc x tc tiling of `mode` (MakeRenderSegmentData order) into the
+// read-ahead frame, in two batched launches.  Called with ctx->mu held.
+int spec_launch(spt_ctx *ctx, int mode, uint32_t tc)
+{
+    SpecFrame &sp = ctx->spec;
+    int rc = spec_drain(ctx);
+    if (rc) return rc;
+    const uint32_t W = ctx->W, H = ctx->H, sw = W / tc, sh = H / tc;
+    if ((rc = ensure(ctx, &sp.d8, &sp.d8_cap, (size_t)W * H * 3))) return rc;
+    std::vector<BatchReq> reqs((size_t)tc * tc);
+    for (uint32_t j = 0; j < tc; ++j)
+        for (uint32_t i = 0; i < tc; ++i)
+            reqs[(size_t)j * tc + i] = BatchReq{mode,    sh * j,    std::min(sh * j + sh, H), sw * i, std::min(sw * i + sw, W),
+                                                nullptr, sp.d8,    SPT_OK,                   true,   false};
+    const uint32_t np = std::min(sp.parts, tc), rpp = (tc + np - 1) / np;  // launches, tile rows each
+    sp.rows_per_part = rpp;
+    for (uint32_t p = 0; p * rpp < tc; ++p) {
+        std::vector<BatchReq *> part;
+        for (uint32_t j = p * rpp; j < std::min(tc, (p + 1) * rpp); ++j)
+            for (uint32_t i = 0; i < tc; ++i) part.push_back(&reqs[(size_t)j * tc + i]);
+        BatchSet *bs = &sp.bs[p];
+        if (!bs->stream) HIP_TRY(ctx, hipStreamCreateWithFlags(&bs->stream, hipStreamNonBlocking));
+        if (!sp.ev[p]) HIP_TRY(ctx, hipEventCreateWithFlags(&sp.ev[p], hipEventDisableTiming));
+        if ((rc = launch_batch(ctx, bs, part, sp.d8))) return rc;
+        HIP_TRY(ctx, hipEventRecord(sp.ev[p], bs->stream));
+        sp.launched[p] = true;
+        ctx->batches++;
+        ctx->batched_calls += part.size();
+    }
+    sp.active = true;
+    sp.mode = mode;
+    sp.tc = tc;
+    sp.sw = sw;
+    sp.sh = sh;
+    sp.gen = ctx->gen;
+    sp.served.assign((size_t)tc * tc, 0);
+    return SPT_OK;
+}
+
+// A RenderSegment call with only g_data: served from the read-ahead frame when it is one
+// of its tiles not yet served (starting a read-ahead on the first tile of a tiling), else
+// kSpecMiss.  Called with lk (ctx->mu) held; waits unlocked.
+int spec_serve(spt_ctx *ctx, std::unique_lock<std::mutex> &lk, int mode, uint32_t yB, uint32_t yE, uint32_t xB,
+               uint32_t xE, uint8_t *g_data)
+{
+    SpecFrame &sp = ctx->spec;
+    const uint32_t W = ctx->W, H = ctx->H;
+    auto tile_of = [&]() -> int64_t {
+        if (!sp.active || sp.mode != mode || sp.gen != ctx->gen) return -1;
+        if (xB % sp.sw || yB % sp.sh || xE != xB + sp.sw || yE != yB + sp.sh) return -1;
+        const uint32_t i = xB / sp.sw, j = yB / sp.sh;
+        if (i >= sp.tc || j >= sp.tc) return -1;
+        const size_t k = (size_t)j * sp.tc + i;
+        return sp.served[k] ? -1 : (int64_t)k;
+    };
+    int64_t k = tile_of();
+    if (k < 0 && xB == 0 && yB == 0) {
+        // the first tile of a tiling (Renderer.hpp:264-273: W / tc x H / tc tiles, tc even)
+        const uint32_t w = xE, h = yE, tc = W / w;
+        if (tc >= 2 && tc % 2 == 0 && (uint64_t)tc * tc <= kSpecMaxTiles && W / tc == w && H / tc == h &&
+            batch_slot_bytes(ctx, mode, (uint64_t)w * h * tc * tc) <= ctx->ws_bytes &&
+            (uint64_t)w * h * (tc * tc + tc) * ctx->spp < 0x7FFF0000ull) {
+            int rc = spec_launch(ctx, mode, tc);
+            if (rc) return rc;
+            k = tile_of();
+        }
+    }
+    if (k < 0) return kSpecMiss;
+    sp.served[(size_t)k] = 1;
+    const uint32_t part = (uint32_t)k / sp.tc / sp.rows_per_part;
+    const hipEvent_t ev = sp.ev[part];
+    uint8_t *const src = sp.d8;
+    lk.unlock();
+    // rows y in [yB, yE) live at g_data rows H-1-y: one band, xB.. per row
+    const size_t pitch = (size_t)W * 3, off = (size_t)(H - yE) * pitch + (size_t)xB * 3;
+    hipError_t e = hipEventSynchronize(ev);
+    if (e == hipSuccess)
+        e = hipMemcpy2D(g_data + off, pitch, src + off, pitch, (size_t)(xE - xB) * 3, yE - yB, hipMemcpyDeviceToHost);
+    lk.lock();
+    if (e != hipSuccess) return fail(ctx, SPT_ERR_HIP, "read-ahead tile copy failed: %s", hipGetErrorString(e));
+    return SPT_OK;
+}
+
 // RenderSegment / RenderSegmentTask with host outputs; with pass_spp > 0 progressively,
 // copying the outputs back and calling cb after every pass.  The context lock is held
 // only while launches are enqueued: each call renders on its own slot (stream,
@@ -1480,6 +1613,7 @@ int render_segment_host(spt_ctx *ctx, int mode, uint32_t yB, uint32_t yE, uint32
                         bool spread = true)
 {
     if (!ctx) return fail(nullptr, SPT_ERR_ARG, "null context");
+    const bool single = ctx->peers.empty();
     if (spread && !ctx->peers.empty()) ctx = pick_member(ctx);  // tiles go to the least busy device
     std::unique_lock<std::mutex> lk(ctx->mu);
     int rc = check_ready(ctx);
@@ -1487,6 +1621,14 @@ int render_segment_host(spt_ctx *ctx, int mode, uint32_t yB, uint32_t yE, uint32
     if ((rc = check_region(ctx, yB, yE, xB, xE))) return rc;
     if (yB >= yE || xB >= xE) return SPT_OK;  // the reference's loops do nothing
     HIP_TRY(ctx, hipSetDevice(ctx->device));
+    // the reference's tiling, g_data only: from the read-ahead frame (SpecFrame)
+    if (pass_spp == 0 && single && ctx->readahead && ctx->batching && !rgba && g_data &&
+        ctx->engine == SPT_ENGINE_MEGAKERNEL) {
+        ctx->inflight.fetch_add(1);
+        rc = spec_serve(ctx, lk, mode, yB, yE, xB, xE, g_data);
+        ctx->inflight.fetch_sub(1);
+        if (rc != kSpecMiss) return rc;
+    }
     // one-shot calls join a batch unless one call's samples exceed the workspace (then
     // it renders alone, in sample batches)
     if (pass_spp == 0 && ctx->batching && ctx->engine == SPT_ENGINE_MEGAKERNEL &&
@@ -1600,6 +1742,7 @@ int spt_set_scene_one(spt_ctx *ctx, const float *centers4, const float *radii, c
     if (!ctx) return fail(nullptr, SPT_ERR_ARG, "null context");
     std::lock_guard<std::mutex> lk(ctx->mu);
     if (int rc_ = svc_end(ctx)) return rc_;  // the session holds the state this setter changes
+    ctx->gen++;                              // a read-ahead frame of the old state is stale
     if (n > 0 && (!centers4 || !radii || !colors4 || !materials || !fuzz))
         return fail(ctx, SPT_ERR_ARG, "null scene array");
     HIP_TRY(ctx, hipSetDevice(ctx->device));
@@ -1625,6 +1768,7 @@ int spt_set_camera_one(spt_ctx *ctx, const float view[16], const float eye[4], c
     if (!ctx) return fail(nullptr, SPT_ERR_ARG, "null context");
     std::lock_guard<std::mutex> lk(ctx->mu);
     if (int rc_ = svc_end(ctx)) return rc_;  // the session holds the state this setter changes
+    ctx->gen++;                              // a read-ahead frame of the old state is stale
     if (!view || !eye || !sky) return fail(ctx, SPT_ERR_ARG, "null camera array");
     for (int j = 12; j < 16; ++j)
         if (view[j] != 0.0f)
@@ -1643,6 +1787,7 @@ int spt_set_params_one(spt_ctx *ctx, uint32_t width, uint32_t height, uint32_t s
     if (!ctx) return fail(nullptr, SPT_ERR_ARG, "null context");
     std::lock_guard<std::mutex> lk(ctx->mu);
     if (int rc_ = svc_end(ctx)) return rc_;  // the session holds the state this setter changes
+    ctx->gen++;                              // a read-ahead frame of the old state is stale
     if (width == 0 || height == 0) return fail(ctx, SPT_ERR_ARG, "empty frame %ux%u", width, height);
     if ((uint64_t)width * height * 3 > 0xFFFFFFFFull)
         return fail(ctx, SPT_ERR_ARG, "frame %ux%u overflows the reference's uint32 g_size", width, height);
@@ -1662,6 +1807,7 @@ int spt_set_cluster_size_one(spt_ctx *ctx, uint32_t k)
     if (!ctx) return fail(nullptr, SPT_ERR_ARG, "null context");
     std::lock_guard<std::mutex> lk(ctx->mu);
     if (int rc_ = svc_end(ctx)) return rc_;  // the session holds the state this setter changes
+    ctx->gen++;                              // a read-ahead frame of the old state is stale
     if (k > spt::kClusterSlots && k != SPT_CLUSTER_AUTO)
         return fail(ctx, SPT_ERR_ARG, "cluster size %u > %u", k, spt::kClusterSlots);
     ctx->cluster_k = k;
@@ -1675,6 +1821,7 @@ int spt_set_cluster_tree_one(spt_ctx *ctx, uint32_t branching)
     if (!ctx) return fail(nullptr, SPT_ERR_ARG, "null context");
     std::lock_guard<std::mutex> lk(ctx->mu);
     if (int rc_ = svc_end(ctx)) return rc_;  // the session holds the state this setter changes
+    ctx->gen++;                              // a read-ahead frame of the old state is stale
     if (branching == 1 || (branching > 64 && branching != SPT_TREE_AUTO))
         return fail(ctx, SPT_ERR_ARG, "tree branching %u not in {0, 2..64, SPT_TREE_AUTO}", branching);
     ctx->tree_branching = branching;
@@ -1688,6 +1835,7 @@ int spt_set_engine_one(spt_ctx *ctx, int engine)
     if (!ctx) return fail(nullptr, SPT_ERR_ARG, "null context");
     std::lock_guard<std::mutex> lk(ctx->mu);
     if (int rc_ = svc_end(ctx)) return rc_;  // the session holds the state this setter changes
+    ctx->gen++;                              // a read-ahead frame of the old state is stale
     if (engine != SPT_ENGINE_MEGAKERNEL && engine != SPT_ENGINE_WAVEFRONT)
         return fail(ctx, SPT_ERR_ARG, "unknown engine %d", engine);
     ctx->engine = engine;
@@ -1699,6 +1847,7 @@ int spt_set_workspace_one(spt_ctx *ctx, uint64_t bytes)
     if (!ctx) return fail(nullptr, SPT_ERR_ARG, "null context");
     std::lock_guard<std::mutex> lk(ctx->mu);
     if (int rc_ = svc_end(ctx)) return rc_;  // the session holds the state this setter changes
+    ctx->gen++;                              // a read-ahead frame of the old state is stale
     if (bytes < sizeof(float4)) return fail(ctx, SPT_ERR_ARG, "workspace too small");
     ctx->ws_bytes = bytes;
     return SPT_OK;
@@ -1758,6 +1907,9 @@ int spt_ctx_create(int device, spt_ctx **out)
     if (const char *e = std::getenv("SPT_WF_CAP")) ctx->wf_cap = (uint32_t)std::max(1024, std::atoi(e));
     if (const char *e = std::getenv("SPT_HOST_GRID_DIV")) ctx->host_grid_div = (uint32_t)std::max(0, std::atoi(e));
     if (const char *e = std::getenv("SPT_BATCH")) ctx->batching = std::atoi(e) != 0;
+    if (const char *e = std::getenv("SPT_READAHEAD")) ctx->readahead = std::atoi(e) != 0;
+    if (const char *e = std::getenv("SPT_READAHEAD_PARTS"))
+        ctx->spec.parts = (uint32_t)std::min(SpecFrame::kParts, std::max(1, std::atoi(e)));
     if (const char *e = std::getenv("SPT_BATCH_DBUF")) ctx->batch_dbuf = std::atoi(e) != 0;
     if (const char *e = std::getenv("SPT_FOLD_HOST")) ctx->fold_to_host = std::atoi(e) != 0;
     if (const char *e = std::getenv("SPT_BATCH_GRID_DIV")) ctx->batch_grid_div = (uint32_t)std::max(1, std::atoi(e));
@@ -1869,6 +2021,15 @@ void spt_ctx_destroy(spt_ctx *ctx)
         if (h->stream) (void)hipStreamDestroy(h->stream);
         delete h;
     }
+    for (BatchSet &b : ctx->spec.bs) {
+        if (b.d_rects) (void)hipFree(b.d_rects);
+        if (b.h_rects) (void)hipHostFree(b.h_rects);
+        if (b.d_stage) (void)hipFree(b.d_stage);
+        if (b.stream) (void)hipStreamDestroy(b.stream);
+    }
+    for (hipEvent_t e : ctx->spec.ev)
+        if (e) (void)hipEventDestroy(e);
+    if (ctx->spec.d8) (void)hipFree(ctx->spec.d8);
     for (BatchSet &b : ctx->bsets) {
         if (b.d_rects) (void)hipFree(b.d_rects);
         if (b.h_rects) (void)hipHostFree(b.h_rects);

@@ -108,16 +108,18 @@ class Context:
     def set_workspace(self, nbytes: int) -> None:
         self._check(_native.lib().spt_set_workspace(self._h, int(nbytes)))
 
-    def render_segment(self, yB, yE, xB, xE, g_data=None, task=False) -> np.ndarray:
-        """Returns region-local float4 pixels; writes g_data bytes of the region if given."""
-        rgba = np.zeros((max(yE - yB, 0) * max(xE - xB, 0), 4), np.float32)
+    def render_segment(self, yB, yE, xB, xE, g_data=None, task=False, rgba=True):
+        """Returns region-local float4 pixels (None with rgba=False: g_data only, the C++
+        drop-in's form, which the tiling read-ahead serves); writes g_data bytes of the
+        region if given."""
+        out = np.zeros((max(yE - yB, 0) * max(xE - xB, 0), 4), np.float32) if rgba else None
         fn = _native.lib().spt_render_segment_task if task else _native.lib().spt_render_segment
         gp = None
         if g_data is not None:
             assert g_data.dtype == np.uint8 and g_data.flags.c_contiguous
             gp = _p(g_data)
-        self._check(fn(self._h, yB, yE, xB, xE, _p(rgba), gp))
-        return rgba
+        self._check(fn(self._h, yB, yE, xB, xE, _p(out) if rgba else None, gp))
+        return out
 
     def render_frame(self, g_data=None, task=False, rgba=True):
         """The whole frame over every member device (spt_render_frame): returns the

@@ -1,0 +1,119 @@
+"""GPU tests of the drop-in's tiling read-ahead (spt_api.cpp SpecFrame):
+RenderSegment / RenderSegmentTask calls over the reference's tc x tc tiling
+(Renderer.hpp:264-273, MakeRenderSegmentData), g_data only, are served from one
+read-ahead render of the whole tiling.  Every output byte must equal a plain render, a
+lone first-tile call must write only its own rows, and a setter between frames must not
+serve a stale frame."""
+import threading
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+EYE, LOOK, UP, SKY = [0, 1, -3, 0], [0, 1, 0, 0], [0, 1, 0, 0], [137, 207, 240, 0]
+
+
+@pytest.fixture(scope="module")
+def spt():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import simplepathtracer_amd as m
+    m.lib()
+    return m
+
+
+def make_ctx(spt, golden_scenes, w, h, spp, seed=1):
+    gs = golden_scenes
+    c = spt.Context(0)
+    c.set_scene(spt.Scene(*(gs[f"random_{k}"] for k in ("centers", "radii", "colors", "materials", "fuzz"))))
+    c.set_camera(spt.camera_basis(EYE, LOOK, UP), EYE, SKY)
+    c.set_params(w, h, spp, 50, seed)
+    return c
+
+
+def tiles(W, H, tc):
+    sw, sh = W // tc, H // tc
+    return [(sh * j, sh * j + sh, sw * i, sw * i + sw) for j in range(tc) for i in range(tc)]
+
+
+def render_tiling(ctx, W, H, tc, task, threads):
+    """RenderImageParallelMain's pattern: every tile, at most `threads` calls at once."""
+    g = np.zeros(W * H * 3, np.uint8)
+    sem = threading.Semaphore(threads)
+    err = []
+
+    def job(t):
+        try:
+            ctx.render_segment(*t, g_data=g, task=task, rgba=False)
+        except Exception as e:  # noqa: BLE001
+            err.append(e)
+        finally:
+            sem.release()
+
+    th = []
+    for t in tiles(W, H, tc):
+        sem.acquire()
+        th.append(threading.Thread(target=job, args=(t,)))
+        th[-1].start()
+    for t in th:
+        t.join()
+    assert not err, err
+    return g
+
+
+@pytest.mark.parametrize("task", [False, True])
+def test_tiling_served_from_readahead_equals_plain_calls(spt, golden_scenes, monkeypatch, task):
+    W, H, spp, tc = 240, 160, 6, 4
+    ctx = make_ctx(spt, golden_scenes, W, H, spp, seed=5)
+    frames = [render_tiling(ctx, W, H, tc, task, 4) for _ in range(2)]
+    st = ctx.stats()
+    ctx.close()
+    monkeypatch.setenv("SPT_READAHEAD", "0")
+    plain = make_ctx(spt, golden_scenes, W, H, spp, seed=5)
+    want = np.zeros(W * H * 3, np.uint8)
+    for t in tiles(W, H, tc):
+        plain.render_segment(*t, g_data=want, task=task, rgba=False)
+    plain.close()
+    for k, g in enumerate(frames):
+        assert np.array_equal(g, want), f"frame {k}: {np.count_nonzero(g != want)} bytes differ"
+    # min(4, tc) read-ahead launches per frame (SPT_READAHEAD_PARTS), every tile in them
+    assert st["batches"] == 2 * min(4, tc) and st["batched_calls"] == 2 * tc * tc
+
+
+def test_lone_first_tile_writes_only_its_rows(spt, golden_scenes):
+    W, H, spp = 200, 120, 4
+    ctx = make_ctx(spt, golden_scenes, W, H, spp)
+    g = np.zeros(W * H * 3, np.uint8)
+    ctx.render_segment(0, H // 2, 0, W // 2, g_data=g, rgba=False)  # tile (0, 0) of tc = 2
+    want = np.zeros(W * H * 3, np.uint8)
+    ref = make_ctx(spt, golden_scenes, W, H, spp)
+    ref.render_segment(0, H // 2, 0, W // 2, g_data=want)  # rgba requested: no read-ahead
+    ref.close()
+    ctx.close()
+    assert np.array_equal(g, want)
+    img = g.reshape(H, W, 3)
+    assert not img[: H // 2].any() and not img[H // 2:, W // 2:].any()  # g_data row r = image row H-1-r
+
+
+def test_setter_between_frames_is_not_served_stale(spt, golden_scenes):
+    W, H, spp, tc = 160, 96, 4, 2
+    ctx = make_ctx(spt, golden_scenes, W, H, spp)
+    render_tiling(ctx, W, H, tc, False, 2)
+    # start a frame, then change the camera before its other tiles are asked for
+    g = np.zeros(W * H * 3, np.uint8)
+    ctx.render_segment(*tiles(W, H, tc)[0], g_data=g, rgba=False)
+    ctx.set_camera(spt.camera_basis([0.5, 1.2, -3, 0], LOOK, UP), EYE, SKY)
+    for t in tiles(W, H, tc)[1:]:
+        ctx.render_segment(*t, g_data=g, rgba=False)
+    ctx.close()
+    ref = make_ctx(spt, golden_scenes, W, H, spp)
+    ref.set_camera(spt.camera_basis([0.5, 1.2, -3, 0], LOOK, UP), EYE, SKY)
+    want2 = np.zeros(W * H * 3, np.uint8)
+    for t in tiles(W, H, tc)[1:]:
+        ref.render_segment(*t, g_data=want2)
+    ref.close()
+    img, ref_img = g.reshape(H, W, 3), want2.reshape(H, W, 3)
+    # tiles 1.. (the new camera) match a plain render with the new camera
+    assert np.array_equal(img[: H // 2], ref_img[: H // 2]) and np.array_equal(img[H // 2:, W // 2:], ref_img[H // 2:, W // 2:])

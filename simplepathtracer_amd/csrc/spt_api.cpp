@@ -48,7 +48,7 @@ constexpr uint32_t kMaxBatchSets = 8;  // batches of host calls in flight (Batch
 // + one companion stream per caller stream / host slot for double-buffered sample
 // batches (render_impl)
 constexpr size_t kMaxCompanions = kMaxCallerStreams + kMaxHostSlots;
-constexpr size_t kMaxWorkspaces = kMaxCallerStreams + kMaxHostSlots + kMaxBatchSets + 1 + kMaxCompanions + 2;
+constexpr size_t kMaxWorkspaces = kMaxCallerStreams + kMaxHostSlots + kMaxBatchSets + 1 + kMaxCompanions + 4;  // + read-ahead parts (SpecFrame::kParts)
 // One in-flight unbatched host call (spt_render_progressive, or any call with
 // SPT_BATCH=0 or too large for one batch): its own stream (hence its own workspace) and
 // output staging, so such calls run on the GPU together instead of one after another.

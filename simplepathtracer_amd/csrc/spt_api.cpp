@@ -28,6 +28,16 @@
 #include <vector>
 
 namespace {
+// An environment variable's value, or null when unset or empty (a variable set to ""
+// reads as unset: SPT_BLOCKS_PER_CU= would otherwise mean a 1-block grid)
+const char *env_var(const char *name)
+{
+    const char *e = std::getenv(name);
+    return e && *e ? e : nullptr;
+}
+}  // namespace
+
+namespace {
 
 thread_local std::string g_thread_error;
 // the context whose progress callback is running on this thread (spt_render_progressive)
@@ -628,7 +638,7 @@ int svc_end(spt_ctx *ctx)
             if (tr[4 * i] != ~0ull)
                 std::fprintf(stderr, "svc trace idx %u: claims %.1f .. %.1f us, last count %.1f us\n", i,
                              (tr[4 * i] - t0) / 100.0, (tr[4 * i + 1] - t0) / 100.0, (tr[4 * i + 2] - t0) / 100.0);
-        if (const char *path = std::getenv("SPT_SVC_TRACE_FILE")) {
+        if (const char *path = env_var("SPT_SVC_TRACE_FILE")) {
             // the per-claim take times (block << 40 | 40-bit time), raw
             if (FILE *f = std::fopen(path, "wb")) {
                 std::fwrite(&t0, sizeof t0, 1, f);
@@ -660,8 +670,8 @@ int svc_begin(spt_ctx *ctx, int mode)
         int lo = 0, hi = 0;
         HIP_TRY(ctx, hipDeviceGetStreamPriorityRange(&lo, &hi));
         int prio = hi, pub_prio = lo;
-        if (const char *e = std::getenv("SPT_SVC_PRIO")) prio = std::atoi(e);
-        if (const char *e = std::getenv("SPT_SVC_PUB_PRIO")) pub_prio = std::atoi(e);
+        if (const char *e = env_var("SPT_SVC_PRIO")) prio = std::atoi(e);
+        if (const char *e = env_var("SPT_SVC_PUB_PRIO")) pub_prio = std::atoi(e);
         HIP_TRY(ctx, hipStreamCreateWithPriority(&v.stream, hipStreamNonBlocking, prio));
         HIP_TRY(ctx, hipStreamCreateWithPriority(&v.pub, hipStreamNonBlocking, pub_prio));
         HIP_TRY(ctx, hipEventCreate(&v.ev_start));
@@ -695,7 +705,7 @@ int svc_begin(spt_ctx *ctx, int mode)
     ra.svc_jobs = v.d_jobs;
     ra.svc_job_claim = v.d_job_claim;
     ra.svc_done = v.d_done;
-    if (std::getenv("SPT_SVC_TRACE")) {
+    if (env_var("SPT_SVC_TRACE")) {
         const size_t n = (size_t)v.done_cap * 4 + spt::kSvcTraceClaims;
         if (!v.d_trace) HIP_TRY(ctx, hipMalloc((void **)&v.d_trace, n * sizeof(unsigned long long)));
         std::vector<unsigned long long> init(n, 0ull);
@@ -1897,40 +1907,40 @@ int spt_ctx_create(int device, spt_ctx **out)
     // launch_bounds / occupancy API may over-report by one block per CU for SGPR-heavy
     // kernels (MI355X_MICROARCH.md, Residency): the kernel needs no co-residency, so
     // extra blocks only queue.  SPT_BLOCKS_PER_CU overrides for tuning.
-    if (const char *e = std::getenv("SPT_BLOCKS_PER_CU")) per_cu = std::max(1, std::atoi(e));
-    if (const char *e = std::getenv("SPT_CLAIM")) ctx->claim = (uint32_t)std::max(0, std::atoi(e));  // 0 = per launch
-    if (const char *e = std::getenv("SPT_CLUSTER_K")) ctx->cluster_k = (uint32_t)std::max(0, std::atoi(e));
-    if (const char *e = std::getenv("SPT_TREE_B")) ctx->tree_branching = (uint32_t)std::max(0, std::atoi(e));
-    if (const char *e = std::getenv("SPT_CLAIMS_PER_WAVE")) ctx->claims_per_wave = (uint32_t)std::max(1, std::atoi(e));
-    if (const char *e = std::getenv("SPT_QUEUES"))
+    if (const char *e = env_var("SPT_BLOCKS_PER_CU")) per_cu = std::max(1, std::atoi(e));
+    if (const char *e = env_var("SPT_CLAIM")) ctx->claim = (uint32_t)std::max(0, std::atoi(e));  // 0 = per launch
+    if (const char *e = env_var("SPT_CLUSTER_K")) ctx->cluster_k = (uint32_t)std::max(0, std::atoi(e));
+    if (const char *e = env_var("SPT_TREE_B")) ctx->tree_branching = (uint32_t)std::max(0, std::atoi(e));
+    if (const char *e = env_var("SPT_CLAIMS_PER_WAVE")) ctx->claims_per_wave = (uint32_t)std::max(1, std::atoi(e));
+    if (const char *e = env_var("SPT_QUEUES"))
         ctx->queues = (uint32_t)std::min<int>((int)spt::kMaxQueues, std::max(1, std::atoi(e)));
-    if (const char *e = std::getenv("SPT_WF_CAP")) ctx->wf_cap = (uint32_t)std::max(1024, std::atoi(e));
-    if (const char *e = std::getenv("SPT_HOST_GRID_DIV")) ctx->host_grid_div = (uint32_t)std::max(0, std::atoi(e));
-    if (const char *e = std::getenv("SPT_BATCH")) ctx->batching = std::atoi(e) != 0;
-    if (const char *e = std::getenv("SPT_READAHEAD")) ctx->readahead = std::atoi(e) != 0;
-    if (const char *e = std::getenv("SPT_READAHEAD_PARTS"))
+    if (const char *e = env_var("SPT_WF_CAP")) ctx->wf_cap = (uint32_t)std::max(1024, std::atoi(e));
+    if (const char *e = env_var("SPT_HOST_GRID_DIV")) ctx->host_grid_div = (uint32_t)std::max(0, std::atoi(e));
+    if (const char *e = env_var("SPT_BATCH")) ctx->batching = std::atoi(e) != 0;
+    if (const char *e = env_var("SPT_READAHEAD")) ctx->readahead = std::atoi(e) != 0;
+    if (const char *e = env_var("SPT_READAHEAD_PARTS"))
         ctx->spec.parts = (uint32_t)std::min(SpecFrame::kParts, std::max(1, std::atoi(e)));
-    if (const char *e = std::getenv("SPT_BATCH_DBUF")) ctx->batch_dbuf = std::atoi(e) != 0;
-    if (const char *e = std::getenv("SPT_FOLD_HOST")) ctx->fold_to_host = std::atoi(e) != 0;
-    if (const char *e = std::getenv("SPT_BATCH_GRID_DIV")) ctx->batch_grid_div = (uint32_t)std::max(1, std::atoi(e));
-    if (const char *e = std::getenv("SPT_INLINE_RECTS")) ctx->inline_rects = std::atoi(e) != 0;
-    if (const char *e = std::getenv("SPT_FOLD_HEAD")) ctx->fold_resets_head = std::atoi(e) != 0;
-    if (const char *e = std::getenv("SPT_SPIN_SYNC")) ctx->spin_sync = std::atoi(e) != 0;
-    if (const char *e = std::getenv("SPT_BATCH_SETS"))
+    if (const char *e = env_var("SPT_BATCH_DBUF")) ctx->batch_dbuf = std::atoi(e) != 0;
+    if (const char *e = env_var("SPT_FOLD_HOST")) ctx->fold_to_host = std::atoi(e) != 0;
+    if (const char *e = env_var("SPT_BATCH_GRID_DIV")) ctx->batch_grid_div = (uint32_t)std::max(1, std::atoi(e));
+    if (const char *e = env_var("SPT_INLINE_RECTS")) ctx->inline_rects = std::atoi(e) != 0;
+    if (const char *e = env_var("SPT_FOLD_HEAD")) ctx->fold_resets_head = std::atoi(e) != 0;
+    if (const char *e = env_var("SPT_SPIN_SYNC")) ctx->spin_sync = std::atoi(e) != 0;
+    if (const char *e = env_var("SPT_BATCH_SETS"))
         ctx->batch_sets = (uint32_t)std::min<int>((int)kMaxBatchSets, std::max(1, std::atoi(e)));
-    if (const char *e = std::getenv("SPT_HOST_SLOTS"))
+    if (const char *e = env_var("SPT_HOST_SLOTS"))
         ctx->host_slots = (uint32_t)std::min<int>((int)kMaxHostSlots, std::max(1, std::atoi(e)));
     // SPT_SERVICE=1: the context starts with the render service on (spt_service_start)
-    if (const char *e = std::getenv("SPT_SERVICE")) ctx->svc.enabled = std::atoi(e) != 0;
-    if (const char *e = std::getenv("SPT_SVC_CLAIM")) ctx->svc.claim = (uint32_t)std::max(64, std::atoi(e) / 64 * 64);
-    if (const char *e = std::getenv("SPT_SVC_QUEUES"))
+    if (const char *e = env_var("SPT_SERVICE")) ctx->svc.enabled = std::atoi(e) != 0;
+    if (const char *e = env_var("SPT_SVC_CLAIM")) ctx->svc.claim = (uint32_t)std::max(64, std::atoi(e) / 64 * 64);
+    if (const char *e = env_var("SPT_SVC_QUEUES"))
         ctx->svc.queues = (uint32_t)std::min<int>((int)spt::kMaxQueues, std::max(1, std::atoi(e)));
-    if (const char *e = std::getenv("SPT_SVC_RING_MB"))
+    if (const char *e = env_var("SPT_SVC_RING_MB"))
         ctx->svc.ring_bytes = (uint64_t)std::max(64, std::atoi(e)) << 20;
     ctx->grid = (uint32_t)(per_cu * ctx->num_cu);
-    ctx->grid_overlap = std::getenv("SPT_BLOCKS_PER_CU") || per_cu < 2 ? ctx->grid : (uint32_t)((per_cu - 1) * ctx->num_cu);
-    ctx->grid_small = std::getenv("SPT_BLOCKS_PER_CU") || per_cu < 3 ? 0u : (uint32_t)((per_cu - 2) * ctx->num_cu);
-    if (const char *e = std::getenv("SPT_SMALL_GRID")) ctx->grid_small = std::atoi(e) != 0 ? ctx->grid_small : 0u;
+    ctx->grid_overlap = env_var("SPT_BLOCKS_PER_CU") || per_cu < 2 ? ctx->grid : (uint32_t)((per_cu - 1) * ctx->num_cu);
+    ctx->grid_small = env_var("SPT_BLOCKS_PER_CU") || per_cu < 3 ? 0u : (uint32_t)((per_cu - 2) * ctx->num_cu);
+    if (const char *e = env_var("SPT_SMALL_GRID")) ctx->grid_small = std::atoi(e) != 0 ? ctx->grid_small : 0u;
     if (hipEventCreate(&ctx->ref_ev) != hipSuccess || hipEventCreateWithFlags(&ctx->frame_ev, hipEventDisableTiming) != hipSuccess ||
         hipMalloc((void **)&ctx->d_counters, kCounters * sizeof(unsigned long long)) != hipSuccess ||
         hipMemset(ctx->d_counters, 0, kCounters * sizeof(unsigned long long)) != hipSuccess) {

@@ -65,7 +65,7 @@ PY
       echo "tc=$tc $v: $(env $v timeout -k 10 120 $H /dev/null 1200 800 100 50 $tc 0 5 | cut -c1-60)"
     done; done ;;
   readahead)
-    for r in 1 2; do for v in "SPT_READAHEAD=0" "SPT_READAHEAD_PARTS=2" "SPT_READAHEAD_PARTS=4"; do for task in 0 1; do
+    for r in 1 2; do for v in "SPT_READAHEAD=0" "SPT_READAHEAD_PARTS=4" "SPT_READAHEAD_PRIO=-1" "SPT_READAHEAD_PRIO=1"; do for task in 0 1; do
       s=$(env $v timeout -k 10 60 $H /dev/null 1200 800 100 50 4 $task 20 | grep -o "seconds=[0-9.]*" | cut -d= -f2)
       echo "r$r $v task=$task: $(python3 -c "print(f'{$s/20*1e3:.3f} ms/frame, {1200*800*100*20/$s/1e6:.0f} Msamples/s')")"
     done; done; done ;;

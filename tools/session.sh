@@ -50,8 +50,8 @@ for step in "$@"; do
     c3) run c3 300 python bench.py --config c3 --steps 2 --warmup 1 --no-cpu-baseline ;;
     scaling) run scaling 300 python tools/scaling_probe.py --streams 2 --reps 5 --service 1 --record "gpurun_out/${TAG}_scaling.txt"
              run scaling0 300 python tools/scaling_probe.py --streams 2 --reps 5 --service 0 --record "gpurun_out/${TAG}_scaling0.txt" ;;
-    dropin) run dropin 300 python -c "import bench; print(bench.dropin_bench(1200, 800, 100, 50, 5, (4, 32)))" ;;
-    dropin1) run dropin1 300 python -c "import bench; print(bench.dropin_bench(1200, 800, 100, 50, 5, (4, 32), {'SPT_SERVICE': '1'}))" ;;
+    dropin) run dropin 300 python -c "import bench; print(bench.dropin_bench(1200, 800, 100, 50, 20, (4, 32)))" ;;
+    dropin1) run dropin1 300 python -c "import bench; print(bench.dropin_bench(1200, 800, 100, 50, 20, (4, 32), {'SPT_SERVICE': '1'}))" ;;
     profile) run profile 900 bash tools/profile.sh "${TAG}_c2" c2 ;;
     profile5) run profile5 900 bash tools/profile.sh "${TAG}_c5" c5 --config c5 --steps 2 --warmup 1 --no-cpu-baseline ;;
     ab:*) run ab 600 python tools/ab.py ${step#ab:} ;;

@@ -123,7 +123,6 @@ struct Workspace {
     uint32_t *d_head = nullptr;    // claim counter
     bool head_clean = false;       // d_head zeroed by the last batched fold (launch_batch)
     spt::WavefrontBuffers wf{};    // queues of the wavefront engine (allocated on first use)
-    uint32_t *h_count = nullptr;   // pinned host word: queue length read back per pass
 };
 
 // The render service: one resident launch of render_kernel_svc per session
@@ -205,7 +204,8 @@ struct spt_ctx {
     uint32_t cluster_k = SPT_CLUSTER_AUTO;  // members per culling cluster; 0 = brute force
     uint32_t tree_branching = SPT_TREE_AUTO;  // children per inner node; 0 = flat cluster list
     int engine = SPT_ENGINE_MEGAKERNEL;
-    uint32_t wf_cap = 1u << 22;  // rays per wavefront queue
+    uint32_t wf_cap = 1u << 24;  // rays in the wavefront engine's block queues (at most)
+    uint32_t wf_queue = 4096;    // rays per block queue (a multiple of 256)
     spt::AccelView accel{};
     // camera (Globals.hpp:21-29)
     spt::Camera cam{};
@@ -561,35 +561,23 @@ hipStream_t companion_for(spt_ctx *ctx, hipStream_t s)
     return c;
 }
 
-// Queues of the wavefront engine in workspace w, for `cap` rays.
-int ensure_wavefront(spt_ctx *ctx, Workspace *w, uint32_t cap)
+// Queues of the wavefront engine in workspace w: `cap` rays in block queues of qcap.
+int ensure_wavefront(spt_ctx *ctx, Workspace *w, uint32_t cap, uint32_t qcap)
 {
     spt::WavefrontBuffers &b = w->wf;
-    if (b.cap >= cap && b.hit) return SPT_OK;
+    cap = std::max(cap / qcap, 1u) * qcap;
+    if (b.cap >= cap && b.qcap == qcap && b.state) return SPT_OK;
     HIP_TRY(ctx, hipDeviceSynchronize());
-    void *old[] = {b.o[0], b.o[1], b.d[0], b.d[1], b.m[0], b.m[1], b.st[0], b.st[1], b.hit, b.cat_idx, b.counts,
-                   b.tag, b.bcount, b.boff, b.scan_tmp};
-    for (void *p : old)
+    for (void *p : {(void *)b.o, (void *)b.d, (void *)b.m, (void *)b.state})
         if (p) (void)hipFree(p);
     b = spt::WavefrontBuffers{};
-    bool ok = true;
-    for (int q = 0; q < 2; ++q) {
-        ok = ok && hipMalloc((void **)&b.o[q], (size_t)cap * sizeof(float4)) == hipSuccess;
-        ok = ok && hipMalloc((void **)&b.d[q], (size_t)cap * sizeof(float4)) == hipSuccess;
-        ok = ok && hipMalloc((void **)&b.m[q], (size_t)cap * sizeof(float4)) == hipSuccess;
-        ok = ok && hipMalloc((void **)&b.st[q], (size_t)cap * sizeof(uint2)) == hipSuccess;
-    }
-    ok = ok && hipMalloc((void **)&b.hit, (size_t)cap * sizeof(float4)) == hipSuccess;
-    ok = ok && hipMalloc((void **)&b.cat_idx, (size_t)cap * sizeof(uint32_t)) == hipSuccess;
-    ok = ok && hipMalloc((void **)&b.counts, (1 + spt::kWfCats) * sizeof(uint32_t)) == hipSuccess;
-    ok = ok && hipMalloc((void **)&b.tag, (size_t)cap) == hipSuccess;
-    ok = ok && hipMalloc((void **)&b.bcount, (size_t)(spt::kWfCats + 1) * (cap / 64 + 1) * sizeof(uint32_t)) == hipSuccess;
-    ok = ok && hipMalloc((void **)&b.boff, (size_t)(spt::kWfCats + 1) * (cap / 64 + 1) * sizeof(uint32_t)) == hipSuccess;
-    b.scan_bytes = std::max<size_t>(spt::wavefront_scan_bytes(cap), 16);
-    ok = ok && hipMalloc(&b.scan_tmp, b.scan_bytes) == hipSuccess;
-    if (!w->h_count) ok = ok && hipHostMalloc((void **)&w->h_count, sizeof(uint32_t)) == hipSuccess;
+    bool ok = hipMalloc((void **)&b.o, (size_t)cap * sizeof(float4)) == hipSuccess;
+    ok = ok && hipMalloc((void **)&b.d, (size_t)cap * sizeof(float4)) == hipSuccess;
+    ok = ok && hipMalloc((void **)&b.m, (size_t)cap * sizeof(uint4)) == hipSuccess;
+    ok = ok && hipMalloc((void **)&b.state, spt::kWfStateWords * sizeof(uint32_t)) == hipSuccess;
     if (!ok) return fail(ctx, SPT_ERR_NOMEM, "wavefront queues for %u rays: allocation failed", cap);
     b.cap = cap;
+    b.qcap = qcap;
     return SPT_OK;
 }
 
@@ -1037,26 +1025,20 @@ int render_impl(spt_ctx *ctx, int mode, const spt::RowMap &map, float4 *d_rgba, 
             HIP_TRY(ctx, hipEventRecord(ev.b, s));
             fa.samples = ctx->svc.d_ring + svc_w0;
         } else if (ctx->engine == SPT_ENGINE_WAVEFRONT) {
-            // queue passes until every item is issued and the queue has drained; the
-            // host reads the queue length back after each pass (4 bytes, pinned)
-            const uint32_t cap = (uint32_t)std::min<uint64_t>(ctx->wf_cap, std::max<uint32_t>(ra.n_items, 1024u));
-            if ((rc = ensure_wavefront(ctx, w, cap))) return rc;
+            // every pass of the batch in one launch of block queue workers; queue
+            // lengths stay on the device
+            // (queues for the resident blocks only: a block past them would start late)
+            const uint64_t blocks = spt::wavefront_blocks(ctx->accel, ctx->device);
+            if (blocks == 0) return fail(ctx, SPT_ERR_HIP, "wavefront engine: no resident blocks");
+            const uint32_t cap = (uint32_t)std::min<uint64_t>(std::min<uint64_t>(ctx->wf_cap, blocks * ctx->wf_queue),
+                                                               std::max<uint32_t>(ra.n_items, 1024u));
+            if ((rc = ensure_wavefront(ctx, w, cap, ctx->wf_queue))) return rc;
             HIP_TRY(ctx, hipEventRecord(ev.a, s));
             if (!ctx->ref_recorded) {
                 HIP_TRY(ctx, hipEventRecord(ctx->ref_ev, s));
                 ctx->ref_recorded = true;
             }
-            uint32_t cur = 0, n_cur = 0, next_item = 0;
-            while (next_item < ra.n_items || n_cur > 0) {
-                const uint32_t gen = std::min(cap - n_cur, ra.n_items - next_item);
-                HIP_TRY(ctx, spt::launch_wavefront_pass(w->wf, ra, cur, n_cur, next_item, gen, s));
-                next_item += gen;
-                HIP_TRY(ctx, hipMemcpyAsync(w->h_count, w->wf.counts, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-                HIP_TRY(ctx, hipStreamSynchronize(s));
-                n_cur = *w->h_count;
-                cur ^= 1u;
-                if (n_cur > cap) return fail(ctx, SPT_ERR_STATE, "wavefront queue overflow (%u > %u)", n_cur, cap);
-            }
+            HIP_TRY(ctx, spt::launch_wavefront(w->wf, ra, s));
             HIP_TRY(ctx, hipEventRecord(ev.b, s));
         } else {
             HIP_TRY(ctx, hipMemsetAsync(w->d_head, 0, sizeof(uint32_t) * spt::kQueueStride * ra.n_queues, s));
@@ -1925,6 +1907,7 @@ int spt_ctx_create(int device, spt_ctx **out)
     if (const char *e = env_var("SPT_QUEUES"))
         ctx->queues = (uint32_t)std::min<int>((int)spt::kMaxQueues, std::max(1, std::atoi(e)));
     if (const char *e = env_var("SPT_WF_CAP")) ctx->wf_cap = (uint32_t)std::max(1024, std::atoi(e));
+    if (const char *e = env_var("SPT_WF_QUEUE")) ctx->wf_queue = (uint32_t)std::min(8192, std::max(1, std::atoi(e) / 256)) * 256u;
     if (const char *e = env_var("SPT_HOST_GRID_DIV")) ctx->host_grid_div = (uint32_t)std::max(0, std::atoi(e));
     if (const char *e = env_var("SPT_BATCH")) ctx->batching = std::atoi(e) != 0;
     if (const char *e = env_var("SPT_READAHEAD")) ctx->readahead = std::atoi(e) != 0;
@@ -2029,12 +2012,9 @@ void spt_ctx_destroy(spt_ctx *ctx)
         if (b) (void)hipFree(b);
     for (Workspace &w : ctx->ws) {
         const spt::WavefrontBuffers &q = w.wf;
-        for (void *b : {(void *)w.d_samples, (void *)w.d_acc, (void *)w.d_head, (void *)q.o[0], (void *)q.o[1],
-                        (void *)q.d[0], (void *)q.d[1], (void *)q.m[0], (void *)q.m[1], (void *)q.st[0],
-                        (void *)q.st[1], (void *)q.hit, (void *)q.cat_idx, (void *)q.counts, (void *)q.tag,
-                        (void *)q.bcount, (void *)q.boff, q.scan_tmp})
+        for (void *b : {(void *)w.d_samples, (void *)w.d_acc, (void *)w.d_head, (void *)q.o, (void *)q.d, (void *)q.m,
+                        (void *)q.state})
             if (b) (void)hipFree(b);
-        if (w.h_count) (void)hipHostFree(w.h_count);
     }
     for (HostSlot *h : ctx->slots) {
         if (h->d_stage) (void)hipFree(h->d_stage);

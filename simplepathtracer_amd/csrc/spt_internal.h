@@ -415,28 +415,21 @@ struct LaunchShape {
 };
 hipError_t launch_render(const RenderArgs &a, LaunchShape &sh, hipStream_t s);
 
-// Wavefront variant (spt_wavefront.hip): double-buffered ray queues of `cap`
-// rays, a hit record per ray, kWfCats category queues and their counters.
+// Wavefront variant (spt_wavefront.hip): per-block ray queues of qcap rays (three
+// 16-byte records per ray; cap = blocks x qcap) and the batch's item counter.
 constexpr uint32_t kWfCats = 5;  // sky/miss, diffuse first hit, mirror, glass, diffuse-loop step
+constexpr uint32_t kWfStateWords = 4;
 struct WavefrontBuffers {
-    float4 *o[2], *d[2], *m[2];
-    uint2 *st[2];
-    float4 *hit;
-    uint32_t *cat_idx;  // [cap] category-major list of ray indices
-    uint8_t *tag;       // [cap] category, then alive flag
-    uint32_t *bcount;   // [kWfCats + 1][cap / 64 + 1] per-wave counts
-    uint32_t *boff;     // their exclusive scan
-    uint32_t *counts;   // [0] next queue length
-    void *scan_tmp;     // hipCUB scan scratch
-    size_t scan_bytes;
-    uint32_t cap;
+    float4 *o, *d;
+    uint4 *m;
+    uint32_t *state;  // [kWfStateWords]
+    uint32_t cap, qcap;
 };
-size_t wavefront_scan_bytes(uint32_t cap);
-// One pass: append gen_n new paths (items gen_base..) after the n_cur queued rays
-// of queue `cur`, cast them all, shade them category by category and compact the
-// survivors, in order, into queue cur^1; the new length is left in counts[0].
-hipError_t launch_wavefront_pass(const WavefrontBuffers &b, const RenderArgs &a, uint32_t cur, uint32_t n_cur,
-                                 uint32_t gen_base, uint32_t gen_n, hipStream_t s);
+// Every pass of a sample batch's paths through the ray queues, in one launch: the
+// host issues it and waits for nothing (queue lengths stay on the device).
+hipError_t launch_wavefront(const WavefrontBuffers &b, const RenderArgs &a, hipStream_t s);
+// Blocks of the engine resident at once on device dev (its launch's grid), 0 on error.
+uint32_t wavefront_blocks(const AccelView &ac, int dev);
 hipError_t launch_fold(const FoldArgs &a, hipStream_t s);
 // spt_render_samples: pixels [p0, p0 + n) of the region, out[(p - p0) * spp + s]
 hipError_t launch_expand(const FoldArgs &a, float4 *out, uint32_t p0, uint32_t n, hipStream_t s);

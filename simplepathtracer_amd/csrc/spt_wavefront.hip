@@ -1,257 +1,270 @@
 // spt_wavefront.hip -- queue-based (wavefront) variant of the render loop.
 //
 // the design of RenderSegmentTask's material queues
-// (TaskBasedPathTracer.hpp:54-193) as separate HIP kernels with ballot/prefix
-// compaction, to compare against the persistent megakernel.  The reference keeps
-// per-material task vectors and runs one material at a time per pass; here a
-// ray queue in HBM is topped up with primary rays, then per pass
+// (TaskBasedPathTracer.hpp:54-193) on the GPU, to compare against the persistent
+// megakernel.  The reference keeps per-material task vectors and runs one material
+// at a time per pass.  Here every block of one launch per sample batch owns a ray
+// queue in HBM (qcap rays) and runs passes over it with no host round trip:
 //
-//   wf_extend   one FindClosestIntersectionSphere per queued ray; the ray's
-//               category (sky/miss, diffuse first hit, mirror, glass,
-//               diffuse-loop step) and per-wave category counts (ballots);
-//   scan        exclusive scan of the [category][wave] counts (hipCUB
-//               DeviceScan, decoupled look-back): the offset of every wave's
-//               rays in one category-major list;
-//   wf_split    that list, by mbcnt rank + the wave offsets (order preserving);
-//   wf_shade    one shading step for every ray of one category (homogeneous
-//               work per launch, like the reference's per-material loops), in
-//               place; finished paths write their sample slot;
-//   wf_count / scan / wf_compact   the surviving rays, in queue order, into
-//               the next queue; new primaries are appended after them.
+//   top-up      new paths for the free positions, from one claim on the batch's
+//               item counter (the only global atomic, one per block and pass);
+//   per 256-ray chunk of the queue
+//     cast      one FindClosestIntersectionSphere per ray; the ray's category
+//               (sky/miss, diffuse first hit, mirror, glass, diffuse-loop step);
+//     split     a counting sort of the chunk by category in LDS (wave ballots,
+//               per-wave counts, block prefix), so each wave shades rays of one
+//               material, like the reference's per-material loops;
+//     shade     one shading step; finished paths write their sample word;
+//     compact   the survivors (wave ballot ranks + the block's prefix) to the front
+//               of the queue, in order.
 //
-// Order-preserving compaction keeps the queue in the megakernel's tile order, so a
-// wave's 64 rays stay spatially coherent and cull together.  Nothing in the pass
-// kernels synchronises a block or hits one global address: statistics come from
-// the scans (rays cast = queue length, finished = length - survivors).  Per-lane
-// counter atomics on one address made the first version 2.4x slower.
-//
-// Per-path arithmetic is the megakernel's own (spt_path.h: start_path,
-// find_closest, shade_step), so every (pixel, sample) gets bit-identical results
-// and the same fold kernel resolves the frame.
+// Queue lengths never leave the block, so nothing is read back and no block waits
+// for another (an earlier version ran global passes with grid barriers in one
+// cooperative launch: 7x the megakernel's frame time, one atomic per chunk on the
+// pass's length).  Every path's arithmetic is the megakernel's own (spt_path.h:
+// start_path, find_closest, shade_step) and its sample word sits at its item's slot,
+// so frames are bit-identical to the megakernel's.
 #include "spt_path.h"
 
-#include <hipcub/hipcub.hpp>
+#include <algorithm>
+#include <mutex>
 
 namespace spt {
 
 namespace {
 
-// Ray queue entry (SoA of 16-byte records, coalesced): o + first diffuse slot, d,
-// {-, item, bounce, phase | spec << 2}, RNG state.
-struct WfRay {
-    float4 *o, *d, *m;
-    uint2 *st;
+constexpr uint32_t kWfBlock = 256;
+constexpr uint32_t kWfWaves = kWfBlock / 64;
+
+struct WfQueue {
+    float4 *o, *d;  // {o, first diffuse slot}, {d, item}
+    uint4 *m;       // {RNG state lo, hi, bounce, phase | spec << 2}
 };
 
 struct WfArgs {
     RenderArgs ra;
-    WfRay cur, next;
-    float4 *hit;         // {p.x, p.y, p.z, slot} of the current queue's rays
-    uint32_t *cat_idx;   // category-major list of ray indices
-    uint8_t *tag;        // per ray: category after the cast, alive flag after shading
-    uint32_t *bcount;    // [kWfCats][nw] per-wave category counts, then [nw] survivor counts
-    uint32_t *boff;      // exclusive scan of bcount (same layout)
-    uint32_t *totals;    // [kWfCats] next queue length (host readback)
+    WfQueue q;        // the blocks' queues, qcap rays each
+    uint32_t *state;  // [0] next batch item to start (claimed by the blocks)
+    uint32_t qcap;    // rays per block queue (a multiple of kWfBlock)
 };
 
-__device__ __forceinline__ Path load_ray(const WfRay &q, uint32_t i)
+__device__ __forceinline__ void load_ray(const WfQueue &q, uint32_t i, Path &ps)
 {
-    const float4 o = q.o[i], d = q.d[i], m = q.m[i];
-    const uint2 st = q.st[i];
-    Path ps;
+    const float4 o = q.o[i], d = q.d[i];
+    const uint4 m = q.m[i];
     ps.o = mk(o.x, o.y, o.z);
-    ps.d = mk(d.x, d.y, d.z);
     ps.slot = __float_as_uint(o.w);
-    ps.item = __float_as_uint(m.y);
-    ps.bounce = __float_as_uint(m.z);
-    const uint32_t ps_bits = __float_as_uint(m.w);
-    ps.phase = ps_bits & 3u;
-    ps.spec = ps_bits >> 2;
-    ps.st = (uint64_t)st.x | ((uint64_t)st.y << 32);
-    return ps;
+    ps.d = mk(d.x, d.y, d.z);
+    ps.item = __float_as_uint(d.w);
+    ps.st = (uint64_t)m.x | ((uint64_t)m.y << 32);
+    ps.bounce = m.z;
+    ps.phase = m.w & 3u;
+    ps.spec = m.w >> 2;
 }
 
-__device__ __forceinline__ void store_ray(const WfRay &q, uint32_t i, const Path &ps)
+__device__ __forceinline__ void store_ray(const WfQueue &q, uint32_t i, const Path &ps)
 {
     q.o[i] = make_float4(ps.o.x, ps.o.y, ps.o.z, __uint_as_float(ps.slot));
-    q.d[i] = make_float4(ps.d.x, ps.d.y, ps.d.z, 0.f);
-    q.m[i] = make_float4(0.f, __uint_as_float(ps.item), __uint_as_float(ps.bounce),
-                         __uint_as_float(ps.phase | (ps.spec << 2)));
-    q.st[i] = make_uint2((uint32_t)ps.st, (uint32_t)(ps.st >> 32));
+    q.d[i] = make_float4(ps.d.x, ps.d.y, ps.d.z, __uint_as_float(ps.item));
+    q.m[i] = make_uint4((uint32_t)ps.st, (uint32_t)(ps.st >> 32), ps.bounce, ps.phase | (ps.spec << 2));
 }
 
-__global__ __launch_bounds__(256) void wf_generate(WfArgs w, uint32_t base_item, uint32_t n_new, uint32_t dst0)
+// One block = one queue worker.  Per pass: top the block's queue up to qcap rays with
+// new paths (one claim on the batch's item counter), then for each 256-ray chunk of
+// the queue cast, sort by category in LDS, shade, and compact the survivors in queue
+// order to the front of the same queue (in place: a chunk's survivors land at or
+// before its own positions, all loaded before the first store).  A block leaves when
+// its queue is empty and the items are exhausted.
+template <bool TREE, int LEAF>
+__global__ __launch_bounds__(kWfBlock) void wf_render(WfArgs w)
 {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n_new) return;
+    __shared__ float4 s_o[kWfBlock], s_d[kWfBlock];
+    __shared__ uint4 s_m[kWfBlock];
+    __shared__ float2 s_h[kWfBlock];                   // the cast's {t, slot} of the sorted rays
+    __shared__ uint32_t s_lds[kWfBlock];               // wave-private scratch of the cooperative sampler
+    __shared__ uint32_t s_cnt[kWfWaves][kWfCats + 1];  // per wave: category counts, survivors
+    __shared__ uint32_t s_claim;
+
+    typedef __attribute__((address_space(1))) uint32_t gu32;
     const RenderArgs &a = w.ra;
+    const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = __lane_id();
     const uint32_t rows = a.npix / a.map.width;
     const Recip rw = recip((float)a.width), rh = recip((float)a.height);
-    Path ps;
-    ps.slot = 0;
-    start_path(a, base_item + i, rows, rw, rh, mk(a.cam.eye[0], a.cam.eye[1], a.cam.eye[2]), ps);
-    store_ray(w.cur, dst0 + i, ps);
+    const f3 eye = mk(a.cam.eye[0], a.cam.eye[1], a.cam.eye[2]);
+    const size_t q0 = (size_t)blockIdx.x * w.qcap;
+    const WfQueue q{w.q.o + q0, w.q.d + q0, w.q.m + q0};
+    uint32_t len = 0;  // rays queued (block-uniform)
+    unsigned long long cast = 0, finished = 0, done = 0, dropped = 0;
+    for (;;) {
+        // top-up: claim qcap - len items (the counter may run past n_items)
+        if (tid == 0) s_claim = __hip_atomic_fetch_add((gu32 *)w.state, w.qcap - len, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+        const uint32_t first = s_claim;
+        const uint32_t got = first < a.n_items ? min(w.qcap - len, a.n_items - first) : 0u;
+        const uint32_t n = len + got;
+        if (n == 0u) break;
+        uint32_t wp = 0;  // the next survivor's position (block-uniform)
+        for (uint32_t base = 0; base < n; base += kWfBlock) {
+            const uint32_t i = base + tid;
+            const uint32_t live = min(n - base, kWfBlock);
+            const bool act = i < n;
+            Path ps;
+            ps.phase = PH_IDLE;
+            ps.item = ps.bounce = ps.spec = ps.slot = 0;
+            ps.st = 0;
+            ps.o = ps.d = mk(0.f, 0.f, 0.f);
+            if (act) {
+                if (i < len) {
+                    load_ray(q, i, ps);
+                } else {
+                    start_path(a, first + (i - len), rows, rw, rh, eye, ps);
+                    ps.slot = 0;
+                }
+            }
+            CastDiag dg;
+            const Hit h = find_closest<TREE, LEAF>(a.scene.accel, ps.o, ps.d, act, dg);
+            // category of the next shading step: the material switch of
+            // TraceAndSampleColor (SingleThreadPathTracer.hpp:98-111) or the diffuse loop
+            uint32_t cat = kWfCats;
+            if (act) {
+                cat = 0u;  // sky / miss / unknown material
+                if (ps.phase == PH_DLOOP) {
+                    cat = 4u;
+                } else if (h.idx != kMiss) {
+                    const uint32_t mt = a.scene.mat[h.idx];
+                    cat = mt == SPT_DIFFUSE_ID ? 1u : mt == SPT_REFLECTIVE_ID ? 2u : mt == SPT_REFRACTIVE_ID ? 3u : 0u;
+                }
+            }
+            // counting sort of the chunk by category: wave ballots, then the block prefix
+            uint32_t rank = 0;
+#pragma unroll
+            for (uint32_t c = 0; c < kWfCats; ++c) {
+                const unsigned long long m = __ballot(cat == c);
+                if (lane == 0) s_cnt[wave][c] = (uint32_t)__popcll(m);
+                if (cat == c) rank = lane_rank(m);
+            }
+            __syncthreads();
+            if (act) {
+                uint32_t pos = rank;
+#pragma unroll
+                for (uint32_t c = 0; c < kWfCats; ++c)
+#pragma unroll
+                    for (uint32_t v = 0; v < kWfWaves; ++v)
+                        if (c < cat || (c == cat && v < wave)) pos += s_cnt[v][c];
+                s_o[pos] = make_float4(ps.o.x, ps.o.y, ps.o.z, __uint_as_float(ps.slot));
+                s_d[pos] = make_float4(ps.d.x, ps.d.y, ps.d.z, __uint_as_float(ps.item));
+                s_m[pos] = make_uint4((uint32_t)ps.st, (uint32_t)(ps.st >> 32), ps.bounce, ps.phase | (ps.spec << 2));
+                s_h[pos] = make_float2(h.t, __uint_as_float(h.idx));
+            }
+            __syncthreads();
+            // shade the sorted chunk: lanes [0, live) hold rays, category by category
+            const bool act2 = tid < live;
+            Hit hh;
+            hh.best = 0.f;
+            hh.t = 0.f;
+            hh.idx = kMiss;
+            if (act2) {
+                const float4 o = s_o[tid], d = s_d[tid];
+                const uint4 m = s_m[tid];
+                const float2 t = s_h[tid];
+                ps.o = mk(o.x, o.y, o.z);
+                ps.slot = __float_as_uint(o.w);
+                ps.d = mk(d.x, d.y, d.z);
+                ps.item = __float_as_uint(d.w);
+                ps.st = (uint64_t)m.x | ((uint64_t)m.y << 32);
+                ps.bounce = m.z;
+                ps.phase = m.w & 3u;
+                ps.spec = m.w >> 2;
+                hh.t = t.x;
+                hh.idx = __float_as_uint(t.y);
+            } else {
+                ps.phase = PH_IDLE;
+            }
+            shade_step(a, ps, hh, act2, done, dropped, s_lds + wave * 64u);
+            // compaction: the survivors, in order, to the front of the queue
+            const bool alive = act2 && ps.phase != PH_IDLE;
+            const unsigned long long am = __ballot(alive);
+            if (lane == 0) s_cnt[wave][kWfCats] = (uint32_t)__popcll(am);
+            __syncthreads();
+            uint32_t at = wp + lane_rank(am), tot = 0;
+#pragma unroll
+            for (uint32_t v = 0; v < kWfWaves; ++v) {
+                const uint32_t k = s_cnt[v][kWfCats];
+                if (v < wave) at += k;
+                tot += k;
+            }
+            if (alive) store_ray(q, at, ps);
+            wp += tot;
+            __syncthreads();  // the chunk's LDS is reused by the next one; its stores precede the next loads
+        }
+        cast += n;
+        finished += n - wp;
+        len = wp;
+    }
+    (void)done;
+    if (tid == 0) {
+        atomicAdd(&a.counters[0], cast);
+        atomicAdd(&a.counters[1], finished);
+    }
+    if (dropped) atomicAdd(&a.counters[2], dropped);  // task mode only, rare
 }
-
-// Global wave index (64-lane waves of the 1-D grid).
-__device__ __forceinline__ uint32_t wave_id() { return (blockIdx.x * blockDim.x + threadIdx.x) >> 6; }
 
 template <bool TREE, int LEAF>
-__global__ __launch_bounds__(256) void wf_extend(WfArgs w, uint32_t n, uint32_t nw)
+uint32_t resident_blocks(int dev)
 {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t wv = wave_id();
-    if (wv >= nw) return;  // whole wave past the queue (wave-uniform); no block barriers below
-    const bool act = i < n;  // every lane of a live wave takes part in the traversal
-    const uint32_t ii = act ? i : 0u;
-    const float4 o4 = w.cur.o[ii], d4 = w.cur.d[ii], m4 = w.cur.m[ii];
-    const f3 o = mk(o4.x, o4.y, o4.z), d = mk(d4.x, d4.y, d4.z);
-    CastDiag dg;
-    const Hit h = find_closest<TREE, LEAF>(w.ra.scene.accel, o, d, act, dg);
-    uint32_t cat = kWfCats;  // none
-    if (act) {
-        w.hit[i] = make_float4(h.t, 0.f, 0.f, __uint_as_float(h.idx));
-        // category of the next shading step: the material switch of
-        // TraceAndSampleColor (SingleThreadPathTracer.hpp:98-111) or the diffuse loop
-        cat = 0;  // sky / miss / unknown material
-        if ((__float_as_uint(m4.w) & 3u) == PH_DLOOP) {
-            cat = 4;
-        } else if (h.idx != kMiss) {
-            const uint32_t mt = w.ra.scene.mat[h.idx];
-            cat = mt == SPT_DIFFUSE_ID ? 1u : mt == SPT_REFLECTIVE_ID ? 2u : mt == SPT_REFRACTIVE_ID ? 3u : 0u;
-        }
-        w.tag[i] = (uint8_t)cat;
+    // blocks per CU at this kernel's register / LDS footprint, per device (cached)
+    static std::mutex mu;
+    static int cached[64];
+    std::lock_guard<std::mutex> lk(mu);
+    if (dev < 0 || dev >= 64) return 0;
+    if (cached[dev] == 0) {
+        int per_cu = 0, cus = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, wf_render<TREE, LEAF>, kWfBlock, 0) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            return 0;
+        cached[dev] = std::max(per_cu, 0) * std::max(cus, 0);
+        if (cached[dev] == 0) cached[dev] = -1;
     }
-#pragma unroll
-    for (uint32_t c = 0; c < kWfCats; ++c) {
-        const uint32_t k = (uint32_t)__popcll(__ballot(cat == c));
-        if (__lane_id() == 0) w.bcount[(size_t)c * nw + wv] = k;
-    }
+    return cached[dev] > 0 ? (uint32_t)cached[dev] : 0u;
 }
 
-// Category lists in queue order (per-wave offsets from the scan + mbcnt rank).
-__global__ __launch_bounds__(256) void wf_split(WfArgs w, uint32_t n, uint32_t nw)
+template <bool TREE, int LEAF>
+hipError_t launch(const WavefrontBuffers &b, const RenderArgs &a, hipStream_t s)
 {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t wv = wave_id();
-    if (wv >= nw) return;
-    const uint32_t cat = i < n ? w.tag[i] : kWfCats;
-#pragma unroll
-    for (uint32_t c = 0; c < kWfCats; ++c) {
-        const unsigned long long m = __ballot(cat == c);
-        if (cat == c) w.cat_idx[w.boff[(size_t)c * nw + wv] + lane_rank(m)] = i;
-    }
-}
-
-__global__ __launch_bounds__(256) void wf_shade(WfArgs w, uint32_t cat, uint32_t n_all, uint32_t nw)
-{
-    __shared__ uint32_t s_lds[256];  // wave-private scratch of the cooperative sampler
-    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t start = w.boff[(size_t)cat * nw];
-    const uint32_t n = (cat + 1 < kWfCats ? w.boff[(size_t)(cat + 1) * nw] : n_all) - start;  // this category's rays
-    if (j - __lane_id() >= n) return;  // whole wave past the list (wave-uniform)
-    const bool act = j < n;
-    const uint32_t i = act ? w.cat_idx[start + j] : 0u;
-    Path ps = load_ray(w.cur, i);
-    if (!act) ps.phase = PH_IDLE;
-    const float4 h4 = w.hit[i];
-    Hit h;
-    h.idx = __float_as_uint(h4.w);
-    h.best = 0.f;
-    h.t = h4.x;
-    unsigned long long done = 0, dropped = 0;
-    shade_step(w.ra, ps, h, act, done, dropped, s_lds + (threadIdx.x & ~63u));
-    if (act) {
-        const bool alive = ps.phase != PH_IDLE;
-        if (alive) store_ray(w.cur, i, ps);  // in place; compacted in queue order below
-        w.tag[i] = alive ? 1u : 0u;
-    }
-    if (dropped) atomicAdd(&w.ra.counters[2], dropped);  // task mode only, rare
-}
-
-__global__ __launch_bounds__(256) void wf_count(WfArgs w, uint32_t n, uint32_t nw)
-{
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t wv = wave_id();
-    if (wv >= nw) return;
-    const uint32_t k = (uint32_t)__popcll(__ballot(i < n && w.tag[i] != 0u));
-    if (__lane_id() == 0) w.bcount[(size_t)kWfCats * nw + wv] = k;
-}
-
-// Next queue length (host readback) and the pass statistics: rays cast = n,
-// paths finished = n - survivors.
-__global__ void wf_totals(WfArgs w, uint32_t n, uint32_t nw)
-{
-    const size_t last = (size_t)kWfCats * nw + nw - 1;
-    const uint32_t alive = w.boff[last] + w.bcount[last];
-    w.totals[0] = alive;
-    atomicAdd(&w.ra.counters[0], (unsigned long long)n);
-    atomicAdd(&w.ra.counters[1], (unsigned long long)(n - alive));
-}
-
-__global__ __launch_bounds__(256) void wf_compact(WfArgs w, uint32_t n, uint32_t nw)
-{
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t wv = wave_id();
-    if (wv >= nw) return;
-    const bool alive = i < n && w.tag[i] != 0u;
-    const unsigned long long m = __ballot(alive);
-    if (!alive) return;
-    const uint32_t at = w.boff[(size_t)kWfCats * nw + wv] + lane_rank(m);
-    w.next.o[at] = w.cur.o[i];
-    w.next.d[at] = w.cur.d[i];
-    w.next.m[at] = w.cur.m[i];
-    w.next.st[at] = w.cur.st[i];
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    const uint32_t resident = resident_blocks<TREE, LEAF>(dev);
+    if (resident == 0) return hipErrorInvalidConfiguration;
+    // one block per queue: as many as are resident at once (a block that waits for a
+    // CU only starts later; no block waits for another)
+    const uint32_t grid = std::max(1u, std::min(resident, b.cap / b.qcap));
+    WfArgs w;
+    w.ra = a;
+    w.q = WfQueue{b.o, b.d, b.m};
+    w.state = b.state;
+    w.qcap = b.qcap;
+    e = hipMemsetAsync(b.state, 0, kWfStateWords * sizeof(uint32_t), s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((wf_render<TREE, LEAF>), dim3(grid), dim3(kWfBlock), 0, s, w);
+    return hipGetLastError();
 }
 
 }  // namespace
 
-size_t wavefront_scan_bytes(uint32_t cap)
+uint32_t wavefront_blocks(const AccelView &ac, int dev)
 {
-    size_t bytes = 0;
-    const uint32_t items = (kWfCats + 1) * (cap / 64 + 1);
-    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, (uint32_t *)nullptr, (uint32_t *)nullptr, items);
-    return bytes;
+    if (ac.tree) return resident_blocks<true, (int)kClusterSlots>(dev);
+    if (ac.leaf_slots == kFlatLeafSlots) return resident_blocks<false, (int)kFlatLeafSlots>(dev);
+    return resident_blocks<false, (int)kClusterSlots>(dev);
 }
 
-hipError_t launch_wavefront_pass(const WavefrontBuffers &b, const RenderArgs &a, uint32_t cur, uint32_t n_cur,
-                                 uint32_t gen_base, uint32_t gen_n, hipStream_t s)
+hipError_t launch_wavefront(const WavefrontBuffers &b, const RenderArgs &a, hipStream_t s)
 {
-    WfArgs w;
-    w.ra = a;
-    const uint32_t nxt = cur ^ 1u;
-    w.cur = WfRay{b.o[cur], b.d[cur], b.m[cur], b.st[cur]};
-    w.next = WfRay{b.o[nxt], b.d[nxt], b.m[nxt], b.st[nxt]};
-    w.hit = b.hit;
-    w.cat_idx = b.cat_idx;
-    w.tag = b.tag;
-    w.bcount = b.bcount;
-    w.boff = b.boff;
-    w.totals = b.counts;
-    if (gen_n) hipLaunchKernelGGL(wf_generate, dim3((gen_n + 255) / 256), dim3(256), 0, s, w, gen_base, gen_n, n_cur);
-    const uint32_t n = n_cur + gen_n;
-    if (n == 0) return hipMemsetAsync(b.counts, 0, sizeof(uint32_t), s);
-    const uint32_t nw = (n + 63) / 64;  // waves
-    const dim3 grid((n + 255) / 256);
-    size_t tmp = b.scan_bytes;
-    if (a.scene.accel.tree)
-        hipLaunchKernelGGL((wf_extend<true, (int)kClusterSlots>), grid, dim3(256), 0, s, w, n, nw);
-    else if (a.scene.accel.leaf_slots == kFlatLeafSlots)
-        hipLaunchKernelGGL((wf_extend<false, (int)kFlatLeafSlots>), grid, dim3(256), 0, s, w, n, nw);
-    else
-        hipLaunchKernelGGL((wf_extend<false, (int)kClusterSlots>), grid, dim3(256), 0, s, w, n, nw);
-    hipError_t e = hipcub::DeviceScan::ExclusiveSum(b.scan_tmp, tmp, b.bcount, b.boff, kWfCats * nw, s);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(wf_split, grid, dim3(256), 0, s, w, n, nw);
-    for (uint32_t c = 0; c < kWfCats; ++c) hipLaunchKernelGGL(wf_shade, grid, dim3(256), 0, s, w, c, n, nw);
-    hipLaunchKernelGGL(wf_count, grid, dim3(256), 0, s, w, n, nw);
-    tmp = b.scan_bytes;
-    e = hipcub::DeviceScan::ExclusiveSum(b.scan_tmp, tmp, b.bcount + (size_t)kWfCats * nw,
-                                         b.boff + (size_t)kWfCats * nw, nw, s);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(wf_totals, dim3(1), dim3(1), 0, s, w, n, nw);
-    hipLaunchKernelGGL(wf_compact, grid, dim3(256), 0, s, w, n, nw);
-    return hipGetLastError();
+    if (a.n_items == 0) return hipSuccess;
+    if (a.scene.accel.tree) return launch<true, (int)kClusterSlots>(b, a, s);
+    if (a.scene.accel.leaf_slots == kFlatLeafSlots) return launch<false, (int)kFlatLeafSlots>(b, a, s);
+    return launch<false, (int)kClusterSlots>(b, a, s);
 }
 
 }  // namespace spt

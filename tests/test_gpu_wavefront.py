@@ -1,7 +1,8 @@
 """GPU parity tests of the wavefront engine (spt_wavefront.hip):
-RenderSegmentTask's material-queue design as separate kernels per pass.  It
-shares the megakernel's per-path code, so frames, ray counts and task-mode drops
-must be bit-identical to the goldens, the oracle and the megakernel."""
+RenderSegmentTask's material-queue design as block queue workers (cast, sort by
+material in LDS, shade, compact per pass).  It shares the megakernel's per-path
+code, so frames, ray counts and task-mode drops must be bit-identical to the
+goldens, the oracle and the megakernel."""
 import os
 
 import numpy as np
@@ -95,18 +96,21 @@ def test_task_mode_drops_match_megakernel(spt, wctx, mctx, oracle):
     assert_bitwise(res[0][0][:, :3], want[:, :3], "task mode vs oracle")
 
 
-def test_small_queue_and_sample_batches(spt, mctx, golden_scenes):
-    """A 2048-ray queue (many top-ups and passes) and a workspace forcing sample
-    batches still give the megakernel's frame."""
-    old = os.environ.get("SPT_WF_CAP")
-    os.environ["SPT_WF_CAP"] = "2048"
+@pytest.mark.parametrize("queue", [256, 2048])
+def test_small_queue_and_sample_batches(spt, mctx, golden_scenes, queue):
+    """Two block queues of 256 or one of 2048 rays (many top-ups and passes) and a
+    workspace forcing sample batches still give the megakernel's frame."""
+    old = {k: os.environ.get(k) for k in ("SPT_WF_CAP", "SPT_WF_QUEUE")}
+    os.environ["SPT_WF_CAP"] = "2048" if queue == 2048 else "512"
+    os.environ["SPT_WF_QUEUE"] = str(queue)
     try:
         c = spt.Context(0)
     finally:
-        if old is None:
-            del os.environ["SPT_WF_CAP"]
-        else:
-            os.environ["SPT_WF_CAP"] = old
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
     try:
         c.set_engine(spt._native.ENGINE_WAVEFRONT)
         scene = scene_from(spt, golden_scenes, "random")
@@ -117,6 +121,27 @@ def test_small_queue_and_sample_batches(spt, mctx, golden_scenes):
         assert_bitwise(got, mctx.render_segment(0, 64, 0, 96), "small queue + batches")
     finally:
         c.close()
+
+
+def test_device_launch_returns_before_the_frame(spt, wctx, mctx, golden_scenes):
+    """No host round trip inside a render: a device-resident config-2 launch returns
+    while its stream is still busy (queue lengths never leave the GPU), and the frame
+    equals the megakernel's."""
+    import torch
+    W, H = 1200, 800
+    scene = scene_from(spt, golden_scenes, "random")
+    outs = []
+    for c in (wctx, mctx):
+        setup(c, scene, W, H, 32, 50)
+        rgba = torch.zeros((W * H, 4), dtype=torch.float32, device="cuda")
+        st = torch.cuda.Stream()
+        torch.cuda.synchronize()  # the fill (current stream) before the render stream writes
+        c.render_rows_async(spt.MODE_SEGMENT, 0, H, 1, 1, 0, 0, W, rgba.data_ptr(), 0, st.cuda_stream)
+        busy = not st.query()
+        st.synchronize()
+        outs.append((rgba.cpu().numpy(), busy))
+    assert outs[0][1], "the wavefront render call waited for its own launch"
+    assert_bitwise(outs[0][0], outs[1][0], "device launch: wavefront vs megakernel")
 
 
 def test_engine_argument_is_checked(spt, wctx):

@@ -75,7 +75,7 @@ __device__ __forceinline__ void store_ray(const WfQueue &q, uint32_t i, const Pa
 // order to the front of the same queue (in place: a chunk's survivors land at or
 // before its own positions, all loaded before the first store).  A block leaves when
 // its queue is empty and the items are exhausted.
-template <bool TREE, int LEAF>
+template <bool TREE, int LEAF, bool GLANE>
 __global__ __launch_bounds__(kWfBlock) void wf_render(WfArgs w)
 {
     __shared__ float4 s_o[kWfBlock], s_d[kWfBlock];
@@ -122,7 +122,10 @@ __global__ __launch_bounds__(kWfBlock) void wf_render(WfArgs w)
                 }
             }
             CastDiag dg;
-            const Hit h = find_closest<TREE, LEAF>(a.scene.accel, ps.o, ps.d, act, dg);
+            // GLANE (trees the megakernel walks lane by lane, lane_walk_tree): each lane
+            // walks layout 0 from global memory; otherwise the wave walk
+            const Hit h = GLANE ? find_closest_lane<LEAF>(a.scene.accel, ps.o, ps.d, act, dg, (const uint32_t *)a.scene.accel.nodes)
+                                : find_closest<TREE, LEAF>(a.scene.accel, ps.o, ps.d, act, dg);
             // category of the next shading step: the material switch of
             // TraceAndSampleColor (SingleThreadPathTracer.hpp:98-111) or the diffuse loop
             uint32_t cat = kWfCats;
@@ -209,7 +212,7 @@ __global__ __launch_bounds__(kWfBlock) void wf_render(WfArgs w)
     if (dropped) atomicAdd(&a.counters[2], dropped);  // task mode only, rare
 }
 
-template <bool TREE, int LEAF>
+template <bool TREE, int LEAF, bool GLANE>
 uint32_t resident_blocks(int dev)
 {
     // blocks per CU at this kernel's register / LDS footprint, per device (cached)
@@ -219,7 +222,7 @@ uint32_t resident_blocks(int dev)
     if (dev < 0 || dev >= 64) return 0;
     if (cached[dev] == 0) {
         int per_cu = 0, cus = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, wf_render<TREE, LEAF>, kWfBlock, 0) != hipSuccess ||
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, wf_render<TREE, LEAF, GLANE>, kWfBlock, 0) != hipSuccess ||
             hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
             return 0;
         cached[dev] = std::max(per_cu, 0) * std::max(cus, 0);
@@ -228,13 +231,13 @@ uint32_t resident_blocks(int dev)
     return cached[dev] > 0 ? (uint32_t)cached[dev] : 0u;
 }
 
-template <bool TREE, int LEAF>
+template <bool TREE, int LEAF, bool GLANE>
 hipError_t launch(const WavefrontBuffers &b, const RenderArgs &a, hipStream_t s)
 {
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
-    const uint32_t resident = resident_blocks<TREE, LEAF>(dev);
+    const uint32_t resident = resident_blocks<TREE, LEAF, GLANE>(dev);
     if (resident == 0) return hipErrorInvalidConfiguration;
     // one block per queue: as many as are resident at once (a block that waits for a
     // CU only starts later; no block waits for another)
@@ -246,7 +249,7 @@ hipError_t launch(const WavefrontBuffers &b, const RenderArgs &a, hipStream_t s)
     w.qcap = b.qcap;
     e = hipMemsetAsync(b.state, 0, kWfStateWords * sizeof(uint32_t), s);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((wf_render<TREE, LEAF>), dim3(grid), dim3(kWfBlock), 0, s, w);
+    hipLaunchKernelGGL((wf_render<TREE, LEAF, GLANE>), dim3(grid), dim3(kWfBlock), 0, s, w);
     return hipGetLastError();
 }
 
@@ -254,17 +257,19 @@ hipError_t launch(const WavefrontBuffers &b, const RenderArgs &a, hipStream_t s)
 
 uint32_t wavefront_blocks(const AccelView &ac, int dev)
 {
-    if (ac.tree) return resident_blocks<true, (int)kClusterSlots>(dev);
-    if (ac.leaf_slots == kFlatLeafSlots) return resident_blocks<false, (int)kFlatLeafSlots>(dev);
-    return resident_blocks<false, (int)kClusterSlots>(dev);
+    if (lane_walk_tree(ac)) return resident_blocks<true, (int)kClusterSlots, true>(dev);
+    if (ac.tree) return resident_blocks<true, (int)kClusterSlots, false>(dev);
+    if (ac.leaf_slots == kFlatLeafSlots) return resident_blocks<false, (int)kFlatLeafSlots, false>(dev);
+    return resident_blocks<false, (int)kClusterSlots, false>(dev);
 }
 
 hipError_t launch_wavefront(const WavefrontBuffers &b, const RenderArgs &a, hipStream_t s)
 {
     if (a.n_items == 0) return hipSuccess;
-    if (a.scene.accel.tree) return launch<true, (int)kClusterSlots>(b, a, s);
-    if (a.scene.accel.leaf_slots == kFlatLeafSlots) return launch<false, (int)kFlatLeafSlots>(b, a, s);
-    return launch<false, (int)kClusterSlots>(b, a, s);
+    if (lane_walk_tree(a.scene.accel)) return launch<true, (int)kClusterSlots, true>(b, a, s);
+    if (a.scene.accel.tree) return launch<true, (int)kClusterSlots, false>(b, a, s);
+    if (a.scene.accel.leaf_slots == kFlatLeafSlots) return launch<false, (int)kFlatLeafSlots, false>(b, a, s);
+    return launch<false, (int)kClusterSlots, false>(b, a, s);
 }
 
 }  // namespace spt

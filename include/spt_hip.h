@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define SPT_ABI_VERSION 6
+#define SPT_ABI_VERSION 7
 
 /* Only the functions below are exported from libspt_hip.so (built with
  * -fvisibility=hidden), so several builds can be loaded side by side. */
@@ -48,7 +48,9 @@ typedef enum spt_status {
     SPT_ERR_STATE = 2,    /* scene / camera / params not set */
     SPT_ERR_HIP = 3,      /* HIP runtime error */
     SPT_ERR_NOMEM = 4,    /* allocation failed */
-    SPT_ERR_NODEVICE = 5  /* no gfx950 device / bad ordinal */
+    SPT_ERR_NODEVICE = 5, /* no gfx950 device / bad ordinal */
+    SPT_ERR_TIMEOUT = 6   /* a render-service session did not end within SPT_SVC_TIMEOUT_MS
+                             (default 30 s); the message counts its unpublished jobs */
 } spt_status;
 
 /* Material ids, Definitions.hpp:7-13 (enum class Material : uint8_t). */
@@ -93,10 +95,13 @@ typedef struct spt_stats {
        waves once the session has ended (spt_service_stop, spt_synchronize) */
     uint64_t svc_sessions;       /* service sessions (resident launches) started */
     uint64_t svc_jobs;           /* jobs published to them */
-    uint64_t svc_watchdog_exits; /* sessions whose waves left after 100 ms without work */
+    uint64_t svc_watchdog_exits; /* sessions whose waves left after 0.5 s without work */
     double svc_kernel_ms;        /* summed device time of the ended sessions' launches */
     uint32_t svc_running;        /* a session is resident now */
     uint32_t svc_grid_blocks;    /* the service's grid (one block slot per CU left free) */
+    uint64_t svc_flow_restarts;  /* sessions ended because a publication would have waited for
+                                    an unfinished fold (ring words or counter still in use) */
+    uint64_t svc_closing_restarts; /* sessions ended because a wave had raised its closing flag */
 } spt_stats;
 
 SPT_API int spt_abi_version(void);
@@ -159,9 +164,11 @@ SPT_API int spt_accel_check(const float *centers4, const float *radii, uint32_t 
 /* Engine of the render loop (results are bit-identical either way):
  * SPT_ENGINE_MEGAKERNEL (default) -- one persistent kernel, per-lane state machines;
  * SPT_ENGINE_WAVEFRONT -- RenderSegmentTask's material-queue design
- *   (TaskBasedPathTracer.hpp:54-193) as separate kernels per pass: extend (cast +
- *   category queues by ballot/prefix compaction) and one shading kernel per
- *   category; the host reads the queue length back after each pass. */
+ *   (TaskBasedPathTracer.hpp:54-193): one launch per sample batch whose blocks are
+ *   queue workers -- each block casts its ray queue, sorts the rays by material in LDS
+ *   (ballot/prefix), shades them and compacts the survivors in place, pass after pass.
+ *   Queue lengths never leave the device: the host issues the launch and reads nothing
+ *   back. */
 enum { SPT_ENGINE_MEGAKERNEL = 0, SPT_ENGINE_WAVEFRONT = 1 };
 SPT_API int spt_set_engine(spt_ctx *ctx, int engine);
 /* Upper bound of the per-sample workspace (default 16 GiB).  Larger frames are
@@ -234,10 +241,15 @@ SPT_API int spt_render_rows_async(spt_ctx *ctx, int mode, uint32_t yBegin, uint3
  * counter on the caller's stream (hipStreamWaitValue32); results are bit-identical to the
  * launched renders.  Sessions start on the first job and end on spt_service_stop,
  * spt_synchronize, a setter, a render the service does not take (lane-walk trees,
- * spt_render_samples, the wavefront engine, jobs over half the 4 GiB slot ring) or a
- * pause of 40 ms without jobs; a session's waves leave after 100 ms without work, so
- * a device-wide synchronisation (hipDeviceSynchronize, torch.cuda.synchronize) waits at
- * most that long.  spt_service_stop drains and ends the session and turns the service off. */
+ * spt_render_samples, the wavefront engine, jobs over half the 4 GiB slot ring), when a
+ * publication would have to wait for an unfinished fold (the ring wrapped onto words a
+ * fold still reads; the next session's launch waits for it instead), or when its waves
+ * have gone idle: a session's waves may leave after 0.5 s without work -- only through
+ * a handshake with the host, so no job is ever published to a session that left -- and a
+ * device-wide synchronisation (hipDeviceSynchronize, torch.cuda.synchronize) therefore
+ * waits at most that long.  spt_service_stop drains and ends the session and turns the
+ * service off.  Every host wait for a session is bounded (SPT_SVC_TIMEOUT_MS, default
+ * 30 s: SPT_ERR_TIMEOUT). */
 SPT_API int spt_service_start(spt_ctx *ctx);
 SPT_API int spt_service_stop(spt_ctx *ctx);
 

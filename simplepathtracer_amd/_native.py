@@ -15,10 +15,10 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG_DIR, "lib", os.environ.get("SPT_LIB", "libspt_hip.so"))
 HEADER_PATH = os.path.join(os.path.dirname(PKG_DIR), "include", "spt_hip.h")
 
-ABI_VERSION = 6  # SPT_ABI_VERSION of include/spt_hip.h
+ABI_VERSION = 7  # SPT_ABI_VERSION of include/spt_hip.h
 SPT_OK = 0
 STATUS_NAMES = {0: "SPT_OK", 1: "SPT_ERR_ARG", 2: "SPT_ERR_STATE", 3: "SPT_ERR_HIP", 4: "SPT_ERR_NOMEM",
-                5: "SPT_ERR_NODEVICE"}
+                5: "SPT_ERR_NODEVICE", 6: "SPT_ERR_TIMEOUT"}
 MODE_SEGMENT, MODE_TASK = 0, 1
 TREE_AUTO = 0xFFFFFFFF  # spt_set_cluster_tree default
 CLUSTER_AUTO = 0xFFFFFFFF  # spt_set_cluster_size default
@@ -53,6 +53,8 @@ class Stats(ctypes.Structure):
         ("svc_kernel_ms", ctypes.c_double),
         ("svc_running", ctypes.c_uint32),
         ("svc_grid_blocks", ctypes.c_uint32),
+        ("svc_flow_restarts", ctypes.c_uint64),
+        ("svc_closing_restarts", ctypes.c_uint64),
     ]
 
 

@@ -92,13 +92,13 @@ struct BatchReq {
 };
 // Read-ahead of the reference's tiling (render_segment_host, DESIGN.md §5 "Drop-in
 // read-ahead"): RenderImageParallelMain (Renderer.hpp:257-302) calls RenderSegment on the
-// tc x tc tiles of MakeRenderSegmentData in a fixed order, at most tc at a time.  When the
-// first tile of such a tiling arrives, every tile of the frame is rendered at once in
-// `parts` batched launches of consecutive tile rows (SPT_READAHEAD_PARTS, default 4) into
-// a device copy of g_data; each
-// tile's call then waits for its part and copies its own rows to the caller's g_data.
-// Every tile is still rendered once per frame; nothing is written to the caller's buffer
-// before its call.
+// tc x tc tiles of MakeRenderSegmentData, at most tc at a time, from detached threads (so
+// in no fixed order).  Once a caller has called every tile of such a tiling (the tiling is
+// "armed": a caller rendering one tile alone never arms it), the first call of a tile of it
+// renders every tile of the frame at once in `parts` batched launches of consecutive tile
+// rows (SPT_READAHEAD_PARTS, default 4) into a device copy of g_data; each tile's call then
+// waits for its part and copies its own rows to the caller's g_data.  Every tile is still
+// rendered once per frame; nothing is written to the caller's buffer before its call.
 struct SpecFrame {
     bool active = false;
     int mode = 0;
@@ -112,6 +112,15 @@ struct SpecFrame {
     BatchSet bs[kParts];
     uint8_t *d8 = nullptr;  // the frame's RGB8 bytes (g_data layout), device
     size_t d8_cap = 0;
+    // serves copying out of d8 with the context unlocked: the next read-ahead neither
+    // rewrites nor reallocates d8 before they are done (readers_cv, ctx->mu)
+    uint32_t readers = 0;
+    std::condition_variable readers_cv;
+    // arming: the tiles of one tiling (mode, tc, frame size) called so far by plain calls
+    int arm_mode = -1;
+    uint32_t arm_tc = 0, arm_w = 0, arm_h = 0, arm_count = 0;
+    std::vector<uint8_t> arm_seen;
+    bool armed = false;
 };
 
 struct Workspace {
@@ -139,7 +148,6 @@ struct Service {
     bool enabled = false;  // spt_service_start: renders go through the service
     bool running = false;  // a session's kernel is resident
     hipStream_t stream = nullptr;  // the session kernel
-    hipStream_t pub = nullptr;     // publish and stop launches
     uint32_t *d_ctl = nullptr;
     spt::SvcJob *d_jobs = nullptr;
     uint32_t *d_job_claim = nullptr, *d_done = nullptr, *d_ring = nullptr;
@@ -162,8 +170,20 @@ struct Service {
     std::vector<SvcInflight> inflight;
     std::vector<hipEvent_t> ev_pool;
     hipEvent_t ev_start = nullptr, ev_end = nullptr, ev_ctl = nullptr;
-    std::chrono::steady_clock::time_point last_pub;
+    // the session's closing-handshake words (spt_internal.h kSvcIdleTicks), page-locked
+    // host memory: host view and device view
+    uint32_t *h_host = nullptr, *d_host = nullptr;
+    // the host job tables the forwarder copies from (same memory kind): host / device views
+    spt::SvcJob *h_jobs = nullptr, *dh_jobs = nullptr;
+    uint32_t *h_job_claim = nullptr, *dh_job_claim = nullptr;
+    uint32_t grid_div = 1;       // SPT_SVC_GRID_DIV: the session takes 1/div of its grid
+    uint32_t pub_delay_us = 0;   // SPT_SVC_TEST_PUB_DELAY_US: fault injection before every publish
+    double timeout_ms = 30000;   // SPT_SVC_TIMEOUT_MS: longest wait for a session to end
+    bool debug = false;          // SPT_SVC_DEBUG: a line on stderr per session event
     uint64_t sessions = 0, jobs = 0, watchdog_exits = 0;
+    // sessions ended early: a publication would have waited for an unfinished fold (flow
+    // control), or a wave of the session had raised the closing flag
+    uint64_t flow_restarts = 0, closing_restarts = 0;
     double kernel_ms = 0;  // summed session spans
     unsigned long long *d_trace = nullptr;  // SPT_SVC_TRACE: printed by svc_end
 };
@@ -263,11 +283,6 @@ struct spt_ctx {
     // then run side by side and each one's tail drains beside the other's blocks (config 2
     // through the C++ shim at tc = 4: 7.93 -> 7.64 ms per frame, its folds 2x shorter)
     uint32_t batch_grid_div = 2;
-    bool fold_to_host = true;     // batched folds write page-locked g_data in place (SPT_FOLD_HOST)
-    // per-batch launch latency (launch_batch): rectangles in the kernel arguments
-    // (SPT_INLINE_RECTS), claim counters zeroed by the previous fold (SPT_FOLD_HEAD); the
-    // leader polls its batch's stream instead of a blocking wait (SPT_SPIN_SYNC)
-    bool inline_rects = true, fold_resets_head = true, spin_sync = false;
     std::condition_variable batch_cv;
     uint64_t batches = 0, batched_calls = 0;
 
@@ -581,12 +596,16 @@ int ensure_wavefront(spt_ctx *ctx, Workspace *w, uint32_t cap, uint32_t qcap)
     return SPT_OK;
 }
 
-// ---- render service (DESIGN.md §5 "Render service") -----------------------------------
-// The host publishes to a session only while it has published within kSvcHostIdleMs;
-// after a longer pause it ends the session and starts a new one.  The session's waves
-// leave after spt::kSvcIdleTicks (0.5 s) without work, far longer than that, so a job is
-// never published to a session that may have left.
-constexpr double kSvcHostIdleMs = 40.0;
+// ---- render service (DESIGN.md §4.7 "Render service") ----------------------------------
+// Liveness rests on two rules (DESIGN.md §4.7 "Liveness"):
+//  * a publication never waits for anything but its session's start: when one would
+//    have to wait for an unfinished fold (its ring words or its completion counter still
+//    in use), the session is ended first and the new session's kernel itself waits for
+//    those folds -- so no publish is ever held behind work that waits for the session;
+//  * a wave leaves an idle session only through the closing handshake (spt_internal.h
+//    kSvcIdleTicks): the host commits every job before publishing it and ends a session
+//    whose closing flag it finds raised, so no job is published to a session that left.
+// Every host wait on a session is bounded (SPT_SVC_TIMEOUT_MS, svc_wait).
 
 hipEvent_t svc_event(spt_ctx *ctx)
 {
@@ -601,20 +620,62 @@ hipEvent_t svc_event(spt_ctx *ctx)
     return e;
 }
 
-// End the session: publish the stop flag after every job, wait for the kernel to drain
-// them and leave.  No-op without a session.
+#define SVC_DBG(ctx, ...)                                                                              \
+    do {                                                                                               \
+        if ((ctx)->svc.debug) {                                                                        \
+            std::fprintf(stderr, "[svc %.3f] ", std::chrono::duration<double, std::milli>(               \
+                                                     std::chrono::steady_clock::now().time_since_epoch()) \
+                                                     .count());                                        \
+            std::fprintf(stderr, __VA_ARGS__);                                                         \
+            std::fputc('\n', stderr);                                                                  \
+        }                                                                                              \
+    } while (0)
+
+// Wait for event e at most the service's timeout: SPT_OK, or SPT_ERR_TIMEOUT.  Spins
+// (yielding) for the first 2 ms, then polls every 50 us.
+int svc_wait(spt_ctx *ctx, hipEvent_t e, const char *what)
+{
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+        const hipError_t q = hipEventQuery(e);
+        if (q == hipSuccess) return SPT_OK;
+        if (q != hipErrorNotReady) return fail(ctx, SPT_ERR_HIP, "%s: %s", what, hipGetErrorString(q));
+        const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        if (ms > ctx->svc.timeout_ms) {
+            const Service &v = ctx->svc;
+            const uint32_t closing = __atomic_load_n(v.h_host + spt::kSvcHostClosing, __ATOMIC_SEQ_CST);
+            return fail(ctx, SPT_ERR_TIMEOUT,
+                        "render service: %s did not finish within %.0f ms (session %llu: %u jobs published, "
+                        "%llu claims; closing flag %u)",
+                        what, v.timeout_ms, (unsigned long long)v.sessions, v.n_jobs, (unsigned long long)v.claims,
+                        closing);
+        }
+        if (ms < 2.0)
+            std::this_thread::yield();
+        else
+            std::this_thread::sleep_for(std::chrono::microseconds(50));
+    }
+}
+
+// End the session: the stop flag after every publication (host memory: the forwarder
+// passes it on after the last record), then wait (bounded) for the kernel to drain the
+// jobs and leave.  No-op without a session.
 int svc_end(spt_ctx *ctx)
 {
     Service &v = ctx->svc;
     if (!v.running) return SPT_OK;
     v.running = false;
-    HIP_TRY(ctx, spt::launch_svc_stop(v.d_ctl, v.pub));
-    HIP_TRY(ctx, hipStreamSynchronize(v.stream));
+    SVC_DBG(ctx, "end session %llu (%u jobs): stop", (unsigned long long)v.sessions, v.n_jobs);
+    __atomic_store_n(v.h_host + spt::kSvcHostStop, 1u, __ATOMIC_SEQ_CST);
+    if (int rc = svc_wait(ctx, v.ev_end, "ending the session")) return rc;
+    SVC_DBG(ctx, "end session %llu: kernel done", (unsigned long long)v.sessions);
     float ms = 0.f;
     if (hipEventElapsedTime(&ms, v.ev_start, v.ev_end) == hipSuccess) v.kernel_ms += ms;
-    uint32_t wd = 0;
-    HIP_TRY(ctx, hipMemcpy(&wd, v.d_ctl + spt::kSvcWatchdog, sizeof wd, hipMemcpyDeviceToHost));
+    // read from host memory: no device call here (a synchronous copy would queue behind
+    // whatever else the device is running)
+    const uint32_t wd = __atomic_load_n(v.h_host + spt::kSvcHostWatchdog, __ATOMIC_SEQ_CST);
     if (wd) v.watchdog_exits++;
+    SVC_DBG(ctx, "end session %llu: watchdog %u", (unsigned long long)v.sessions, wd);
     if (v.d_trace) {
         // per counter used this session: first / last claim taken, last count, in us
         // from the session's first claim (s_memrealtime: 100 MHz)
@@ -638,30 +699,46 @@ int svc_end(spt_ctx *ctx)
     return SPT_OK;
 }
 
+// Page-locked, fine-grained (coherent) host memory: the host's stores and the device's
+// system-scope accesses reach the same bytes.  Host and device views.
+template <class T>
+int host_shared(spt_ctx *ctx, size_t count, T **host, T **dev)
+{
+    void *p = nullptr, *d = nullptr;
+    HIP_TRY(ctx, hipHostMalloc(&p, count * sizeof(T), hipHostMallocCoherent | hipHostMallocMapped));
+    std::memset(p, 0, count * sizeof(T));
+    HIP_TRY(ctx, hipHostGetDevicePointer(&d, p, 0));
+    *host = (T *)p;
+    *dev = (T *)d;
+    return SPT_OK;
+}
+
 // Start a session for `mode` (the session's kernel arguments hold the scene, camera,
-// frame and mode of the context as they are now; the setters end the session).
-int svc_begin(spt_ctx *ctx, int mode)
+// frame and mode of the context as they are now; the setters end the session).  The
+// session's kernel waits for `waits` (folds whose ring words or counters its first
+// publication reuses); reset_idx (or -1): a completion counter zeroed before it, with
+// the caller's stream s ordered after that.
+int svc_begin(spt_ctx *ctx, int mode, const std::vector<hipEvent_t> &waits, int64_t reset_idx, hipStream_t s)
 {
     Service &v = ctx->svc;
+    if (!v.h_host) {
+        int rc = host_shared(ctx, spt::kSvcHostWords, &v.h_host, &v.d_host);
+        if (!rc) rc = host_shared(ctx, v.job_cap, &v.h_jobs, &v.dh_jobs);
+        if (!rc) rc = host_shared(ctx, v.job_cap, &v.h_job_claim, &v.dh_job_claim);
+        if (rc) return rc;
+    }
     if (!v.stream) {
         // The resident kernel never ends while the session runs, so nothing may queue
         // behind it: HIP maps a process's streams of one priority round-robin onto
         // GPU_MAX_HW_QUEUES hardware queues (4 on the box), and a stream sharing the
-        // kernel's queue would wait for the session's end (a publish stuck there: a hang
-        // until the waves idle out).  A stream of another priority gets a queue of its own
-        // (tools/ubench/queue_probe T6/T7, profiles/queue_probe_r04.txt); SPT_SVC_PRIO
-        // picks it (default: the greatest priority).
-        // The publish stream must not share a queue with the callers' streams either: a
-        // caller's counter wait would hold every later publish behind it, so jobs would be
-        // published one fold at a time (SPT_SVC_PUB_PRIO; default: the least priority;
-        // T9).
+        // kernel's queue would wait for the session's end.  A stream of another priority
+        // gets a queue of its own (tools/ubench/queue_probe T6/T7,
+        // profiles/queue_probe_r04.txt); SPT_SVC_PRIO picks it (default: the greatest).
         int lo = 0, hi = 0;
         HIP_TRY(ctx, hipDeviceGetStreamPriorityRange(&lo, &hi));
-        int prio = hi, pub_prio = lo;
+        int prio = hi;
         if (const char *e = env_var("SPT_SVC_PRIO")) prio = std::atoi(e);
-        if (const char *e = env_var("SPT_SVC_PUB_PRIO")) pub_prio = std::atoi(e);
         HIP_TRY(ctx, hipStreamCreateWithPriority(&v.stream, hipStreamNonBlocking, prio));
-        HIP_TRY(ctx, hipStreamCreateWithPriority(&v.pub, hipStreamNonBlocking, pub_prio));
         HIP_TRY(ctx, hipEventCreate(&v.ev_start));
         HIP_TRY(ctx, hipEventCreate(&v.ev_end));
         HIP_TRY(ctx, hipEventCreateWithFlags(&v.ev_ctl, hipEventDisableTiming));
@@ -673,9 +750,9 @@ int svc_begin(spt_ctx *ctx, int mode)
                         hipMalloc((void **)&v.d_ring, (size_t)v.ring_words * sizeof(uint32_t)) == hipSuccess;
         if (!ok) return fail(ctx, SPT_ERR_NOMEM, "render service buffers (%llu MiB ring) allocation failed",
                              (unsigned long long)(v.ring_bytes >> 20));
-        HIP_TRY(ctx, hipMemset(v.d_done, 0, (size_t)v.done_cap * sizeof(uint32_t)));
-        v.done_cum.assign(v.done_cap, 0);
+        HIP_TRY(ctx, hipMemsetAsync(v.d_done, 0, (size_t)v.done_cap * sizeof(uint32_t), v.stream));
     }
+    const uint32_t grid = std::max<uint32_t>(1u, ctx->svc_grid / v.grid_div);
     spt::RenderArgs ra{};
     ra.scene = device_scene(ctx);
     ra.cam = ctx->cam;
@@ -693,6 +770,9 @@ int svc_begin(spt_ctx *ctx, int mode)
     ra.svc_jobs = v.d_jobs;
     ra.svc_job_claim = v.d_job_claim;
     ra.svc_done = v.d_done;
+    ra.svc_host = v.d_host;
+    ra.svc_host_jobs = v.dh_jobs;
+    ra.svc_host_job_claim = v.dh_job_claim;
     if (env_var("SPT_SVC_TRACE")) {
         const size_t n = (size_t)v.done_cap * 4 + spt::kSvcTraceClaims;
         if (!v.d_trace) HIP_TRY(ctx, hipMalloc((void **)&v.d_trace, n * sizeof(unsigned long long)));
@@ -701,19 +781,34 @@ int svc_begin(spt_ctx *ctx, int mode)
         HIP_TRY(ctx, hipMemcpy(v.d_trace, init.data(), n * sizeof(unsigned long long), hipMemcpyHostToDevice));
         ra.svc_trace = v.d_trace;
     }
-    // control words zeroed before the kernel and before any publish of the session
+    // the previous session's kernel has ended (svc_end), so no wave reads the host words
+    // while they are reset; the kernel launch below orders these stores before it
+    __atomic_store_n(v.h_host + spt::kSvcHostCommitted, 0u, __ATOMIC_SEQ_CST);
+    __atomic_store_n(v.h_host + spt::kSvcHostClosing, 0u, __ATOMIC_SEQ_CST);
+    __atomic_store_n((uint64_t *)(v.h_host + spt::kSvcHostPub), (uint64_t)0, __ATOMIC_SEQ_CST);
+    __atomic_store_n(v.h_host + spt::kSvcHostStop, 0u, __ATOMIC_SEQ_CST);
+    __atomic_store_n(v.h_host + spt::kSvcHostWatchdog, 0u, __ATOMIC_SEQ_CST);
+    for (hipEvent_t e : waits) HIP_TRY(ctx, hipStreamWaitEvent(v.stream, e, 0));
+    // control words zeroed, the render-wave count set, before the kernel
     HIP_TRY(ctx, hipMemsetAsync(v.d_ctl, 0, spt::kSvcCtlWords * sizeof(uint32_t), v.stream));
-    HIP_TRY(ctx, hipEventRecord(v.ev_ctl, v.stream));
-    HIP_TRY(ctx, hipStreamWaitEvent(v.pub, v.ev_ctl, 0));
+    HIP_TRY(ctx, hipMemsetD32Async((hipDeviceptr_t)(v.d_ctl + spt::kSvcLive), (int)(grid * (spt::kRenderBlock / 64u) - 1u),
+                                   1, v.stream));
+    if (reset_idx >= 0) {
+        // a completion counter whose running total restarts: zeroed after the folds that
+        // waited on it (waits), and the caller's stream ordered after the zeroing
+        HIP_TRY(ctx, hipMemsetAsync(v.d_done + reset_idx, 0, sizeof(uint32_t), v.stream));
+        HIP_TRY(ctx, hipEventRecord(v.ev_ctl, v.stream));
+        HIP_TRY(ctx, hipStreamWaitEvent(s, v.ev_ctl, 0));
+    }
     HIP_TRY(ctx, hipEventRecord(v.ev_start, v.stream));
-    HIP_TRY(ctx, spt::launch_render_svc(ra, ctx->svc_grid, v.stream));
+    HIP_TRY(ctx, spt::launch_render_svc(ra, grid, v.stream));
     HIP_TRY(ctx, hipEventRecord(v.ev_end, v.stream));
     v.running = true;
     v.mode = mode;
     v.n_jobs = 0;
     v.claims = 0;
     v.sessions++;
-    v.last_pub = std::chrono::steady_clock::now();
+    SVC_DBG(ctx, "begin session %llu, grid %u, %zu waits", (unsigned long long)v.sessions, grid, waits.size());
     return SPT_OK;
 }
 
@@ -751,84 +846,95 @@ int svc_submit_jobs(spt_ctx *ctx, int mode, const SvcJobSpec *jobs, size_t n, ui
     }
     if (items > 0xFFFFFFFFull) return fail(ctx, SPT_ERR_ARG, "render service: %llu samples in one publication",
                                            (unsigned long long)items);
+    if (n > v.job_cap) return fail(ctx, SPT_ERR_ARG, "render service: %zu jobs in one publication", n);
     const uint64_t words = total_slots * slot_words;
-    const auto now = std::chrono::steady_clock::now();
-    const double idle_ms = std::chrono::duration<double, std::milli>(now - v.last_pub).count();
-    // a new session: none yet, another mode, a pause (the kernel may idle out), a kernel
-    // that left already, or the session's job table / claim range full
-    if (!v.running || v.mode != mode || idle_ms >= kSvcHostIdleMs || hipEventQuery(v.ev_end) != hipErrorNotReady ||
-        v.n_jobs + n > v.job_cap || (v.claims + nclaims) * v.claim > 0x7FFFFFFFull) {
-        int rc = svc_end(ctx);
-        if (!rc) rc = svc_begin(ctx, mode);
-        if (rc) return rc;
-    }
-    if (v.ring_head + words > v.ring_words) v.ring_head = 0;
-    const uint64_t w0 = v.ring_head, w1 = w0 + words;
-    v.ring_head = w1;
+    // the publication's ring words and completion counter
+    const uint64_t w0 = v.ring_head + words > v.ring_words ? 0 : v.ring_head, w1 = w0 + words;
     const uint32_t idx = v.next_done;
-    v.next_done = (v.next_done + 1u) % v.done_cap;
+    if (v.done_cum.empty()) v.done_cum.assign(v.done_cap, 0);  // counters zeroed with their allocation
     uint64_t target = v.done_cum[idx] + items;
     const bool reset = target > 0xFFFFFFFFull;
-    if (reset) target = items;
-    v.done_cum[idx] = target;
-    // flow control on the publish stream: folds still reading the ring words, or jobs
-    // whose fold still waits on the counter, finish first (at most 1024 jobs in flight)
+    // Flow control: earlier jobs whose folds still read these ring words or still wait on
+    // this counter (or the oldest, with 1024 jobs in flight) must be folded first.  Folds
+    // found finished are retired; an unfinished one is never waited for inside the running
+    // session -- a fold can sit behind work that itself waits for the session to end (an
+    // RCCL gather cannot become resident beside it) -- so the session is ended
+    // and the next one's kernel waits for those folds instead.
+    std::vector<hipEvent_t> waits;
     for (size_t i = 0; i < v.inflight.size();) {
         SvcInflight &e = v.inflight[i];
         const bool busy = (e.w0 < w1 && w0 < e.w1) || e.done_idx == idx || (i == 0 && v.inflight.size() >= 1024);
-        if (busy) {
-            HIP_TRY(ctx, hipStreamWaitEvent(v.pub, e.ev, 0));
-            v.ev_pool.push_back(e.ev);
-            v.inflight.erase(v.inflight.begin() + (std::ptrdiff_t)i);
-        } else {
+        if (!busy) {
             ++i;
+            continue;
         }
+        const hipError_t q = hipEventQuery(e.ev);
+        if (q != hipSuccess && q != hipErrorNotReady) return fail(ctx, SPT_ERR_HIP, "fold event: %s", hipGetErrorString(q));
+        if (q == hipErrorNotReady) waits.push_back(e.ev);
+        else v.ev_pool.push_back(e.ev);
+        v.inflight.erase(v.inflight.begin() + (std::ptrdiff_t)i);
     }
-    // the records, kSvcPubMax per publish launch; the first zeroes the counter on a reset
-    for (size_t i0 = 0; i0 < n; i0 += spt::kSvcPubMax) {
-        spt::SvcPublish p{};
-        p.ctl = v.d_ctl;
-        p.jobs = v.d_jobs;
-        p.job_claim = v.d_job_claim;
-        p.done = v.d_done;
-        p.first_job = v.n_jobs;
-        p.n_jobs = (uint32_t)std::min<size_t>(spt::kSvcPubMax, n - i0);
-        p.n_zero = i0 == 0 && reset ? 1u : 0u;
-        p.zero_idx[0] = idx;
-        for (uint32_t k = 0; k < p.n_jobs; ++k) {
-            const SvcJobSpec &js = jobs[i0 + k];
-            const uint64_t it = (uint64_t)spt::rows_owned(js.map) * js.map.width * js.spp_batch;
-            const uint64_t nc = (it + v.claim - 1) / v.claim;
-            spt::SvcJob &j = p.rec[k];
-            j.item_off = (uint32_t)(v.claims * v.claim);
-            j.item_end = (uint32_t)(j.item_off + it);
-            j.slot_off = (uint32_t)(w0 / slot_words + js.slot_local);
-            j.done_idx = idx;
-            j.rows = js.rows;
-            j.spp_batch = js.spp_batch;
-            j.s0 = js.s0;
-            j.claim_end = (uint32_t)(v.claims + nc);
-            j.map = js.map;
-            j.div_band = js.div_band;
-            j.div_tile = js.div_tile;
-            j.div_strip = js.div_strip;
-            j.claim_first = (uint32_t)v.claims;
-            v.claims += nc;
-            v.n_jobs++;
-            v.jobs++;
+    // a new session: none yet, another mode, a kernel that left already, the session's job
+    // table / claim range full, folds to wait for, or a counter to zero
+    bool fresh = !v.running || v.mode != mode || hipEventQuery(v.ev_end) != hipErrorNotReady ||
+                 v.n_jobs + n > v.job_cap || (v.claims + nclaims) * v.claim > 0x7FFFFFFFull || !waits.empty() || reset;
+    if (!fresh) {
+        // commit the jobs to the running session, then look for a raised closing flag
+        // (store, full fence, load: the host half of the handshake)
+        __atomic_store_n(v.h_host + spt::kSvcHostCommitted, v.n_jobs + (uint32_t)n, __ATOMIC_SEQ_CST);
+        __atomic_thread_fence(__ATOMIC_SEQ_CST);
+        if (__atomic_load_n(v.h_host + spt::kSvcHostClosing, __ATOMIC_SEQ_CST) != 0u) {
+            fresh = true;
+            v.closing_restarts++;
         }
-        p.pub_claims = (uint32_t)v.claims;
-        HIP_TRY(ctx, spt::launch_svc_publish(p, v.pub));
+    } else if (!waits.empty() && v.running) {
+        v.flow_restarts++;
     }
-    v.last_pub = now;
-    if (reset) {
-        hipEvent_t e = svc_event(ctx);
-        if (!e) return fail(ctx, SPT_ERR_HIP, "event creation failed");
-        HIP_TRY(ctx, hipEventRecord(e, v.pub));
-        HIP_TRY(ctx, hipStreamWaitEvent(s, e, 0));
-        v.ev_pool.push_back(e);
+    SVC_DBG(ctx, "submit %zu job(s), words [%llu, %llu), counter %u: %zu waits, fresh %d", n, (unsigned long long)w0,
+            (unsigned long long)w1, idx, waits.size(), (int)fresh);
+    if (fresh) {
+        int rc = svc_end(ctx);
+        if (!rc) rc = svc_begin(ctx, mode, waits, reset ? (int64_t)idx : -1, s);
+        for (hipEvent_t e : waits) v.ev_pool.push_back(e);  // the waits are enqueued (or abandoned)
+        if (rc) return rc;
+        __atomic_store_n(v.h_host + spt::kSvcHostCommitted, (uint32_t)n, __ATOMIC_SEQ_CST);
     }
+    v.ring_head = w1;
+    v.next_done = (v.next_done + 1u) % v.done_cap;
+    if (reset) target = items;
+    v.done_cum[idx] = target;
+    // SPT_SVC_TEST_PUB_DELAY_US (fault injection): committed, not yet published
+    if (v.pub_delay_us) std::this_thread::sleep_for(std::chrono::microseconds(v.pub_delay_us));
+    // the records and first claims (host tables, the forwarder copies them), then the pair
+    for (size_t k = 0; k < n; ++k) {
+        const SvcJobSpec &js = jobs[k];
+        const uint64_t it = (uint64_t)spt::rows_owned(js.map) * js.map.width * js.spp_batch;
+        const uint64_t nc = (it + v.claim - 1) / v.claim;
+        spt::SvcJob j{};
+        j.item_off = (uint32_t)(v.claims * v.claim);
+        j.item_end = (uint32_t)(j.item_off + it);
+        j.slot_off = (uint32_t)(w0 / slot_words + js.slot_local);
+        j.done_idx = idx;
+        j.rows = js.rows;
+        j.spp_batch = js.spp_batch;
+        j.s0 = js.s0;
+        j.claim_end = (uint32_t)(v.claims + nc);
+        j.map = js.map;
+        j.div_band = js.div_band;
+        j.div_tile = js.div_tile;
+        j.div_strip = js.div_strip;
+        j.claim_first = (uint32_t)v.claims;
+        std::memcpy(&v.h_jobs[v.n_jobs], &j, sizeof j);
+        v.h_job_claim[v.n_jobs] = j.claim_first;
+        v.claims += nc;
+        v.n_jobs++;
+        v.jobs++;
+    }
+    // x86 keeps stores in order: the device sees the pair only after the records it covers
+    __atomic_store_n((uint64_t *)(v.h_host + spt::kSvcHostPub), (uint64_t)(uint32_t)v.claims | ((uint64_t)v.n_jobs << 32),
+                     __ATOMIC_RELEASE);
     HIP_TRY(ctx, hipStreamWaitValue32(s, v.d_done + idx, (uint32_t)target, hipStreamWaitValueGte, 0xFFFFFFFFu));
+    SVC_DBG(ctx, "submitted, %u jobs in session", v.n_jobs);
     *w0_out = w0;
     *idx_out = idx;
     return SPT_OK;
@@ -1259,7 +1365,7 @@ int launch_batch(spt_ctx *ctx, BatchSet *bs, const std::vector<BatchReq *> &batc
         } else if (r->g_data) {
             b.rgb8 = ctx->d_frame8;
             const size_t fb = (size_t)W * H * 3;
-            for (const spt_ctx::Pinned &p : ctx->fold_to_host ? ctx->pinned : std::vector<spt_ctx::Pinned>{}) {
+            for (const spt_ctx::Pinned &p : ctx->pinned) {
                 const uint8_t *base = (const uint8_t *)p.ptr;
                 if (p.dev && r->g_data >= base && r->g_data + fb <= base + p.bytes) {
                     b.rgb8 = p.dev + (r->g_data - base);
@@ -1304,7 +1410,7 @@ int launch_batch(spt_ctx *ctx, BatchSet *bs, const std::vector<BatchReq *> &batc
         ctx->launches++;
     }
     // up to kInlineRects rectangles travel in the kernel arguments; more in the table
-    const bool inl = ctx->inline_rects && n <= spt::kInlineRects;
+    const bool inl = n <= spt::kInlineRects;
     if (!inl)
         HIP_TRY(ctx, hipMemcpyAsync(bs->d_rects, bs->h_rects, n * sizeof(spt::BatchRect), hipMemcpyHostToDevice, s));
 
@@ -1343,7 +1449,7 @@ int launch_batch(spt_ctx *ctx, BatchSet *bs, const std::vector<BatchReq *> &batc
     // the claim counters are zeroed by the previous batch's fold on this workspace
     // (FoldArgs::head_reset), or here when that fold did not run
     if (!use_svc) {
-        if (!w->head_clean || !ctx->fold_resets_head)
+        if (!w->head_clean)
             HIP_TRY(ctx, hipMemsetAsync(w->d_head, 0, sizeof(uint32_t) * spt::kQueueStride * ra.n_queues, s));
         w->head_clean = false;
         if (!ctx->ref_recorded) {
@@ -1380,7 +1486,7 @@ int launch_batch(spt_ctx *ctx, BatchSet *bs, const std::vector<BatchReq *> &batc
     fa.inline_rects = inl ? 1u : 0u;
     if (inl)
         for (size_t i = 0; i < n; ++i) fa.rects_inline[i] = bs->h_rects[i];
-    fa.head_reset = ctx->fold_resets_head && !use_svc ? w->d_head : nullptr;
+    fa.head_reset = !use_svc ? w->d_head : nullptr;
     fa.head_queues = ra.n_queues;
     EventPair ef = get_pair(ctx);
     HIP_TRY(ctx, hipEventRecord(ef.a, s));
@@ -1470,12 +1576,7 @@ int render_batched(spt_ctx *ctx, std::unique_lock<std::mutex> &lk, int mode, uin
         int rc = bs->stream ? launch_batch(ctx, bs, batch) : fail(ctx, SPT_ERR_HIP, "stream creation failed");
         if (rc == SPT_OK) {
             lk.unlock();
-            hipError_t e;
-            if (ctx->spin_sync) {
-                while ((e = hipStreamQuery(bs->stream)) == hipErrorNotReady) std::this_thread::yield();
-            } else {
-                e = hipStreamSynchronize(bs->stream);
-            }
+            const hipError_t e = hipStreamSynchronize(bs->stream);
             lk.lock();
             if (e != hipSuccess) rc = fail(ctx, SPT_ERR_HIP, "hipStreamSynchronize failed: %s", hipGetErrorString(e));
         } else if (bs->stream) {
@@ -1512,10 +1613,12 @@ int spec_drain(spt_ctx *ctx)
 }
 
 // Render every tile of the tc x tc tiling of `mode` (MakeRenderSegmentData order) into the
-// read-ahead frame, in two batched launches.  Called with ctx->mu held.
-int spec_launch(spt_ctx *ctx, int mode, uint32_t tc)
+// read-ahead frame, in sp.parts batched launches.  Called with lk (ctx->mu) held; waits
+// (unlocked) for the previous frame's serves still copying out of d8.
+int spec_launch(spt_ctx *ctx, std::unique_lock<std::mutex> &lk, int mode, uint32_t tc)
 {
     SpecFrame &sp = ctx->spec;
+    sp.readers_cv.wait(lk, [&] { return sp.readers == 0; });
     int rc = spec_drain(ctx);
     if (rc) return rc;
     const uint32_t W = ctx->W, H = ctx->H, sw = W / tc, sh = H / tc;
@@ -1561,7 +1664,8 @@ int spec_launch(spt_ctx *ctx, int mode, uint32_t tc)
 }
 
 // A RenderSegment call with only g_data: served from the read-ahead frame when it is one
-// of its tiles not yet served (starting a read-ahead on the first tile of a tiling), else
+// of its tiles not yet served (starting a read-ahead at any tile of an armed tiling: the
+// reference's detached RenderJob threads call the tiles in no fixed order), else
 // kSpecMiss.  Called with lk (ctx->mu) held; waits unlocked.
 int spec_serve(spt_ctx *ctx, std::unique_lock<std::mutex> &lk, int mode, uint32_t yB, uint32_t yE, uint32_t xB,
                uint32_t xE, uint8_t *g_data)
@@ -1577,22 +1681,42 @@ int spec_serve(spt_ctx *ctx, std::unique_lock<std::mutex> &lk, int mode, uint32_
         return sp.served[k] ? -1 : (int64_t)k;
     };
     int64_t k = tile_of();
-    if (k < 0 && xB == 0 && yB == 0) {
-        // the first tile of a tiling (Renderer.hpp:264-273: W / tc x H / tc tiles, tc even)
-        const uint32_t w = xE, h = yE, tc = W / w;
-        if (tc >= 2 && tc % 2 == 0 && (uint64_t)tc * tc <= kSpecMaxTiles && W / tc == w && H / tc == h &&
-            batch_slot_bytes(ctx, mode, (uint64_t)w * h * tc * tc) <= ctx->ws_bytes &&
-            (uint64_t)w * h * (tc * tc + tc) * ctx->spp < 0x7FFF0000ull) {
-            int rc = spec_launch(ctx, mode, tc);
-            if (rc) return rc;
-            k = tile_of();
+    if (k < 0) {
+        // a tile of a tiling (Renderer.hpp:264-273: W / tc x H / tc tiles, tc even)?
+        const uint32_t w = xE - xB, h = yE - yB, tc = W / w;
+        if (!(tc >= 2 && tc % 2 == 0 && (uint64_t)tc * tc <= kSpecMaxTiles && W / tc == w && H / tc == h &&
+              xB % w == 0 && yB % h == 0 && xB / w < tc && yB / h < tc &&
+              batch_slot_bytes(ctx, mode, (uint64_t)w * h * tc * tc) <= ctx->ws_bytes &&
+              (uint64_t)w * h * (tc * tc + tc) * ctx->spp < 0x7FFF0000ull))
+            return kSpecMiss;
+        if (!(sp.armed && sp.arm_mode == mode && sp.arm_tc == tc && sp.arm_w == W && sp.arm_h == H)) {
+            // not armed: note the tile; the tiling arms once all its tiles have been called
+            if (sp.arm_mode != mode || sp.arm_tc != tc || sp.arm_w != W || sp.arm_h != H) {
+                sp.arm_mode = mode;
+                sp.arm_tc = tc;
+                sp.arm_w = W;
+                sp.arm_h = H;
+                sp.arm_seen.assign((size_t)tc * tc, 0);
+                sp.arm_count = 0;
+                sp.armed = false;
+            }
+            uint8_t &seen = sp.arm_seen[(size_t)(yB / h) * tc + xB / w];
+            if (!seen) {
+                seen = 1;
+                sp.armed = ++sp.arm_count == tc * tc;
+            }
+            return kSpecMiss;
         }
+        int rc = spec_launch(ctx, lk, mode, tc);
+        if (rc) return rc;
+        k = tile_of();
+        if (k < 0) return kSpecMiss;
     }
-    if (k < 0) return kSpecMiss;
     sp.served[(size_t)k] = 1;
     const uint32_t part = (uint32_t)k / sp.tc / sp.rows_per_part;
     const hipEvent_t ev = sp.ev[part];
     uint8_t *const src = sp.d8;
+    sp.readers++;
     lk.unlock();
     // rows y in [yB, yE) live at g_data rows H-1-y: one band, xB.. per row
     const size_t pitch = (size_t)W * 3, off = (size_t)(H - yE) * pitch + (size_t)xB * 3;
@@ -1600,6 +1724,7 @@ int spec_serve(spt_ctx *ctx, std::unique_lock<std::mutex> &lk, int mode, uint32_
     if (e == hipSuccess)
         e = hipMemcpy2D(g_data + off, pitch, src + off, pitch, (size_t)(xE - xB) * 3, yE - yB, hipMemcpyDeviceToHost);
     lk.lock();
+    if (--sp.readers == 0) sp.readers_cv.notify_all();
     if (e != hipSuccess) return fail(ctx, SPT_ERR_HIP, "read-ahead tile copy failed: %s", hipGetErrorString(e));
     return SPT_OK;
 }
@@ -1914,11 +2039,7 @@ int spt_ctx_create(int device, spt_ctx **out)
     if (const char *e = env_var("SPT_READAHEAD_PARTS"))
         ctx->spec.parts = (uint32_t)std::min(SpecFrame::kParts, std::max(1, std::atoi(e)));
     if (const char *e = env_var("SPT_BATCH_DBUF")) ctx->batch_dbuf = std::atoi(e) != 0;
-    if (const char *e = env_var("SPT_FOLD_HOST")) ctx->fold_to_host = std::atoi(e) != 0;
     if (const char *e = env_var("SPT_BATCH_GRID_DIV")) ctx->batch_grid_div = (uint32_t)std::max(1, std::atoi(e));
-    if (const char *e = env_var("SPT_INLINE_RECTS")) ctx->inline_rects = std::atoi(e) != 0;
-    if (const char *e = env_var("SPT_FOLD_HEAD")) ctx->fold_resets_head = std::atoi(e) != 0;
-    if (const char *e = env_var("SPT_SPIN_SYNC")) ctx->spin_sync = std::atoi(e) != 0;
     if (const char *e = env_var("SPT_BATCH_SETS"))
         ctx->batch_sets = (uint32_t)std::min<int>((int)kMaxBatchSets, std::max(1, std::atoi(e)));
     if (const char *e = env_var("SPT_HOST_SLOTS"))
@@ -1930,6 +2051,14 @@ int spt_ctx_create(int device, spt_ctx **out)
         ctx->svc.queues = (uint32_t)std::min<int>((int)spt::kMaxQueues, std::max(1, std::atoi(e)));
     if (const char *e = env_var("SPT_SVC_RING_MB"))
         ctx->svc.ring_bytes = (uint64_t)std::max(64, std::atoi(e)) << 20;
+    // a fraction of the session grid (rehearsing several ranks' sessions on one GPU), the
+    // bound on waiting for a session to end, and the publish-delay fault injection of the
+    // liveness tests (tests/test_gpu_service.py)
+    if (const char *e = env_var("SPT_SVC_GRID_DIV")) ctx->svc.grid_div = (uint32_t)std::max(1, std::atoi(e));
+    if (const char *e = env_var("SPT_SVC_TIMEOUT_MS")) ctx->svc.timeout_ms = std::max(1.0, std::atof(e));
+    if (const char *e = env_var("SPT_SVC_DEBUG")) ctx->svc.debug = std::atoi(e) != 0;
+    if (const char *e = env_var("SPT_SVC_TEST_PUB_DELAY_US"))
+        ctx->svc.pub_delay_us = (uint32_t)std::min(5000000, std::max(0, std::atoi(e)));
     ctx->grid = (uint32_t)(per_cu * ctx->num_cu);
     ctx->grid_overlap = env_var("SPT_BLOCKS_PER_CU") || per_cu < 2 ? ctx->grid : (uint32_t)((per_cu - 1) * ctx->num_cu);
     ctx->grid_small = env_var("SPT_BLOCKS_PER_CU") || per_cu < 3 ? 0u : (uint32_t)((per_cu - 2) * ctx->num_cu);
@@ -2051,8 +2180,9 @@ void spt_ctx_destroy(spt_ctx *ctx)
         for (hipEvent_t e : v.ev_pool) (void)hipEventDestroy(e);
         for (hipEvent_t e : {v.ev_start, v.ev_end, v.ev_ctl})
             if (e) (void)hipEventDestroy(e);
-        for (hipStream_t st : {v.stream, v.pub})
-            if (st) (void)hipStreamDestroy(st);
+        if (v.stream) (void)hipStreamDestroy(v.stream);
+        for (void *h : {(void *)v.h_host, (void *)v.h_jobs, (void *)v.h_job_claim})
+            if (h) (void)hipHostFree(h);
     }
     for (spt_ctx *p : ctx->peers) spt_ctx_destroy(p);
     delete ctx;
@@ -2479,7 +2609,9 @@ int stats_one(spt_ctx *ctx, spt_stats *out)
     out->svc_watchdog_exits = ctx->svc.watchdog_exits;
     out->svc_kernel_ms = ctx->svc.kernel_ms;
     out->svc_running = ctx->svc.running ? 1u : 0u;
-    out->svc_grid_blocks = ctx->svc_grid;
+    out->svc_grid_blocks = std::max<uint32_t>(1u, ctx->svc_grid / ctx->svc.grid_div);
+    out->svc_flow_restarts = ctx->svc.flow_restarts;
+    out->svc_closing_restarts = ctx->svc.closing_restarts;
     return SPT_OK;
 }
 
@@ -2495,6 +2627,7 @@ int reset_one(spt_ctx *ctx)
     ctx->launches = 0;
     ctx->batches = ctx->batched_calls = 0;
     ctx->svc.sessions = ctx->svc.jobs = ctx->svc.watchdog_exits = 0;
+    ctx->svc.flow_restarts = ctx->svc.closing_restarts = 0;
     ctx->svc.kernel_ms = 0;
     ctx->spans.clear();
     ctx->ref_recorded = false;

@@ -304,10 +304,10 @@ struct RenderArgs {
     // kernel arguments (inline_rects = 1: no table upload before the launch)
     uint32_t inline_rects;
     BatchRect rects_inline[kInlineRects];
-    // render service (render_kernel_svc): the session's control words
-    // (SvcCtl), job table, first claim of every job and completion counters; the fields
-    // above then hold the session's constants only (scene, camera, frame, mode, ring of
-    // sample slots in `samples`, claim size, n_queues)
+    // render service (render_kernel_svc): the session's device control words
+    // (SvcCtl), its job table and first claim of every job (device copies, written by the
+    // forwarder wave) and completion counters; the fields above then hold the session's constants only (scene,
+    // camera, frame, mode, ring of sample slots in `samples`, claim size, n_queues)
     uint32_t *svc_ctl;
     const struct SvcJob *svc_jobs;
     const uint32_t *svc_job_claim;
@@ -315,20 +315,36 @@ struct RenderArgs {
     // SPT_SVC_TRACE (diagnostics, null otherwise): per completion counter, the
     // s_memrealtime of the first and last claim taken and of the last count added
     unsigned long long *svc_trace;
+    // the session's SvcHost words and host job tables in page-locked host memory (committed
+    // jobs, closing flag, published pair, stop flag; records and first claims the forwarder
+    // copies into svc_jobs / svc_job_claim), as the device sees them
+    uint32_t *svc_host;
+    const struct SvcJob *svc_host_jobs;
+    const uint32_t *svc_host_job_claim;
 };
 
 // claim counters: at most one per XCD, 256 bytes apart (separate cache lines)
 constexpr uint32_t kMaxQueues = 8, kQueueStride = 64;
 
-// ---- render service (DESIGN.md §5 "Render service") --------------------------------
+// ---- render service (DESIGN.md §4.7 "Render service") --------------------------------
 // One resident launch of render_kernel_svc renders a stream of jobs (a frame, a rank's
 // strips, a sample batch, a drop-in tile), published while it runs.  A session's claims
 // form one sequence: job j owns claims [job_claim[j], job_claim[j] + n) of `claim` items,
 // its items [item_off, item_end) (item_off = its first claim * claim, the rest of its last
 // claim is padding).  Queue q of n_queues reserves claims q, q + n_queues, ... from its
-// counter; a wave keeps one reserved claim and takes it once the publish kernel has
-// published it.  Finished samples are counted per completion counter (several jobs may
-// share one); hipStreamWaitValue32 on the counter gates the job's fold.
+// counter; a wave keeps one reserved claim and takes it once the host has published it.
+// Finished samples are counted per completion counter (several jobs may share one);
+// hipStreamWaitValue32 on the counter gates the job's fold.
+//
+// Publication needs no GPU queue: the host writes the job records, their first claims and
+// the published pair {claims, jobs} into fine-grained page-locked host memory (the SvcHost
+// block and tables); one wave of the session kernel -- the forwarder, wave 0 of block 0,
+// which renders nothing -- polls that pair with system-scope loads and copies new records
+// into the device job table, then stores the device pair the render waves poll (the R1
+// hand-off of MI355X_MICROARCH.md, as round 4's publish kernel did).  Round 4 published from
+// a one-wave kernel on a stream of its own; a dispatch waiting for CU resources the session
+// holds (an RCCL gather, the liveness test's blocker) held that kernel back, and with it
+// the session (tests/test_gpu_service.py).
 struct SvcJob {
     uint32_t item_off, item_end;  // session items of the job
     uint32_t slot_off;            // slot of its item 0 in the ring (samples, item order)
@@ -342,34 +358,32 @@ struct SvcJob {
 };
 static_assert(sizeof(SvcJob) == 128, "SvcJob: 32 words, one per lane of the loading wave");
 constexpr uint32_t kSvcJobWords = 32;
-// SvcCtl words (svc_ctl): claim counters head[q * kQueueStride] (q < kMaxQueues), then on
-// lines of their own the published pair {claims, jobs} (one 64-bit word, stored and
-// loaded as one), the stop flag, and the watchdog word (nonzero: the session ended
-// after kSvcIdleTicks without work; the host restarts it).
+// SvcCtl words (device memory, svc_ctl): claim counters head[q * kQueueStride]
+// (q < kMaxQueues), then on lines of their own the device copy of the published pair
+// {claims, jobs} (one 64-bit word, stored and loaded as one), the stop flag, and the
+// render waves still in the session (the forwarder leaves at 0).
 constexpr uint32_t kSvcPub = kMaxQueues * kQueueStride;  // uint64_t: claims | jobs << 32
 constexpr uint32_t kSvcStop = kSvcPub + 64;
-constexpr uint32_t kSvcWatchdog = kSvcStop + 64;
-constexpr uint32_t kSvcCtlWords = kSvcWatchdog + 64;
-// a wave with no work for 0.5 s (s_memrealtime, 100 MHz) leaves; the host never publishes
-// to a session it has not published to for 40 ms (it restarts it), so no job is ever lost
+constexpr uint32_t kSvcLive = kSvcStop + 64;
+constexpr uint32_t kSvcCtlWords = kSvcLive + 64;
+// A wave with no work for 0.5 s (s_memrealtime, 100 MHz) may leave, but only through the
+// closing handshake with the host (SvcHost words):
+//   wave:  closing = 1; fence; c = committed; read the published pair; leave iff every one
+//          of the c committed jobs is published and its reserved claim is not among them
+//   host:  committed = jobs of the session after this publication; fence; if closing is
+//          set, end the session and publish to a new one instead
+// Store-then-load on both sides (system scope on the device, seq_cst on the host): at
+// least one side sees the other's store, so a wave never leaves a session that is still
+// owed a publication.  "Published" is the device pair (forwarded).
 constexpr unsigned long long kSvcIdleTicks = 50000000ull;
-// jobs published by one publish launch (their records travel in its kernel arguments)
-constexpr uint32_t kSvcPubMax = 16;
+// SvcHost words (page-locked host memory), each on a 128-byte line of its own: the
+// committed job count, the closing flag, the host's published pair (uint64: claims |
+// jobs << 32), the stop flag (stored after the session's last publication) and the
+// watchdog flag (a wave left the session through the closing handshake)
+constexpr uint32_t kSvcHostCommitted = 0, kSvcHostClosing = 32, kSvcHostPub = 64, kSvcHostStop = 96,
+                   kSvcHostWatchdog = 128, kSvcHostWords = 160;
 constexpr uint32_t kSvcTraceClaims = 1u << 21;  // SPT_SVC_TRACE: claims with a take time
-struct SvcPublish {
-    uint32_t *ctl;
-    SvcJob *jobs;
-    uint32_t *job_claim;
-    uint32_t *done;
-    uint32_t first_job, n_jobs;  // records [first_job, first_job + n_jobs)
-    uint32_t pub_claims;         // claims published after them
-    uint32_t n_zero;             // completion counters zeroed before the jobs are published (total restarts)
-    uint32_t zero_idx[kSvcPubMax];
-    SvcJob rec[kSvcPubMax];
-};
 hipError_t launch_render_svc(const RenderArgs &a, uint32_t grid, hipStream_t s);
-hipError_t launch_svc_publish(const SvcPublish &p, hipStream_t s);
-hipError_t launch_svc_stop(uint32_t *ctl, hipStream_t s);
 // the service covers the wave-walk kernels (render_kernel's shapes); the lane-walk
 // trees (LDS / global-memory node tables) keep their own launches
 bool svc_supported(const AccelView &ac);

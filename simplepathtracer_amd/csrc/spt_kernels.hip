@@ -180,8 +180,8 @@ __device__ __forceinline__ uint32_t svc_reserve(uint32_t q, uint32_t lane, uint3
 // current job and the first claim after it
 constexpr uint32_t kSvcSt = 28;
 
-// The published pair {claims, jobs} (one 64-bit sc1 load: the publish kernel stores it
-// after its records, sc1, with its stores drained -- MI355X_MICROARCH.md, hand-off table)
+// The published pair {claims, jobs} (one 64-bit sc1 load: the forwarder stores it after
+// its records, sc1, with its stores drained -- MI355X_MICROARCH.md, hand-off table)
 __device__ __forceinline__ unsigned long long svc_pub()
 {
     kargs_t &k = *kernarg_args();
@@ -192,6 +192,67 @@ __device__ __forceinline__ bool svc_stopped()
 {
     kargs_t &k = *kernarg_args();
     return __hip_atomic_load((gu32 *)(k.svc_ctl + kSvcStop), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+}
+
+// The forwarder (wave 0 of block 0 of a session; it renders nothing and takes no claim):
+// polls the host's published pair and stop flag (system-scope loads of page-locked host
+// memory), copies each newly published record and first claim into the device tables
+// (sc1 stores, drained), then stores the device pair -- or, after the stop flag, the pair
+// covering every publication and then the device stop flag -- and leaves on the stop or
+// once no render wave is left (all left through the closing handshake).  Host publication
+// thus needs no GPU queue: nothing a dispatch stuck behind the session's CU residency can
+// hold back (spt_internal.h).
+__device__ __forceinline__ void svc_forward(uint32_t lane)
+{
+    kargs_t &k = *kernarg_args();
+    const gu32 *hw = (const gu32 *)k.svc_host;
+    uint32_t fwd = 0;  // records forwarded
+    for (uint32_t idle = 0;; ++idle) {
+        const uint32_t st = lane == 0 ? __hip_atomic_load(hw + kSvcHostStop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0u;
+        const bool stop = __builtin_amdgcn_readfirstlane(st) != 0u;
+        // after the stop flag, the pair is read after it (the host stores the pair first)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned long long pv =
+            lane == 0 ? __hip_atomic_load((const gu64 *)(hw + kSvcHostPub), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+                      : 0ull;
+        const uint32_t plo = __builtin_amdgcn_readfirstlane((uint32_t)pv);
+        const uint32_t phi = __builtin_amdgcn_readfirstlane((uint32_t)(pv >> 32));
+        if (phi > fwd) {
+            // records [fwd, phi): lanes 0-31 one record's words, lane 32 its first claim
+            const gu32 *hj = (const gu32 *)k.svc_host_jobs;
+            const gu32 *hc = (const gu32 *)k.svc_host_job_claim;
+            for (uint32_t j = fwd; j < phi; ++j) {
+                if (lane < kSvcJobWords) {
+                    const uint32_t w = __hip_atomic_load(hj + (size_t)j * kSvcJobWords + lane, __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_SYSTEM);
+                    __hip_atomic_store((gu32 *)(k.svc_jobs + j) + lane, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                } else if (lane == kSvcJobWords) {
+                    const uint32_t c = __hip_atomic_load(hc + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    __hip_atomic_store((gu32 *)(k.svc_job_claim + j), c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (lane == 0)
+                __hip_atomic_store((gu64 *)(k.svc_ctl + kSvcPub), (unsigned long long)plo | ((unsigned long long)phi << 32),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            fwd = phi;
+            idle = 0;
+        }
+        if (stop) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (lane == 0) __hip_atomic_store((gu32 *)(k.svc_ctl + kSvcStop), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return;
+        }
+        const uint32_t live = lane == 0 ? __hip_atomic_load((gu32 *)(k.svc_ctl + kSvcLive), __ATOMIC_RELAXED,
+                                                            __HIP_MEMORY_SCOPE_AGENT)
+                                        : 1u;
+        if (__builtin_amdgcn_readfirstlane(live) == 0u) return;
+        // ~0.1 us between polls while publications arrive, ~3 us once idle for a while
+        if (idle < 256u)
+            __builtin_amdgcn_s_sleep(2);
+        else
+            __builtin_amdgcn_s_sleep(127);
+    }
 }
 
 // The job holding published claim nb, searched forward from job `cur` (a wave's claims
@@ -274,6 +335,11 @@ __device__ __forceinline__ void render_body(const RenderArgs &a)
     __shared__ uint32_t s_rec[SVC ? (BLOCK / 64u) * kSvcJobWords : 1];
     uint32_t *const rec = s_rec + (SVC ? (threadIdx.x >> 6) * kSvcJobWords : 0u);
     if (SVC && lane < 4u) rec[kSvcSt + lane] = 0u;
+    // the session's forwarder: wave 0 of block 0 (before any claim is reserved)
+    if (SVC && blockIdx.x == 0u && (threadIdx.x >> 6) == 0u) {
+        svc_forward(lane);
+        return;
+    }
     uint32_t q_n = 0, q_pos = 0;  // the wave's queue: rows [q_pos, q_n) hold parked paths
     if (LDSN) {
         // the host launches this variant only when n_nodes + 1 <= kLdsNodeRecords
@@ -495,12 +561,15 @@ __device__ __forceinline__ void render_body(const RenderArgs &a)
             if (SVC && q_pos == q_n) {
                 // no path and no published claim: publish the finished samples, then wait
                 // for a publication or the stop flag (read before the last look at the
-                // published pair: jobs are published before the stop), at most
-                // kSvcIdleTicks (then the watchdog word tells the host)
+                // published pair: jobs are published before the stop).  After kSvcIdleTicks
+                // without work the wave may leave through the closing handshake with the
+                // host (spt_internal.h kSvcIdleTicks), then the watchdog word tells the host.
                 svc_flush(acc_idx, acc_cnt, lane);
                 acc_cnt = 0;
-                const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+                unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
                 bool leave = false;
+                bool closing = false;  // this wave has raised the closing flag
+                uint32_t committed = 0;
                 for (;;) {
                     // the stop flag is stored after every publication: once it is seen, the
                     // published pair must be read after it (the two loads would otherwise be
@@ -511,19 +580,51 @@ __device__ __forceinline__ void render_body(const RenderArgs &a)
                         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
                     }
+                    if (closing) {
+                        // the jobs the host has committed to this session, read after the
+                        // closing store reached host memory; the published pair is read
+                        // after this (next_claim_svc re-reads it: the wave is exhausted)
+                        kargs_t &k = *kernarg_args();
+                        const uint32_t c = lane == 0 ? __hip_atomic_load((gu32 *)(k.svc_host + kSvcHostCommitted),
+                                                                         __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM)
+                                                     : 0u;
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                        committed = __builtin_amdgcn_readfirstlane(c);
+                    }
                     next_claim_svc();
                     if (!exhausted) break;
                     if (stop) {
                         leave = true;
                         break;
                     }
-                    if (__builtin_amdgcn_s_memrealtime() - t0 > kSvcIdleTicks) {
+                    if (closing) {
+                        // every committed job published and none holds the wave's reserved
+                        // claim: the host publishes nothing more to this session (it saw the
+                        // flag, or the wave saw its commit), so the wave may leave
+                        if (__builtin_amdgcn_readfirstlane(rec[kSvcSt + 1]) >= committed) {
+                            kargs_t &k = *kernarg_args();
+                            if (lane == 0)
+                                __hip_atomic_store((gu32 *)(k.svc_host + kSvcHostWatchdog), 1u, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_SYSTEM);
+                            leave = true;
+                            break;
+                        }
+                        // a committed job is not published yet (its publish launch is still
+                        // queued): keep waiting for it
+                        closing = false;
+                        t0 = __builtin_amdgcn_s_memrealtime();
+                    } else if (__builtin_amdgcn_s_memrealtime() - t0 > kSvcIdleTicks) {
+                        // raise the closing flag: a system-scope store to host memory, drained
+                        // before the committed count is read
                         kargs_t &k = *kernarg_args();
                         if (lane == 0)
-                            __hip_atomic_store((gu32 *)(k.svc_ctl + kSvcWatchdog), 1u, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT);
-                        leave = true;
-                        break;
+                            __hip_atomic_store((gu32 *)(k.svc_host + kSvcHostClosing), 1u, __ATOMIC_SEQ_CST,
+                                               __HIP_MEMORY_SCOPE_SYSTEM);
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "");
+                        closing = true;
+                        continue;
                     }
                     __builtin_amdgcn_s_sleep(8);
                 }
@@ -595,7 +696,12 @@ __device__ __forceinline__ void render_body(const RenderArgs &a)
         SPT_STAMP(dc.shade);
     }
 
-    if (SVC) svc_flush(acc_idx, acc_cnt, lane);
+    if (SVC) {
+        svc_flush(acc_idx, acc_cnt, lane);
+        // one render wave fewer (the forwarder leaves when none is left)
+        kargs_t &k = *kernarg_args();
+        if (lane == 0) __hip_atomic_fetch_add((gu32 *)(k.svc_ctl + kSvcLive), 0xFFFFFFFFu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     // per-lane done/dropped -> wave sums (butterfly), one atomic per counter and wave
     // (same-address atomics from every lane cost a launch ~10%; see render_grid)
 #pragma unroll
@@ -648,37 +754,6 @@ template <bool TREE, int LEAF>
 __global__ __launch_bounds__(kRenderBlock) SPT_RENDER_ATTR void render_kernel_svc(RenderArgs a)
 {
     render_body<TREE, LEAF, false, kRenderBlock, false, false, true>(a);
-}
-
-// The publish launch: one wave stores the job records, their first claims and (when the
-// host restarts a counter's running total) the zeroed completion counter write-through
-// (sc1), drains its stores, then lane 0 stores the
-// published pair {claims, jobs} (the R1 hand-off of MI355X_MICROARCH.md: the service polls
-// the pair and reads the records with sc1 loads).
-__global__ __launch_bounds__(64) void svc_publish_kernel(SvcPublish p)
-{
-    const uint32_t lane = threadIdx.x;
-    for (uint32_t i = 0; i < p.n_zero; ++i)
-        if (lane == 0) __hip_atomic_store((gu32 *)(p.done + p.zero_idx[i]), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    for (uint32_t r = 0; r < p.n_jobs; ++r) {
-        const uint32_t *w = (const uint32_t *)&p.rec[r];
-        if (lane < kSvcJobWords)
-            __hip_atomic_store((gu32 *)(p.jobs + p.first_job + r) + lane, w[lane], __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-        if (lane == 0)
-            __hip_atomic_store((gu32 *)(p.job_claim + p.first_job + r), p.rec[r].claim_first, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (lane == 0) {
-        const unsigned long long v = (unsigned long long)p.pub_claims | ((unsigned long long)(p.first_job + p.n_jobs) << 32);
-        __hip_atomic_store((gu64 *)(p.ctl + kSvcPub), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-}
-
-__global__ __launch_bounds__(64) void svc_stop_kernel(uint32_t *ctl)
-{
-    if (threadIdx.x == 0) __hip_atomic_store((gu32 *)(ctl + kSvcStop), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // trees of kLdsNodeRecords to kGlaneMaxNodes nodes: the lane walk reading layout 0 from
@@ -1137,7 +1212,7 @@ bool svc_supported(const AccelView &ac)
 
 hipError_t launch_render_svc(const RenderArgs &a, uint32_t grid, hipStream_t s)
 {
-    if (!svc_supported(a.scene.accel)) return hipErrorInvalidValue;
+    if (!svc_supported(a.scene.accel) || !a.svc_host) return hipErrorInvalidValue;
     if (a.scene.accel.tree)
         hipLaunchKernelGGL((render_kernel_svc<true, (int)kClusterSlots>), dim3(grid), dim3(kRenderBlock), 0, s, a);
     else if (a.scene.accel.leaf_slots == kFlatLeafSlots)
@@ -1147,18 +1222,6 @@ hipError_t launch_render_svc(const RenderArgs &a, uint32_t grid, hipStream_t s)
     return hipGetLastError();
 }
 
-hipError_t launch_svc_publish(const SvcPublish &p, hipStream_t s)
-{
-    if (p.n_jobs > kSvcPubMax || p.n_zero > kSvcPubMax) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(svc_publish_kernel, dim3(1), dim3(64), 0, s, p);
-    return hipGetLastError();
-}
-
-hipError_t launch_svc_stop(uint32_t *ctl, hipStream_t s)
-{
-    hipLaunchKernelGGL(svc_stop_kernel, dim3(1), dim3(64), 0, s, ctl);
-    return hipGetLastError();
-}
 
 hipError_t launch_fold(const FoldArgs &a, hipStream_t s)
 {

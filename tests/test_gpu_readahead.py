@@ -1,9 +1,11 @@
 """GPU tests of the drop-in's tiling read-ahead (spt_api.cpp SpecFrame):
 RenderSegment / RenderSegmentTask calls over the reference's tc x tc tiling
 (Renderer.hpp:264-273, MakeRenderSegmentData), g_data only, are served from one
-read-ahead render of the whole tiling.  Every output byte must equal a plain render, a
-lone first-tile call must write only its own rows, and a setter between frames must not
-serve a stale frame."""
+read-ahead render of the whole tiling, once the caller has called every tile of that
+tiling (the tiling is armed).  Every output byte must equal a plain render, a lone
+first-tile call must write only its own rows and start no read-ahead, a frame whose
+first call is another tile (the reference's detached threads keep no order) must be
+served too, and a setter between frames must not serve a stale frame."""
 import threading
 
 import numpy as np
@@ -67,7 +69,9 @@ def render_tiling(ctx, W, H, tc, task, threads):
 def test_tiling_served_from_readahead_equals_plain_calls(spt, golden_scenes, monkeypatch, task):
     W, H, spp, tc = 240, 160, 6, 4
     ctx = make_ctx(spt, golden_scenes, W, H, spp, seed=5)
-    frames = [render_tiling(ctx, W, H, tc, task, 4) for _ in range(2)]
+    frames = [render_tiling(ctx, W, H, tc, task, 4)]  # plain calls: arms the tiling
+    ctx.reset_stats()
+    frames += [render_tiling(ctx, W, H, tc, task, 4) for _ in range(2)]
     st = ctx.stats()
     ctx.close()
     monkeypatch.setenv("SPT_READAHEAD", "0")
@@ -86,7 +90,10 @@ def test_lone_first_tile_writes_only_its_rows(spt, golden_scenes):
     W, H, spp = 200, 120, 4
     ctx = make_ctx(spt, golden_scenes, W, H, spp)
     g = np.zeros(W * H * 3, np.uint8)
-    ctx.render_segment(0, H // 2, 0, W // 2, g_data=g, rgba=False)  # tile (0, 0) of tc = 2
+    for _ in range(2):  # tile (0, 0) of tc = 2, twice: the tiling never arms
+        ctx.render_segment(0, H // 2, 0, W // 2, g_data=g, rgba=False)
+    st = ctx.stats()
+    assert st["batched_calls"] == 2 and st["samples"] == 2 * (W // 2) * (H // 2) * spp  # no read-ahead
     want = np.zeros(W * H * 3, np.uint8)
     ref = make_ctx(spt, golden_scenes, W, H, spp)
     ref.render_segment(0, H // 2, 0, W // 2, g_data=want)  # rgba requested: no read-ahead
@@ -117,3 +124,28 @@ def test_setter_between_frames_is_not_served_stale(spt, golden_scenes):
     img, ref_img = g.reshape(H, W, 3), want2.reshape(H, W, 3)
     # tiles 1.. (the new camera) match a plain render with the new camera
     assert np.array_equal(img[: H // 2], ref_img[: H // 2]) and np.array_equal(img[H // 2:, W // 2:], ref_img[H // 2:, W // 2:])
+
+
+@pytest.mark.parametrize("first", [(0, 1), (1, 1), (3, 2)])
+def test_readahead_starts_at_any_tile(spt, golden_scenes, first):
+    """Renderer.hpp:282-290 detaches its RenderJob threads, so a frame's first call may be
+    any tile: once armed, the first call of a frame -- tile (i, j) = `first` here -- starts
+    the read-ahead, every tile of the frame is served from it (one frame's launches, no
+    plain render), and the bytes equal plain calls."""
+    W, H, spp, tc = 240, 160, 4, 4
+    ctx = make_ctx(spt, golden_scenes, W, H, spp, seed=8)
+    want = render_tiling(ctx, W, H, tc, False, 4)  # plain calls: arms the tiling
+    ctx.reset_stats()
+    order = tiles(W, H, tc)
+    sw, sh = W // tc, H // tc
+    i, j = first
+    lead = (sh * j, sh * j + sh, sw * i, sw * i + sw)
+    order.remove(lead)
+    g = np.zeros(W * H * 3, np.uint8)
+    ctx.render_segment(*lead, g_data=g, rgba=False)
+    for t in reversed(order):
+        ctx.render_segment(*t, g_data=g, rgba=False)
+    st = ctx.stats()
+    ctx.close()
+    assert np.array_equal(g, want), f"{np.count_nonzero(g != want)} bytes differ"
+    assert st["batches"] == min(4, tc) and st["batched_calls"] == tc * tc and st["samples"] == W * H * spp

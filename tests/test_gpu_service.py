@@ -192,3 +192,98 @@ def test_service_host_slot_calls(spt, golden_scenes, monkeypatch):
     ctx.close()
     assert np.array_equal(got, want)
     assert st["svc_jobs"] == len(tiles)
+
+
+def _hooks():
+    """The test-only kernels (tests/cpp/spt_testhooks.hip, built by the csrc Makefile)."""
+    import ctypes
+    import os
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "simplepathtracer_amd", "lib",
+                        "libspt_testhooks.so")
+    h = ctypes.CDLL(path)
+    h.spt_test_blocker.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p]
+    h.spt_test_blocker.restype = ctypes.c_int
+    h.spt_test_blocker_vgprs.argtypes = [ctypes.c_void_p]
+    h.spt_test_blocker_vgprs.restype = ctypes.c_int
+    return h
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_service_ring_wrap_behind_blockers(spt, golden_scenes, monkeypatch, mode):
+    """Liveness.  A 64 MiB slot ring wraps every few
+    jobs, and on each caller stream, ahead of every render's fold, sits a kernel that cannot
+    be resident beside a session (512 threads x 256 VGPRs, standing in for RCCL's gather
+    kernels): so a fold cannot run while the session does.  A publication
+    whose ring words such a fold still reads must not be held inside the running session
+    (the fold waits for the blocker, the blocker for the session to end, the session for
+    the publication: round 4's build hung here); the host ends the session and the next
+    session's launch waits for the fold instead.  Every frame bit-identical to a launch."""
+    import ctypes
+    import os
+
+    import torch
+    monkeypatch.setenv("SPT_SVC_RING_MB", "64")
+    monkeypatch.setenv("SPT_SVC_TIMEOUT_MS", "30000")
+    hooks = _hooks()
+    vg = ctypes.c_int(0)
+    assert hooks.spt_test_blocker_vgprs(ctypes.byref(vg)) == 0 and vg.value == 256
+    W, H, spp = 320, 200, 16  # 1.02 M sample words (4.1 MB segment, 8.2 MB task): 15 / 7 jobs per ring
+    ctx = make_ctx(spt, golden_scenes, W, H, spp, 50, seed=5)
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    ref = render_frames(ctx, [(0, H, 1, 1, 0, 0, W)], W, H, mode, streams, service=False)[0]
+    n = 36
+    outs = [torch.zeros((W * H, 4), dtype=torch.float32, device="cuda") for _ in range(n)]
+    g8s = [torch.zeros(W * H * 3, dtype=torch.uint8, device="cuda") for _ in range(n)]
+    ran = torch.zeros(1, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    ctx.reset_stats()
+    ctx.service_start()
+    block_us = int(os.environ.get("SPT_TEST_BLOCK_US", "2000"))  # 0: no blockers (diagnostics)
+    for k in range(n):
+        s = streams[k % 2]
+        if block_us:
+            assert hooks.spt_test_blocker(ctypes.c_void_p(s.cuda_stream), block_us, 8, ctypes.c_void_p(ran.data_ptr())) == 0
+        ctx.render_rows_async(mode, 0, H, 1, 1, 0, 0, W, outs[k].data_ptr(), g8s[k].data_ptr(), s.cuda_stream)
+    ctx.service_stop()
+    st = ctx.stats()
+    ctx.synchronize()
+    torch.cuda.synchronize()
+    ctx.close()
+    for k in range(n):
+        assert_bitwise(outs[k].cpu().numpy()[:, :3], ref[0][:, :3], f"frame {k}")
+        assert np.array_equal(g8s[k].cpu().numpy(), ref[1]), f"frame {k} g_data"
+    assert int(ran.item()) == (8 * n if block_us else 0)
+    assert st["svc_jobs"] == n and st["svc_running"] == 0
+    # the ring wrapped onto words whose folds were still held by the blockers
+    assert st["svc_flow_restarts"] >= 1 and st["svc_sessions"] >= 2, st
+
+
+def test_service_publish_delayed_past_the_idle_limit(spt, golden_scenes, monkeypatch):
+    """Liveness: every publication is held 0.7 s between its commit and its publication
+    (fault injection, SPT_SVC_TEST_PUB_DELAY_US), longer than a wave may idle
+    (kSvcIdleTicks, 0.5 s).  The waves may not leave while the host has committed jobs the
+    device has not published (the closing handshake, spt_internal.h): every frame is
+    rendered, bit-identical, and no session ends through its watchdog -- the second
+    publication finds the closing flag the idle waves raised and goes to a fresh session,
+    the first one ending on its stop flag.  (Round 4's waves left at 0.5 s and the fold of
+    a frame published later waited forever.)"""
+    import torch
+    monkeypatch.setenv("SPT_SVC_TEST_PUB_DELAY_US", "700000")
+    monkeypatch.setenv("SPT_SVC_TIMEOUT_MS", "30000")
+    W, H = 160, 96
+    ctx = make_ctx(spt, golden_scenes, W, H, 8, 50, seed=6)
+    st0 = torch.cuda.Stream()
+    job = [(0, H, 1, 1, 0, 0, W)]
+    ref = render_frames(ctx, job, W, H, 0, [st0], service=False)[0]
+    ctx.reset_stats()
+    t0 = time.perf_counter()
+    got = render_frames(ctx, job * 2, W, H, 0, [st0], service=True)
+    dt = time.perf_counter() - t0
+    st = ctx.stats()
+    ctx.close()
+    for k, (a, b) in enumerate(got):
+        assert_bitwise(a[:, :3], ref[0][:, :3], f"frame {k}")
+        assert np.array_equal(b, ref[1])
+    assert dt > 1.3  # both publications were really held
+    assert st["svc_jobs"] == 2 and st["svc_watchdog_exits"] == 0, st
+    assert st["svc_sessions"] == 1 + st["svc_closing_restarts"] and st["svc_closing_restarts"] <= 1, st

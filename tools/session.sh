@@ -6,6 +6,7 @@
 # Usage: tools/session.sh <tag> <step> [<step> ...]
 #   steps: svc          pytest tests/test_gpu_service.py
 #          gpu          pytest -m gpu (the whole GPU suite)
+#          mr           bench.py --gpus 2 rehearsals (gloo ranks on one GPU, launches and service)
 #          smoke        __graft_entry__.smoke()
 #          bench        python bench.py (default arguments: config 2, service on)
 #          bench0       python bench.py --service 0 (one launch per frame)
@@ -40,6 +41,10 @@ for step in "$@"; do
   case $step in
     svc) run svc 300 $PYT -v tests/test_gpu_service.py ;;
     gpu) run gpu 600 $PYT -m gpu tests ;;
+    svcdbg) SPT_SVC_DEBUG=1 run svcdbg 300 python -u -m pytest -x -v -s --timeout 90 --timeout-method thread tests/test_gpu_service.py ;;
+    rw0) SPT_SVC_DEBUG=1 SPT_TEST_BLOCK_US=0 run rw0 120 python -u -m pytest -x -v -s --timeout 60 --timeout-method thread tests/test_gpu_service.py -k ring_wrap ;;
+    rw) SPT_SVC_DEBUG=1 run rw 120 python -u -m pytest -x -v -s --timeout 60 --timeout-method thread tests/test_gpu_service.py -k ring_wrap ;;
+    mr) run mr 300 $PYT -v -m gpu tests/test_gpu_parity.py -k two_ranks ;;
     smoke) run smoke 120 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 400 python bench.py ;;
     bench1q) run bench1q 120 python bench.py --no-cpu-baseline --no-dropin --service 1 ;;

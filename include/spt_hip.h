@@ -66,6 +66,8 @@ enum {
 
 typedef struct spt_ctx spt_ctx;
 
+#define SPT_DIAG_WORDS 19
+
 typedef struct spt_stats {
     uint64_t samples;      /* (pixel, sample) paths completed */
     uint64_t casts;        /* FindClosestIntersectionSphere calls (rays) */
@@ -80,7 +82,7 @@ typedef struct spt_stats {
     double render_busy_ms; /* length of the union of the render launches' intervals: with
                               frames in flight on several streams launches overlap, and
                               this is the device time during which some render launch ran */
-    uint64_t diag[14];     /* diagnostic build only (-DSPT_DIAG=1): wave iterations,
+    uint64_t diag[SPT_DIAG_WORDS]; /* diagnostic build only (-DSPT_DIAG=1): wave iterations,
                               clusters entered, tree nodes tested, s_memtime cycles in
                               cast / shading / refill, (lane, cluster) pairs that may
                               pass, live lanes of entered clusters, spheres tested per
@@ -88,7 +90,10 @@ typedef struct spt_stats {
                               lanes passing in those branches, branches that
                               improve some lane's winner, RaySphereIntersection
                               evaluations for live lanes (lane-tests), member pretests
-                              for live lanes (lane-pretests) */
+                              for live lanes (lane-pretests); then, of the primary
+                              batches (64 new paths of one 8x8 tile cast together):
+                              iterations, tree nodes tested, spheres tested, update
+                              branches taken, s_memtime cycles of their casts */
     uint64_t batches;       /* batched launches of concurrent spt_render_segment[_task] calls */
     uint64_t batched_calls; /* calls rendered in them */
     /* render service (spt_service_start); the device counters above include a session's
@@ -102,6 +107,9 @@ typedef struct spt_stats {
     uint64_t svc_flow_restarts;  /* sessions ended because a publication would have waited for
                                     an unfinished fold (ring words or counter still in use) */
     uint64_t svc_closing_restarts; /* sessions ended because a wave had raised its closing flag */
+    uint32_t prim_list_blocks;   /* 8x8 pixel blocks with a primary-ray candidate list (0: lists off) */
+    uint32_t prim_list_entries;  /* candidate slots over all blocks' lists (8x8 and 8x4) */
+    double prim_list_build_ms;   /* host time of their last build */
 } spt_stats;
 
 SPT_API int spt_abi_version(void);
@@ -161,6 +169,18 @@ SPT_API int spt_set_cluster_tree(spt_ctx *ctx, uint32_t branching);
  * member below it).  *out_nodes (nullable) = tree nodes per layout. */
 SPT_API int spt_accel_check(const float *centers4, const float *radii, uint32_t n, uint32_t cluster_k,
                             uint32_t branching, uint32_t *out_nodes);
+/* Host-only check (no device needed): the primary-ray candidate lists (DESIGN.md §4.2
+ * item 6) a context builds for this scene (default traversal shape), camera (view as
+ * spt_set_camera) and frame size.  counts[4] = {list entries, slots, blocks per row,
+ * lists on}.  blocks8 (2 * ceil(width/8) * ceil(height/8) words) and blocks4
+ * (2 * ceil(width/8) * ceil(height/4)) receive {first entry, count} per block (count
+ * 0xFFFFFFFF: the block walks the tree), slot_ids the entries and slot_orig the sphere
+ * index of every slot (0xFFFFFFFF: dummy); each nullable, the last two of capacity cap.
+ * max_count: longer lists walk (the contexts use 24, SPT_PRIM_MAX). */
+SPT_API int spt_prim_lists_check(const float *centers4, const float *radii, uint32_t n, const float view[16],
+                                 const float eye[4], uint32_t width, uint32_t height, uint32_t max_count,
+                                 uint32_t *blocks8, uint32_t *blocks4, uint32_t *slot_ids, uint32_t *slot_orig,
+                                 uint32_t cap, uint32_t *counts);
 /* Engine of the render loop (results are bit-identical either way):
  * SPT_ENGINE_MEGAKERNEL (default) -- one persistent kernel, per-lane state machines;
  * SPT_ENGINE_WAVEFRONT -- RenderSegmentTask's material-queue design

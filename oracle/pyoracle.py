@@ -67,6 +67,7 @@ def lib():
         L.spo_find_closest.argtypes = [P, P, P]; L.spo_find_closest.restype = u32
         L.spo_write_pixel.argtypes = [P, P]; L.spo_write_pixel.restype = None
         L.spo_trace_sample.argtypes = [P, P, u32, u32, u32, ctypes.c_int, P]; L.spo_trace_sample.restype = u32
+        L.spo_primary_winners.argtypes = [P, P, P, u32, P]; L.spo_primary_winners.restype = None
         for fn in (L.spo_render_segment, L.spo_render_segment_task):
             fn.argtypes = [P, P, u32, u32, u32, u32, P, P]; fn.restype = u64
         L.spo_render_image_parallel.argtypes = [P, P, u32, ctypes.c_int, P, P]
@@ -149,3 +150,11 @@ def trace_sample(scene: OracleScene, frame: Frame, x, y, s, task=False):
     out = np.zeros(4, np.float32)
     casts = lib().spo_trace_sample(scene.ref, ctypes.byref(frame), x, y, s, int(task), _p(out))
     return out, casts
+
+
+def primary_winners(scene: OracleScene, frame: Frame, xys) -> np.ndarray:
+    """Closest sphere (index; scene.n = none) of the primary ray of each (x, y, s) row."""
+    xys = np.ascontiguousarray(xys, np.uint32)
+    out = np.zeros(len(xys), np.uint32)
+    lib().spo_primary_winners(scene.ref, ctypes.byref(frame), _p(xys), len(xys), _p(out))
+    return out

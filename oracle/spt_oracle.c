@@ -388,6 +388,19 @@ static inline v4 primary_dir(const spo_frame *fr, uint64_t *st, uint32_t x, uint
     return vnorm(vmatvec(fr->view, V3(-1.f + 2.f * v, -1.f + 2.f * u, 1.f)));
 }
 
+/* The primary ray of sample s of pixel (x, y) (SingleThreadPathTracer.hpp:123-130) and its
+ * closest sphere (Collision.hpp:87-109; sc->n = none), for n (x, y, s) triples: the
+ * checker of the GPU's primary-ray candidate lists (tests/test_prim_lists.py). */
+void spo_primary_winners(const spo_scene *sc, const spo_frame *fr, const uint32_t *xys, uint32_t n, uint32_t *winner)
+{
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint32_t x = xys[3 * i], y = xys[3 * i + 1], s = xys[3 * i + 2];
+        uint64_t st = spo_sample_key(fr->seed, y * fr->width + x, s);
+        v4 d = primary_dir(fr, &st, x, y);
+        winner[i] = find_closest(sc, d, ld4(fr->eye));
+    }
+}
+
 uint32_t spo_trace_sample(const spo_scene *sc, const spo_frame *fr, uint32_t x, uint32_t y, uint32_t s,
                           int task_mode, float out[4])
 {

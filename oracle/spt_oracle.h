@@ -91,6 +91,7 @@ void spo_write_pixel(const float c[4], uint8_t out[3]);
 /* One (pixel, sample) path of RenderSegment: out[0..3] = color, returns number
  * of FindClosest calls.  task_mode: apply RenderSegmentTask's pass cap; out[3]
  * becomes 1.0 if the sample is counted, 0.0 if dropped. */
+void spo_primary_winners(const spo_scene *sc, const spo_frame *fr, const uint32_t *xys, uint32_t n, uint32_t *winner);
 uint32_t spo_trace_sample(const spo_scene *sc, const spo_frame *fr, uint32_t x, uint32_t y,
                           uint32_t s, int task_mode, float out[4]);
 /* RenderSegment over [yB,yE)x[xB,xE).  rgba: region-local float4 per pixel

@@ -44,7 +44,7 @@ class Stats(ctypes.Structure):
         ("grid_blocks", ctypes.c_uint32),
         ("block_threads", ctypes.c_uint32),
         ("render_busy_ms", ctypes.c_double),
-        ("diag", ctypes.c_uint64 * 14),
+        ("diag", ctypes.c_uint64 * 19),  # SPT_DIAG_WORDS
         ("batches", ctypes.c_uint64),
         ("batched_calls", ctypes.c_uint64),
         ("svc_sessions", ctypes.c_uint64),
@@ -55,6 +55,9 @@ class Stats(ctypes.Structure):
         ("svc_grid_blocks", ctypes.c_uint32),
         ("svc_flow_restarts", ctypes.c_uint64),
         ("svc_closing_restarts", ctypes.c_uint64),
+        ("prim_list_blocks", ctypes.c_uint32),
+        ("prim_list_entries", ctypes.c_uint32),
+        ("prim_list_build_ms", ctypes.c_double),
     ]
 
 
@@ -102,6 +105,7 @@ def lib() -> ctypes.CDLL:
         "spt_set_cluster_tree": ([P, u32], I),
         "spt_set_engine": ([P, I], I),
         "spt_accel_check": ([P, P, u32, u32, u32, P], I),
+        "spt_prim_lists_check": ([P, P, u32, P, P, u32, u32, u32, P, P, P, P, u32, P], I),
         "spt_render_segment": ([P, u32, u32, u32, u32, P, P], I),
         "spt_render_segment_task": ([P, u32, u32, u32, u32, P, P], I),
         "spt_render_rows_async": ([P, I, u32, u32, u32, u32, u32, u32, u32, P, P, P], I),

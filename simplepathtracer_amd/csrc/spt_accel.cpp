@@ -40,6 +40,7 @@
 
 #include <algorithm>
 #include <array>
+#include <chrono>
 #include <cmath>
 #include <cstring>
 #include <cstdio>
@@ -529,6 +530,183 @@ std::string validate_accel(const AccelTables &t, const float *centers4, const fl
                 if (L[i].slot != cbase + (size_t)i * t.leaf_slots) return bad("flat layout %u not in slot order", oct);
     }
     return std::string();
+}
+
+// ---- primary-ray candidate lists (PrimLists) ---------------------
+//
+// A primary ray of pixel (x, y) (start_path, SingleThreadPathTracer.hpp:123-130) leaves the
+// eye along d = normalize(M (vx, vy, 1, 0)), vx = -1 + 2 (x + U) / H, vy = -1 + 2 (y + U') / W
+// with jitters U, U' in [-1, 1) (the reference divides the row coordinate by g_width and
+// the column coordinate by g_height; the kernel follows).  Over a pixel block the exact
+// (vx, vy) fill a rectangle, so the exact directions fill the cone over a quadrilateral:
+// with `a` the direction of the rectangle's centre, every direction of the block lies
+// within theta = max over the four corners of angle(a, corner) of a (the angle from a is
+// a monotone function of the distance from a's point in the gnomonic projection onto the
+// plane normal to a, where the quadrilateral stays convex: its maximum is at a vertex).
+// The kernel's fp direction deviates from the exact one by at most delta (its rounding
+// of the rectangle coordinates is inside the rectangle's slack; the matrix product and
+// the normalisation add <= 8u |M| / |Md| + 6u, u = 2^-24).
+//
+// The member test of sphere (C, r) passes only if the computed d2 < r^2 - 1e-3 and tc >
+// 1e-3; d2 is at least p^2 - eps X^2 with p the exact distance of C from the line through
+// the eye along the computed d, X = |C - eye| and eps = 2.6e-6 (for
+// | |d| - 1 | <= 6e-7, true of a normalised primary direction), and tc > 1e-3 puts C
+// within 90 deg + 3e-7 rad of d.  So a passing member has angle(d, C - eye) < asin(R / X),
+// R = sqrt(r^2 + eps X^2), and the sphere can be dropped from the block's list when
+//     angle(a, C - eye) > theta + asin(R / X) + delta
+// (triangle inequality on the sphere of directions).  R gets 0.1% + 1e-4 and the angles
+// 1e-6 rad of extra slack; spheres with X <= R (the eye at or inside their reach),
+// non-finite values, and every block of a camera that is not finite (or whose block
+// cones exceed 0.5 rad) keep the tree walk.  The closest hit of a primary ray is then in
+// its block's list, and the list cast's (distance, original index) minimum over the list
+// is the reference's winner over all spheres.  tests/test_abi.py checks every winner of
+// 4 096 sampled primary rays per scene against the lists (oracle rays, CPU);
+// tests/test_gpu_parity.py renders with and without the lists, bit for bit.
+namespace {
+
+struct PrimCone {
+    double a[3];
+    double theta, delta;
+    bool ok;
+};
+
+constexpr double kU = 1.0 / 16777216.0;  // 2^-24
+
+double norm3(const double v[3]) { return std::sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]); }
+
+// angle between unit a and v (any length), robust near 0 and pi
+double angle_to(const double a[3], const double v[3])
+{
+    const double cx = a[1] * v[2] - a[2] * v[1], cy = a[2] * v[0] - a[0] * v[2], cz = a[0] * v[1] - a[1] * v[0];
+    const double s = std::sqrt(cx * cx + cy * cy + cz * cz), c = a[0] * v[0] + a[1] * v[1] + a[2] * v[2];
+    return std::atan2(s, c);
+}
+
+// Cone of the primary rays of pixel columns [x0, x1), rows [y0, y1).
+PrimCone prim_cone(const Camera &cam, uint32_t W, uint32_t H, uint32_t x0, uint32_t x1, uint32_t y0, uint32_t y1)
+{
+    PrimCone pc{};
+    // jittered row / column coordinates un = y + U, vn = x + U' (U in [-1, 1)), widened by
+    // their fp rounding, then u = un / W, v = vn / H (correctly rounded), vy = -1 + 2u,
+    // vx = -1 + 2v, each widened by its rounding
+    auto widen = [](double lo, double hi, double rel, double abs_) {
+        const double m = std::max(std::fabs(lo), std::fabs(hi));
+        return std::pair<double, double>(lo - m * rel - abs_, hi + m * rel + abs_);
+    };
+    auto un = widen((double)y0 - 1.0, (double)y1, 4 * kU, 1e-6);
+    auto vn = widen((double)x0 - 1.0, (double)x1, 4 * kU, 1e-6);
+    auto u = widen(un.first / (double)W, un.second / (double)W, 4 * kU, 1e-12);
+    auto v = widen(vn.first / (double)H, vn.second / (double)H, 4 * kU, 1e-12);
+    auto vy = widen(-1.0 + 2.0 * u.first, -1.0 + 2.0 * u.second, 4 * kU, 1e-7);
+    auto vx = widen(-1.0 + 2.0 * v.first, -1.0 + 2.0 * v.second, 4 * kU, 1e-7);
+    const float *m = cam.view;
+    auto dir = [&](double px, double py, double out[3], double &mag) {
+        mag = 0;
+        for (int r = 0; r < 3; ++r) {
+            const double t0 = (double)m[4 * r] * px, t1 = (double)m[4 * r + 1] * py, t2 = (double)m[4 * r + 2];
+            out[r] = t0 + t1 + t2;
+            mag += std::fabs(t0) + std::fabs(t1) + std::fabs(t2);
+        }
+    };
+    double c[3], cm;
+    dir(0.5 * (vx.first + vx.second), 0.5 * (vy.first + vy.second), c, cm);
+    const double cl = norm3(c);
+    if (!(cl > 0) || !std::isfinite(cl)) return pc;
+    for (int k = 0; k < 3; ++k) pc.a[k] = c[k] / cl;
+    double theta = 0, smax = cm, amin = 1e300;
+    for (int k = 0; k < 4; ++k) {
+        double d[3], dm;
+        dir(k & 1 ? vx.second : vx.first, k & 2 ? vy.second : vy.first, d, dm);
+        const double along = pc.a[0] * d[0] + pc.a[1] * d[1] + pc.a[2] * d[2];
+        if (!(along > 0) || !std::isfinite(along)) return pc;
+        theta = std::max(theta, angle_to(pc.a, d));
+        smax = std::max(smax, dm);
+        amin = std::min(amin, along);
+    }
+    if (!(theta < 0.5)) return pc;
+    pc.theta = theta;
+    pc.delta = 8 * kU * smax / amin + 6 * kU + 1e-6;
+    pc.ok = std::isfinite(pc.delta) && pc.delta < 1e-3;
+    return pc;
+}
+
+// Can a primary ray of cone pc pass the member test of slot s (eye e)?
+bool prim_candidate(const PrimCone &pc, const float4 &sl, const double e[3])
+{
+    if (sl.w == -INFINITY) return false;  // dummy slot: never passes
+    const double c[3] = {(double)sl.x - e[0], (double)sl.y - e[1], (double)sl.z - e[2]};
+    const double L = norm3(c), r2 = (double)sl.w;
+    if (!std::isfinite(L) || !std::isfinite(r2)) return true;
+    const double R = std::sqrt(std::max(r2 + 2.6e-6 * L * L, 0.0)) * 1.001 + 1e-4;
+    if (!(L > R * 1.01 + 1e-3)) return true;
+    const double alpha = std::asin(std::min(1.0, R / L));
+    return angle_to(pc.a, c) <= pc.theta + alpha + pc.delta + 1e-6;
+}
+
+}  // namespace
+
+PrimListTables build_prim_lists(const AccelTables &t, const Camera &cam, uint32_t W, uint32_t H, uint32_t max_count)
+{
+    const auto t_start = std::chrono::steady_clock::now();
+    PrimListTables out;
+    if (W == 0 || H == 0) return out;
+    out.bw = (W + 7) / 8;
+    const uint32_t bh8 = (H + 7) / 8, bh4 = (H + 3) / 4;
+    out.b8.assign((size_t)out.bw * bh8, make_uint2(0, kPrimWalk));
+    out.b4.assign((size_t)out.bw * bh4, make_uint2(0, kPrimWalk));
+    bool finite = true;
+    for (int i = 0; i < 12; ++i) finite = finite && std::isfinite(cam.view[i]);
+    double e[3];
+    for (int i = 0; i < 3; ++i) {
+        e[i] = cam.eye[i];
+        finite = finite && std::isfinite(cam.eye[i]) && std::fabs(cam.eye[i]) < 1e15;
+    }
+    if (!finite || t.slots.empty()) {
+        out.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count();
+        return out;
+    }
+    // a dummy slot (r*r = -inf) to pad the runs with; the tables end with pad slots
+    uint32_t pad = kPrimWalk;
+    for (size_t s = t.slots.size(); s-- > 0;)
+        if (t.slots[s].w == -INFINITY) {
+            pad = (uint32_t)s;
+            break;
+        }
+    if (pad == kPrimWalk) return out;
+    std::vector<uint32_t> all(t.slots.size());
+    std::iota(all.begin(), all.end(), 0u);
+    // super-blocks of 64 x 64 pixels first: a slot culled for a super-block's cone is
+    // culled for every block inside it (its rectangle holds theirs)
+    std::vector<uint32_t> sup, cand;
+    for (uint32_t sy = 0; sy < H; sy += 64)
+        for (uint32_t sx = 0; sx < W; sx += 64) {
+            const PrimCone sc = prim_cone(cam, W, H, sx, std::min(W, sx + 64), sy, std::min(H, sy + 64));
+            sup.clear();
+            for (uint32_t s : all)
+                if (!sc.ok || prim_candidate(sc, t.slots[s], e)) sup.push_back(s);
+            for (int level = 0; level < 2; ++level) {
+                const uint32_t bhgt = level == 0 ? 8u : 4u;
+                std::vector<uint2> &dst = level == 0 ? out.b8 : out.b4;
+                for (uint32_t y = sy; y < std::min(H, sy + 64); y += bhgt)
+                    for (uint32_t x = sx; x < std::min(W, sx + 64); x += 8) {
+                        const PrimCone pc = prim_cone(cam, W, H, x, std::min(W, x + 8), y, std::min(H, y + bhgt));
+                        if (!pc.ok) continue;  // walk
+                        cand.clear();
+                        for (uint32_t s : sup)
+                            if (prim_candidate(pc, t.slots[s], e)) cand.push_back(s);
+                        if (cand.size() > max_count) continue;  // walk
+                        // runs of whole groups of 4 (the kernel loads 4 entries at a time),
+                        // padded with a dummy slot (never passes)
+                        while (cand.size() % 4) cand.push_back(pad);
+                        dst[(size_t)(y / bhgt) * out.bw + x / 8] = make_uint2((uint32_t)out.slots.size(), (uint32_t)cand.size());
+                        out.slots.insert(out.slots.end(), cand.begin(), cand.end());
+                    }
+            }
+        }
+    if (out.slots.empty()) out.slots.assign(4, pad);  // a valid pointer for the device copy
+    out.on = true;
+    out.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count();
+    return out;
 }
 
 }  // namespace spt

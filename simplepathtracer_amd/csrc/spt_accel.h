@@ -70,4 +70,18 @@ AccelTables build_accel(const float *centers4, const float *radii, uint32_t n, u
 // exactness and in-bounds loads; empty string = valid, else the first problem.
 std::string validate_accel(const AccelTables &t, const float *centers4, const float *radii, uint32_t n);
 
+// Primary-ray candidate lists (PrimLists, spt_internal.h) of a scene's traversal tables
+// for a camera and frame size: host copies of the device arrays.  `on` is false (every
+// block walks) when the camera or the scene makes the cone test unsound (non-finite or
+// huge values, a degenerate view).  Blocks with more than max_count candidates walk.
+struct PrimListTables {
+    std::vector<uint2> b8, b4;
+    std::vector<uint32_t> slots;
+    uint32_t bw = 0;
+    bool on = false;
+    double seconds = 0;  // build time (host)
+};
+PrimListTables build_prim_lists(const AccelTables &t, const Camera &cam, uint32_t width, uint32_t height,
+                                uint32_t max_count);
+
 }  // namespace spt

@@ -52,7 +52,7 @@ struct EventPair {
 namespace {
 // caller streams (spt_render_rows_async) + the host-call slots below
 constexpr size_t kMaxCallerStreams = 4;
-constexpr size_t kCounters = 18;  // device counters: casts, samples, dropped, -, diag[14]
+constexpr size_t kCounters = 4 + SPT_DIAG_WORDS;  // device counters: casts, samples, dropped, -, diag[]
 constexpr size_t kMaxHostSlots = 8;
 constexpr uint32_t kMaxBatchSets = 8;  // batches of host calls in flight (BatchSet below)
 // + one companion stream per caller stream / host slot for double-buffered sample
@@ -213,6 +213,17 @@ struct spt_ctx {
     size_t shade_cap = 0, mat_cap = 0, slots_cap = 0, orig_cap = 0, nodes_cap = 0, kpre_cap = 0;
     spt::AccelTables tables;
     uint32_t n = 0;
+    // primary-ray candidate lists (spt_internal.h PrimLists), rebuilt by the setters once
+    // scene, camera and frame are set; SPT_PRIM_LISTS=0 turns them off, SPT_PRIM_MAX caps a
+    // block's list (longer ones walk the tree)
+    bool prim_enabled = true;
+    uint32_t prim_max = 24;
+    spt::PrimLists prim{};
+    uint2 *d_prim_b8 = nullptr, *d_prim_b4 = nullptr;
+    uint32_t *d_prim_slots = nullptr;
+    size_t prim_b8_cap = 0, prim_b4_cap = 0, prim_slots_cap = 0;
+    double prim_build_s = 0;  // host time of the last build
+    uint32_t prim_blocks = 0, prim_entries = 0;  // 8x8 blocks with a list, list entries
     // diffuse sample codes (spt_internal.h diffuse_code): the slot count, and the halvings
     // after which every finite albedo of the scene is 0 (j saturates at min(bounces - 1, jz))
     uint32_t code_stride = 1, code_jz = 0;
@@ -755,6 +766,7 @@ int svc_begin(spt_ctx *ctx, int mode, const std::vector<hipEvent_t> &waits, int6
     const uint32_t grid = std::max<uint32_t>(1u, ctx->svc_grid / v.grid_div);
     spt::RenderArgs ra{};
     ra.scene = device_scene(ctx);
+    ra.prim = ctx->prim;
     ra.cam = ctx->cam;
     ra.width = ctx->W;
     ra.height = ctx->H;
@@ -1058,6 +1070,7 @@ int render_impl(spt_ctx *ctx, int mode, const spt::RowMap &map, float4 *d_rgba, 
 
     spt::RenderArgs ra{};
     ra.scene = device_scene(ctx);
+    ra.prim = ctx->prim;
     ra.cam = ctx->cam;
     ra.width = ctx->W;
     ra.height = ctx->H;
@@ -1255,6 +1268,29 @@ int rebuild_accel(spt_ctx *ctx)
     return SPT_OK;
 }
 
+// Build and upload the primary-ray candidate lists for the current scene, camera and frame
+// size (none for trees walked lane by lane, which have no primary batches).
+int rebuild_prim(spt_ctx *ctx)
+{
+    ctx->prim = spt::PrimLists{};
+    ctx->prim_blocks = ctx->prim_entries = 0;
+    if (!ctx->prim_enabled || !ctx->scene_set || !ctx->cam_set || !ctx->params_set || spt::lane_walk_tree(ctx->accel))
+        return SPT_OK;
+    spt::PrimListTables pl = spt::build_prim_lists(ctx->tables, ctx->cam, ctx->W, ctx->H, ctx->prim_max);
+    ctx->prim_build_s = pl.seconds;
+    if (!pl.on) return SPT_OK;
+    // every stream: renders in flight may still read the previous lists
+    HIP_TRY(ctx, hipDeviceSynchronize());
+    int rc = upload(ctx, &ctx->d_prim_b8, &ctx->prim_b8_cap, pl.b8);
+    if (!rc) rc = upload(ctx, &ctx->d_prim_b4, &ctx->prim_b4_cap, pl.b4);
+    if (!rc) rc = upload(ctx, &ctx->d_prim_slots, &ctx->prim_slots_cap, pl.slots);
+    if (rc) return rc;
+    ctx->prim = spt::PrimLists{ctx->d_prim_b8, ctx->d_prim_b4, ctx->d_prim_slots, pl.bw, 1u};
+    for (const uint2 &b : pl.b8) ctx->prim_blocks += b.y != spt::kPrimWalk ? 1u : 0u;
+    ctx->prim_entries = (uint32_t)pl.slots.size();
+    return SPT_OK;
+}
+
 int check_region(spt_ctx *ctx, uint32_t yB, uint32_t yE, uint32_t xB, uint32_t xE)
 {
     if (yE > ctx->H || xE > ctx->W)
@@ -1416,6 +1452,7 @@ int launch_batch(spt_ctx *ctx, BatchSet *bs, const std::vector<BatchReq *> &batc
 
     spt::RenderArgs ra{};
     ra.scene = device_scene(ctx);
+    ra.prim = ctx->prim;
     ra.cam = ctx->cam;
     ra.width = W;
     ra.height = H;
@@ -1887,7 +1924,7 @@ int spt_set_scene_one(spt_ctx *ctx, const float *centers4, const float *radii, c
     int rc = rebuild_accel(ctx);
     if (rc) return rc;
     ctx->scene_set = true;
-    return SPT_OK;
+    return rebuild_prim(ctx);
 }
 
 int spt_set_camera_one(spt_ctx *ctx, const float view[16], const float eye[4], const float sky[4])
@@ -1906,7 +1943,8 @@ int spt_set_camera_one(spt_ctx *ctx, const float view[16], const float eye[4], c
         ctx->cam.sky[j] = sky[j];
     }
     ctx->cam_set = true;
-    return SPT_OK;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    return rebuild_prim(ctx);
 }
 
 int spt_set_params_one(spt_ctx *ctx, uint32_t width, uint32_t height, uint32_t spp, uint32_t bounces, uint64_t seed)
@@ -1926,7 +1964,8 @@ int spt_set_params_one(spt_ctx *ctx, uint32_t width, uint32_t height, uint32_t s
     ctx->bounces = bounces;
     ctx->seed = seed;
     ctx->params_set = true;
-    return SPT_OK;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    return rebuild_prim(ctx);
 }
 
 int spt_set_cluster_size_one(spt_ctx *ctx, uint32_t k)
@@ -1940,7 +1979,8 @@ int spt_set_cluster_size_one(spt_ctx *ctx, uint32_t k)
     ctx->cluster_k = k;
     if (!ctx->scene_set) return SPT_OK;
     HIP_TRY(ctx, hipSetDevice(ctx->device));
-    return rebuild_accel(ctx);
+    int rc = rebuild_accel(ctx);
+    return rc ? rc : rebuild_prim(ctx);
 }
 
 int spt_set_cluster_tree_one(spt_ctx *ctx, uint32_t branching)
@@ -1954,7 +1994,8 @@ int spt_set_cluster_tree_one(spt_ctx *ctx, uint32_t branching)
     ctx->tree_branching = branching;
     if (!ctx->scene_set) return SPT_OK;
     HIP_TRY(ctx, hipSetDevice(ctx->device));
-    return rebuild_accel(ctx);
+    int rc = rebuild_accel(ctx);
+    return rc ? rc : rebuild_prim(ctx);
 }
 
 int spt_set_engine_one(spt_ctx *ctx, int engine)
@@ -2054,6 +2095,8 @@ int spt_ctx_create(int device, spt_ctx **out)
     // a fraction of the session grid (rehearsing several ranks' sessions on one GPU), the
     // bound on waiting for a session to end, and the publish-delay fault injection of the
     // liveness tests (tests/test_gpu_service.py)
+    if (const char *e = env_var("SPT_PRIM_LISTS")) ctx->prim_enabled = std::atoi(e) != 0;
+    if (const char *e = env_var("SPT_PRIM_MAX")) ctx->prim_max = (uint32_t)std::max(0, std::atoi(e));
     if (const char *e = env_var("SPT_SVC_GRID_DIV")) ctx->svc.grid_div = (uint32_t)std::max(1, std::atoi(e));
     if (const char *e = env_var("SPT_SVC_TIMEOUT_MS")) ctx->svc.timeout_ms = std::max(1.0, std::atof(e));
     if (const char *e = env_var("SPT_SVC_DEBUG")) ctx->svc.debug = std::atoi(e) != 0;
@@ -2136,7 +2179,8 @@ void spt_ctx_destroy(spt_ctx *ctx)
         if (p.owner) (void)hipHostUnregister(p.ptr);
     if (ctx->ref_ev) (void)hipEventDestroy(ctx->ref_ev);
     void *bufs[] = {ctx->d_shade, ctx->d_mat, ctx->d_slots, ctx->d_orig, ctx->d_nodes,
-                    ctx->d_kpre, ctx->d_counters, ctx->d_frame8};
+                    ctx->d_kpre, ctx->d_counters, ctx->d_frame8, ctx->d_prim_b8, ctx->d_prim_b4,
+                    ctx->d_prim_slots};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     for (Workspace &w : ctx->ws) {
@@ -2232,6 +2276,39 @@ int spt_accel_check(const float *centers4, const float *radii, uint32_t n, uint3
     const std::string bad = spt::validate_accel(t, centers4, radii, n);
     if (!bad.empty()) return fail(nullptr, SPT_ERR_STATE, "traversal tables invalid: %s", bad.c_str());
     if (out_nodes) *out_nodes = t.n_nodes;
+    return SPT_OK;
+}
+
+int spt_prim_lists_check(const float *centers4, const float *radii, uint32_t n, const float view[16], const float eye[4],
+                         uint32_t width, uint32_t height, uint32_t max_count, uint32_t *blocks8, uint32_t *blocks4,
+                         uint32_t *slot_ids, uint32_t *slot_orig, uint32_t cap, uint32_t *counts)
+{
+    if (n > 0 && (!centers4 || !radii)) return fail(nullptr, SPT_ERR_ARG, "null scene array");
+    if (!view || !eye || !counts || width == 0 || height == 0) return fail(nullptr, SPT_ERR_ARG, "bad arguments");
+    // the default traversal shape (resolve_shape with both settings on auto)
+    const uint32_t branching = n > 512 ? 3u : 4u;
+    const spt::AccelTables t =
+        spt::build_accel(centers4, radii, n, spt::kClusterSlots, spt::render_group_size(), branching, spt::kClusterSlots);
+    spt::Camera cam{};
+    for (int j = 0; j < 12; ++j) cam.view[j] = view[j];
+    for (int j = 0; j < 3; ++j) cam.eye[j] = eye[j];
+    const spt::PrimListTables pl = spt::build_prim_lists(t, cam, width, height, max_count);
+    counts[0] = (uint32_t)pl.slots.size();
+    counts[1] = (uint32_t)t.slots.size();
+    counts[2] = pl.bw;
+    counts[3] = pl.on ? 1u : 0u;
+    if ((slot_ids && cap < pl.slots.size()) || (slot_orig && cap < t.slots.size()))
+        return fail(nullptr, SPT_ERR_ARG, "capacity %u < %zu list entries / %zu slots", cap, pl.slots.size(), t.slots.size());
+    for (size_t i = 0; blocks8 && i < pl.b8.size(); ++i) {
+        blocks8[2 * i] = pl.b8[i].x;
+        blocks8[2 * i + 1] = pl.b8[i].y;
+    }
+    for (size_t i = 0; blocks4 && i < pl.b4.size(); ++i) {
+        blocks4[2 * i] = pl.b4[i].x;
+        blocks4[2 * i + 1] = pl.b4[i].y;
+    }
+    if (slot_ids) std::copy(pl.slots.begin(), pl.slots.end(), slot_ids);
+    if (slot_orig) std::copy(t.orig.begin(), t.orig.end(), slot_orig);
     return SPT_OK;
 }
 
@@ -2594,7 +2671,7 @@ int stats_one(spt_ctx *ctx, spt_stats *out)
     out->casts = c[0];
     out->samples = c[1];
     out->dropped = c[2];
-    for (int i = 0; i < 14; ++i) out->diag[i] = c[4 + i];
+    for (int i = 0; i < SPT_DIAG_WORDS; ++i) out->diag[i] = c[4 + i];
     out->launches = ctx->launches;
     out->render_ms = ctx->render_ms;
     out->fold_ms = ctx->fold_ms;
@@ -2612,6 +2689,9 @@ int stats_one(spt_ctx *ctx, spt_stats *out)
     out->svc_grid_blocks = std::max<uint32_t>(1u, ctx->svc_grid / ctx->svc.grid_div);
     out->svc_flow_restarts = ctx->svc.flow_restarts;
     out->svc_closing_restarts = ctx->svc.closing_restarts;
+    out->prim_list_blocks = ctx->prim_blocks;
+    out->prim_list_entries = ctx->prim_entries;
+    out->prim_list_build_ms = ctx->prim_build_s * 1e3;
     return SPT_OK;
 }
 
@@ -2647,7 +2727,7 @@ int spt_get_stats(spt_ctx *ctx, spt_stats *out)
         out->casts += q.casts;
         out->samples += q.samples;
         out->dropped += q.dropped;
-        for (int i = 0; i < 14; ++i) out->diag[i] += q.diag[i];
+        for (int i = 0; i < SPT_DIAG_WORDS; ++i) out->diag[i] += q.diag[i];
         out->launches += q.launches;
         out->batches += q.batches;
         out->batched_calls += q.batched_calls;

@@ -244,6 +244,21 @@ struct AccelView {
     float pre_cm;         // >= max |C| + r over the cluster members
 };
 
+// Primary-ray candidate lists (round 5): for every 8x8 and 8x4
+// pixel block of the frame, the slots a primary ray of the block -- from the eye, through
+// any pixel of the block with any jitter -- can pass RaySphereIntersection for (a
+// conservative cone test with the member test's fp reach, spt_accel.cpp
+// build_prim_lists).  The closest hit of such a ray is in its block's list, so a
+// primary batch (64 rays of one 8x8 tile) tests that list instead of walking the tree,
+// with the same (distance, original index) winner.
+struct PrimLists {
+    const uint2 *b8, *b4;       // {first entry, count} per block, row-major; count kPrimWalk: walk
+    const uint32_t *slots;      // candidate slots (each block's run ascending)
+    uint32_t bw;                // blocks per row: ceil(width / 8)
+    uint32_t on;                // lists built for this scene, camera and frame size
+};
+constexpr uint32_t kPrimWalk = 0xFFFFFFFFu;
+
 struct DeviceScene {
     const float4 *shade;    // {red, green, blue, fuzz} per slot (hit geometry: accel.slots)
     const uint32_t *mat;    // material id per slot
@@ -321,6 +336,8 @@ struct RenderArgs {
     uint32_t *svc_host;
     const struct SvcJob *svc_host_jobs;
     const uint32_t *svc_host_job_claim;
+    // primary-ray candidate lists (PrimLists; on = 0: every primary batch walks the tree)
+    PrimLists prim;
 };
 
 // claim counters: at most one per XCD, 256 bytes apart (separate cache lines)

@@ -378,6 +378,8 @@ __device__ __forceinline__ void render_body(const RenderArgs &a)
     unsigned long long casts = 0, done = 0, dropped = 0;
     struct {
         unsigned long long iters = 0, cast = 0, shade = 0, refill = 0;  // SPT_DIAG counts and s_memtime split
+        // the primary batches' share: iterations, nodes, spheres, update branches, cast cycles
+        unsigned long long p_iters = 0, p_nodes = 0, p_spheres = 0, p_branches = 0, p_cast = 0;
     } dc;
     CastDiag dg;
     // resumable lane walk (SPT_LANE_BUDGET): the cast state of lanes whose walk ran
@@ -494,6 +496,7 @@ __device__ __forceinline__ void render_body(const RenderArgs &a)
         unsigned long long need = __ballot(ps.phase == PH_IDLE);
         if (__popcll(need) < (PRIM ? SPT_PRIM_REFILL_MIN : SPT_REFILL_MIN) && need != ~0ull) need = 0ull;
         bool prim_iter = false;  // PRIM: this iteration runs a primary batch
+        uint32_t pxy = 0;        // PRIM: the lane's pixel in the batch (y << 16 | x)
         if (PRIM) {
             if (need != 0ull) {
                 const uint32_t cnt = (uint32_t)__popcll(need);
@@ -519,7 +522,7 @@ __device__ __forceinline__ void render_body(const RenderArgs &a)
                         const uint32_t n = min(64u, blk_end - blk_cur);
                         const uint32_t mine = blk_cur + lane;
                         blk_cur += n;
-                        if (lane < n) start_path_svc(mine, rec, ps);
+                        if (lane < n) start_path_svc(mine, rec, ps, &pxy);
                     } else if (BATCH) {
                         // claims are multiples of 64 items and never span two rectangles:
                         // a batch is 64 items of one claim (fewer at the launch's end)
@@ -528,11 +531,11 @@ __device__ __forceinline__ void render_body(const RenderArgs &a)
                             const uint32_t n = min(64u, blk_end - blk_cur);
                             const uint32_t mine = blk_cur + lane;
                             blk_cur += n;
-                            if (lane < n) start_path_rect(mine, rect, ps);
+                            if (lane < n) start_path_rect(mine, rect, ps, &pxy);
                         }
                     } else {
                         const uint32_t mine = take_items(~0ull);
-                        if (mine != 0xFFFFFFFFu) start_path_kernarg(mine, rows, ps);
+                        if (mine != 0xFFFFFFFFu) start_path_kernarg(mine, rows, ps, &pxy);
                     }
                     prim_iter = true;
                 }
@@ -635,6 +638,9 @@ __device__ __forceinline__ void render_body(const RenderArgs &a)
             continue;
         }
         SPT_STAMP(dc.refill);
+#if SPT_DIAG
+        const unsigned long long d_n0 = dg.nodes, d_s0 = dg.spheres, d_b0 = dg.branches, d_c0 = dc.cast;
+#endif
         // the lane walks are resumable: a lane still walking after SPT_LANE_BUDGET walk
         // iterations and leaf passes keeps its cast state (winner, node, parked leaves)
         // and continues it next iteration while the other lanes shade and refill, so a
@@ -653,6 +659,13 @@ __device__ __forceinline__ void render_body(const RenderArgs &a)
                                     (uint32_t)SPT_LANE_BUDGET, hres, li, lleaf, lleaf2);
             h = hres;
             casts += (unsigned long long)__popcll(__ballot(act && cdone));
+        } else if constexpr (PRIM) {
+            // a primary batch casts against its block's candidate list when there is one
+            // (prim_list_cast); every other cast walks the tree
+            bool listed = false;
+            if (prim_iter && kernarg_args()->prim.on)
+                listed = prim_list_cast(a.scene.accel, ps.o, ps.d, act, pxy, h, dg);
+            if (!listed) h = find_closest<TREE, LEAF, LDSN>(a.scene.accel, ps.o, ps.d, act, dg, (const uint32_t *)s_nodes);
         } else {
             h = (LDSN && SPT_LANE_WALK)
                     ? find_closest_lane<LEAF>(a.scene.accel, ps.o, ps.d, act, dg, (const uint32_t *)s_nodes)
@@ -661,6 +674,15 @@ __device__ __forceinline__ void render_body(const RenderArgs &a)
                     : find_closest<TREE, LEAF, LDSN>(a.scene.accel, ps.o, ps.d, act, dg, (const uint32_t *)s_nodes);
         }
         SPT_STAMP(dc.cast);
+#if SPT_DIAG
+        if (prim_iter) {
+            dc.p_iters += 1;
+            dc.p_nodes += dg.nodes - d_n0;
+            dc.p_spheres += dg.spheres - d_s0;
+            dc.p_branches += dg.branches - d_b0;
+            dc.p_cast += dc.cast - d_c0;
+        }
+#endif
         shade_step<true, SVC && SPT_SVC_WT>(a, ps, h, act && cdone, done, dropped, s_lds + (threadIdx.x & ~63u));
         fresh = cdone;
         if (SVC) {
@@ -730,6 +752,11 @@ __device__ __forceinline__ void render_body(const RenderArgs &a)
         atomicAdd(&a.counters[15], dg.improving);
         atomicAdd(&a.counters[16], dg.lane_tests);
         atomicAdd(&a.counters[17], dg.lane_pretests);
+        atomicAdd(&a.counters[18], dc.p_iters);
+        atomicAdd(&a.counters[19], dc.p_nodes);
+        atomicAdd(&a.counters[20], dc.p_spheres);
+        atomicAdd(&a.counters[21], dc.p_branches);
+        atomicAdd(&a.counters[22], dc.p_cast);
     }
 #endif
 #undef SPT_STAMP

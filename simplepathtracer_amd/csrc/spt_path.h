@@ -793,6 +793,79 @@ __device__ __forceinline__ kargs_t *kernarg_args()
     return (kargs_t *)((kchar *)__builtin_amdgcn_kernarg_segment_ptr() + z);
 }
 
+// FindClosestIntersectionSphere for a primary batch from its block's candidate list
+// (PrimLists, spt_internal.h): every lane's closest hit is in the
+// list of its pixel's block, so the (distance, original index) minimum over the list --
+// the winner update_member keeps, independent of the order members are tested in -- is
+// the reference's.  pxy: the lane's pixel (y << 16 | x).  The lanes' common 8x8 block's
+// list, or when they span several blocks (ragged edge tiles, interleaved rank strips)
+// the union of their 8x4 blocks' lists (a member tested twice cannot replace itself).
+// Returns false, with h undefined, when the wave must walk the tree instead: a block
+// without a list, or a lane that may not cull (direction off unit length, |o| > 1e15).
+__device__ __forceinline__ bool prim_list_cast(const AccelView &ac, const f3 &o, const f3 &d, bool active, uint32_t pxy,
+                                               Hit &h, CastDiag &dg)
+{
+    kargs_t &k = *kernarg_args();
+    const float ddev = lensq(d) - 1.0f;
+    if (__ballot(active && !(ddev <= 1e-6f && ddev >= -1e-6f && lensq(o) <= 1e30f)) != 0ull) return false;
+    h.idx = kMiss;
+    h.best = FLT_MAX;
+    h.t = 0.f;
+    const unsigned long long live = __ballot(active);
+    if (live == 0ull) return true;
+    const uint32_t bw = k.prim.bw;
+    const uint32_t x = pxy & 0xFFFFu, y = pxy >> 16;
+    const float dod = dot(o, d);
+    cfloat *slots = (cfloat *)ac.slots;
+    cuint *ids = (cuint *)k.prim.slots;
+    if (SPT_DIAG) dg.live_now = (uint32_t)__popcll(live);
+    // one run of candidate slots, 4 at a time (runs are padded with a dummy slot)
+    auto test_run = [&](uint2 e) {
+        for (uint32_t i = e.x; i < e.x + e.y; i += 4u) {
+            uint32_t s[4];
+            float4 sp[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) s[q] = ids[i + q];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) sp[q] = ld_uniform(slots, s[q]);
+            float tcv[4], hv[4];
+            bool pass[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) pass[q] = ray_sphere(sp[q], o, d, tcv[q], hv[q]);
+            if (SPT_DIAG) dg.lane_tests += 4ull * dg.live_now;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const unsigned long long pm = __ballot(pass[q]);
+                if (SPT_DIAG) {
+                    dg.spheres += 1;
+                    dg.branches += pm != 0ull ? 1 : 0;
+                }
+                if (pm != 0ull) update_member(pm, tcv[q], hv[q], ac.orig, s[q], o, d, dod, h, dg);
+            }
+        }
+    };
+    const uint32_t b8 = (y >> 3) * bw + (x >> 3);
+    const uint32_t lead = __builtin_amdgcn_readlane(b8, (int)__builtin_ctzll(live));
+    if (__ballot(active && b8 != lead) == 0ull) {
+        cuint *blk = (cuint *)k.prim.b8 + 2u * lead;
+        const uint2 e = make_uint2(blk[0], blk[1]);
+        if (e.y == kPrimWalk) return false;
+        test_run(e);
+        return true;
+    }
+    const uint32_t b4 = (y >> 2) * bw + (x >> 3);
+    unsigned long long todo = live;
+    while (todo != 0ull) {
+        const uint32_t b = __builtin_amdgcn_readlane(b4, (int)__builtin_ctzll(todo));
+        cuint *blk = (cuint *)k.prim.b4 + 2u * b;
+        const uint2 e = make_uint2(blk[0], blk[1]);
+        if (e.y == kPrimWalk) return false;
+        test_run(e);
+        todo &= ~__ballot(active && b4 == b);
+    }
+    return true;
+}
+
 // SampleColorRefractive (SingleThreadPathTracer.hpp:48-92) for a lane whose ray hit
 // the glass slot idx at the contact point ps.o: new ps.o (exit point) and ps.d.
 __device__ __forceinline__ void refract_event(const float4 *__restrict__ slots, Path &ps, uint32_t idx)
@@ -989,7 +1062,7 @@ __device__ __forceinline__ void shade_step(const RenderArgs &a, Path &ps, const 
 // of g_width, g_height (div_core); `rows` = rows of the region.
 
 __device__ __forceinline__ void start_path(const RenderArgs &a, uint32_t mine, uint32_t rows, const Recip &rw,
-                                           const Recip &rh, const f3 &eye, Path &ps)
+                                           const Recip &rh, const f3 &eye, Path &ps, uint32_t *pxy = nullptr)
 {
     // primary ray, SingleThreadPathTracer.hpp:123-130.  A claim of
     // consecutive items stays inside one 8x8 tile (ts_item).
@@ -999,6 +1072,7 @@ __device__ __forceinline__ void start_path(const RenderArgs &a, uint32_t mine, u
     ps.item = mine;  // slots in item order (ts_slot_base)
     const uint32_t x = a.map.x0 + cx;
     const uint32_t y = a.map.parts == 1u ? a.map.y0 + lr : row_of_fast(a.map, lr, a.div_strip);
+    if (pxy) *pxy = (y << 16) | x;  // the primary batch's candidate-list lookup (prim_list_cast)
     ps.st = fmix64(a.seed_key ^ (((uint64_t)(y * a.width + x) << 32) | (uint64_t)s));
     const float un = (float)y + uniform(ps.st, -1.f, 1.f);
     const float vn = (float)x + uniform(ps.st, -1.f, 1.f);
@@ -1020,7 +1094,7 @@ __device__ __forceinline__ void start_path(const RenderArgs &a, uint32_t mine, u
 
 // start_path with the refill parameters copied out of the kernarg segment at the
 // point of use (scalar loads); render_kernel only.
-__device__ __forceinline__ void start_path_kernarg(uint32_t mine, uint32_t rows, Path &ps)
+__device__ __forceinline__ void start_path_kernarg(uint32_t mine, uint32_t rows, Path &ps, uint32_t *pxy = nullptr)
 {
     kargs_t &k = *kernarg_args();
     RenderArgs a;
@@ -1039,7 +1113,7 @@ __device__ __forceinline__ void start_path_kernarg(uint32_t mine, uint32_t rows,
 #pragma unroll
     for (int q = 0; q < 12; ++q) a.cam.view[q] = k.cam.view[q];
     start_path(a, mine, rows, recip((float)a.width), recip((float)a.height),
-               mk(k.cam.eye[0], k.cam.eye[1], k.cam.eye[2]), ps);
+               mk(k.cam.eye[0], k.cam.eye[1], k.cam.eye[2]), ps, pxy);
 }
 
 // Batched launches (RenderArgs::rects): the rectangle holding item `nb` (the first
@@ -1061,7 +1135,7 @@ __device__ __forceinline__ uint32_t find_rect(uint32_t nb)
 // start_path for item `mine` of a batched launch, in rectangle `ri` (wave-uniform):
 // the rectangle's own region, item order and slot range.  Items past its item_end
 // (claim padding) start nothing: the lane stays idle.
-__device__ __forceinline__ void start_path_rect(uint32_t mine, uint32_t ri, Path &ps)
+__device__ __forceinline__ void start_path_rect(uint32_t mine, uint32_t ri, Path &ps, uint32_t *pxy = nullptr)
 {
     kargs_t &k = *kernarg_args();
     crect_t &r = (k.inline_rects ? (crect_t *)k.rects_inline : (crect_t *)k.rects)[ri];
@@ -1081,14 +1155,14 @@ __device__ __forceinline__ void start_path_rect(uint32_t mine, uint32_t ri, Path
 #pragma unroll
     for (int q = 0; q < 12; ++q) a.cam.view[q] = k.cam.view[q];
     start_path(a, mine - r.item_off, r.rows, recip((float)a.width), recip((float)a.height),
-               mk(k.cam.eye[0], k.cam.eye[1], k.cam.eye[2]), ps);
+               mk(k.cam.eye[0], k.cam.eye[1], k.cam.eye[2]), ps, pxy);
     ps.item += r.slot_off;
 }
 
 // start_path for session item `mine` of the render service: the job's fields from the
 // wave's LDS copy of its record (SvcJob words, wave-uniform), the session's constants
 // from the kernel arguments.  Items past the job's item_end (claim padding) start nothing.
-__device__ __forceinline__ void start_path_svc(uint32_t mine, const uint32_t *rec, Path &ps)
+__device__ __forceinline__ void start_path_svc(uint32_t mine, const uint32_t *rec, Path &ps, uint32_t *pxy = nullptr)
 {
     auto f = [&](int i) -> uint32_t { return (uint32_t)__builtin_amdgcn_readfirstlane(rec[i]); };
     if (mine >= f(1)) return;
@@ -1107,7 +1181,7 @@ __device__ __forceinline__ void start_path_svc(uint32_t mine, const uint32_t *re
 #pragma unroll
     for (int q = 0; q < 12; ++q) a.cam.view[q] = k.cam.view[q];
     start_path(a, mine - f(0), f(4), recip((float)a.width), recip((float)a.height),
-               mk(k.cam.eye[0], k.cam.eye[1], k.cam.eye[2]), ps);
+               mk(k.cam.eye[0], k.cam.eye[1], k.cam.eye[2]), ps, pxy);
     ps.item += f(2);
     ps.job = f(3);
 }

@@ -1173,3 +1173,65 @@ def test_small_launches_on_two_streams_render_the_same(spt, ctx, golden_scenes):
     ctx.assemble_rows_async(two.data_ptr(), mr, 0, 800, strip, parts, 0, 1200, frame.data_ptr(), 0)
     ctx.synchronize()
     assert torch.equal(frame.view(torch.int32), full.view(torch.int32))
+
+
+def _render_variants(spt, golden_scenes, view, eye, W, H, spp):
+    """Outputs of one context for the list tests: full frame (segment, task), a rank share
+    of interleaved 4-row strips, a batched drop-in tile, two service jobs; and ray counts."""
+    import torch
+    c = spt.Context(0)
+    c.set_scene(scene_from(spt, golden_scenes, "random"))
+    c.set_camera(view, eye, SKY)
+    c.set_params(W, H, spp, 50, 4)
+    out, casts = {}, []
+    for name, (mode, strip, parts, part) in {"seg": (0, 1, 1, 0), "task": (1, 1, 1, 0), "share": (0, 4, 8, 3)}.items():
+        n = spt.rows_count(0, H, strip, parts, part) * W
+        rgba = torch.zeros((n, 4), dtype=torch.float32, device="cuda")
+        g8 = torch.zeros(W * H * 3, dtype=torch.uint8, device="cuda")
+        c.reset_stats()
+        c.render_rows_async(mode, 0, H, strip, parts, part, 0, W, rgba.data_ptr(), g8.data_ptr() if parts == 1 else 0)
+        c.synchronize()
+        out[name] = (rgba.cpu().numpy(), g8.cpu().numpy())
+        casts.append(c.stats()["casts"])
+    g = np.zeros(W * H * 3, np.uint8)
+    c.reset_stats()
+    out["tile"] = (c.render_segment(H // 3, H // 3 + 37, W // 5, W // 5 + 61, g_data=g), g)
+    casts.append(c.stats()["casts"])
+    c.service_start()
+    jobs = []
+    for k in range(2):
+        rgba = torch.zeros((W * H, 4), dtype=torch.float32, device="cuda")
+        torch.cuda.synchronize()
+        c.render_rows_async(0, 0, H, 1, 1, 0, 0, W, rgba.data_ptr(), 0)
+        jobs.append(rgba)
+    c.service_stop()
+    c.synchronize()
+    out["svc"] = (jobs[0].cpu().numpy(), jobs[1].cpu().numpy())
+    st = c.stats()
+    c.close()
+    return out, casts, st
+
+
+@pytest.mark.parametrize("case", ["default", "closeup", "low", "inside", "ragged"])
+def test_primary_lists_equal_tree_walk(spt, golden_scenes, monkeypatch, case):
+    """Primary batches cast against their block's candidate list (DESIGN.md §4.2 item 6,
+    spt_path.h prim_list_cast): frames, ray counts and g_data bytes equal the tree walk's
+    (SPT_PRIM_LISTS=0) -- full frames in both modes, a rank share of 4-row strips (its
+    8x8 tiles span two 8x4 blocks: union of lists), a batched drop-in tile and service
+    jobs -- for the default camera, a close-up of a big ball, a low view among the small
+    spheres, an eye inside the glass ball, and a ragged 203 x 117 frame."""
+    cams = {"default": (EYE, LOOK), "closeup": ([4.0, 1.0, 3.0, 0.0], [4.0, 1.0, 0.0, 0.0]),
+            "low": ([0.3, 0.25, 0.4, 0.0], [3.0, 0.2, 2.0, 0.0]), "inside": ([0.0, 1.0, 0.0, 0.0], [1.0, 1.0, 0.0, 0.0]),
+            "ragged": (EYE, LOOK)}
+    eye, look = cams[case]
+    W, H = (203, 117) if case == "ragged" else (320, 200)
+    view = spt.camera_basis(eye, look, UP)
+    got, casts, st = _render_variants(spt, golden_scenes, view, eye, W, H, 8)
+    assert st["prim_list_blocks"] > 0
+    monkeypatch.setenv("SPT_PRIM_LISTS", "0")
+    want, casts0, st0 = _render_variants(spt, golden_scenes, view, eye, W, H, 8)
+    assert st0["prim_list_blocks"] == 0
+    for k in want:
+        assert_bitwise(got[k][0], want[k][0], f"{case} {k}")
+        assert np.array_equal(got[k][1], want[k][1]), f"{case} {k}: second output differs"
+    assert casts == casts0

@@ -42,6 +42,12 @@ print(f"per wave cast: spheres tested={sph/max(it,1):.2f} update branches taken=
 lt, lp = st["diag"][12:14]
 print(f"lane-level RaySphereIntersection evaluations per ray={lt/max(st['casts'],1):.2f} "
       f"member pretests per ray={lp/max(st['casts'],1):.2f} (brute force: {scene.n})")
+pi, pn, ps_, pb, pc = st["diag"][14:19]
+if pi:
+    print(f"primary batches: {pi} of {it} wave iterations ({pi/max(it,1):.3f}); per primary cast: nodes={pn/pi:.2f} "
+          f"spheres={ps_/pi:.2f} update branches={pb/pi:.2f}; per other cast: nodes={(nodes-pn)/max(it-pi,1):.2f} "
+          f"spheres={(sph-ps_)/max(it-pi,1):.2f} update branches={(br-pb)/max(it-pi,1):.2f}; "
+          f"primary casts' share of cast cycles {pc/max(cc,1):.3f}")
 print(f"render_ms={st['render_ms']:.3f}")
 print("raw diag", list(st["diag"]))
 # the LDS kernel (1024-thread blocks) walks lane by lane (spt_path.h find_closest_lane):
@@ -57,6 +63,10 @@ if json_out:
                "samples": st["samples"], "lane_tests_per_ray": lt / max(st["casts"], 1),
                "lane_pretests_per_ray": lp / max(st["casts"], 1), "clusters_entered_per_wave_cast": leaves / max(it, 1),
                "tree_nodes_per_wave_cast": nodes / max(it, 1), "live_lanes_per_iter": st["casts"] / max(it, 1),
+               "wave_iters": it, "spheres_per_wave_cast": sph / max(it, 1), "update_branches_per_wave_cast": br / max(it, 1),
+               "cycle_split": {"cast": cc / tot, "shade": cs / tot, "refill": cr / tot},
+               "primary": {"iters": pi, "nodes_per_cast": pn / max(pi, 1), "spheres_per_cast": ps_ / max(pi, 1),
+                           "update_branches_per_cast": pb / max(pi, 1), "cast_cycle_share": pc / max(cc, 1)},
                "build": "SPT_DIAG=1 (libspt_hip_diag.so), counters only, never timed",
                **({"walk": "lane", "lane_node_visits_per_ray": nodes / max(st["casts"], 1),
                    "walk_iters_per_wave_cast": live / max(it, 1), "leaf_passes_per_wave_cast": leaves / max(it, 1),

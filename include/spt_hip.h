@@ -66,7 +66,7 @@ enum {
 
 typedef struct spt_ctx spt_ctx;
 
-#define SPT_DIAG_WORDS 19
+#define SPT_DIAG_WORDS 21
 
 typedef struct spt_stats {
     uint64_t samples;      /* (pixel, sample) paths completed */
@@ -93,7 +93,9 @@ typedef struct spt_stats {
                               for live lanes (lane-pretests); then, of the primary
                               batches (64 new paths of one 8x8 tile cast together):
                               iterations, tree nodes tested, spheres tested, update
-                              branches taken, s_memtime cycles of their casts */
+                              branches taken, s_memtime cycles of their casts; the
+                              cube-minus-ball sampler's calls and its cooperative rounds
+                              after round 0 */
     uint64_t batches;       /* batched launches of concurrent spt_render_segment[_task] calls */
     uint64_t batched_calls; /* calls rendered in them */
     /* render service (spt_service_start); the device counters above include a session's

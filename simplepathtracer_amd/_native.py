@@ -44,7 +44,7 @@ class Stats(ctypes.Structure):
         ("grid_blocks", ctypes.c_uint32),
         ("block_threads", ctypes.c_uint32),
         ("render_busy_ms", ctypes.c_double),
-        ("diag", ctypes.c_uint64 * 19),  # SPT_DIAG_WORDS
+        ("diag", ctypes.c_uint64 * 21),  # SPT_DIAG_WORDS
         ("batches", ctypes.c_uint64),
         ("batched_calls", ctypes.c_uint64),
         ("svc_sessions", ctypes.c_uint64),

@@ -380,6 +380,7 @@ __device__ __forceinline__ void render_body(const RenderArgs &a)
         unsigned long long iters = 0, cast = 0, shade = 0, refill = 0;  // SPT_DIAG counts and s_memtime split
         // the primary batches' share: iterations, nodes, spheres, update branches, cast cycles
         unsigned long long p_iters = 0, p_nodes = 0, p_spheres = 0, p_branches = 0, p_cast = 0;
+        unsigned long long s_rounds[2] = {0, 0};  // sampler calls, cooperative rounds after round 0
     } dc;
     CastDiag dg;
     // resumable lane walk (SPT_LANE_BUDGET): the cast state of lanes whose walk ran
@@ -683,7 +684,8 @@ __device__ __forceinline__ void render_body(const RenderArgs &a)
             dc.p_cast += dc.cast - d_c0;
         }
 #endif
-        shade_step<true, SVC && SPT_SVC_WT>(a, ps, h, act && cdone, done, dropped, s_lds + (threadIdx.x & ~63u));
+        shade_step<true, SVC && SPT_SVC_WT>(a, ps, h, act && cdone, done, dropped, s_lds + (threadIdx.x & ~63u),
+                                            SPT_DIAG ? dc.s_rounds : nullptr);
         fresh = cdone;
         if (SVC) {
             // finished samples per completion counter, summed in the wave (acc) and added
@@ -757,6 +759,8 @@ __device__ __forceinline__ void render_body(const RenderArgs &a)
         atomicAdd(&a.counters[20], dc.p_spheres);
         atomicAdd(&a.counters[21], dc.p_branches);
         atomicAdd(&a.counters[22], dc.p_cast);
+        atomicAdd(&a.counters[23], dc.s_rounds[0]);
+        atomicAdd(&a.counters[24], dc.s_rounds[1]);
     }
 #endif
 #undef SPT_STAMP

@@ -731,7 +731,7 @@ struct Path {
 // accepted one.  The result and the advanced state st0 + 3 (j* + 1) gamma equal
 // the sequential loop's.  Must be called in wave-uniform control flow.
 // `lds`: 64 words of wave-private LDS.
-__device__ __forceinline__ f3 coop_ball_vector(uint64_t &st, bool need, uint32_t *lds)
+__device__ __forceinline__ f3 coop_ball_vector(uint64_t &st, bool need, uint32_t *lds, unsigned long long *rounds = nullptr)
 {
     const uint32_t lane = __lane_id();
     const uint64_t st0 = st;
@@ -744,7 +744,9 @@ __device__ __forceinline__ f3 coop_ball_vector(uint64_t &st, bool need, uint32_t
     unsigned long long pend = __ballot(need && lensq(r) < 0.25f);
     uint32_t jb = 1;
     const uint32_t s_lo = (uint32_t)st0, s_hi = (uint32_t)(st0 >> 32);
+    if (SPT_DIAG && rounds) rounds[0] += 1;  // calls (round 0 for every lane)
     while (pend != 0ull) {
+        if (SPT_DIAG && rounds) rounds[1] += 1;  // cooperative rounds after round 0
         const uint32_t np = (uint32_t)__popcll(pend);
         // lg = min(floor(log2(64 / np)), 4) = min(6 - ceil(log2 np), 4) on the scalar unit
         // (64 / np compiled to a float reciprocal sequence on the vector unit)
@@ -969,7 +971,8 @@ __device__ __forceinline__ void finish_step(uint32_t mode, uint32_t *samples, Pa
 // cooperative cube-minus-ball sampler runs in uniform control flow.
 template <bool KARG = false, bool WT = false>
 __device__ __forceinline__ void shade_step(const RenderArgs &a, Path &ps, const Hit &h, bool act,
-                                           unsigned long long &done, unsigned long long &dropped, uint32_t *lds)
+                                           unsigned long long &done, unsigned long long &dropped, uint32_t *lds,
+                                           unsigned long long *diag_rounds = nullptr)
 {
     // hit, shade and material tables are in slot order (spt_accel.cpp)
     const float4 *__restrict__ hit = a.scene.accel.slots;
@@ -1025,7 +1028,7 @@ __device__ __forceinline__ void shade_step(const RenderArgs &a, Path &ps, const 
         }
     }
     bool spec_event = false;
-    const f3 rv_coop = coop_ball_vector(ps.st, scatter, lds);
+    const f3 rv_coop = coop_ball_vector(ps.st, scatter, lds, diag_rounds);
     if (scatter) {
         // contact point + normal + cube-minus-ball vector, shared by the diffuse
         // first hit (lines 23-26), the diffuse loop (30-33) and the mirror (41-43)

@@ -48,6 +48,10 @@ if pi:
           f"spheres={ps_/pi:.2f} update branches={pb/pi:.2f}; per other cast: nodes={(nodes-pn)/max(it-pi,1):.2f} "
           f"spheres={(sph-ps_)/max(it-pi,1):.2f} update branches={(br-pb)/max(it-pi,1):.2f}; "
           f"primary casts' share of cast cycles {pc/max(cc,1):.3f}")
+scalls, srounds = st["diag"][19:21]
+if scalls:
+    print(f"sampler: {scalls} calls ({scalls/max(it,1):.3f} per wave iteration), {srounds/scalls:.3f} cooperative "
+          f"rounds per call after round 0")
 print(f"render_ms={st['render_ms']:.3f}")
 print("raw diag", list(st["diag"]))
 # the LDS kernel (1024-thread blocks) walks lane by lane (spt_path.h find_closest_lane):
@@ -67,6 +71,7 @@ if json_out:
                "cycle_split": {"cast": cc / tot, "shade": cs / tot, "refill": cr / tot},
                "primary": {"iters": pi, "nodes_per_cast": pn / max(pi, 1), "spheres_per_cast": ps_ / max(pi, 1),
                            "update_branches_per_cast": pb / max(pi, 1), "cast_cycle_share": pc / max(cc, 1)},
+               "sampler": {"calls": scalls, "rounds_after_first_per_call": srounds / max(scalls, 1)},
                "build": "SPT_DIAG=1 (libspt_hip_diag.so), counters only, never timed",
                **({"walk": "lane", "lane_node_visits_per_ray": nodes / max(st["casts"], 1),
                    "walk_iters_per_wave_cast": live / max(it, 1), "leaf_passes_per_wave_cast": leaves / max(it, 1),

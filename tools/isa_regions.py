@@ -56,9 +56,10 @@ def kind(op):
     return "other"
 
 
-PHASES = [  # (function-name fragment, region), innermost-first priority is NOT used: outermost phase wins
+PHASES = [  # (function-name fragment, region)
     ("update_member", "cast:update"),
     ("test_leaf", "cast:members"), ("test_group", "cast:members"), ("ray_sphere", "cast:members"),
+    ("prim_list_cast", "cast:list"),
     ("find_closest", "cast:walk+setup"),
     ("coop_ball_vector", "sampler"),
     ("refract_event", "shade"), ("finish_step", "shade"), ("shade_step", "shade"),
@@ -67,20 +68,14 @@ PHASES = [  # (function-name fragment, region), innermost-first priority is NOT 
 
 
 def region_of(chain):
-    """chain: function names innermost first.  The first phase function found walking from
-    the outermost caller inwards decides (a normalize inside shade_step is shade; a
-    ray_sphere inside find_closest is cast:members, the more specific of the two)."""
-    names = list(reversed(chain))  # outermost first
-    best = None
-    for n in names:
+    """chain: function names innermost first.  The innermost phase function decides (a
+    uniform() draw inside coop_ball_vector is sampler; a normalize inside shade_step is
+    shade; ray_sphere inside find_closest is cast:members)."""
+    for n in chain:
         for frag, reg in PHASES:
             if frag in n:
-                if best is None:
-                    best = reg
-                elif best.startswith("cast") and reg.startswith("cast"):
-                    best = reg  # refine inside the cast
-                break
-    return best or "loop"
+                return reg
+    return "loop"
 
 
 def symbolize(co, addrs):

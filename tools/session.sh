@@ -46,6 +46,9 @@ for step in "$@"; do
     rw) SPT_SVC_DEBUG=1 run rw 120 python -u -m pytest -x -v -s --timeout 60 --timeout-method thread tests/test_gpu_service.py -k ring_wrap ;;
     diag) SPT_LIB=libspt_hip_diag.so run diag 200 python tools/diag.py c2 --json "gpurun_out/${TAG}_diag_c2.json" ;;
     diag5) SPT_LIB=libspt_hip_diag.so run diag5 300 python tools/diag.py c5 --json "gpurun_out/${TAG}_diag_c5.json" ;;
+    pl) run pl 300 $PYT -v -m gpu tests/test_gpu_parity.py -k primary_lists ;;
+    benchq_nol) SPT_PRIM_LISTS=0 run benchq_nol 120 python bench.py --no-cpu-baseline --no-dropin ;;
+    diag_nol) SPT_PRIM_LISTS=0 SPT_LIB=libspt_hip_diag.so run diag_nol 200 python tools/diag.py c2 --json "gpurun_out/${TAG}_diag_nol_c2.json" ;;
     mr) run mr 300 $PYT -v -m gpu tests/test_gpu_parity.py -k two_ranks ;;
     smoke) run smoke 120 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 400 python bench.py ;;

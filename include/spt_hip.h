@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define SPT_ABI_VERSION 7
+#define SPT_ABI_VERSION 8
 
 /* Only the functions below are exported from libspt_hip.so (built with
  * -fvisibility=hidden), so several builds can be loaded side by side. */
@@ -66,7 +66,7 @@ enum {
 
 typedef struct spt_ctx spt_ctx;
 
-#define SPT_DIAG_WORDS 21
+#define SPT_DIAG_WORDS 26
 
 typedef struct spt_stats {
     uint64_t samples;      /* (pixel, sample) paths completed */
@@ -95,7 +95,10 @@ typedef struct spt_stats {
                               iterations, tree nodes tested, spheres tested, update
                               branches taken, s_memtime cycles of their casts; the
                               cube-minus-ball sampler's calls and its cooperative rounds
-                              after round 0 */
+                              after round 0; tree leaves entered by at most 8 and at
+                              most 16 lanes; s_memtime cycles in the sampler; wave
+                              iterations after the launch's items ran out (the drain)
+                              and their live lanes */
     uint64_t batches;       /* batched launches of concurrent spt_render_segment[_task] calls */
     uint64_t batched_calls; /* calls rendered in them */
     /* render service (spt_service_start); the device counters above include a session's

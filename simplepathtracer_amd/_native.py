@@ -15,7 +15,7 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG_DIR, "lib", os.environ.get("SPT_LIB", "libspt_hip.so"))
 HEADER_PATH = os.path.join(os.path.dirname(PKG_DIR), "include", "spt_hip.h")
 
-ABI_VERSION = 7  # SPT_ABI_VERSION of include/spt_hip.h
+ABI_VERSION = 8  # SPT_ABI_VERSION of include/spt_hip.h
 SPT_OK = 0
 STATUS_NAMES = {0: "SPT_OK", 1: "SPT_ERR_ARG", 2: "SPT_ERR_STATE", 3: "SPT_ERR_HIP", 4: "SPT_ERR_NOMEM",
                 5: "SPT_ERR_NODEVICE", 6: "SPT_ERR_TIMEOUT"}
@@ -44,7 +44,7 @@ class Stats(ctypes.Structure):
         ("grid_blocks", ctypes.c_uint32),
         ("block_threads", ctypes.c_uint32),
         ("render_busy_ms", ctypes.c_double),
-        ("diag", ctypes.c_uint64 * 21),  # SPT_DIAG_WORDS
+        ("diag", ctypes.c_uint64 * 26),  # SPT_DIAG_WORDS
         ("batches", ctypes.c_uint64),
         ("batched_calls", ctypes.c_uint64),
         ("svc_sessions", ctypes.c_uint64),

@@ -42,9 +42,11 @@
 #include <array>
 #include <chrono>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <cstdio>
 #include <numeric>
+#include <thread>
 #include <string>
 
 namespace spt {
@@ -676,17 +678,28 @@ PrimListTables build_prim_lists(const AccelTables &t, const Camera &cam, uint32_
     std::vector<uint32_t> all(t.slots.size());
     std::iota(all.begin(), all.end(), 0u);
     // super-blocks of 64 x 64 pixels first: a slot culled for a super-block's cone is
-    // culled for every block inside it (its rectangle holds theirs)
-    std::vector<uint32_t> sup, cand;
+    // culled for every block inside it (its rectangle holds theirs).  Super-blocks are
+    // independent: host threads build their lists, concatenated in super-block order (the
+    // tables are the same as one thread's)
+    struct Sup {
+        uint32_t sx, sy;
+        std::vector<std::pair<uint32_t, uint2>> runs;  // (level << 31 | block, {offset in slots, count})
+        std::vector<uint32_t> slots;
+    };
+    std::vector<Sup> sups;
     for (uint32_t sy = 0; sy < H; sy += 64)
-        for (uint32_t sx = 0; sx < W; sx += 64) {
+        for (uint32_t sx = 0; sx < W; sx += 64) sups.push_back(Sup{sx, sy, {}, {}});
+    auto work = [&](size_t first, size_t step) {
+        std::vector<uint32_t> sup, cand;
+        for (size_t q = first; q < sups.size(); q += step) {
+            Sup &S = sups[q];
+            const uint32_t sx = S.sx, sy = S.sy;
             const PrimCone sc = prim_cone(cam, W, H, sx, std::min(W, sx + 64), sy, std::min(H, sy + 64));
             sup.clear();
             for (uint32_t s : all)
                 if (!sc.ok || prim_candidate(sc, t.slots[s], e)) sup.push_back(s);
-            for (int level = 0; level < 2; ++level) {
+            for (uint32_t level = 0; level < 2; ++level) {
                 const uint32_t bhgt = level == 0 ? 8u : 4u;
-                std::vector<uint2> &dst = level == 0 ? out.b8 : out.b4;
                 for (uint32_t y = sy; y < std::min(H, sy + 64); y += bhgt)
                     for (uint32_t x = sx; x < std::min(W, sx + 64); x += 8) {
                         const PrimCone pc = prim_cone(cam, W, H, x, std::min(W, x + 8), y, std::min(H, y + bhgt));
@@ -698,11 +711,33 @@ PrimListTables build_prim_lists(const AccelTables &t, const Camera &cam, uint32_
                         // runs of whole groups of 4 (the kernel loads 4 entries at a time),
                         // padded with a dummy slot (never passes)
                         while (cand.size() % 4) cand.push_back(pad);
-                        dst[(size_t)(y / bhgt) * out.bw + x / 8] = make_uint2((uint32_t)out.slots.size(), (uint32_t)cand.size());
-                        out.slots.insert(out.slots.end(), cand.begin(), cand.end());
+                        const uint32_t blk = (y / bhgt) * out.bw + x / 8;
+                        S.runs.push_back({level << 31 | blk, make_uint2((uint32_t)S.slots.size(), (uint32_t)cand.size())});
+                        S.slots.insert(S.slots.end(), cand.begin(), cand.end());
                     }
             }
         }
+    };
+    const size_t work_units = sups.size() * t.slots.size();
+    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    size_t nth = work_units < (1u << 20) ? 1 : std::min<size_t>({(size_t)hw, (size_t)16, sups.size()});
+    if (const char *ev = std::getenv("SPT_PRIM_THREADS"))  // tests: one thread vs many give the same tables
+        if (*ev) nth = std::max(1, std::atoi(ev));
+    if (nth <= 1) {
+        work(0, 1);
+    } else {
+        std::vector<std::thread> th;
+        for (size_t k = 0; k < nth; ++k) th.emplace_back(work, k, nth);
+        for (std::thread &x : th) x.join();
+    }
+    for (const Sup &S : sups) {
+        const uint32_t base = (uint32_t)out.slots.size();
+        for (const auto &r : S.runs) {
+            std::vector<uint2> &dst = (r.first >> 31) == 0 ? out.b8 : out.b4;
+            dst[r.first & 0x7FFFFFFFu] = make_uint2(base + r.second.x, r.second.y);
+        }
+        out.slots.insert(out.slots.end(), S.slots.begin(), S.slots.end());
+    }
     if (out.slots.empty()) out.slots.assign(4, pad);  // a valid pointer for the device copy
     out.on = true;
     out.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count();

@@ -1269,7 +1269,9 @@ int rebuild_accel(spt_ctx *ctx)
 }
 
 // Build and upload the primary-ray candidate lists for the current scene, camera and frame
-// size (none for trees walked lane by lane, which have no primary batches).
+// size (none for trees walked lane by lane, which have no primary batches: casting their
+// freshly started paths against the lists cut config 5's node visits per ray 17.1 -> 12.7
+// but not its walk iterations or time).
 int rebuild_prim(spt_ctx *ctx)
 {
     ctx->prim = spt::PrimLists{};

@@ -380,7 +380,8 @@ __device__ __forceinline__ void render_body(const RenderArgs &a)
         unsigned long long iters = 0, cast = 0, shade = 0, refill = 0;  // SPT_DIAG counts and s_memtime split
         // the primary batches' share: iterations, nodes, spheres, update branches, cast cycles
         unsigned long long p_iters = 0, p_nodes = 0, p_spheres = 0, p_branches = 0, p_cast = 0;
-        unsigned long long s_rounds[2] = {0, 0};  // sampler calls, cooperative rounds after round 0
+        unsigned long long s_rounds[3] = {0, 0, 0};  // sampler calls, cooperative rounds after round 0, cycles
+        unsigned long long t_iters = 0, t_live = 0;  // iterations after the items ran out, their live lanes
     } dc;
     CastDiag dg;
     // resumable lane walk (SPT_LANE_BUDGET): the cast state of lanes whose walk ran
@@ -537,6 +538,16 @@ __device__ __forceinline__ void render_body(const RenderArgs &a)
                     } else {
                         const uint32_t mine = take_items(~0ull);
                         if (mine != 0xFFFFFFFFu) start_path_kernarg(mine, rows, ps, &pxy);
+                        if ((SPT_DUP & 4) && mine != 0xFFFFFFFFu) {
+                            Path p2;
+                            uint32_t pxy2 = 0;
+                            start_path_kernarg(opaque_v(mine), rows, p2, &pxy2);
+                            sink_v(p2.d.x);
+                            sink_v(p2.d.y);
+                            sink_v(p2.d.z);
+                            sink_v(p2.st);
+                            sink_v(pxy2);
+                        }
                     }
                     prim_iter = true;
                 }
@@ -548,7 +559,9 @@ __device__ __forceinline__ void render_body(const RenderArgs &a)
                 const uint32_t rank = lane_rank(need);
                 const uint32_t mine = blk_cur + rank;
                 blk_cur += take;
-                if (ps.phase == PH_IDLE && rank < take) start_path_rect(mine, rect, ps);
+                if (ps.phase == PH_IDLE && rank < take) {
+                    start_path_rect(mine, rect, ps);
+                }
             }
         } else if (!BATCH && need != 0ull && !exhausted) {
             const uint32_t mine = take_items(need);
@@ -649,6 +662,10 @@ __device__ __forceinline__ void render_body(const RenderArgs &a)
         constexpr bool RES = SPT_LANE_BUDGET > 0 && (LDSN || GLANE);
         if (!RES) casts += (unsigned long long)__popcll(live);
         ++dc.iters;
+        if (SPT_DIAG && exhausted) {
+            dc.t_iters += 1;
+            dc.t_live += (unsigned long long)__popcll(live);
+        }
         // ---- one cast + one shading step ----
         const bool act = ps.phase != PH_IDLE;
         // GLANE: the lane walk over layout 0 in global memory (trees too large for LDS)
@@ -667,6 +684,16 @@ __device__ __forceinline__ void render_body(const RenderArgs &a)
             if (prim_iter && kernarg_args()->prim.on)
                 listed = prim_list_cast(a.scene.accel, ps.o, ps.d, act, pxy, h, dg);
             if (!listed) h = find_closest<TREE, LEAF, LDSN>(a.scene.accel, ps.o, ps.d, act, dg, (const uint32_t *)s_nodes);
+            if (SPT_DUP & 1) {
+                const f3 o2 = opaque_v3(ps.o), d2 = opaque_v3(ps.d);
+                Hit h2;
+                bool l2 = false;
+                if (prim_iter && kernarg_args()->prim.on) l2 = prim_list_cast(a.scene.accel, o2, d2, act, pxy, h2, dg);
+                if (!l2) h2 = find_closest<TREE, LEAF, LDSN>(a.scene.accel, o2, d2, act, dg, (const uint32_t *)s_nodes);
+                sink_v(h2.idx);
+                sink_v(h2.best);
+                sink_v(h2.t);
+            }
         } else {
             h = (LDSN && SPT_LANE_WALK)
                     ? find_closest_lane<LEAF>(a.scene.accel, ps.o, ps.d, act, dg, (const uint32_t *)s_nodes)
@@ -761,6 +788,11 @@ __device__ __forceinline__ void render_body(const RenderArgs &a)
         atomicAdd(&a.counters[22], dc.p_cast);
         atomicAdd(&a.counters[23], dc.s_rounds[0]);
         atomicAdd(&a.counters[24], dc.s_rounds[1]);
+        atomicAdd(&a.counters[25], dg.leaves8);
+        atomicAdd(&a.counters[26], dg.leaves16);
+        atomicAdd(&a.counters[27], dc.s_rounds[2]);
+        atomicAdd(&a.counters[28], dc.t_iters);
+        atomicAdd(&a.counters[29], dc.t_live);
     }
 #endif
 #undef SPT_STAMP

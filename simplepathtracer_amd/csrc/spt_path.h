@@ -20,6 +20,14 @@
 #ifndef SPT_LEAF_SPLIT
 #define SPT_LEAF_SPLIT 1
 #endif
+// Attribution builds only (tools/attrib.sh, never the product library): SPT_DUP runs one
+// phase a second time on opaque copies of its inputs and discards the result, so the
+// difference in SQ_INSTS_VALU per launch against the product build is that phase's
+// instruction count.  Bits: 1 the whole cast, 2 the cooperative sampler, 4 the primary
+// ray (start_path), 8 the tree node test, 16 the member tests + updates of entered leaves.
+#ifndef SPT_DUP
+#define SPT_DUP 0
+#endif
 
 // Item order of a batch: [band][8x8 tile][sample][pixel] (ts_item, spt_internal.h)
 
@@ -82,6 +90,19 @@ __device__ __forceinline__ uint32_t lane_rank(unsigned long long mask)
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
 }
 
+template <class T>
+__device__ __forceinline__ T opaque_v(T x)
+{
+    asm volatile("" : "+v"(x));
+    return x;
+}
+__device__ __forceinline__ f3 opaque_v3(f3 a) { return mk(opaque_v(a.x), opaque_v(a.y), opaque_v(a.z)); }
+template <class T>
+__device__ __forceinline__ void sink_v(T x)
+{
+    asm volatile("" ::"v"(x));
+}
+
 // Closest-hit state of one FindClosestIntersectionSphere call.
 struct Hit {
     uint32_t idx;        // slot of the winner (traversal order), kMiss = none
@@ -104,6 +125,7 @@ struct CastDiag {
     // lane-level work: RaySphereIntersection evaluations (17 FLOP each) and
     // member pretests (10 VALU each) for the wave's live lanes
     unsigned long long lane_tests = 0, lane_pretests = 0;
+    unsigned long long leaves8 = 0, leaves16 = 0;  // tree leaves entered by <= 8 / <= 16 lanes
     uint32_t live_now = 0;  // live lanes of the current cast
 };
 
@@ -492,18 +514,40 @@ __device__ __forceinline__ Hit find_closest(const AccelView &ac, const f3 &o, co
                                   min_raw(__builtin_fmaxf(az, bz), sbl));
         // inactive lanes have sbl = -inf, so t_f < t_n: no AND with the live mask
         const unsigned long long mm = __ballot(tn <= tf) | tree_nocull;
+        if (SPT_DUP & 8) {
+            const float jx = opaque_v(irx), jy = opaque_v(iry), jz = opaque_v(irz);
+            const float ax2 = __builtin_fmaf(lx, jx, qlx), bx2 = __builtin_fmaf(hx, jx, qhx);
+            const float ay2 = __builtin_fmaf(ly, jy, qly), by2 = __builtin_fmaf(hy, jy, qhy);
+            const float az2 = __builtin_fmaf(lz, jz, qlz), bz2 = __builtin_fmaf(hz, jz, qhz);
+            const float tn2 = max3_raw(__builtin_fminf(ax2, bx2), __builtin_fminf(ay2, by2),
+                                       max_raw(__builtin_fminf(az2, bz2), neta));
+            const float tf2 = min3_raw(__builtin_fmaxf(ax2, bx2), __builtin_fmaxf(ay2, by2),
+                                       min_raw(__builtin_fmaxf(az2, bz2), sbl));
+            const unsigned long long mm2 = __ballot(tn2 <= tf2);
+            asm volatile("" ::"s"(mm2));
+        }
         const bool leaf = leaf_slot != kNoSlot;
         if (SPT_DIAG) {
             dg.nodes += 1;
             dg.leaves += (mm != 0ull && leaf) ? 1 : 0;
             if (leaf) {
                 dg.pairs += (unsigned long long)__popcll(mm);
+                dg.leaves8 += (mm != 0ull && __popcll(mm) <= 8) ? 1 : 0;
+                dg.leaves16 += (mm != 0ull && __popcll(mm) <= 16) ? 1 : 0;
                 dg.live += mm != 0ull ? (unsigned long long)__popcll(live_mask) : 0ull;
             }
         }
         // (one branch per outcome -- culled inner node / entered leaf / else -- measured
         // 2% slower on config 2 and 8% on config 5 than this form)
         if (mm != 0ull && leaf) {
+            if (SPT_DUP & 16) {
+                Hit h2 = h;
+                h2.best = opaque_v(h2.best);
+                test_leaf<LEAF>(slots, ac.orig, leaf_slot, opaque_v3(o), opaque_v3(d), dod, h2, dg);
+                sink_v(h2.idx);
+                sink_v(h2.best);
+                sink_v(h2.t);
+            }
             test_leaf<LEAF>(slots, ac.orig, leaf_slot, o, d, dod, h, dg);
             sbl = near_bound(h.best);
         }
@@ -745,6 +789,9 @@ __device__ __forceinline__ f3 coop_ball_vector(uint64_t &st, bool need, uint32_t
     uint32_t jb = 1;
     const uint32_t s_lo = (uint32_t)st0, s_hi = (uint32_t)(st0 >> 32);
     if (SPT_DIAG && rounds) rounds[0] += 1;  // calls (round 0 for every lane)
+#if SPT_DIAG
+    const unsigned long long t_in = __builtin_amdgcn_s_memtime();
+#endif
     while (pend != 0ull) {
         if (SPT_DIAG && rounds) rounds[1] += 1;  // cooperative rounds after round 0
         const uint32_t np = (uint32_t)__popcll(pend);
@@ -779,6 +826,9 @@ __device__ __forceinline__ f3 coop_ball_vector(uint64_t &st, bool need, uint32_t
         jb += 1u << lg;
     }
     if (need) st = st0 + (uint64_t)(3u * (jacc + 1u)) * kGamma;
+#if SPT_DIAG
+    if (rounds) rounds[2] += __builtin_amdgcn_s_memtime() - t_in;  // sampler cycles
+#endif
     return r;
 }
 
@@ -1029,6 +1079,14 @@ __device__ __forceinline__ void shade_step(const RenderArgs &a, Path &ps, const 
     }
     bool spec_event = false;
     const f3 rv_coop = coop_ball_vector(ps.st, scatter, lds, diag_rounds);
+    if (SPT_DUP & 2) {
+        uint64_t st2 = opaque_v(ps.st);
+        const f3 r2 = coop_ball_vector(st2, opaque_v(scatter ? 1u : 0u) != 0u, lds);
+        sink_v(r2.x);
+        sink_v(r2.y);
+        sink_v(r2.z);
+        sink_v(st2);
+    }
     if (scatter) {
         // contact point + normal + cube-minus-ball vector, shared by the diffuse
         // first hit (lines 23-26), the diffuse loop (30-33) and the mirror (41-43)

@@ -115,6 +115,17 @@ def test_stress_and_small_scenes(oracle, native, spt_mod):
     check_winners(oracle, native, c3, v3, [0.0, 1.0, -3.0, 0.0], 200, 100, 4, samples=4000, seed=9)
 
 
+def test_config5_stress_scene(oracle, native, spt_mod):
+    """Config 5's 10 000-sphere stress scene at full size (the host check; the lane-walk
+    kernels that render it do not use the lists); half the samples in a window over the
+    grazing far field of the sphere layer."""
+    stress = spt_mod.generate_stress(1, 10000)
+    view = spt_mod.camera_basis()
+    walk, mean_len = check_winners(oracle, native, stress, view, spt_mod.scene.DEFAULT_EYE, 1920, 1080, 256,
+                                   samples=6000, seed=11, focus=(0, 380, 1920, 620))
+    assert walk < 0.1 and mean_len < 16
+
+
 def test_degenerate_camera_walks(oracle, native, spt_mod):
     """A non-finite view or eye turns the lists off (every block walks the tree)."""
     scene = spt_mod.generate_spheres(1)
@@ -122,3 +133,18 @@ def test_degenerate_camera_walks(oracle, native, spt_mod):
     view.reshape(16)[0] = np.inf
     check_winners(oracle, native, scene, view, spt_mod.scene.DEFAULT_EYE, 64, 64, 4, want_on=False)
     check_winners(oracle, native, scene, spt_mod.camera_basis(), [np.nan, 2.0, 3.0, 0.0], 64, 64, 4, want_on=False)
+
+
+def test_threaded_build_equals_one_thread(native, monkeypatch):
+    """The host builder splits large builds over threads by 64 x 64 super-block; the tables
+    must be those of one thread (config 5's 10 000-sphere stress scene at 1920 x 1080)."""
+    import simplepathtracer_amd as spt
+    sc = spt.generate_stress(1, 10000)
+    view = spt.camera_basis()
+    eye = list(spt.scene.DEFAULT_EYE)
+    got = []
+    for th in ("1", "8"):
+        monkeypatch.setenv("SPT_PRIM_THREADS", th)
+        got.append(prim_lists(native, sc.centers, sc.radii, view, eye, 1920, 1080))
+    for a, b in zip(got[0], got[1]):
+        assert np.array_equal(np.asarray(a), np.asarray(b))

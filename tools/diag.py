@@ -52,6 +52,13 @@ scalls, srounds = st["diag"][19:21]
 if scalls:
     print(f"sampler: {scalls} calls ({scalls/max(it,1):.3f} per wave iteration), {srounds/scalls:.3f} cooperative "
           f"rounds per call after round 0")
+l8, l16, scyc = st["diag"][21:24]
+if leaves:
+    print(f"tree leaves entered by <= 8 lanes: {l8/leaves:.3f}, by <= 16 lanes: {l16/leaves:.3f}; "
+          f"sampler cycles {scyc/max(cc + cs + cr, 1):.3f} of the phases' total")
+ti, tlv = st["diag"][24:26]
+if ti:
+    print(f"drain (items run out): {ti} wave iterations ({ti/max(it,1):.4f} of all), {tlv/ti:.2f} live lanes per iteration")
 print(f"render_ms={st['render_ms']:.3f}")
 print("raw diag", list(st["diag"]))
 # the LDS kernel (1024-thread blocks) walks lane by lane (spt_path.h find_closest_lane):

@@ -18,7 +18,8 @@
 #          dropin1      the same with SPT_SERVICE=1 (the shim's calls through the render service)
 #          profile      tools/profile.sh <tag>_c2 c2 (kernel trace + PMC passes + SPT_DIAG)
 #          profile5     tools/profile.sh <tag>_c5 c5 --config c5 --steps 2 --warmup 1 ...
-#          ab:<args>    tools/ab.py <args>
+#          attrib       tools/attrib.sh (per-phase VALU from the SPT_DUP builds)
+#          ab:<args>    tools/ab.py <args> (one quoted step; logs ab1, ab2, ...)
 set -o pipefail
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd "$R" || exit 2
@@ -27,7 +28,7 @@ TAG=${1:?tag}
 shift
 run() {  # name seconds cmd...
   local name=$1 t=$2; shift 2
-  local log="gpurun_out/${TAG}_${name}.log"
+  local log="$R/gpurun_out/${TAG}_${name}.log"
   echo "== $name ($(date +%T))"
   timeout -k 10 "$t" "$@" > "$log" 2>&1
   local rc=$?
@@ -48,6 +49,8 @@ for step in "$@"; do
     diag5) SPT_LIB=libspt_hip_diag.so run diag5 300 python tools/diag.py c5 --json "gpurun_out/${TAG}_diag_c5.json" ;;
     pl) run pl 300 $PYT -v -m gpu tests/test_gpu_parity.py -k primary_lists ;;
     benchq_nol) SPT_PRIM_LISTS=0 run benchq_nol 120 python bench.py --no-cpu-baseline --no-dropin ;;
+    diag5_nol) SPT_PRIM_LISTS=0 SPT_LIB=libspt_hip_diag.so run diag5_nol 300 python tools/diag.py c5 --json "gpurun_out/${TAG}_diag_nol_c5.json" ;;
+    trace) (cd /tmp && TMPDIR=/tmp run trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/${TAG}_trace" -o run -- python3 "$R/bench.py" --no-cpu-baseline --no-dropin) ;;
     diag_nol) SPT_PRIM_LISTS=0 SPT_LIB=libspt_hip_diag.so run diag_nol 200 python tools/diag.py c2 --json "gpurun_out/${TAG}_diag_nol_c2.json" ;;
     mr) run mr 300 $PYT -v -m gpu tests/test_gpu_parity.py -k two_ranks ;;
     smoke) run smoke 120 python -c "import __graft_entry__ as g; g.smoke()" ;;
@@ -56,6 +59,11 @@ for step in "$@"; do
     bench0) run bench0 400 python bench.py --service 0 ;;
     benchq) run benchq 120 python bench.py --no-cpu-baseline --no-dropin ;;
     bench0q) run bench0q 120 python bench.py --no-cpu-baseline --no-dropin --service 0 ;;
+    c5_nol) SPT_PRIM_LISTS=0 run c5_nol 300 python bench.py --config c5 --steps 4 --warmup 1 --no-cpu-baseline --no-dropin ;;
+    c5q) run c5q 300 python bench.py --config c5 --steps 4 --warmup 1 --no-cpu-baseline --no-dropin ;;
+    tl1) run tl1 300 python tools/svc_timeline.py --n 1 --frames 20 --service 1 ;;
+    tl0) run tl0 300 python tools/svc_timeline.py --n 1 --frames 20 --service 0 ;;
+    bench1q_896) SPT_SVC_CLAIM=896 run bench1q_896 120 python bench.py --no-cpu-baseline --no-dropin --service 1 ;;
     c5) run c5 300 python bench.py --config c5 --steps 4 --warmup 1 --no-cpu-baseline ;;
     c3) run c3 300 python bench.py --config c3 --steps 2 --warmup 1 --no-cpu-baseline ;;
     scaling) run scaling 300 python tools/scaling_probe.py --streams 2 --reps 5 --service 1 --record "gpurun_out/${TAG}_scaling.txt"
@@ -64,7 +72,8 @@ for step in "$@"; do
     dropin1) run dropin1 300 python -c "import bench; print(bench.dropin_bench(1200, 800, 100, 50, 20, (4, 32), {'SPT_SERVICE': '1'}))" ;;
     profile) run profile 900 bash tools/profile.sh "${TAG}_c2" c2 ;;
     profile5) run profile5 900 bash tools/profile.sh "${TAG}_c5" c5 --config c5 --steps 2 --warmup 1 --no-cpu-baseline ;;
-    ab:*) run ab 600 python tools/ab.py ${step#ab:} ;;
+    attrib) run attrib 600 bash tools/attrib.sh "${TAG}_attrib" ;;
+    ab:*) NAB=$((${NAB:-0} + 1)); run ab$NAB 600 python tools/ab.py ${step#ab:} ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

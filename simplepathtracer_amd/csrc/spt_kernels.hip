@@ -683,7 +683,9 @@ __device__ __forceinline__ void render_body(const RenderArgs &a)
             bool listed = false;
             if (prim_iter && kernarg_args()->prim.on)
                 listed = prim_list_cast(a.scene.accel, ps.o, ps.d, act, pxy, h, dg);
-            if (!listed) h = find_closest<TREE, LEAF, LDSN>(a.scene.accel, ps.o, ps.d, act, dg, (const uint32_t *)s_nodes);
+            if (!listed)
+                h = find_closest<TREE, LEAF, LDSN>(a.scene.accel, ps.o, ps.d, act, dg, (const uint32_t *)s_nodes,
+                                                   s_lds + (threadIdx.x & ~63u));
             if (SPT_DUP & 1) {
                 const f3 o2 = opaque_v3(ps.o), d2 = opaque_v3(ps.d);
                 Hit h2;

@@ -28,6 +28,11 @@
 #ifndef SPT_DUP
 #define SPT_DUP 0
 #endif
+// wave walk: leaves entered by at most 8 lanes are tested as dealt (lane, member) pairs
+// (test_leaf_pairs)
+#ifndef SPT_LEAF_PAIRS
+#define SPT_LEAF_PAIRS 1
+#endif
 
 // Item order of a batch: [band][8x8 tile][sample][pixel] (ts_item, spt_internal.h)
 
@@ -295,6 +300,101 @@ __device__ __forceinline__ void test_leaf(cfloat *slots, const uint32_t *__restr
 #endif
 }
 
+// Leaf test for a leaf that few lanes need (the wave walk's `mm`, at most 64 / LEAF lanes;
+// config 2: 60% of the leaves entered): the (lane, member) pairs are dealt one per lane --
+// lane L tests member L % LEAF for the (L / LEAF)-th lane of mm, on that lane's ray (six
+// ds_bpermute) and the member's record (vector loads, cache-resident) -- instead of every
+// lane testing every member.  Each pair forms update_member's candidate (contact distance,
+// original index, slot, t), never-winning ones (the member test fails, the contact lies
+// behind, NaN) as +inf; the lexicographic minimum over a lane's LEAF pairs (three DPP
+// butterflies inside each group of 8 lanes) goes back to the lane and is merged into its
+// winner by update_member's rule.  The winner is the (distance, original index) minimum
+// over every member tested, whatever the order, and lanes outside mm cannot improve on
+// this leaf (the box test's proof): the result is test_leaf's.
+// scratch: 64 words of wave-private LDS.
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_u(uint32_t x)
+{
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xF, 0xF, false);
+}
+template <int CTRL>
+__device__ __forceinline__ float dpp_fl(float x)
+{
+    return __uint_as_float(dpp_u<CTRL>(__float_as_uint(x)));
+}
+// one butterfly step of test_leaf_pairs' minimum: the partner lane's candidate via DPP
+template <int CTRL>
+__device__ __forceinline__ void pair_min_step(float &cds, uint32_t &cor, uint32_t &csl, float &ct)
+{
+    const float pds = dpp_fl<CTRL>(cds), pt = dpp_fl<CTRL>(ct);
+    const uint32_t por = dpp_u<CTRL>(cor), psl = dpp_u<CTRL>(csl);
+    const bool take = pds < cds || (pds == cds && por < cor);
+    cds = take ? pds : cds;
+    cor = take ? por : cor;
+    csl = take ? psl : csl;
+    ct = take ? pt : ct;
+}
+template <int LEAF>
+__device__ __forceinline__ void test_leaf_pairs(const AccelView &ac, uint32_t leaf_slot, unsigned long long mm,
+                                                const f3 &o, const f3 &d, Hit &h, uint32_t *scratch, CastDiag &dg)
+{
+    static_assert(LEAF == 8, "pairs are dealt in groups of 8 lanes");
+    const uint32_t lane = __lane_id();
+    const uint32_t rank = lane_rank(mm);
+    const bool owner = __builtin_amdgcn_inverse_ballot_w64(mm);
+    if (owner) scratch[rank] = lane;
+    const uint32_t q = lane >> 3, s = leaf_slot + (lane & 7u);
+    const bool valid = q < (uint32_t)__popcll(mm);
+    // the member's record and original index (vector loads, issued before the shuffles)
+    const float4 sp = ac.slots[s];
+    const uint32_t so = ac.orig[s];
+    const uint32_t src = scratch[valid ? q : 0u];
+    const f3 po = mk(__shfl(o.x, (int)src), __shfl(o.y, (int)src), __shfl(o.z, (int)src));
+    const f3 pd = mk(__shfl(d.x, (int)src), __shfl(d.y, (int)src), __shfl(d.z, (int)src));
+    if (SPT_DIAG) {
+        dg.spheres += LEAF;
+        dg.lane_tests += (unsigned long long)LEAF * __popcll(mm);
+    }
+    float tc, hh;
+    const bool pass = valid && ray_sphere(sp, po, pd, tc, hh);
+    if (__ballot(pass) == 0ull) return;
+    if (SPT_DIAG) dg.branches += 1;
+    // update_member's arithmetic for the pair (Collision.hpp:19-27,49-56)
+    const float t = tc - sqrt_pos_normal(hh);
+    const f3 p = contact(po, pd, t);
+    const bool ok = pass && dot(po, pd) < dot(p, pd);
+    const float dv = lensq(sub(po, p));
+    float cds = ok && dv == dv ? dv : INFINITY;
+    uint32_t cor = so, csl = s;
+    float ct = t;
+    // lexicographic (distance, original index) minimum within each group of 8 lanes:
+    // quad_perm [1,0,3,2], quad_perm [2,3,0,1], row_half_mirror
+    pair_min_step<0xB1>(cds, cor, csl, ct);
+    pair_min_step<0x4E>(cds, cor, csl, ct);
+    pair_min_step<0x141>(cds, cor, csl, ct);
+    // each owner takes its group's minimum and merges it like update_member
+    const int from = (int)(rank << 3);
+    const float gds = __shfl(cds, from), gt = __shfl(ct, from);
+    const uint32_t gor = (uint32_t)__shfl((int)cor, from), gsl = (uint32_t)__shfl((int)csl, from);
+    unsigned long long bm = mm & __ballot(gds < h.best);
+    unsigned long long tm = mm & __ballot(gds == h.best) & __ballot(h.idx != kMiss);
+    if (__builtin_expect(tm != 0ull, 0)) {
+        // exact tie with the current winner (rare): the lower original index wins
+        while (tm != 0ull) {
+            const int l = (int)__builtin_ctzll(tm);
+            const uint32_t wo = ((cuint *)ac.orig)[__builtin_amdgcn_readlane(h.idx, l)];
+            const uint32_t go = __builtin_amdgcn_readlane(gor, l);
+            if (go < wo) bm |= 1ull << l;
+            tm &= tm - 1ull;
+        }
+    }
+    if (SPT_DIAG) dg.improving += bm != 0ull ? 1 : 0;
+    const bool better = __builtin_amdgcn_inverse_ballot_w64(bm);
+    h.best = better ? gds : h.best;
+    h.idx = better ? gsl : h.idx;
+    h.t = better ? gt : h.t;
+}
+
 // Leaf test behind the member pretest: the S slots plus their S pretest constants.
 template <int S>
 __device__ __forceinline__ void test_leaf_pre(cfloat *slots, cfloat *kpre, const uint32_t *__restrict__ orig,
@@ -325,7 +425,7 @@ __device__ __forceinline__ void test_leaf_pre(cfloat *slots, cfloat *kpre, const
 // (`lnodes`, render_kernel's prologue) instead of scalar loads of the octant layouts.
 template <bool TREE, int LEAF, bool LDSN = false>
 __device__ __forceinline__ Hit find_closest(const AccelView &ac, const f3 &o, const f3 &d, bool active,
-                                            CastDiag &dg, const uint32_t *lnodes = nullptr)
+                                            CastDiag &dg, const uint32_t *lnodes = nullptr, uint32_t *scratch = nullptr)
 {
     Hit h;
     h.idx = kMiss;
@@ -548,7 +648,15 @@ __device__ __forceinline__ Hit find_closest(const AccelView &ac, const f3 &o, co
                 sink_v(h2.best);
                 sink_v(h2.t);
             }
-            test_leaf<LEAF>(slots, ac.orig, leaf_slot, o, d, dod, h, dg);
+            // few lanes need the leaf: deal its (lane, member) pairs (SPT_LEAF_PAIRS)
+            bool paired = false;
+            if constexpr (SPT_LEAF_PAIRS && LEAF == 8 && !LDSN) {
+                if (scratch && __popcll(mm) <= 64 / LEAF) {
+                    test_leaf_pairs<LEAF>(ac, leaf_slot, mm, o, d, h, scratch, dg);
+                    paired = true;
+                }
+            }
+            if (!paired) test_leaf<LEAF>(slots, ac.orig, leaf_slot, o, d, dod, h, dg);
             sbl = near_bound(h.best);
         }
         const uint32_t next = (mm != 0ull && !leaf) ? i + 1 : skip;

@@ -266,7 +266,8 @@ SPT_API int spt_render_rows_async(spt_ctx *ctx, int mode, uint32_t yBegin, uint3
  * counter on the caller's stream (hipStreamWaitValue32); results are bit-identical to the
  * launched renders.  Sessions start on the first job and end on spt_service_stop,
  * spt_synchronize, a setter, a render the service does not take (lane-walk trees,
- * spt_render_samples, the wavefront engine, jobs over half the 4 GiB slot ring), when a
+ * spt_render_samples, the wavefront engine, jobs over half the slot ring: 1/16 of device
+ * memory within [4, 16] GiB), when a
  * publication would have to wait for an unfinished fold (the ring wrapped onto words a
  * fold still reads; the next session's launch waits for it instead), or when its waves
  * have gone idle: a session's waves may leave after 0.5 s without work -- only through

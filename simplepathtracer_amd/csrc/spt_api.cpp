@@ -152,7 +152,8 @@ struct Service {
     spt::SvcJob *d_jobs = nullptr;
     uint32_t *d_job_claim = nullptr, *d_done = nullptr, *d_ring = nullptr;
     uint64_t ring_words = 0;
-    uint64_t ring_bytes = 4ull << 30;  // SPT_SVC_RING_MB
+    uint64_t ring_bytes = 4ull << 30;  // SPT_SVC_RING_MB, else sized at the first session (svc_start)
+    bool ring_set = false;             // SPT_SVC_RING_MB given
     uint32_t job_cap = 1u << 16, done_cap = 4096;
     uint32_t claim = 448, queues = spt::kMaxQueues;  // SPT_SVC_CLAIM, SPT_SVC_QUEUES
     // session
@@ -753,6 +754,16 @@ int svc_begin(spt_ctx *ctx, int mode, const std::vector<hipEvent_t> &waits, int6
         HIP_TRY(ctx, hipEventCreate(&v.ev_start));
         HIP_TRY(ctx, hipEventCreate(&v.ev_end));
         HIP_TRY(ctx, hipEventCreateWithFlags(&v.ev_ctl, hipEventDisableTiming));
+        if (!v.ring_set) {
+            // default ring: 1/16 of the device's memory within [4, 16] GiB (MI355X: 16 GiB = 44
+            // config-2 frames of sample words).  A publication that would overwrite words whose
+            // fold has not run ends the session (flow control above), so the ring bounds how
+            // far a caller may run ahead without a restart: 4 GiB held 10 such frames, and a
+            // 20-frame bench restarted its session once (14.0 vs 10.7 ms to the 11th frame)
+            size_t fr = 0, tot = 0;
+            if (hipMemGetInfo(&fr, &tot) == hipSuccess && tot > 0)
+                v.ring_bytes = std::min<uint64_t>(16ull << 30, std::max<uint64_t>(4ull << 30, (uint64_t)tot / 16 >> 20 << 20));
+        }
         v.ring_words = v.ring_bytes / sizeof(uint32_t) / 2 * 2;
         const bool ok = hipMalloc((void **)&v.d_ctl, spt::kSvcCtlWords * sizeof(uint32_t)) == hipSuccess &&
                         hipMalloc((void **)&v.d_jobs, (size_t)v.job_cap * sizeof(spt::SvcJob)) == hipSuccess &&
@@ -2092,8 +2103,10 @@ int spt_ctx_create(int device, spt_ctx **out)
     if (const char *e = env_var("SPT_SVC_CLAIM")) ctx->svc.claim = (uint32_t)std::max(64, std::atoi(e) / 64 * 64);
     if (const char *e = env_var("SPT_SVC_QUEUES"))
         ctx->svc.queues = (uint32_t)std::min<int>((int)spt::kMaxQueues, std::max(1, std::atoi(e)));
-    if (const char *e = env_var("SPT_SVC_RING_MB"))
+    if (const char *e = env_var("SPT_SVC_RING_MB")) {
         ctx->svc.ring_bytes = (uint64_t)std::max(64, std::atoi(e)) << 20;
+        ctx->svc.ring_set = true;
+    }
     // a fraction of the session grid (rehearsing several ranks' sessions on one GPU), the
     // bound on waiting for a session to end, and the publish-delay fault injection of the
     // liveness tests (tests/test_gpu_service.py)

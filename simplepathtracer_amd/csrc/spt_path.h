@@ -640,23 +640,26 @@ __device__ __forceinline__ Hit find_closest(const AccelView &ac, const f3 &o, co
         // (one branch per outcome -- culled inner node / entered leaf / else -- measured
         // 2% slower on config 2 and 8% on config 5 than this form)
         if (mm != 0ull && leaf) {
+            // few lanes need the leaf: deal its (lane, member) pairs (SPT_LEAF_PAIRS)
+            auto leaf_test = [&](const f3 &lo, const f3 &ld, Hit &lh) {
+                bool paired = false;
+                if constexpr (SPT_LEAF_PAIRS && LEAF == 8 && !LDSN) {
+                    if (scratch && __popcll(mm) <= 64 / LEAF) {
+                        test_leaf_pairs<LEAF>(ac, leaf_slot, mm, lo, ld, lh, scratch, dg);
+                        paired = true;
+                    }
+                }
+                if (!paired) test_leaf<LEAF>(slots, ac.orig, leaf_slot, lo, ld, dot(lo, ld), lh, dg);
+            };
             if (SPT_DUP & 16) {
                 Hit h2 = h;
                 h2.best = opaque_v(h2.best);
-                test_leaf<LEAF>(slots, ac.orig, leaf_slot, opaque_v3(o), opaque_v3(d), dod, h2, dg);
+                leaf_test(opaque_v3(o), opaque_v3(d), h2);
                 sink_v(h2.idx);
                 sink_v(h2.best);
                 sink_v(h2.t);
             }
-            // few lanes need the leaf: deal its (lane, member) pairs (SPT_LEAF_PAIRS)
-            bool paired = false;
-            if constexpr (SPT_LEAF_PAIRS && LEAF == 8 && !LDSN) {
-                if (scratch && __popcll(mm) <= 64 / LEAF) {
-                    test_leaf_pairs<LEAF>(ac, leaf_slot, mm, o, d, h, scratch, dg);
-                    paired = true;
-                }
-            }
-            if (!paired) test_leaf<LEAF>(slots, ac.orig, leaf_slot, o, d, dod, h, dg);
+            leaf_test(o, d, h);
             sbl = near_bound(h.best);
         }
         const uint32_t next = (mm != 0ull && !leaf) ? i + 1 : skip;

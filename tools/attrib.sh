@@ -37,7 +37,11 @@ for lib in libs:
     for f in glob.glob(os.path.join(out, lib[:-3], "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
             if "spt::render_kernel<" in r["Kernel_Name"]:
-                agg.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
+                agg.setdefault(r["Counter_Name"], []).append((r.get("Dispatch_Id", ""), float(r["Counter_Value"])))
+    # bench.py's one-row probe launch is a render_kernel dispatch too: frames only (VALU
+    # above 1% of the largest dispatch's)
+    big = {d for d, v in agg.get("SQ_INSTS_VALU", []) if v > 0.01 * max(x for _, x in agg["SQ_INSTS_VALU"])}
+    agg = {c: [v for d, v in xs if d in big] for c, xs in agg.items()}
     res[lib] = {k: sum(v) / len(v) for k, v in agg.items()}
     res[lib]["launches"] = len(agg.get("SQ_INSTS_VALU", []))
 base = res[libs[0]]

@@ -18,7 +18,10 @@
 #          dropin1      the same with SPT_SERVICE=1 (the shim's calls through the render service)
 #          profile      tools/profile.sh <tag>_c2 c2 (kernel trace + PMC passes + SPT_DIAG)
 #          profile5     tools/profile.sh <tag>_c5 c5 --config c5 --steps 2 --warmup 1 ...
+#          profile3     the same for config 3 (3840x2160, 1024 spp)
+#          tdrop        tools/trace_dropin.sh (kernel trace of the C++ drop-in at tc = 4)
 #          attrib       tools/attrib.sh (per-phase VALU from the SPT_DUP builds)
+#          benchenv:V=X,W=Y  benchq with those environment variables (logs benchenv1, 2, ...)
 #          ab:<args>    tools/ab.py <args> (one quoted step; logs ab1, ab2, ...)
 set -o pipefail
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
@@ -71,8 +74,17 @@ for step in "$@"; do
     dropin) run dropin 300 python -c "import bench; print(bench.dropin_bench(1200, 800, 100, 50, 20, (4, 32)))" ;;
     dropin1) run dropin1 300 python -c "import bench; print(bench.dropin_bench(1200, 800, 100, 50, 20, (4, 32), {'SPT_SERVICE': '1'}))" ;;
     profile) run profile 900 bash tools/profile.sh "${TAG}_c2" c2 ;;
-    profile5) run profile5 900 bash tools/profile.sh "${TAG}_c5" c5 --config c5 --steps 2 --warmup 1 --no-cpu-baseline ;;
+    profile5) run profile5 900 bash tools/profile.sh "${TAG}_c5" c5 --config c5 --steps 2 --warmup 1 --no-cpu-baseline --no-dropin ;;
     attrib) run attrib 600 bash tools/attrib.sh "${TAG}_attrib" ;;
+    benchenv:*) NBE=$((${NBE:-0} + 1)); (for kv in $(echo "${step#benchenv:}" | tr ',' ' '); do export "$kv"; done
+                run benchenv$NBE 120 python bench.py --no-cpu-baseline --no-dropin) ;;
+    bench1env:*) NB1=$((${NB1:-0} + 1)); (for kv in $(echo "${step#bench1env:}" | tr ',' ' '); do export "$kv"; done
+                run bench1env$NB1 120 python bench.py --no-cpu-baseline --no-dropin --service 1) ;;
+    tlenv:*) NTL=$((${NTL:-0} + 1)); (for kv in $(echo "${step#tlenv:}" | tr ',' ' '); do export "$kv"; done
+                run tlenv$NTL 300 python tools/svc_timeline.py --n 1 --frames 20 --service 1 --reps 2) ;;
+    streams3) run streams3 120 python bench.py --no-cpu-baseline --no-dropin --streams 3 ;;
+    profile3) run profile3 1100 bash tools/profile.sh "${TAG}_c3" c3 --config c3 --steps 2 --warmup 1 --no-cpu-baseline --no-dropin ;;
+    tdrop) run tdrop 200 bash tools/trace_dropin.sh ;;
     ab:*) NAB=$((${NAB:-0} + 1)); run ab$NAB 600 python tools/ab.py ${step#ab:} ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac

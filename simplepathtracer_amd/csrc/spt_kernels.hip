@@ -681,8 +681,16 @@ __device__ __forceinline__ void render_body(const RenderArgs &a)
             // a primary batch casts against its block's candidate list when there is one
             // (prim_list_cast); every other cast walks the tree
             bool listed = false;
-            if (prim_iter && kernarg_args()->prim.on)
+            if (prim_iter && kernarg_args()->prim.on) {
+                if (SPT_DUP & 64) {
+                    Hit h2;
+                    prim_list_cast(a.scene.accel, opaque_v3(ps.o), opaque_v3(ps.d), act, pxy, h2, dg);
+                    sink_v(h2.idx);
+                    sink_v(h2.best);
+                    sink_v(h2.t);
+                }
                 listed = prim_list_cast(a.scene.accel, ps.o, ps.d, act, pxy, h, dg);
+            }
             if (!listed)
                 h = find_closest<TREE, LEAF, LDSN>(a.scene.accel, ps.o, ps.d, act, dg, (const uint32_t *)s_nodes,
                                                    s_lds + (threadIdx.x & ~63u));

@@ -24,7 +24,9 @@
 // phase a second time on opaque copies of its inputs and discards the result, so the
 // difference in SQ_INSTS_VALU per launch against the product build is that phase's
 // instruction count.  Bits: 1 the whole cast, 2 the cooperative sampler, 4 the primary
-// ray (start_path), 8 the tree node test, 16 the member tests + updates of entered leaves.
+// ray (start_path), 8 the tree node test, 16 the member tests + updates of entered leaves,
+// 32 the always-tested group, 64 the primary batches' candidate-list casts, 128 the
+// shading step less the sampler.
 #ifndef SPT_DUP
 #define SPT_DUP 0
 #endif
@@ -450,6 +452,14 @@ __device__ __forceinline__ Hit find_closest(const AccelView &ac, const f3 &o, co
             float4 g4[SPT_GROUP];
 #pragma unroll
             for (int k = 0; k < SPT_GROUP; ++k) g4[k] = ld_uniform(slots, g * SPT_GROUP + k);
+            if (SPT_DUP & 32) {
+                Hit h2 = h;
+                h2.best = opaque_v(h2.best);
+                test_group<SPT_GROUP>(g4, ac.orig, g * SPT_GROUP, opaque_v3(o), opaque_v3(d), dod, h2, dg);
+                sink_v(h2.idx);
+                sink_v(h2.best);
+                sink_v(h2.t);
+            }
             test_group<SPT_GROUP>(g4, ac.orig, g * SPT_GROUP, o, d, dod, h, dg);
         }
     }
@@ -1130,10 +1140,10 @@ __device__ __forceinline__ void finish_step(uint32_t mode, uint32_t *samples, Pa
 // bounce loop (21-37) in PH_DLOOP.  Finishing paths write their sample slot.
 // Called by every lane of the wave (`act` = the lane holds a path), so the
 // cooperative cube-minus-ball sampler runs in uniform control flow.
-template <bool KARG = false, bool WT = false>
-__device__ __forceinline__ void shade_step(const RenderArgs &a, Path &ps, const Hit &h, bool act,
-                                           unsigned long long &done, unsigned long long &dropped, uint32_t *lds,
-                                           unsigned long long *diag_rounds = nullptr)
+template <bool KARG, bool WT, bool SAMPLER>
+__device__ __forceinline__ void shade_step_body(const RenderArgs &a, Path &ps, const Hit &h, bool act,
+                                                unsigned long long &done, unsigned long long &dropped, uint32_t *lds,
+                                                unsigned long long *diag_rounds)
 {
     // hit, shade and material tables are in slot order (spt_accel.cpp)
     const float4 *__restrict__ hit = a.scene.accel.slots;
@@ -1189,8 +1199,9 @@ __device__ __forceinline__ void shade_step(const RenderArgs &a, Path &ps, const 
         }
     }
     bool spec_event = false;
-    const f3 rv_coop = coop_ball_vector(ps.st, scatter, lds, diag_rounds);
-    if (SPT_DUP & 2) {
+    // (SAMPLER = false: SPT_DUP attribution's copy of the step, without the sampler)
+    const f3 rv_coop = SAMPLER ? coop_ball_vector(ps.st, scatter, lds, diag_rounds) : opaque_v3(mk(0.1f, 0.2f, 0.3f));
+    if ((SPT_DUP & 2) && SAMPLER) {
         uint64_t st2 = opaque_v(ps.st);
         const f3 r2 = coop_ball_vector(st2, opaque_v(scatter ? 1u : 0u) != 0u, lds);
         sink_v(r2.x);
@@ -1226,6 +1237,27 @@ __device__ __forceinline__ void shade_step(const RenderArgs &a, Path &ps, const 
         spec_event = true;
     }
     finish_step<WT>(mode, samples, ps, fin, spec_event, refr, !dl, word, done, dropped);
+}
+template <bool KARG = false, bool WT = false>
+__device__ __forceinline__ void shade_step(const RenderArgs &a, Path &ps, const Hit &h, bool act,
+                                           unsigned long long &done, unsigned long long &dropped, uint32_t *lds,
+                                           unsigned long long *diag_rounds = nullptr)
+{
+    if (SPT_DUP & 128) {
+        // attribution: the shading step less the sampler, a second time on a copy of the path
+        // (its sample stores go to an opaque null-offset copy of the same words: same values)
+        Path p2 = ps;
+        p2.o = opaque_v3(p2.o);
+        p2.d = opaque_v3(p2.d);
+        Hit h2 = h;
+        h2.t = opaque_v(h2.t);
+        unsigned long long d2 = 0, x2 = 0;
+        shade_step_body<KARG, WT, false>(a, p2, h2, act, d2, x2, lds, nullptr);
+        sink_v(p2.o.x);
+        sink_v(p2.d.x);
+        sink_v(p2.st);
+    }
+    shade_step_body<KARG, WT, true>(a, ps, h, act, done, dropped, lds, diag_rounds);
 }
 
 

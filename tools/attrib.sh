@@ -5,14 +5,14 @@
 # discards the copy) -- over the same short bench command; the difference in VALU per
 # render launch is the duplicated phase's instruction count.
 # Build first (build host): make -C simplepathtracer_amd/csrc variants \
-#   VARIANTS="dup1:-DSPT_DUP=1 dup2:-DSPT_DUP=2 dup4:-DSPT_DUP=4 dup8:-DSPT_DUP=8 dup16:-DSPT_DUP=16"
+#   VARIANTS="$(for b in 1 2 4 8 16 32 64 128; do echo -n "dup$b:-DSPT_DUP=$b "; done)"
 # Usage (GPU box): tools/attrib.sh <tag> [lib ...]
 set -o pipefail
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 TAG=${1:-attrib}
 shift
 LIBS="$*"
-[ -z "$LIBS" ] && LIBS="libspt_hip.so libspt_hip_dup1.so libspt_hip_dup2.so libspt_hip_dup4.so libspt_hip_dup8.so libspt_hip_dup16.so"
+[ -z "$LIBS" ] && LIBS="libspt_hip.so $(for b in 1 2 4 8 16 32 64 128; do echo libspt_hip_dup$b.so; done)"
 OUT="$R/gpurun_out/$TAG"
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp

@@ -10,7 +10,10 @@ ROWS = [("cast: whole FindClosestIntersectionSphere (list or tree walk, always-l
         ("  tree node tests (box slabs, near / front bounds)", "libspt_hip_dup8.so"),
         ("  member tests + closest-contact updates of entered leaves", "libspt_hip_dup16.so"),
         ("cube-minus-ball sampler (coop_ball_vector, splitmix draws)", "libspt_hip_dup2.so"),
-        ("primary ray (start_path: keyed RNG, jitter, camera, normalize)", "libspt_hip_dup4.so")]
+        ("primary ray (start_path: keyed RNG, jitter, camera, normalize)", "libspt_hip_dup4.so"),
+        ("  (of the cast) the always-tested group (ground, big balls)", "libspt_hip_dup32.so"),
+        ("  (of the cast) the primary batches' candidate-list casts", "libspt_hip_dup64.so"),
+        ("shading step less the sampler", "libspt_hip_dup128.so")]
 dst = sys.argv[1]
 out = ["# Per-phase VALU attribution of the config-2 render kernel (round 5)", "",
        "Method (`tools/attrib.sh`): one `rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES` pass per library over",
@@ -31,6 +34,8 @@ for arg in sys.argv[2:]:
             f"| whole kernel (product build) | {V:,.0f} | 1.000 | {V / ITERS:.0f} | {V * 64 / RAYS:.0f} | {S:,.0f} |"]
     dv = {}
     for name, lib in ROWS:
+        if lib not in res:
+            continue
         dv[lib] = res[lib]["SQ_INSTS_VALU"] - V
         ds = res[lib]["SQ_INSTS_SALU"] - S
         out.append(f"| {name} | {dv[lib]:,.0f} | {dv[lib] / V:.3f} | {dv[lib] / ITERS:.0f} | {dv[lib] * 64 / RAYS:.0f} | {ds:,.0f} |")

@@ -1193,6 +1193,7 @@ int render_impl(spt_ctx *ctx, int mode, const spt::RowMap &map, float4 *d_rgba, 
         EventPair ef = get_pair(ctx);
         // double-buffered: fold j after fold j-1 (the other stream; shared accumulator)
         if (s2 && j > 0) HIP_TRY(ctx, hipStreamWaitEvent(s, ctx->dbuf_fold, 0));
+        fa.prio = use_svc ? 0 : 1;
         HIP_TRY(ctx, hipEventRecord(ef.a, s));
         HIP_TRY(ctx, spt::launch_fold(fa, s));
         HIP_TRY(ctx, hipEventRecord(ef.b, s));

@@ -419,6 +419,7 @@ struct FoldArgs {
     uint32_t s_done;     // samples folded after this batch (s0 + spp_batch)
     int first, last, mode;
     int preview;         // write the outputs after every batch (progressive rendering)
+    int prio;            // fold_kernel raises its waves' priority (launched renders; not beside the service)
     int alias;           // task mode, one non-square rectangle: RenderSegmentTask's colorIndex
                          // (dx + dy * segmentHeight, TaskBasedPathTracer.hpp:103,186) aliases pixels
     const BatchRect *rects;  // batched fold: n_rects rectangles over npix = their total pixels

@@ -1081,6 +1081,13 @@ __device__ __forceinline__ void fold_pixel(const FoldArgs &a, const uint32_t *sa
 // a wave read 64 consecutive slots per sample.
 __global__ __launch_bounds__(256) void fold_kernel(FoldArgs a)
 {
+    // a launched render's fold runs beside the next frame's persistent render launch, whose
+    // waves are older and win the SIMDs' issue arbitration: at the default priority the
+    // fold's waves stalled for 2.8 ms (config 2) and the caller's next render waited on them;
+    // at priority 3 the fold takes 0.6 ms and the bench gains 0.8%.  Beside
+    // the render service nothing waits to start after a fold, and the raised priority only
+    // took issue cycles from the service's waves (-1.5%): FoldArgs::prio is 0 there.
+    if (a.prio) __builtin_amdgcn_s_setprio(3);
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= a.npix) return;
     const uint32_t rows = a.npix / a.map.width;

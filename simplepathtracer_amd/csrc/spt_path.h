@@ -31,9 +31,9 @@
 #define SPT_DUP 0
 #endif
 // wave walk: leaves entered by at most 8 lanes are tested as dealt (lane, member) pairs
-// (test_leaf_pairs)
+// (test_leaf_pairs); 2: also those entered by 9-16 lanes, two members per lane
 #ifndef SPT_LEAF_PAIRS
-#define SPT_LEAF_PAIRS 1
+#define SPT_LEAF_PAIRS 2
 #endif
 
 // Item order of a batch: [band][8x8 tile][sample][pixel] (ts_item, spt_internal.h)
@@ -336,20 +336,29 @@ __device__ __forceinline__ void pair_min_step(float &cds, uint32_t &cor, uint32_
     csl = take ? psl : csl;
     ct = take ? pt : ct;
 }
-template <int LEAF>
+// PER members per lane (1: groups of 8 lanes per owner, at most 8 owners; 2: groups of 4
+// lanes, at most 16 owners, each lane testing members m and m + 4 and keeping the lesser
+// candidate before the two butterflies).
+template <int LEAF, int PER>
 __device__ __forceinline__ void test_leaf_pairs(const AccelView &ac, uint32_t leaf_slot, unsigned long long mm,
                                                 const f3 &o, const f3 &d, Hit &h, uint32_t *scratch, CastDiag &dg)
 {
-    static_assert(LEAF == 8, "pairs are dealt in groups of 8 lanes");
+    static_assert(LEAF == 8 && (PER == 1 || PER == 2), "pairs are dealt in groups of 8 / PER lanes");
+    constexpr uint32_t G = 8 / PER, LG = PER == 1 ? 3 : 2;
     const uint32_t lane = __lane_id();
     const uint32_t rank = lane_rank(mm);
     const bool owner = __builtin_amdgcn_inverse_ballot_w64(mm);
     if (owner) scratch[rank] = lane;
-    const uint32_t q = lane >> 3, s = leaf_slot + (lane & 7u);
+    const uint32_t q = lane >> LG, s0 = leaf_slot + (lane & (G - 1u));
     const bool valid = q < (uint32_t)__popcll(mm);
-    // the member's record and original index (vector loads, issued before the shuffles)
-    const float4 sp = ac.slots[s];
-    const uint32_t so = ac.orig[s];
+    // the members' records and original indices (vector loads, issued before the shuffles)
+    float4 sp[PER];
+    uint32_t so[PER];
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        sp[j] = ac.slots[s0 + j * G];
+        so[j] = ac.orig[s0 + j * G];
+    }
     const uint32_t src = scratch[valid ? q : 0u];
     const f3 po = mk(__shfl(o.x, (int)src), __shfl(o.y, (int)src), __shfl(o.z, (int)src));
     const f3 pd = mk(__shfl(d.x, (int)src), __shfl(d.y, (int)src), __shfl(d.z, (int)src));
@@ -357,25 +366,48 @@ __device__ __forceinline__ void test_leaf_pairs(const AccelView &ac, uint32_t le
         dg.spheres += LEAF;
         dg.lane_tests += (unsigned long long)LEAF * __popcll(mm);
     }
-    float tc, hh;
-    const bool pass = valid && ray_sphere(sp, po, pd, tc, hh);
-    if (__ballot(pass) == 0ull) return;
+    float tc[PER], hh[PER];
+    bool pass[PER];
+    unsigned long long anyp = 0ull;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        pass[j] = valid && ray_sphere(sp[j], po, pd, tc[j], hh[j]);
+        anyp |= __ballot(pass[j]);
+    }
+    if (anyp == 0ull) return;
     if (SPT_DIAG) dg.branches += 1;
-    // update_member's arithmetic for the pair (Collision.hpp:19-27,49-56)
-    const float t = tc - sqrt_pos_normal(hh);
-    const f3 p = contact(po, pd, t);
-    const bool ok = pass && dot(po, pd) < dot(p, pd);
-    const float dv = lensq(sub(po, p));
-    float cds = ok && dv == dv ? dv : INFINITY;
-    uint32_t cor = so, csl = s;
-    float ct = t;
-    // lexicographic (distance, original index) minimum within each group of 8 lanes:
-    // quad_perm [1,0,3,2], quad_perm [2,3,0,1], row_half_mirror
+    // update_member's arithmetic for each pair (Collision.hpp:19-27,49-56); the lane keeps
+    // its lexicographic (distance, original index) minimum
+    const float pdod = dot(po, pd);
+    float cds = INFINITY, ct = 0.f;
+    uint32_t cor = 0xFFFFFFFFu, csl = 0u;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        const float t = tc[j] - sqrt_pos_normal(hh[j]);
+        const f3 p = contact(po, pd, t);
+        const bool ok = pass[j] && pdod < dot(p, pd);
+        const float dv = lensq(sub(po, p));
+        const float jds = ok && dv == dv ? dv : INFINITY;
+        if (j == 0) {
+            cds = jds;
+            cor = so[0];
+            csl = s0;
+            ct = t;
+        } else {
+            const bool take = jds < cds || (jds == cds && so[j] < cor);
+            cds = take ? jds : cds;
+            cor = take ? so[j] : cor;
+            csl = take ? s0 + j * G : csl;
+            ct = take ? t : ct;
+        }
+    }
+    // the minimum within each group of G lanes: quad_perm [1,0,3,2], quad_perm [2,3,0,1],
+    // and for groups of 8 row_half_mirror
     pair_min_step<0xB1>(cds, cor, csl, ct);
     pair_min_step<0x4E>(cds, cor, csl, ct);
-    pair_min_step<0x141>(cds, cor, csl, ct);
+    if (G == 8) pair_min_step<0x141>(cds, cor, csl, ct);
     // each owner takes its group's minimum and merges it like update_member
-    const int from = (int)(rank << 3);
+    const int from = (int)(rank << LG);
     const float gds = __shfl(cds, from), gt = __shfl(ct, from);
     const uint32_t gor = (uint32_t)__shfl((int)cor, from), gsl = (uint32_t)__shfl((int)csl, from);
     unsigned long long bm = mm & __ballot(gds < h.best);
@@ -654,8 +686,12 @@ __device__ __forceinline__ Hit find_closest(const AccelView &ac, const f3 &o, co
             auto leaf_test = [&](const f3 &lo, const f3 &ld, Hit &lh) {
                 bool paired = false;
                 if constexpr (SPT_LEAF_PAIRS && LEAF == 8 && !LDSN) {
-                    if (scratch && __popcll(mm) <= 64 / LEAF) {
-                        test_leaf_pairs<LEAF>(ac, leaf_slot, mm, lo, ld, lh, scratch, dg);
+                    const uint32_t nm = (uint32_t)__popcll(mm);
+                    if (scratch && nm <= 8u) {
+                        test_leaf_pairs<LEAF, 1>(ac, leaf_slot, mm, lo, ld, lh, scratch, dg);
+                        paired = true;
+                    } else if (SPT_LEAF_PAIRS >= 2 && scratch && nm <= 16u) {
+                        test_leaf_pairs<LEAF, 2>(ac, leaf_slot, mm, lo, ld, lh, scratch, dg);
                         paired = true;
                     }
                 }

@@ -1539,6 +1539,7 @@ int launch_batch(spt_ctx *ctx, BatchSet *bs, const std::vector<BatchReq *> &batc
         for (size_t i = 0; i < n; ++i) fa.rects_inline[i] = bs->h_rects[i];
     fa.head_reset = !use_svc ? w->d_head : nullptr;
     fa.head_queues = ra.n_queues;
+    fa.prio = use_svc ? 0 : 1;
     EventPair ef = get_pair(ctx);
     HIP_TRY(ctx, hipEventRecord(ef.a, s));
     HIP_TRY(ctx, spt::launch_fold(fa, s));
@@ -1663,6 +1664,59 @@ int spec_drain(spt_ctx *ctx)
     return SPT_OK;
 }
 
+// The stream of read-ahead part p (created on first use).  The parts' streams take the
+// least priority (SPT_READAHEAD_PRIO overrides): a priority the callers' streams do not
+// use gives the parts hardware queues of their own, so a part's render does not queue
+// behind another part's fold (tc = 4: 5.75-6.04 -> 5.48-5.60 ms per frame in segment mode).
+int spec_stream(spt_ctx *ctx, int p)
+{
+    SpecFrame &sp = ctx->spec;
+    BatchSet *bs = &sp.bs[p];
+    if (!bs->stream) {
+        int lo = 0, hi = 0;
+        HIP_TRY(ctx, hipDeviceGetStreamPriorityRange(&lo, &hi));
+        int prio = lo;
+        if (const char *e = env_var("SPT_READAHEAD_PRIO")) prio = std::atoi(e);
+        HIP_TRY(ctx, hipStreamCreateWithPriority(&bs->stream, hipStreamNonBlocking, prio));
+    }
+    if (!sp.ev[p]) HIP_TRY(ctx, hipEventCreateWithFlags(&sp.ev[p], hipEventDisableTiming));
+    return SPT_OK;
+}
+
+// The buffers the read-ahead of a tc x tc tiling will use (its parts' streams, rectangle
+// tables and sample-word workspaces, the frame's device bytes), allocated when the tiling
+// arms: allocated by the first read-ahead itself, each part's first allocations held its
+// launch until the previous part's render had ended (the four parts of the first read-ahead
+// frame ran one after another, 15 ms apart, profiles/r05_dropin_trace.md).
+int spec_prepare(spt_ctx *ctx, int mode, uint32_t tc)
+{
+    SpecFrame &sp = ctx->spec;
+    const uint32_t W = ctx->W, H = ctx->H, sw = W / tc, sh = H / tc;
+    const uint32_t slot_words = mode == SPT_MODE_SEGMENT ? 1u : 2u;
+    int rc = ensure(ctx, &sp.d8, &sp.d8_cap, (size_t)W * H * 3);
+    if (rc) return rc;
+    const uint32_t np = std::min(sp.parts, tc), rpp = (tc + np - 1) / np;
+    for (uint32_t p = 0; p * rpp < tc; ++p) {
+        if ((rc = spec_stream(ctx, (int)p))) return rc;
+        BatchSet *bs = &sp.bs[p];
+        const size_t tiles = (size_t)(std::min(tc, (p + 1) * rpp) - p * rpp) * tc;
+        if (bs->h_rects_cap < tiles) {
+            if ((rc = svc_end(ctx))) return rc;
+            const size_t cap = std::max<size_t>(tiles, 64);
+            if (bs->h_rects) HIP_TRY(ctx, hipHostFree(bs->h_rects));
+            bs->h_rects = nullptr;
+            bs->h_rects_cap = 0;
+            HIP_TRY(ctx, hipHostMalloc((void **)&bs->h_rects, cap * sizeof(spt::BatchRect)));
+            bs->h_rects_cap = cap;
+        }
+        if ((rc = ensure(ctx, &bs->d_rects, &bs->rects_cap, tiles))) return rc;
+        Workspace *w = workspace_for(ctx, bs->stream);
+        if (!w) return SPT_ERR_STATE;
+        if ((rc = ensure(ctx, &w->d_samples, &w->samples_cap, tiles * sw * sh * ctx->spp * slot_words))) return rc;
+    }
+    return SPT_OK;
+}
+
 // Render every tile of the tc x tc tiling of `mode` (MakeRenderSegmentData order) into the
 // read-ahead frame, in sp.parts batched launches.  Called with lk (ctx->mu) held; waits
 // (unlocked) for the previous frame's serves still copying out of d8.
@@ -1686,18 +1740,7 @@ int spec_launch(spt_ctx *ctx, std::unique_lock<std::mutex> &lk, int mode, uint32
         for (uint32_t j = p * rpp; j < std::min(tc, (p + 1) * rpp); ++j)
             for (uint32_t i = 0; i < tc; ++i) part.push_back(&reqs[(size_t)j * tc + i]);
         BatchSet *bs = &sp.bs[p];
-        if (!bs->stream) {
-            // the parts' streams take the least priority (SPT_READAHEAD_PRIO overrides): a
-            // priority the callers' streams do not use gives the parts hardware queues of
-            // their own, so a part's render does not queue behind another part's fold
-            // (tc = 4: 5.75-6.04 -> 5.48-5.60 ms per frame in segment mode)
-            int lo = 0, hi = 0;
-            HIP_TRY(ctx, hipDeviceGetStreamPriorityRange(&lo, &hi));
-            int prio = lo;
-            if (const char *e = env_var("SPT_READAHEAD_PRIO")) prio = std::atoi(e);
-            HIP_TRY(ctx, hipStreamCreateWithPriority(&bs->stream, hipStreamNonBlocking, prio));
-        }
-        if (!sp.ev[p]) HIP_TRY(ctx, hipEventCreateWithFlags(&sp.ev[p], hipEventDisableTiming));
+        if ((rc = spec_stream(ctx, (int)p))) return rc;
         if ((rc = launch_batch(ctx, bs, part, sp.d8))) return rc;
         HIP_TRY(ctx, hipEventRecord(sp.ev[p], bs->stream));
         sp.launched[p] = true;
@@ -1755,6 +1798,11 @@ int spec_serve(spt_ctx *ctx, std::unique_lock<std::mutex> &lk, int mode, uint32_
             if (!seen) {
                 seen = 1;
                 sp.armed = ++sp.arm_count == tc * tc;
+                // the read-ahead's buffers now, while this frame's tiles render as usual
+                if (sp.armed) {
+                    const int rc = spec_prepare(ctx, mode, tc);
+                    if (rc) return rc;
+                }
             }
             return kSpecMiss;
         }

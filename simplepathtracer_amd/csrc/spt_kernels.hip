@@ -1100,6 +1100,7 @@ __global__ __launch_bounds__(256) void fold_kernel(FoldArgs a)
 // float4 output at out_rgba[t] (g_data is written by the assemble step).
 __global__ __launch_bounds__(256) void fold_alias_range_kernel(FoldArgs a)
 {
+    if (a.prio) __builtin_amdgcn_s_setprio(3);  // as fold_kernel
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= a.npix) return;
     float4 acc = a.first ? make_float4(0.f, 0.f, 0.f, 0.f) : a.acc[t];
@@ -1128,6 +1129,10 @@ __device__ __forceinline__ uint32_t fold_rect(crect_k *rs, uint32_t n, uint32_t 
 // 0 also zeroes the render's claim counters for the workspace's next batch.
 __global__ __launch_bounds__(256) void fold_kernel_batch(FoldArgs a)
 {
+#ifndef SPT_FOLD_PRIO_BATCH
+#define SPT_FOLD_PRIO_BATCH 1
+#endif
+    if (SPT_FOLD_PRIO_BATCH && a.prio) __builtin_amdgcn_s_setprio(3);  // as fold_kernel
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (blockIdx.x == 0 && a.head_reset && threadIdx.x < a.head_queues) a.head_reset[threadIdx.x * kQueueStride] = 0u;
     if (i >= a.npix) return;

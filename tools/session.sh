@@ -50,6 +50,7 @@ for step in "$@"; do
     rw) SPT_SVC_DEBUG=1 run rw 120 python -u -m pytest -x -v -s --timeout 60 --timeout-method thread tests/test_gpu_service.py -k ring_wrap ;;
     diag) SPT_LIB=libspt_hip_diag.so run diag 200 python tools/diag.py c2 --json "gpurun_out/${TAG}_diag_c2.json" ;;
     diag5) SPT_LIB=libspt_hip_diag.so run diag5 300 python tools/diag.py c5 --json "gpurun_out/${TAG}_diag_c5.json" ;;
+    ra) run ra 300 $PYT -v tests/test_gpu_readahead.py ;;
     pl) run pl 300 $PYT -v -m gpu tests/test_gpu_parity.py -k primary_lists ;;
     benchq_nol) SPT_PRIM_LISTS=0 run benchq_nol 120 python bench.py --no-cpu-baseline --no-dropin ;;
     diag5_nol) SPT_PRIM_LISTS=0 SPT_LIB=libspt_hip_diag.so run diag5_nol 300 python tools/diag.py c5 --json "gpurun_out/${TAG}_diag_nol_c5.json" ;;
@@ -72,6 +73,9 @@ for step in "$@"; do
     scaling) run scaling 300 python tools/scaling_probe.py --streams 2 --reps 5 --service 1 --record "gpurun_out/${TAG}_scaling.txt"
              run scaling0 300 python tools/scaling_probe.py --streams 2 --reps 5 --service 0 --record "gpurun_out/${TAG}_scaling0.txt" ;;
     dropin) run dropin 300 python -c "import bench; print(bench.dropin_bench(1200, 800, 100, 50, 20, (4, 32)))" ;;
+    dropin4) NDI=$((${NDI:-0} + 1)); run dropin4_$NDI 300 python -c "import bench; print(bench.dropin_bench(1200, 800, 100, 50, 20, (4,)))" ;;
+    dropinenv:*) NDE=$((${NDE:-0} + 1)); (for kv in $(echo "${step#dropinenv:}" | tr ',' ' '); do export "$kv"; done
+                run dropinenv$NDE 300 python -c "import bench; print(bench.dropin_bench(1200, 800, 100, 50, 20, (4,)))") ;;
     dropin1) run dropin1 300 python -c "import bench; print(bench.dropin_bench(1200, 800, 100, 50, 20, (4, 32), {'SPT_SERVICE': '1'}))" ;;
     profile) run profile 900 bash tools/profile.sh "${TAG}_c2" c2 ;;
     profile5) run profile5 900 bash tools/profile.sh "${TAG}_c5" c5 --config c5 --steps 2 --warmup 1 --no-cpu-baseline --no-dropin ;;
@@ -85,6 +89,7 @@ for step in "$@"; do
     streams3) run streams3 120 python bench.py --no-cpu-baseline --no-dropin --streams 3 ;;
     profile3) run profile3 1100 bash tools/profile.sh "${TAG}_c3" c3 --config c3 --steps 2 --warmup 1 --no-cpu-baseline --no-dropin ;;
     tdrop) run tdrop 200 bash tools/trace_dropin.sh ;;
+    tdrop20) TDROP_FRAMES=20 run tdrop20 200 bash tools/trace_dropin.sh ;;
     ab:*) NAB=$((${NAB:-0} + 1)); run ab$NAB 600 python tools/ab.py ${step#ab:} ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac

@@ -6,4 +6,4 @@ OUT="$R/gpurun_out/tdrop"
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 -s KILL 120 rocprofv3 --kernel-trace --output-format csv -d "$OUT" -o run -- \
-  "$R/simplepathtracer_amd/lib/spt_dropin_harness" /dev/null 1200 800 100 50 4 0 3 > "$OUT/run.log" 2>&1
+  "$R/simplepathtracer_amd/lib/spt_dropin_harness" /dev/null 1200 800 100 50 4 0 ${TDROP_FRAMES:-3} > "$OUT/run.log" 2>&1

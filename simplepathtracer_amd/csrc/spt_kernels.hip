@@ -672,6 +672,18 @@ __device__ __forceinline__ void render_body(const RenderArgs &a)
         bool cdone = true;
         Hit h;
         if constexpr (RES) {
+            if (SPT_DUP & 512) {
+                Hit h2 = hres;
+                h2.best = opaque_v(h2.best);
+                uint32_t li2 = opaque_v(li), ll2 = lleaf, ll22 = lleaf2;
+                const bool c2 = lane_cast<LEAF, LDS_BYTES>(a.scene.accel, opaque_v3(ps.o), opaque_v3(ps.d), act, dg,
+                                    LDSN ? (const uint32_t *)s_nodes : (const uint32_t *)a.scene.accel.nodes, fresh,
+                                    (uint32_t)SPT_LANE_BUDGET, h2, li2, ll2, ll22);
+                sink_v(h2.idx);
+                sink_v(h2.best);
+                sink_v(li2);
+                sink_v(c2 ? 1u : 0u);
+            }
             cdone = lane_cast<LEAF, LDS_BYTES>(a.scene.accel, ps.o, ps.d, act, dg,
                                     LDSN ? (const uint32_t *)s_nodes : (const uint32_t *)a.scene.accel.nodes, fresh,
                                     (uint32_t)SPT_LANE_BUDGET, hres, li, lleaf, lleaf2);

@@ -26,7 +26,7 @@
 // instruction count.  Bits: 1 the whole cast, 2 the cooperative sampler, 4 the primary
 // ray (start_path), 8 the tree node test, 16 the member tests + updates of entered leaves,
 // 32 the always-tested group, 64 the primary batches' candidate-list casts, 128 the
-// shading step less the sampler.
+// shading step less the sampler, 256 the refraction event, 512 the lane walk (lane_cast).
 #ifndef SPT_DUP
 #define SPT_DUP 0
 #endif
@@ -1269,6 +1269,14 @@ __device__ __forceinline__ void shade_step_body(const RenderArgs &a, Path &ps, c
     }
     if (refr) {
         ps.o = contact(ps.o, ps.d, h.t);
+        if (SPT_DUP & 256) {
+            Path p2 = ps;
+            p2.o = opaque_v3(p2.o);
+            refract_event(hit, p2, idx);
+            sink_v(p2.d.x);
+            sink_v(p2.o.x);
+            sink_v(p2.st);
+        }
         refract_event(hit, ps, idx);
         spec_event = true;
     }

@@ -22,7 +22,7 @@ for lib in $LIBS; do
   mkdir -p "$d"
   echo "== $lib"
   SPT_LIB=$lib timeout -k 10 -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES --output-format csv \
-    -d "$d" -o run -- python3 "$R/bench.py" --steps 4 --warmup 1 --no-cpu-baseline --no-dropin --service 0 \
+    -d "$d" -o run -- python3 "$R/bench.py" ${ATTRIB_ARGS:---steps 4 --warmup 1} --no-cpu-baseline --no-dropin --service 0 \
     > "$d/log" 2>&1
   rc=$?
   echo "== $lib rc=$rc"
@@ -36,7 +36,7 @@ for lib in libs:
     agg = {}
     for f in glob.glob(os.path.join(out, lib[:-3], "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            if "spt::render_kernel<" in r["Kernel_Name"]:
+            if "spt::render_kernel" in r["Kernel_Name"]:
                 agg.setdefault(r["Counter_Name"], []).append((r.get("Dispatch_Id", ""), float(r["Counter_Value"])))
     # bench.py's one-row probe launch is a render_kernel dispatch too: frames only (VALU
     # above 1% of the largest dispatch's)

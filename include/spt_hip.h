@@ -168,6 +168,18 @@ SPT_API int spt_set_cluster_size(spt_ctx *ctx, uint32_t k);
  * wave.  Results are identical for any value. */
 #define SPT_TREE_AUTO 0xFFFFFFFFu
 SPT_API int spt_set_cluster_tree(spt_ctx *ctx, uint32_t branching);
+/* Keep `n` CUs free of render launches (0, the default: none).  A launched render then
+ * runs on a stream of ctx's own whose CU mask leaves out the mask's last n bits
+ * (hipExtStreamCreateWithCUMask; the driver deals mask bits out XCC first, then shader
+ * engine, so n = 8 is one CU per XCC and n = 32 one per shader engine on MI355X), ordered
+ * after the caller's stream and before its later work, with a persistent grid sized to
+ * the CUs it may use.  For co-scheduling other work beside a render: a block that needs
+ * a whole CU (RCCL's gfx950 collective kernels: 248-256 VGPRs per wave) waits for room in
+ * the shader engine it is dispatched to, so it starts at once only with one free CU per
+ * engine (DESIGN.md §5 "Reserved CUs": 3.1 ms vs 18.5 ms into a 19 ms render at n = 32;
+ * not bench.py's default -- the multi-rank bench is faster with the render service).
+ * Results are identical for any n; the render service ignores it.  n < the CU count. */
+SPT_API int spt_set_reserved_cus(spt_ctx *ctx, uint32_t n);
 /* Host-only check (no device needed): build the traversal tables for a scene and
  * verify the properties exactness rests on (every sphere once, preorder/skip
  * structure of all 8 octant layouts, each node's bounding sphere contains every

@@ -258,6 +258,14 @@ struct spt_ctx {
     // the other's samples are folded (render_impl); SPT_BATCH_DBUF=0 turns it off
     bool batch_dbuf = true;
     std::vector<std::pair<hipStream_t, hipStream_t>> companions;  // (caller stream, companion)
+    // spt_set_reserved_cus: launched renders run on CU-masked streams of the context
+    // (masked_for), one per caller stream, with the two events that order them
+    uint32_t reserve_cus = 0;
+    struct Masked {
+        hipStream_t caller, stream;
+        hipEvent_t go, done;
+    };
+    std::vector<Masked> masked;
     hipEvent_t dbuf_start = nullptr, dbuf_fold = nullptr;
     unsigned long long *d_counters = nullptr;
     uint8_t *d_frame8 = nullptr;
@@ -501,7 +509,33 @@ constexpr uint64_t kSmallGridItems = 3072;
 
 uint32_t full_grid(const spt_ctx *ctx)
 {
-    return ctx->ws.size() > 1 ? ctx->grid_overlap : ctx->grid;
+    const uint32_t g = ctx->ws.size() > 1 ? ctx->grid_overlap : ctx->grid;
+    // reserved CUs (spt_set_reserved_cus): the persistent grid of the CUs the launch may use
+    if (ctx->reserve_cus && ctx->num_cu > 0)
+        return std::max<uint32_t>(1u, (uint32_t)((uint64_t)g * (uint32_t)(ctx->num_cu - (int)ctx->reserve_cus) / (uint32_t)ctx->num_cu));
+    return g;
+}
+
+// The CU-masked stream a launched render of caller stream s runs on (spt_set_reserved_cus;
+// created on first use: every CU but the device's last reserve_cus), or nullptr.
+spt_ctx::Masked *masked_for(spt_ctx *ctx, hipStream_t s)
+{
+    if (ctx->reserve_cus == 0) return nullptr;
+    for (spt_ctx::Masked &m : ctx->masked)
+        if (m.caller == s) return &m;
+    if (ctx->masked.size() >= kMaxCompanions) return nullptr;
+    const uint32_t n = (uint32_t)ctx->num_cu, keep = n - ctx->reserve_cus;
+    std::vector<uint32_t> mask((n + 31) / 32, 0u);
+    for (uint32_t i = 0; i < keep; ++i) mask[i / 32] |= 1u << (i % 32);
+    spt_ctx::Masked m{s, nullptr, nullptr, nullptr};
+    if (hipExtStreamCreateWithCUMask(&m.stream, (uint32_t)mask.size(), mask.data()) != hipSuccess) return nullptr;
+    if (hipEventCreateWithFlags(&m.go, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&m.done, hipEventDisableTiming) != hipSuccess) {
+        (void)hipStreamDestroy(m.stream);
+        return nullptr;
+    }
+    ctx->masked.push_back(m);
+    return &ctx->masked.back();
 }
 
 // Items per claim: 256, or 512 for launches of at least 64 Ki items per wave (config 3's
@@ -1078,6 +1112,14 @@ int render_impl(spt_ctx *ctx, int mode, const spt::RowMap &map, float4 *d_rgba, 
     }
     const hipStream_t s_caller = s;
     Workspace *const w_caller = w;
+    // reserved CUs: the launches of this call on the caller stream's CU-masked stream,
+    // ordered after the caller's queued work (and the caller after them, below)
+    spt_ctx::Masked *mk_ = !use_svc && !s2 && !pg ? masked_for(ctx, s) : nullptr;
+    if (mk_) {
+        HIP_TRY(ctx, hipEventRecord(mk_->go, s));
+        HIP_TRY(ctx, hipStreamWaitEvent(mk_->stream, mk_->go, 0));
+        s = mk_->stream;
+    }
 
     spt::RenderArgs ra{};
     ra.scene = device_scene(ctx);
@@ -1208,6 +1250,10 @@ int render_impl(spt_ctx *ctx, int mode, const spt::RowMap &map, float4 *d_rgba, 
     }
     // the caller's stream continues after the last fold (and with it every batch)
     if (s2 && s != s_caller) HIP_TRY(ctx, hipStreamWaitEvent(s_caller, ctx->dbuf_fold, 0));
+    if (mk_) {
+        HIP_TRY(ctx, hipEventRecord(mk_->done, mk_->stream));
+        HIP_TRY(ctx, hipStreamWaitEvent(s_caller, mk_->done, 0));
+    }
     if (ctx->pending_render.size() > 256) return collect_timings(ctx);
     return SPT_OK;
 }
@@ -2156,6 +2202,9 @@ int spt_ctx_create(int device, spt_ctx **out)
         ctx->svc.ring_bytes = (uint64_t)std::max(64, std::atoi(e)) << 20;
         ctx->svc.ring_set = true;
     }
+    // CUs kept free of launched renders (spt_set_reserved_cus)
+    if (const char *e = env_var("SPT_RESERVE_CUS"))
+        ctx->reserve_cus = (uint32_t)std::min(std::max(0, std::atoi(e)), std::max(0, ctx->num_cu - 1));
     // a fraction of the session grid (rehearsing several ranks' sessions on one GPU), the
     // bound on waiting for a session to end, and the publish-delay fault injection of the
     // liveness tests (tests/test_gpu_service.py)
@@ -2277,6 +2326,11 @@ void spt_ctx_destroy(spt_ctx *ctx)
         if (b) (void)hipFree(b);
     if (ctx->frame_ev) (void)hipEventDestroy(ctx->frame_ev);
     for (const auto &c : ctx->companions) (void)hipStreamDestroy(c.second);
+    for (const spt_ctx::Masked &m : ctx->masked) {
+        (void)hipStreamDestroy(m.stream);
+        (void)hipEventDestroy(m.go);
+        (void)hipEventDestroy(m.done);
+    }
     for (hipEvent_t e : {ctx->dbuf_start, ctx->dbuf_fold})
         if (e) (void)hipEventDestroy(e);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -2326,6 +2380,28 @@ int spt_set_cluster_size(spt_ctx *ctx, uint32_t k)
 int spt_set_cluster_tree(spt_ctx *ctx, uint32_t branching)
 {
     return for_members(ctx, [&](spt_ctx *c) { return spt_set_cluster_tree_one(c, branching); });
+}
+
+int spt_set_reserved_cus(spt_ctx *ctx, uint32_t n)
+{
+    return for_members(ctx, [&](spt_ctx *c) -> int {
+        std::lock_guard<std::mutex> lk(c->mu);
+        if (c->num_cu > 0 && n >= (uint32_t)c->num_cu)
+            return fail(c, SPT_ERR_ARG, "%u reserved CUs of %d", n, c->num_cu);
+        if (n != c->reserve_cus) {
+            // streams masked for the old count: retired once their work is done
+            if (int rc = svc_end(c)) return rc;
+            HIP_TRY(c, hipDeviceSynchronize());
+            for (const spt_ctx::Masked &m : c->masked) {
+                (void)hipStreamDestroy(m.stream);
+                (void)hipEventDestroy(m.go);
+                (void)hipEventDestroy(m.done);
+            }
+            c->masked.clear();
+        }
+        c->reserve_cus = n;
+        return SPT_OK;
+    });
 }
 
 int spt_accel_check(const float *centers4, const float *radii, uint32_t n, uint32_t cluster_k, uint32_t branching,

@@ -101,6 +101,12 @@ class Context:
         _native.TREE_AUTO = default heuristic); results identical."""
         self._check(_native.lib().spt_set_cluster_tree(self._h, int(branching)))
 
+    def set_reserved_cus(self, n: int) -> None:
+        """Keep n CUs free of launched renders (spt_set_reserved_cus: 32 = one per shader
+        engine lets a whole-CU kernel on another stream start beside a render); results
+        identical."""
+        self._check(_native.lib().spt_set_reserved_cus(self._h, int(n)))
+
     def set_engine(self, engine: int) -> None:
         """_native.ENGINE_MEGAKERNEL (default) or _native.ENGINE_WAVEFRONT; results identical."""
         self._check(_native.lib().spt_set_engine(self._h, int(engine)))

@@ -36,3 +36,61 @@ extern "C" __attribute__((visibility("default"))) int spt_test_blocker_vgprs(int
     *vgprs = fa.numRegs;
     return 0;
 }
+
+// Placement probes for the reserved-CU tests (tests/test_gpu_reserve.py, tools/cu_mask_probe.py):
+// each block's first thread records HW_ID (gfx9: wave[3:0] simd[5:4] cu[11:8] sh[12]
+// se[15:13]), XCC_ID and its start time (100 MHz ticks), then the block spins `us`.
+__device__ inline void record_where(uint32_t *where, unsigned long long t0)
+{
+    if (where && threadIdx.x == 0) {
+        where[4 * blockIdx.x + 0] = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_REG_HW_ID
+        where[4 * blockIdx.x + 1] = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // HW_REG_XCC_ID
+        where[4 * blockIdx.x + 2] = (uint32_t)t0;
+        where[4 * blockIdx.x + 3] = (uint32_t)(t0 >> 32);
+    }
+}
+
+__global__ __launch_bounds__(512) void blocker_where_kernel(uint32_t us, uint32_t *where)
+{
+    asm volatile("" ::: "v255");
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    record_where(where, t0);
+    while (__builtin_amdgcn_s_memrealtime() - t0 < 100ull * us) __builtin_amdgcn_s_sleep(32);
+}
+
+__global__ __launch_bounds__(64) void where_kernel(uint32_t us, uint32_t *where)
+{
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    record_where(where, t0);
+    while (__builtin_amdgcn_s_memrealtime() - t0 < 100ull * us) __builtin_amdgcn_s_sleep(32);
+}
+
+// big != 0: the blocker's shape (512 threads, 256 VGPRs); else 64-thread blocks.
+// where: 4 words per block
+extern "C" __attribute__((visibility("default"))) int spt_test_where(void *stream, uint32_t us, uint32_t blocks,
+                                                                     int big, uint32_t *where)
+{
+    if (big)
+        hipLaunchKernelGGL(blocker_where_kernel, dim3(blocks ? blocks : 1u), dim3(512), 0, (hipStream_t)stream, us, where);
+    else
+        hipLaunchKernelGGL(where_kernel, dim3(blocks ? blocks : 1u), dim3(64), 0, (hipStream_t)stream, us, where);
+    return hipGetLastError() == hipSuccess ? 0 : 3;
+}
+
+// A stream whose CU mask holds the low `keep` of `total` bits (the layout spt_api.cpp's
+// masked_for uses); *out receives the hipStream_t.
+extern "C" __attribute__((visibility("default"))) int spt_test_masked_stream(uint32_t keep, uint32_t total, void **out)
+{
+    uint32_t mask[64] = {};
+    if (total == 0 || total > 64 * 32 || keep > total) return 1;
+    for (uint32_t i = 0; i < keep; ++i) mask[i / 32] |= 1u << (i % 32);
+    hipStream_t s = nullptr;
+    if (hipExtStreamCreateWithCUMask(&s, (total + 31) / 32, mask) != hipSuccess) return 3;
+    *out = (void *)s;
+    return 0;
+}
+
+extern "C" __attribute__((visibility("default"))) int spt_test_stream_destroy(void *s)
+{
+    return hipStreamDestroy((hipStream_t)s) == hipSuccess ? 0 : 3;
+}

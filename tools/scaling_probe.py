@@ -28,14 +28,25 @@ ap.add_argument("--record", default="")
 ap.add_argument("--ns", default="1,2,4,8", help="rank counts to probe")
 ap.add_argument("--stats", type=int, default=0, help="print the context's service counters per N")
 ap.add_argument("--strip", type=int, default=0, help="rows per interleaved strip (0: even_strip, the bench's)")
+ap.add_argument("--reserve", type=int, default=0, help="CUs kept free of launched renders (spt_set_reserved_cus)")
+ap.add_argument("--blocker", type=int, default=0,
+                help="after each frame, a collective stand-in of this many us (tests/cpp/spt_testhooks.hip's "
+                     "blocker: 8 blocks of 256-VGPR waves, like RCCL's gather kernel) on a third stream")
 args = ap.parse_args()
 W, H, SPP, B = {"c2": (1200, 800, 100, 50), "c3": (3840, 2160, 1024, 50)}[args.config]
 ctx = spt.Context(0)
 ctx.set_scene(spt.generate_spheres(1))
 ctx.set_camera(spt.camera_basis(), spt.scene.DEFAULT_EYE, spt.INIT_COLOR)
 ctx.set_params(W, H, SPP, B, 1)
+ctx.set_reserved_cus(args.reserve)
 base = None
 streams = [torch.cuda.Stream() for _ in range(args.streams)]
+comm = torch.cuda.Stream()
+if args.blocker:
+    import ctypes
+    hooks = ctypes.CDLL(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "simplepathtracer_amd",
+                                     "lib", "libspt_testhooks.so"))
+    hooks.spt_test_blocker.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p]
 lines = []
 for n in [int(x) for x in args.ns.split(",")]:
     split = FrameSplit(W, H, n, args.strip or even_strip(H, n))
@@ -44,6 +55,13 @@ for n in [int(x) for x in args.ns.split(",")]:
     def frame(k):
         ctx.render_rows_async(spt.MODE_SEGMENT, 0, H, split.strip if n > 1 else 1, n, 0, 0, W,
                               tiles[k % len(streams)].data_ptr(), 0, streams[k % len(streams)].cuda_stream)
+        if args.blocker:
+            # the frame's gather: on the comm stream once the frame is done; the next frame
+            # on the render stream waits for it (the bench's tile buffer reuse)
+            s = streams[k % len(streams)]
+            comm.wait_stream(s)
+            assert hooks.spt_test_blocker(ctypes.c_void_p(comm.cuda_stream), args.blocker, 8, None) == 0
+            s.wait_stream(comm)
 
     ts = []
     ctx.reset_stats()
@@ -81,7 +99,7 @@ if args.record:
                       "libspt_hip.so")
     with open(args.record, "w") as f:
         f.write(f"# tools/scaling_probe.py --config {args.config} --streams {args.streams} --frames {args.frames} "
-                f"--reps {args.reps} --service {args.service}\n")
+                f"--reps {args.reps} --service {args.service} --reserve {args.reserve} --blocker {args.blocker}\n")
         f.write(f"# {datetime.datetime.now().isoformat(timespec='seconds')}, git {head}, libspt_hip.so mtime "
                 f"{datetime.datetime.fromtimestamp(os.path.getmtime(so)).isoformat(timespec='seconds')}, "
                 f"env SPT_*: {' '.join(f'{k}={v}' for k, v in sorted(os.environ.items()) if k.startswith('SPT_')) or '-'}\n")

@@ -94,3 +94,34 @@ extern "C" __attribute__((visibility("default"))) int spt_test_stream_destroy(vo
 {
     return hipStreamDestroy((hipStream_t)s) == hipSuccess ? 0 : 3;
 }
+
+// WRITE_SIZE calibration for 4-byte sample words (tools/write_calib.sh):
+// `words` u32 words written once each, by 64-lane waves over 256-word (1 KiB) chunks.
+// pattern 0: four coalesced stores per wave (64 lanes x 4 B each, the whole chunk);
+// pattern 1: the chunk's 256 words one lane at a time, 256 stores per wave, in a
+// scrambled order (stride 97 mod 256): the lines are assembled in L2 from single words,
+// the way lanes finishing their paths at different times write their slots.
+__global__ __launch_bounds__(256) void write_calib_kernel(uint32_t *out, uint32_t words, int pattern)
+{
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t chunk = (blockIdx.x * 256u + threadIdx.x) >> 6;
+    const uint32_t base = chunk * 256u;
+    if (base >= words) return;
+    if (pattern == 0) {
+        for (uint32_t r = 0; r < 4u; ++r) out[base + r * 64u + lane] = base + r * 64u + lane;
+    } else {
+        for (uint32_t r = 0; r < 256u; ++r) {
+            const uint32_t w = (r * 97u) & 255u;
+            if ((w & 63u) == lane) out[base + w] = base + w;
+        }
+    }
+}
+
+extern "C" __attribute__((visibility("default"))) int spt_test_write_calib(void *stream, uint32_t *out, uint32_t words,
+                                                                           int pattern)
+{
+    if (words % 256u) return 1;
+    const uint32_t waves = words / 256u;
+    hipLaunchKernelGGL(write_calib_kernel, dim3((waves + 3u) / 4u), dim3(256), 0, (hipStream_t)stream, out, words, pattern);
+    return hipGetLastError() == hipSuccess ? 0 : 3;
+}

@@ -38,6 +38,7 @@ for r in range(args.reps + 1):
     t0 = time.perf_counter()
     if args.service:
         ctx.service_start()
+    t_svc = (time.perf_counter() - t0) * 1e3  # host time of service_start
     evs = []
     for k in range(args.frames):
         st = streams[k % 2]
@@ -46,6 +47,8 @@ for r in range(args.reps + 1):
         e = torch.cuda.Event(enable_timing=True)
         e.record(st)
         evs.append(e)
+        if k == 0:
+            t_first = (time.perf_counter() - t0) * 1e3
     t_enq = (time.perf_counter() - t0) * 1e3
     if args.service:
         ctx.service_stop()
@@ -56,7 +59,8 @@ for r in range(args.reps + 1):
         continue
     k = np.arange(len(ts))
     sl, ic = np.polyfit(k[2:-1], ts[2:-1], 1)
-    print(f"rep {r}: N={n} service={args.service} enqueue {t_enq:.2f} ms, wall {wall:.2f} ms, "
+    print(f"rep {r}: N={n} service={args.service} host: start {t_svc:.3f}, first job {t_first:.3f}, "
+          f"enqueue {t_enq:.2f} ms, wall {wall:.2f} ms, "
           f"frames done at {' '.join(f'{x:.2f}' for x in ts)} ms; slope {sl:.4f} ms/frame, intercept {ic:.3f} ms",
           flush=True)
 ctx.close()

@@ -117,3 +117,22 @@ def test_reserved_cus_region_vs_oracle(spt, oracle, golden_scenes):
     want, _ = oracle.render_segment(sc, fr, 20, 180, 30, 290, rgb8=gw)
     assert_bitwise(got[:, :3], want[:, :3], "reserved-CU region")
     assert np.array_equal(g, gw)
+
+
+@pytest.mark.parametrize("w,h,spp,bounces", [(1, 1, 1, 1), (7, 3, 3, 2), (9, 17, 1, 50), (65, 1, 2, 5), (1, 70, 4, 3)])
+@pytest.mark.parametrize("task", [False, True])
+def test_tiny_and_thin_frames_vs_oracle(spt, oracle, golden_scenes, w, h, spp, bounces, task):
+    """Whole frames smaller than one 8x8 tile, one pixel wide or high, a single sample, a
+    single bounce: the tile decomposition's ragged edges (ts_item / ts_slot_base) and the
+    primary batches' partial blocks against RenderSegment / RenderSegmentTask."""
+    ctx = spt.Context(0)
+    setup(ctx, scene_from(spt, golden_scenes, "random"), w, h, spp, bounces, seed=13, view=golden_scenes["view"])
+    g = np.zeros(w * h * 3, np.uint8)
+    got = ctx.render_segment(0, h, 0, w, g_data=g, task=task)
+    ctx.close()
+    sc = oscene_from(oracle, golden_scenes, "random")
+    fr = oracle.make_frame(golden_scenes["view"], EYE, SKY, w, h, spp, bounces, 13)
+    gw = np.zeros(w * h * 3, np.uint8)
+    want, _ = oracle.render_segment(sc, fr, 0, h, 0, w, task=task, rgb8=gw)
+    assert_bitwise(got[:, :3], want[:, :3], f"{w}x{h}")
+    assert np.array_equal(g, gw)

@@ -121,11 +121,15 @@ def test_reserved_cus_region_vs_oracle(spt, oracle, golden_scenes):
 
 @pytest.mark.parametrize("w,h,spp,bounces", [(1, 1, 1, 1), (7, 3, 3, 2), (9, 17, 1, 50), (65, 1, 2, 5), (1, 70, 4, 3)])
 @pytest.mark.parametrize("task", [False, True])
-def test_tiny_and_thin_frames_vs_oracle(spt, oracle, golden_scenes, w, h, spp, bounces, task):
+@pytest.mark.parametrize("engine", ["megakernel", "wavefront"])
+def test_tiny_and_thin_frames_vs_oracle(spt, oracle, golden_scenes, w, h, spp, bounces, task, engine):
     """Whole frames smaller than one 8x8 tile, one pixel wide or high, a single sample, a
     single bounce: the tile decomposition's ragged edges (ts_item / ts_slot_base) and the
-    primary batches' partial blocks against RenderSegment / RenderSegmentTask."""
+    primary batches' partial blocks against RenderSegment / RenderSegmentTask, on both
+    engines (the megakernel and the wavefront queue workers)."""
     ctx = spt.Context(0)
+    if engine == "wavefront":
+        ctx.set_engine(spt._native.ENGINE_WAVEFRONT)
     setup(ctx, scene_from(spt, golden_scenes, "random"), w, h, spp, bounces, seed=13, view=golden_scenes["view"])
     g = np.zeros(w * h * 3, np.uint8)
     got = ctx.render_segment(0, h, 0, w, g_data=g, task=task)

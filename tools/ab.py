@@ -23,7 +23,7 @@ import simplepathtracer_amd as spt  # noqa: E402
 
 W, H, SPP, B = {"c1": (200, 100, 4, 8), "c2": (1200, 800, 100, 50), "c2x10": (1200, 800, 1000, 50),
                 "c2hi": (2400, 1600, 25, 50), "c3s": (3840, 2160, 16, 50),
-                "c5": (1920, 1080, 256, 50),
+                "c5": (1920, 1080, 256, 50), "c5x2": (1920, 1080, 512, 50), "c2x2": (1200, 800, 200, 50),
                 "c5s": (1920, 1080, 4, 50), "s20k": (1920, 1080, 16, 50), "s30k": (1920, 1080, 16, 50), "s40k": (1920, 1080, 16, 50),
                 "s50k": (1920, 1080, 16, 50)}[args.config]
 scene = (spt.generate_stress(1, int(args.config[1:3]) * 1000) if args.config in ("s20k", "s30k", "s40k", "s50k") else spt.generate_stress(1, 10000) if args.config.startswith("c5")

@@ -2160,6 +2160,7 @@ int spt_ctx_create(int device, spt_ctx **out)
         return fail(nullptr, SPT_ERR_NODEVICE, "device %d is %s, this build targets gfx950", device, prop.gcnArchName);
     spt_ctx *ctx = new spt_ctx();
     ctx->ws.reserve(kMaxWorkspaces);
+    ctx->masked.reserve(kMaxCompanions);  // masked_for hands out pointers into it
     ctx->block = spt::render_block_size();
     ctx->device = device;
     ctx->num_cu = prop.multiProcessorCount;

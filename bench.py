@@ -304,16 +304,12 @@ def main():
     one_batch = W * H * spp * slot_bytes <= (16 << 30)  # the context's default workspace
     nst = args.streams
     if nst <= 0:
-        nst = 1
-        if one_batch:
-            # frames in flight pay off on the 256-thread kernels; the LDS tree kernel's
-            # 1024-thread blocks (two per CU, config 5) leave the next frame no slot:
-            # one stream there (config 5: 91.9 vs 93.1 ms per frame).  Probe which kernel
-            # the scene takes with a one-row render on the current stream.
-            cur = torch.cuda.current_stream(dev)
-            ctx.render_rows_async(mode, 0, 1, 1, 1, 0, 0, min(W, 64), 0, 0, cur.cuda_stream)
-            cur.synchronize()
-            nst = 2 if ctx.stats()["block_threads"] <= 256 else 1
+        # two frames in flight when a frame is one sample batch (the next frame's blocks
+        # take the CUs as this one's drain; config 2: 22 849-22 878 vs 3 streams 22 685-
+        # 22 728; config 5's 1024-thread LDS-tree blocks: 7 478-7 495 vs one stream
+        # 7 459-7 474 on the round-5 kernels); several sample batches
+        # (config 3) overlap through their own companion stream
+        nst = 2 if one_batch else 1
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(nst - 1)]
     bufs = []
     for _ in range(nst):  # per-stream frame buffers: frames in flight do not share outputs

@@ -287,6 +287,17 @@ def main():
         else:
             dist.init_process_group(backend)
 
+    # the render service (--service 1) is started around each timed region and stopped
+    # (drained) inside it: a device-wide synchronisation must not wait for its resident kernel
+    # (auto: rank shares of N > 1 ranks, each on a GPU of its own -- ranks rehearsed on a
+    # shared GPU would hold each other's resident kernels off the CUs).  The session takes
+    # every block slot (SPT_SVC_FULL_GRID): the folds and gathers of a region's frames run
+    # after its session ends (N = 8 shares with a gather stand-in: 0.740 vs 0.756 ms per
+    # share; whole frames 4.46 vs 4.67 ms)
+    auto_svc = world > 1 and world <= torch.cuda.device_count()
+    use_svc = (args.service if args.service >= 0 else auto_svc) and args.engine == "megakernel"
+    if use_svc:
+        os.environ.setdefault("SPT_SVC_FULL_GRID", "1")
     scene_name, W, H, spp, bounces = CONFIGS[args.config]
     scene = make_scene(spt, scene_name)
     view = spt.camera_basis()
@@ -337,12 +348,6 @@ def main():
             render_frame(ctx, split, rank, mode, b["local"], b["gathered"], b["frame"], b["g_data"],
                          streams[k].cuda_stream, gather_events=ev)
 
-    # the render service (--service 1) is started around each timed region and stopped
-    # (drained) inside it: a device-wide synchronisation must not wait for its resident kernel
-    # (auto: rank shares of N > 1 ranks, each on a GPU of its own -- ranks rehearsed on a
-    # shared GPU would hold each other's resident kernels off the CUs)
-    auto_svc = world > 1 and world <= torch.cuda.device_count()
-    use_svc = (args.service if args.service >= 0 else auto_svc) and args.engine == "megakernel"
     if use_svc:
         ctx.service_start()
     for _ in range(args.warmup):
@@ -427,7 +432,8 @@ def main():
                                    f"{spp} spp, depth {bounces}, {args.mode} mode, {args.engine}",
                        "width": W, "height": H, "spp": spp, "bounces": bounces, "spheres": scene.n,
                        "parallelism": f"row-strips{split.strip}x{world}" if world > 1 else "1 GPU",
-                       "frames_in_flight": nst, "render_service": bool(use_svc)},
+                       "frames_in_flight": nst, "render_service": bool(use_svc),
+                       "service_full_grid": bool(use_svc) and os.environ.get("SPT_SVC_FULL_GRID", "0") != "0"},
             # contract form: the render kernel against HBM with SURVEY §8(d)'s algorithmic
             # bytes; HBM does not bind this kernel (VALU issue + latency do: roofline_valu)
             "roofline": {"bound": "hbm", "achieved": round(algo_bytes / t_launch / 1e9, 4),

@@ -2171,6 +2171,11 @@ int spt_ctx_create(int device, spt_ctx **out)
     int per_cu = 0;
     if (spt::render_occupancy(ctx->block, &per_cu) != hipSuccess || per_cu <= 0) per_cu = 1;
     ctx->svc_grid = (uint32_t)(std::max(1, per_cu - 1) * ctx->num_cu);
+    // SPT_SVC_FULL_GRID=1: the session takes every block slot (folds and other streams'
+    // kernels then wait for the session's end; for pipelines that end their sessions
+    // themselves, like bench.py's timed regions: DESIGN.md §5)
+    if (const char *e = env_var("SPT_SVC_FULL_GRID"))
+        if (std::atoi(e) != 0) ctx->svc_grid = (uint32_t)(per_cu * ctx->num_cu);
     // launch_bounds / occupancy API may over-report by one block per CU for SGPR-heavy
     // kernels (MI355X_MICROARCH.md, Residency): the kernel needs no co-residency, so
     // extra blocks only queue.  SPT_BLOCKS_PER_CU overrides for tuning.

@@ -68,10 +68,14 @@ def render_frames(ctx, jobs, W, H, mode, streams, service):
     return [(a.cpu().numpy(), b.cpu().numpy()) for a, b in outs]
 
 
+@pytest.mark.parametrize("full", [0, 1])
 @pytest.mark.parametrize("mode", [0, 1])
-def test_service_frames_equal_launched_frames(spt, golden_scenes, mode):
-    """K consecutive frames through the queue, each compared with a one-shot render."""
+def test_service_frames_equal_launched_frames(spt, golden_scenes, monkeypatch, mode, full):
+    """K consecutive frames through the queue, each compared with a one-shot render; also
+    with the session on every block slot (SPT_SVC_FULL_GRID, bench.py's N > 1 regions:
+    the folds run after the session ends)."""
     import torch
+    monkeypatch.setenv("SPT_SVC_FULL_GRID", str(full))
     W, H = 320, 200
     ctx = make_ctx(spt, golden_scenes, W, H, 16, 50, seed=3)
     streams = [torch.cuda.Stream(), torch.cuda.Stream()]
@@ -208,8 +212,9 @@ def _hooks():
     return h
 
 
+@pytest.mark.parametrize("full", [0, 1])
 @pytest.mark.parametrize("mode", [0, 1])
-def test_service_ring_wrap_behind_blockers(spt, golden_scenes, monkeypatch, mode):
+def test_service_ring_wrap_behind_blockers(spt, golden_scenes, monkeypatch, mode, full):
     """Liveness.  A 64 MiB slot ring wraps every few
     jobs, and on each caller stream, ahead of every render's fold, sits a kernel that cannot
     be resident beside a session (512 threads x 256 VGPRs, standing in for RCCL's gather
@@ -224,6 +229,7 @@ def test_service_ring_wrap_behind_blockers(spt, golden_scenes, monkeypatch, mode
     import torch
     monkeypatch.setenv("SPT_SVC_RING_MB", "64")
     monkeypatch.setenv("SPT_SVC_TIMEOUT_MS", "30000")
+    monkeypatch.setenv("SPT_SVC_FULL_GRID", str(full))  # 1: no fold can run inside a session at all
     hooks = _hooks()
     vg = ctypes.c_int(0)
     assert hooks.spt_test_blocker_vgprs(ctypes.byref(vg)) == 0 and vg.value == 256

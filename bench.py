@@ -34,6 +34,9 @@ CONFIGS = {
     "c3": ("random", 3840, 2160, 1024, 50),
     "c5": ("stress10k", 1920, 1080, 256, 50),
     "c1": ("cornell3", 200, 100, 4, 8),
+    # BASELINE.json config 2's "~500 spheres": GenerateSpheres' rows run to z < 37.5
+    # (488 spheres; the reference's own generator stops at z < 20: 149)
+    "c2w": ("random500", 1200, 800, 100, 50),
 }
 # VALU issue: a wave64 VALU instruction occupies its SIMD-32 for 2 cycles
 # (MI355X_MICROARCH.md: 4 SIMD-32 per CU), 1024 SIMDs at 2.4 GHz
@@ -60,6 +63,8 @@ CPU_CALIBRATION = {"reference_msps": {"segment": 4.26, "task": 4.33},
 def make_scene(spt, name):
     if name == "random":
         return spt.generate_spheres(1)
+    if name == "random500":
+        return spt.generate_spheres(1, z_end=37.5)
     if name == "stress10k":
         return spt.generate_stress(1, 10000)
     if name == "cornell3":
@@ -141,6 +146,23 @@ def dropin_bench(w, h, spp, bounces, frames, tcs, env=None):
         return None
     out = {}
     run_env = dict(os.environ, **(env or {}))
+    # the reference app's own pattern (Renderer.hpp:335-344 MainLoop renders one frame per
+    # process): a fresh process per run, its one frame timed in parts (median of 3 runs)
+    for task in (0, 1):
+        tc = 4
+        runs = []
+        for _ in range(3):
+            r = subprocess.run([exe, "/dev/null", str(w), str(h), str(spp), str(bounces), str(tc), str(task), "0"],
+                               capture_output=True, text=True, timeout=600, env=dict(run_env, SPT_HARNESS_COLD="1"))
+            if r.returncode != 0:
+                raise RuntimeError(f"dropin harness (cold) failed: {r.stderr[-400:]}")
+            line = r.stdout.split("cold ", 1)[1].split("\n")[0]
+            runs.append({k: float(v) for k, v in (kv.split("=") for kv in line.split())})
+        med = {k: float(np.median([x[k] for x in runs])) for k in ("ctx_ms", "setup_ms", "frame_ms", "accel_ms", "prim_ms")}
+        key = f"cold_{'task' if task else 'segment'}_tc{tc}"
+        out[key] = {k: round(v, 3) for k, v in med.items()}
+        out[key]["total_ms"] = round(med["ctx_ms"] + med["setup_ms"] + med["frame_ms"], 3)
+        out[key]["frame_msamples_s"] = round(tiled_pixels(w, h, tc) * spp / med["frame_ms"] / 1e3, 1)
     for tc in tcs:
         r = subprocess.run([exe, "/dev/null", str(w), str(h), str(spp), str(bounces), str(tc), "0", str(frames)],
                            capture_output=True, text=True, timeout=600, env=dict(run_env, SPT_HARNESS_NOOP="1"))
@@ -461,6 +483,11 @@ def main():
             "world_size": world_seen,
             "backend": backend_seen,
             "rays_per_sample": round(casts_all / max(samples_all, 1), 4),
+            # host setup outside the timed region, once per scene / camera / frame size: the
+            # traversal tables (build, check, upload) and the primary-ray candidate lists
+            "setup_ms": {"accel_build_ms": round(st["accel_build_ms"], 3),
+                         "prim_list_build_ms": round(st["prim_list_build_ms"], 3),
+                         "total_ms": round(st["accel_build_ms"] + st["prim_list_build_ms"], 3)},
             # a fold overlapped by another stream's render (frames in flight, or the double-buffered
             # sample batches of a multi-batch frame) spans its wait for free CU slots: not reported
             "fold_ms_per_step": round(st["fold_ms"] / args.steps, 4) if nst == 1 and one_batch else None,
@@ -512,11 +539,16 @@ def main():
                 out["dropin"] = {"unit": "Msamples/s", **d,
                                  "def": "C++ shim under RenderImageParallelMain tiling (tools/dropin_harness.cpp), "
                                         "host g_data, tc=4 (shipped g_maxThreads) and tc=2*cores; rates count the "
-                                        "pixels the tiling renders ((W/tc)*tc x (H/tc)*tc, Renderer.hpp:264-265); "
-                                        f"{args.dropin_frames} timed frames each; every frame's tiles served "
-                                        "from the shim's tiling read-ahead (spt_api.cpp SpecFrame: the whole "
-                                        "tiling rendered once per frame in 4 launches when its first tile is "
-                                        "called; SPT_READAHEAD=0 turns it off)"}
+                                        "pixels the tiling renders ((W/tc)*tc x (H/tc)*tc, Renderer.hpp:264-265). "
+                                        "cold_*: what the reference app gets -- MainLoop renders ONE frame per "
+                                        "process (Renderer.hpp:335-344): a fresh process, context creation, the "
+                                        "globals' upload (scene, traversal tables, primary-ray lists, g_data "
+                                        "page-locking) and that one frame, each timed (median of 3 processes). "
+                                        f"segment_tc*/task_tc*: REPEATED frames, {args.dropin_frames} timed after "
+                                        "an untimed one; a pattern the reference app never produces, served by "
+                                        "the shim's tiling read-ahead (spt_api.cpp SpecFrame: once a tiling has "
+                                        "been called whole, the whole frame renders in 4 launches at its next "
+                                        "first tile; SPT_READAHEAD=0 turns it off)"}
         print(json.dumps(out), flush=True)
         if args.dump:
             torch.cuda.synchronize(dev)

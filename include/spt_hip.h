@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define SPT_ABI_VERSION 8
+#define SPT_ABI_VERSION 9
 
 /* Only the functions below are exported from libspt_hip.so (built with
  * -fvisibility=hidden), so several builds can be loaded side by side. */
@@ -115,6 +115,10 @@ typedef struct spt_stats {
     uint32_t prim_list_blocks;   /* 8x8 pixel blocks with a primary-ray candidate list (0: lists off) */
     uint32_t prim_list_entries;  /* candidate slots over all blocks' lists (8x8 and 8x4) */
     double prim_list_build_ms;   /* host time of their last build */
+    uint64_t prim_list_builds;   /* builds so far (a setter rebuilds the lists only when the
+                                    accel tables, the camera or the frame size changed) */
+    double accel_build_ms;       /* host time of the last traversal-table build + upload
+                                    (spt_set_scene / cluster setters) */
 } spt_stats;
 
 SPT_API int spt_abi_version(void);
@@ -315,6 +319,11 @@ SPT_API int spt_reset_stats(spt_ctx *ctx);
  * splitmix(seed) (Random.hpp:19) instead of the clock; capacity in spheres. */
 SPT_API int spt_scene_generate_random(uint32_t seed, uint32_t capacity, float *centers4, float *radii, float *colors4,
                               uint8_t *materials, float *fuzz, uint32_t *n_out);
+/* GenerateSpheres with its row loop (SceneGenerators.hpp:32) run to z < z_end instead of
+ * 20 (z_end = 20 is spt_scene_generate_random): BASELINE.json's "~500-sphere" RTIOW scene
+ * with the reference's placement rule and draw order (z_end 37.5: 488 spheres, seed 1). */
+SPT_API int spt_scene_generate_random_rows(uint32_t seed, float z_end, uint32_t capacity, float *centers4, float *radii,
+                                           float *colors4, uint8_t *materials, float *fuzz, uint32_t *n_out);
 SPT_API int spt_scene_init_reference(uint32_t seed, float *centers4, float *radii, float *colors4, uint8_t *materials,
                              float *fuzz, uint32_t *n_out);
 /* Stress scene for the >255-sphere extension (BASELINE config 5): the four big

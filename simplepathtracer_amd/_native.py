@@ -15,7 +15,7 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG_DIR, "lib", os.environ.get("SPT_LIB", "libspt_hip.so"))
 HEADER_PATH = os.path.join(os.path.dirname(PKG_DIR), "include", "spt_hip.h")
 
-ABI_VERSION = 8  # SPT_ABI_VERSION of include/spt_hip.h
+ABI_VERSION = 9  # SPT_ABI_VERSION of include/spt_hip.h
 SPT_OK = 0
 STATUS_NAMES = {0: "SPT_OK", 1: "SPT_ERR_ARG", 2: "SPT_ERR_STATE", 3: "SPT_ERR_HIP", 4: "SPT_ERR_NOMEM",
                 5: "SPT_ERR_NODEVICE", 6: "SPT_ERR_TIMEOUT"}
@@ -58,6 +58,8 @@ class Stats(ctypes.Structure):
         ("prim_list_blocks", ctypes.c_uint32),
         ("prim_list_entries", ctypes.c_uint32),
         ("prim_list_build_ms", ctypes.c_double),
+        ("prim_list_builds", ctypes.c_uint64),
+        ("accel_build_ms", ctypes.c_double),
     ]
 
 
@@ -117,6 +119,7 @@ def lib() -> ctypes.CDLL:
         "spt_get_stats": ([P, P], I),
         "spt_reset_stats": ([P], I),
         "spt_scene_generate_random": ([u32, u32, P, P, P, P, P, P], I),
+        "spt_scene_generate_random_rows": ([u32, ctypes.c_float, u32, P, P, P, P, P, P], I),
         "spt_scene_init_reference": ([u32, P, P, P, P, P, P], I),
         "spt_scene_generate_stress": ([u32, u32, P, P, P, P, P], I),
         "spt_camera_basis": ([P, P, P, P], I),

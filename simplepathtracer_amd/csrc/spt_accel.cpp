@@ -651,7 +651,9 @@ PrimListTables build_prim_lists(const AccelTables &t, const Camera &cam, uint32_
 {
     const auto t_start = std::chrono::steady_clock::now();
     PrimListTables out;
-    if (W == 0 || H == 0) return out;
+    // the device packs a batch lane's pixel as (y << 16 | x) (spt_path.h prim_list_cast):
+    // frames of 65 536 or more columns or rows walk the tree
+    if (W == 0 || H == 0 || W > 0xFFFFu || H > 0xFFFFu) return out;
     out.bw = (W + 7) / 8;
     const uint32_t bh8 = (H + 7) / 8, bh4 = (H + 3) / 4;
     out.b8.assign((size_t)out.bw * bh8, make_uint2(0, kPrimWalk));

@@ -179,7 +179,13 @@ struct Service {
     uint32_t *h_job_claim = nullptr, *dh_job_claim = nullptr;
     uint32_t grid_div = 1;       // SPT_SVC_GRID_DIV: the session takes 1/div of its grid
     uint32_t pub_delay_us = 0;   // SPT_SVC_TEST_PUB_DELAY_US: fault injection before every publish
-    double timeout_ms = 30000;   // SPT_SVC_TIMEOUT_MS: longest wait for a session to end
+    // SPT_SVC_TIMEOUT_MS: the longest wait for a session to end beyond the time its
+    // published work may take at kSvcMinRate (svc_wait)
+    double timeout_ms = 30000;
+    uint64_t session_items = 0;  // samples published to the running session
+    // a session whose end timed out: its kernel may still be resident, so no new session
+    // starts (and no host word is reset) until its end event completes (svc_end)
+    bool draining = false;
     bool debug = false;          // SPT_SVC_DEBUG: a line on stderr per session event
     uint64_t sessions = 0, jobs = 0, watchdog_exits = 0;
     // sessions ended early: a publication would have waited for an unfinished fold (flow
@@ -224,6 +230,23 @@ struct spt_ctx {
     uint32_t *d_prim_slots = nullptr;
     size_t prim_b8_cap = 0, prim_b4_cap = 0, prim_slots_cap = 0;
     double prim_build_s = 0;  // host time of the last build
+    uint64_t prim_builds = 0;
+    double accel_build_s = 0;  // host time of the last rebuild_accel (build, check, upload)
+    // what the lists were built for (rebuild_prim skips a rebuild when nothing the lists
+    // depend on changed: spp, depth and seed setters do not touch them)
+    struct PrimKey {
+        float view[12], eye[3];
+        uint32_t W, H, prim_max;
+        uint64_t accel_gen;
+        bool valid;
+        bool same(const PrimKey &o) const
+        {
+            return valid && o.valid && std::memcmp(view, o.view, sizeof view) == 0 &&
+                   std::memcmp(eye, o.eye, sizeof eye) == 0 && W == o.W && H == o.H && prim_max == o.prim_max &&
+                   accel_gen == o.accel_gen;
+        }
+    } prim_key{};
+    uint64_t accel_gen = 0;  // rebuild_accel count
     uint32_t prim_blocks = 0, prim_entries = 0;  // 8x8 blocks with a list, list entries
     // diffuse sample codes (spt_internal.h diffuse_code): the slot count, and the halvings
     // after which every finite albedo of the scene is 0 (j saturates at min(bounces - 1, jz))
@@ -507,35 +530,43 @@ uint64_t fmix64(uint64_t z)
 // items per wave below which a launch with frames in flight takes grid_small
 constexpr uint64_t kSmallGridItems = 3072;
 
-uint32_t full_grid(const spt_ctx *ctx)
+// masked: the launch runs on a CU-masked stream (spt_set_reserved_cus, masked_for)
+uint32_t full_grid(const spt_ctx *ctx, bool masked = false)
 {
     const uint32_t g = ctx->ws.size() > 1 ? ctx->grid_overlap : ctx->grid;
-    // reserved CUs (spt_set_reserved_cus): the persistent grid of the CUs the launch may use
-    if (ctx->reserve_cus && ctx->num_cu > 0)
+    // reserved CUs: the persistent grid of the CUs the masked launch may use
+    if (masked && ctx->reserve_cus && ctx->num_cu > 0)
         return std::max<uint32_t>(1u, (uint32_t)((uint64_t)g * (uint32_t)(ctx->num_cu - (int)ctx->reserve_cus) / (uint32_t)ctx->num_cu));
     return g;
 }
 
 // The CU-masked stream a launched render of caller stream s runs on (spt_set_reserved_cus;
-// created on first use: every CU but the device's last reserve_cus), or nullptr.
-spt_ctx::Masked *masked_for(spt_ctx *ctx, hipStream_t s)
+// created on first use: every CU but the device's last reserve_cus) in *out.  A stream
+// that cannot be created is an error (the render would otherwise keep no CU free).
+int masked_for(spt_ctx *ctx, hipStream_t s, spt_ctx::Masked **out)
 {
-    if (ctx->reserve_cus == 0) return nullptr;
+    *out = nullptr;
     for (spt_ctx::Masked &m : ctx->masked)
-        if (m.caller == s) return &m;
-    if (ctx->masked.size() >= kMaxCompanions) return nullptr;
+        if (m.caller == s) {
+            *out = &m;
+            return SPT_OK;
+        }
+    if (ctx->masked.size() >= kMaxCompanions)
+        return fail(ctx, SPT_ERR_STATE, "reserved CUs: more than %zu caller streams", kMaxCompanions);
     const uint32_t n = (uint32_t)ctx->num_cu, keep = n - ctx->reserve_cus;
     std::vector<uint32_t> mask((n + 31) / 32, 0u);
     for (uint32_t i = 0; i < keep; ++i) mask[i / 32] |= 1u << (i % 32);
     spt_ctx::Masked m{s, nullptr, nullptr, nullptr};
-    if (hipExtStreamCreateWithCUMask(&m.stream, (uint32_t)mask.size(), mask.data()) != hipSuccess) return nullptr;
+    HIP_TRY(ctx, hipExtStreamCreateWithCUMask(&m.stream, (uint32_t)mask.size(), mask.data()));
     if (hipEventCreateWithFlags(&m.go, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&m.done, hipEventDisableTiming) != hipSuccess) {
         (void)hipStreamDestroy(m.stream);
-        return nullptr;
+        return fail(ctx, SPT_ERR_HIP, "reserved CUs: event creation failed");
     }
+    ctx->masked.reserve(kMaxCompanions);  // pointers handed out stay valid
     ctx->masked.push_back(m);
-    return &ctx->masked.back();
+    *out = &ctx->masked.back();
+    return SPT_OK;
 }
 
 // Items per claim: 256, or 512 for launches of at least 64 Ki items per wave (config 3's
@@ -553,10 +584,10 @@ spt_ctx::Masked *masked_for(spt_ctx *ctx, hipStream_t s)
 // / 20 699-20 707 (512) Msamples/s, while its rank shares still prefer 256 (384: the 1/2
 // share 2.414 -> 2.447 ms); trees walked lane by lane keep 256.
 constexpr uint32_t kSmallClaim = 192, kClaim = 256, kMidClaim = 448, kBigClaim = 512;
-uint32_t claim_size(const spt_ctx *ctx, uint64_t items)
+uint32_t claim_size(const spt_ctx *ctx, uint64_t items, bool masked = false)
 {
     if (ctx->claim) return ctx->claim;
-    const uint64_t waves = std::max<uint64_t>((uint64_t)full_grid(ctx) * (ctx->block / 64), 1);
+    const uint64_t waves = std::max<uint64_t>((uint64_t)full_grid(ctx, masked) * (ctx->block / 64), 1);
     const uint64_t fair = items / (waves * 4);
     const uint64_t per_wave = items / waves;
     const bool lane = spt::lane_walk_tree(ctx->accel);
@@ -572,18 +603,18 @@ uint32_t claim_size(const spt_ctx *ctx, uint64_t items)
 // finds the counter exhausted and exits, and on config 1 (1250 claims, 8192
 // waves) those waves tripled the launch time.
 // div: host calls sharing the GPU side by side (each gets 1/div of the grid).
-uint32_t render_grid(const spt_ctx *ctx, uint64_t items, uint32_t claim, uint32_t div)
+uint32_t render_grid(const spt_ctx *ctx, uint64_t items, uint32_t claim, uint32_t div, bool masked = false)
 {
     const uint64_t claims = (items + claim - 1) / claim;
     const uint64_t per_block = (uint64_t)(ctx->block / 64) * ctx->claims_per_wave;
-    uint64_t full = (full_grid(ctx) + div - 1) / div;
+    uint64_t full = (full_grid(ctx, masked) + div - 1) / div;
     // frames in flight, a launch of under 3 Ki items per wave (config 2's 1/8 rank share):
     // one more block slot per CU left free, so fewer of the launch's paths are still in
     // flight when its claims run out and the other stream's launch takes the CUs sooner
     // (the 1/8 share 0.755-0.762 -> 0.725 ms per frame; the 1/4 share, 3.9 Ki items per
     // wave, would lose 0.5%: tools/scaling_probe.py)
     if (div == 1 && ctx->ws.size() > 1 && ctx->grid_small &&
-        items < (uint64_t)full_grid(ctx) * (ctx->block / 64) * kSmallGridItems)
+        items < (uint64_t)full_grid(ctx, masked) * (ctx->block / 64) * kSmallGridItems)
         full = ctx->grid_small;
     return (uint32_t)std::min<uint64_t>(full, std::max<uint64_t>(1, (claims + per_block - 1) / per_block));
 }
@@ -677,24 +708,32 @@ hipEvent_t svc_event(spt_ctx *ctx)
         }                                                                                              \
     } while (0)
 
-// Wait for event e at most the service's timeout: SPT_OK, or SPT_ERR_TIMEOUT.  Spins
-// (yielding) for the first 2 ms, then polls every 50 us.
+// The slowest rate a session's published work is assumed to render at, samples per ms
+// (100 M samples/s: config 5, the slowest config, renders 7.5 G/s): a session may take
+// its timeout plus its published samples at this rate to end.  A whole 16 GiB ring of
+// sample words queued on a slow scene is real work, not a hang.
+constexpr double kSvcMinRate = 1e5;
+
+// Wait for event e at most the service's timeout plus the time the running session's
+// published work may take (kSvcMinRate): SPT_OK, or SPT_ERR_TIMEOUT.  Spins (yielding)
+// for the first 2 ms, then polls every 50 us.
 int svc_wait(spt_ctx *ctx, hipEvent_t e, const char *what)
 {
     const auto t0 = std::chrono::steady_clock::now();
+    const double limit = ctx->svc.timeout_ms + (double)ctx->svc.session_items / kSvcMinRate;
     for (;;) {
         const hipError_t q = hipEventQuery(e);
         if (q == hipSuccess) return SPT_OK;
         if (q != hipErrorNotReady) return fail(ctx, SPT_ERR_HIP, "%s: %s", what, hipGetErrorString(q));
         const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-        if (ms > ctx->svc.timeout_ms) {
+        if (ms > limit) {
             const Service &v = ctx->svc;
             const uint32_t closing = __atomic_load_n(v.h_host + spt::kSvcHostClosing, __ATOMIC_SEQ_CST);
             return fail(ctx, SPT_ERR_TIMEOUT,
                         "render service: %s did not finish within %.0f ms (session %llu: %u jobs published, "
-                        "%llu claims; closing flag %u)",
-                        what, v.timeout_ms, (unsigned long long)v.sessions, v.n_jobs, (unsigned long long)v.claims,
-                        closing);
+                        "%llu claims, %llu samples; closing flag %u)",
+                        what, limit, (unsigned long long)v.sessions, v.n_jobs, (unsigned long long)v.claims,
+                        (unsigned long long)v.session_items, closing);
         }
         if (ms < 2.0)
             std::this_thread::yield();
@@ -709,11 +748,18 @@ int svc_wait(spt_ctx *ctx, hipEvent_t e, const char *what)
 int svc_end(spt_ctx *ctx)
 {
     Service &v = ctx->svc;
-    if (!v.running) return SPT_OK;
-    v.running = false;
-    SVC_DBG(ctx, "end session %llu (%u jobs): stop", (unsigned long long)v.sessions, v.n_jobs);
-    __atomic_store_n(v.h_host + spt::kSvcHostStop, 1u, __ATOMIC_SEQ_CST);
-    if (int rc = svc_wait(ctx, v.ev_end, "ending the session")) return rc;
+    if (v.draining) {
+        // an earlier end timed out: the session is over only once its kernel has left
+        if (int rc = svc_wait(ctx, v.ev_end, "ending the session (after an earlier timeout)")) return rc;
+    } else {
+        if (!v.running) return SPT_OK;
+        v.running = false;
+        v.draining = true;
+        SVC_DBG(ctx, "end session %llu (%u jobs): stop", (unsigned long long)v.sessions, v.n_jobs);
+        __atomic_store_n(v.h_host + spt::kSvcHostStop, 1u, __ATOMIC_SEQ_CST);
+        if (int rc = svc_wait(ctx, v.ev_end, "ending the session")) return rc;
+    }
+    v.draining = false;
     SVC_DBG(ctx, "end session %llu: kernel done", (unsigned long long)v.sessions);
     float ms = 0.f;
     if (hipEventElapsedTime(&ms, v.ev_start, v.ev_end) == hipSuccess) v.kernel_ms += ms;
@@ -864,6 +910,7 @@ int svc_begin(spt_ctx *ctx, int mode, const std::vector<hipEvent_t> &waits, int6
     v.mode = mode;
     v.n_jobs = 0;
     v.claims = 0;
+    v.session_items = 0;
     v.sessions++;
     SVC_DBG(ctx, "begin session %llu, grid %u, %zu waits", (unsigned long long)v.sessions, grid, waits.size());
     return SPT_OK;
@@ -957,6 +1004,7 @@ int svc_submit_jobs(spt_ctx *ctx, int mode, const SvcJobSpec *jobs, size_t n, ui
         __atomic_store_n(v.h_host + spt::kSvcHostCommitted, (uint32_t)n, __ATOMIC_SEQ_CST);
     }
     v.ring_head = w1;
+    v.session_items += items;
     v.next_done = (v.next_done + 1u) % v.done_cap;
     if (reset) target = items;
     v.done_cum[idx] = target;
@@ -1114,7 +1162,10 @@ int render_impl(spt_ctx *ctx, int mode, const spt::RowMap &map, float4 *d_rgba, 
     Workspace *const w_caller = w;
     // reserved CUs: the launches of this call on the caller stream's CU-masked stream,
     // ordered after the caller's queued work (and the caller after them, below)
-    spt_ctx::Masked *mk_ = !use_svc && !s2 && !pg ? masked_for(ctx, s) : nullptr;
+    // (renders through the service, double-buffered batches and progressive passes run on
+    // every CU with the whole grid)
+    spt_ctx::Masked *mk_ = nullptr;
+    if (ctx->reserve_cus && !use_svc && !s2 && !pg && (rc = masked_for(ctx, s, &mk_))) return rc;
     if (mk_) {
         HIP_TRY(ctx, hipEventRecord(mk_->go, s));
         HIP_TRY(ctx, hipStreamWaitEvent(mk_->stream, mk_->go, 0));
@@ -1133,7 +1184,7 @@ int render_impl(spt_ctx *ctx, int mode, const spt::RowMap &map, float4 *d_rgba, 
     ra.map = map;
     ra.div_strip = spt::make_fastdiv(std::max<uint32_t>(map.strip, 1u));
     ra.npix = npix;
-    ra.claim = claim_size(ctx, (uint64_t)npix * spp_batch);
+    ra.claim = claim_size(ctx, (uint64_t)npix * spp_batch, mk_ != nullptr);
     ra.samples = w->d_samples;
     ra.slot_words = slot_words;
     ra.head = w->d_head;
@@ -1219,7 +1270,7 @@ int render_impl(spt_ctx *ctx, int mode, const spt::RowMap &map, float4 *d_rgba, 
                 ctx->ref_recorded = true;
             }
             HIP_TRY(ctx, hipEventRecord(ev.a, s));
-            spt::LaunchShape sh{render_grid(ctx, ra.n_items, ra.claim, grid_div), ctx->block, grid_div, 0, 0};
+            spt::LaunchShape sh{render_grid(ctx, ra.n_items, ra.claim, grid_div, mk_ != nullptr), ctx->block, grid_div, 0, 0};
             HIP_TRY(ctx, spt::launch_render(ra, sh, s));
             ctx->last_grid = sh.ran_grid;
             ctx->last_block = sh.ran_block;
@@ -1290,6 +1341,7 @@ Shape resolve_shape(const spt_ctx *ctx)
 // Build and upload the hot-loop traversal tables (spt_accel.cpp) for the current scene.
 int rebuild_accel(spt_ctx *ctx)
 {
+    const auto t_start = std::chrono::steady_clock::now();
     const uint32_t g = spt::render_group_size();
     const Shape sh = resolve_shape(ctx);
     spt::AccelTables t = spt::build_accel(ctx->h_centers.data(), ctx->h_radii.data(), ctx->n, sh.k, g, sh.branching,
@@ -1323,6 +1375,16 @@ int rebuild_accel(spt_ctx *ctx)
     ctx->code_stride = (uint32_t)std::max<size_t>(t.slots.size(), 1);
     ctx->code_jz = jz;
     ctx->tables = std::move(t);
+    ctx->accel_gen++;
+    ctx->accel_build_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count();
+    return SPT_OK;
+}
+
+// Wait for every render launch this context has enqueued (on any stream) -- not for the
+// device: unrelated work of the process (torch kernels, RCCL) keeps running.
+int wait_own_renders(spt_ctx *ctx)
+{
+    for (const EventPair &p : ctx->pending_render) HIP_TRY(ctx, hipEventSynchronize(p.b));
     return SPT_OK;
 }
 
@@ -1332,15 +1394,29 @@ int rebuild_accel(spt_ctx *ctx)
 // but not its walk iterations or time).
 int rebuild_prim(spt_ctx *ctx)
 {
+    const bool want = ctx->prim_enabled && ctx->scene_set && ctx->cam_set && ctx->params_set &&
+                      !spt::lane_walk_tree(ctx->accel);
+    spt_ctx::PrimKey key{};
+    for (int i = 0; i < 12; ++i) key.view[i] = ctx->cam.view[i];
+    for (int i = 0; i < 3; ++i) key.eye[i] = ctx->cam.eye[i];
+    key.W = ctx->W;
+    key.H = ctx->H;
+    key.prim_max = ctx->prim_max;
+    key.accel_gen = ctx->accel_gen;
+    key.valid = true;
+    // the lists depend on the accel tables, the camera and the frame size only
+    if (want && key.same(ctx->prim_key)) return SPT_OK;
     ctx->prim = spt::PrimLists{};
     ctx->prim_blocks = ctx->prim_entries = 0;
-    if (!ctx->prim_enabled || !ctx->scene_set || !ctx->cam_set || !ctx->params_set || spt::lane_walk_tree(ctx->accel))
-        return SPT_OK;
+    ctx->prim_key = spt_ctx::PrimKey{};
+    if (!want) return SPT_OK;
     spt::PrimListTables pl = spt::build_prim_lists(ctx->tables, ctx->cam, ctx->W, ctx->H, ctx->prim_max);
     ctx->prim_build_s = pl.seconds;
+    ctx->prim_builds++;
+    ctx->prim_key = key;
     if (!pl.on) return SPT_OK;
-    // every stream: renders in flight may still read the previous lists
-    HIP_TRY(ctx, hipDeviceSynchronize());
+    // this context's renders in flight may still read the previous lists
+    if (int rc = wait_own_renders(ctx)) return rc;
     int rc = upload(ctx, &ctx->d_prim_b8, &ctx->prim_b8_cap, pl.b8);
     if (!rc) rc = upload(ctx, &ctx->d_prim_b4, &ctx->prim_b4_cap, pl.b4);
     if (!rc) rc = upload(ctx, &ctx->d_prim_slots, &ctx->prim_slots_cap, pl.slots);
@@ -1734,9 +1810,12 @@ int spec_stream(spt_ctx *ctx, int p)
 // arms: allocated by the first read-ahead itself, each part's first allocations held its
 // launch until the previous part's render had ended (the four parts of the first read-ahead
 // frame ran one after another, 15 ms apart, profiles/r05_dropin_trace.md).
-int spec_prepare(spt_ctx *ctx, int mode, uint32_t tc)
+// Called with lk (ctx->mu) held; waits (unlocked) for serves still copying out of d8, which
+// ensure() may free when this tiling's frame is larger.
+int spec_prepare(spt_ctx *ctx, std::unique_lock<std::mutex> &lk, int mode, uint32_t tc)
 {
     SpecFrame &sp = ctx->spec;
+    sp.readers_cv.wait(lk, [&] { return sp.readers == 0; });
     const uint32_t W = ctx->W, H = ctx->H, sw = W / tc, sh = H / tc;
     const uint32_t slot_words = mode == SPT_MODE_SEGMENT ? 1u : 2u;
     int rc = ensure(ctx, &sp.d8, &sp.d8_cap, (size_t)W * H * 3);
@@ -1846,7 +1925,7 @@ int spec_serve(spt_ctx *ctx, std::unique_lock<std::mutex> &lk, int mode, uint32_
                 sp.armed = ++sp.arm_count == tc * tc;
                 // the read-ahead's buffers now, while this frame's tiles render as usual
                 if (sp.armed) {
-                    const int rc = spec_prepare(ctx, mode, tc);
+                    const int rc = spec_prepare(ctx, lk, mode, tc);
                     if (rc) return rc;
                 }
             }
@@ -2838,6 +2917,8 @@ int stats_one(spt_ctx *ctx, spt_stats *out)
     out->prim_list_blocks = ctx->prim_blocks;
     out->prim_list_entries = ctx->prim_entries;
     out->prim_list_build_ms = ctx->prim_build_s * 1e3;
+    out->prim_list_builds = ctx->prim_builds;
+    out->accel_build_ms = ctx->accel_build_s * 1e3;
     return SPT_OK;
 }
 

@@ -82,7 +82,19 @@ struct Out {
 extern "C" int spt_scene_generate_random(uint32_t seed, uint32_t capacity, float *centers4, float *radii,
                                          float *colors4, uint8_t *materials, float *fuzz, uint32_t *n_out)
 {
+    return spt_scene_generate_random_rows(seed, 20.0f, capacity, centers4, radii, colors4, materials, fuzz, n_out);
+}
+
+// GenerateSpheres with its row loop run to z < z_end (the reference: 20).  Wider z ranges
+// give BASELINE.json's "~500-sphere" RTIOW scene (z_end 37.5: 488 spheres for seed 1)
+// with the reference's own placement rule, draw order and materials; only the row count
+// changes.  More than 255 spheres need the 32-bit index.
+extern "C" int spt_scene_generate_random_rows(uint32_t seed, float z_end, uint32_t capacity, float *centers4,
+                                              float *radii, float *colors4, uint8_t *materials, float *fuzz,
+                                              uint32_t *n_out)
+{
     if (!centers4 || !radii || !colors4 || !materials || !fuzz || !n_out || capacity < 4) return SPT_ERR_ARG;
+    if (!(z_end >= 0.0f && z_end <= 1000.0f)) return SPT_ERR_ARG;
     SplitMix rng(seed);
     Out o{centers4, radii, colors4, fuzz, materials};
     uint32_t n = 0;
@@ -95,7 +107,7 @@ extern "C" int spt_scene_generate_random(uint32_t seed, uint32_t capacity, float
     const V s1 = o.center(1), s2 = o.center(2), s3 = o.center(3);
     // SceneGenerators.hpp:32-53.  abs(z) binds std::abs(float) in the reference's TU
     // (oracle/probe_overloads.cpp).
-    for (float z = 0; z < 20; z += 1.25f) {
+    for (float z = 0; z < z_end; z += 1.25f) {
         const float bound = std::fabs(z) * 0.85f;
         for (float x = -5 - bound; x < 6 + bound; x += 1.25f) {
             if (rng.uniform(0, 1.f) > 0.5f) {

@@ -62,12 +62,18 @@ def _alloc(cap: int):
             np.zeros(cap, np.uint8), np.zeros(cap, np.float32))
 
 
-def generate_spheres(seed: int = 1, capacity: int = 4096) -> Scene:
-    """GenerateSpheres (SceneGenerators.hpp:6-66), the RANDOM scene (~140-160 spheres)."""
+def generate_spheres(seed: int = 1, capacity: int = 4096, z_end: float = 20.0) -> Scene:
+    """GenerateSpheres (SceneGenerators.hpp:6-66), the RANDOM scene (~140-160 spheres).
+    z_end: the row loop's bound (SceneGenerators.hpp:32, the reference's 20); 37.5 gives
+    BASELINE.json's "~500-sphere" scene (488 spheres for seed 1)."""
     c, r, col, m, f = _alloc(capacity)
     n = ctypes.c_uint32(0)
-    _native.check(_native.lib().spt_scene_generate_random(seed, capacity, _p(c), _p(r), _p(col), _p(m), _p(f),
-                                                          ctypes.byref(n)))
+    if z_end == 20.0:
+        _native.check(_native.lib().spt_scene_generate_random(seed, capacity, _p(c), _p(r), _p(col), _p(m), _p(f),
+                                                              ctypes.byref(n)))
+    else:
+        _native.check(_native.lib().spt_scene_generate_random_rows(seed, ctypes.c_float(z_end), capacity, _p(c), _p(r),
+                                                                   _p(col), _p(m), _p(f), ctypes.byref(n)))
     k = n.value
     return Scene(c[:k], r[:k], col[:k], m[:k], f[:k])
 

@@ -77,6 +77,16 @@ extern "C" __attribute__((visibility("default"))) int spt_test_where(void *strea
     return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 
+// One thread stores s_memrealtime (100 MHz ticks) to *out: queued on a stream after a
+// render, its value is a time at which the render had ended (tests/test_gpu_reserve.py)
+__global__ void stamp_kernel(unsigned long long *out) { *out = __builtin_amdgcn_s_memrealtime(); }
+
+extern "C" __attribute__((visibility("default"))) int spt_test_stamp(void *stream, unsigned long long *out)
+{
+    hipLaunchKernelGGL(stamp_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, out);
+    return hipGetLastError() == hipSuccess ? 0 : 3;
+}
+
 // A stream whose CU mask holds the low `keep` of `total` bits (the layout spt_api.cpp's
 // masked_for uses); *out receives the hipStream_t.
 extern "C" __attribute__((visibility("default"))) int spt_test_masked_stream(uint32_t keep, uint32_t total, void **out)

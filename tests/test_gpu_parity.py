@@ -1235,3 +1235,75 @@ def test_primary_lists_equal_tree_walk(spt, golden_scenes, monkeypatch, case):
         assert_bitwise(got[k][0], want[k][0], f"{case} {k}")
         assert np.array_equal(got[k][1], want[k][1]), f"{case} {k}: second output differs"
     assert casts == casts0
+
+
+@pytest.mark.parametrize("W,H,y0,y1,x0,x1", [(70000, 4, 0, 4, 65504, 65600), (70000, 4, 0, 4, 69936, 70000),
+                                              (4, 70000, 65520, 65560, 0, 4), (4, 70000, 69980, 70000, 0, 4)])
+def test_frames_of_65536_or_more_columns_or_rows(spt, ctx, oracle, golden_scenes, W, H, y0, y1, x0, x1):
+    """A primary batch packs its lanes' pixels as (y << 16 | x) for the candidate-list lookup
+    (spt_path.h prim_list_cast): frames of 65 536 or more columns or rows have no
+    lists (the batches walk the tree) and render like the oracle past column / row 65 535."""
+    setup(ctx, scene_from(spt, golden_scenes, "random"), W, H, 2, 12, seed=5)
+    assert ctx.stats()["prim_list_blocks"] == 0
+    g = np.zeros(W * H * 3, np.uint8)
+    got = ctx.render_segment(y0, y1, x0, x1, g_data=g)
+    osc = oscene_from(oracle, golden_scenes, "random")
+    fr = oracle.make_frame(spt.camera_basis(EYE, LOOK, UP), EYE, SKY, W, H, 2, 12, 5)
+    gw = np.zeros_like(g)
+    want, _ = oracle.render_segment(osc, fr, y0, y1, x0, x1, rgb8=gw)
+    assert_bitwise(got[:, :3], want[:, :3], f"{W}x{H} region")
+    assert np.array_equal(g, gw)
+
+
+def test_setters_rebuild_lists_only_when_they_change(spt, golden_scenes):
+    """The primary-ray candidate lists depend on the accel tables, the camera and the frame
+    size only: spp / depth / seed setters and a repeated camera keep them."""
+    c = spt.Context(0)
+    try:
+        view = spt.camera_basis(EYE, LOOK, UP)
+        c.set_scene(scene_from(spt, golden_scenes, "random"))
+        c.set_camera(view, EYE, SKY)
+        c.set_params(320, 200, 4, 50, 1)
+        st = c.stats()
+        assert st["prim_list_builds"] == 1 and st["prim_list_blocks"] > 0 and st["accel_build_ms"] > 0
+        before = c.render_segment(0, 200, 0, 320)
+        c.set_params(320, 200, 8, 20, 7)
+        c.set_params(320, 200, 4, 50, 1)
+        c.set_camera(view, EYE, SKY)
+        assert c.stats()["prim_list_builds"] == 1
+        assert_bitwise(c.render_segment(0, 200, 0, 320), before, "after setters that keep the lists")
+        c.set_params(321, 200, 4, 50, 1)
+        assert c.stats()["prim_list_builds"] == 2
+        c.set_camera(spt.camera_basis([0.5, 1.2, -3, 0], LOOK, UP), [0.5, 1.2, -3, 0], SKY)
+        assert c.stats()["prim_list_builds"] == 3
+        c.set_scene(scene_from(spt, golden_scenes, "random"))
+        assert c.stats()["prim_list_builds"] == 4
+    finally:
+        c.close()
+
+
+@pytest.mark.parametrize("task", [False, True])
+def test_config2_500_sphere_scene_region_vs_oracle(spt, ctx, oracle, task):
+    """BASELINE.json config 2's "~500-sphere" RTIOW scene: GenerateSpheres with its rows run
+    to z < 37.5 (488 spheres, uint32 index; SceneGenerators.hpp:32-53, Collision.hpp:87-92
+    cap the reference at 255).  A 1200 x 800 frame's regions (one across the horizon with
+    the far rows of small spheres, one on the big balls) at 8 spp, depth 50, against the
+    oracle, float bits and g_data bytes; whichever walk the tree's size selects."""
+    s = spt.generate_spheres(1, z_end=37.5)
+    assert 480 <= s.n <= 520
+    view = spt.camera_basis()
+    ctx.set_scene(s)
+    ctx.set_camera(view, spt.scene.DEFAULT_EYE, spt.INIT_COLOR)
+    ctx.set_params(1200, 800, 8, 50, 1)
+    osc = oracle.OracleScene(s.centers, s.radii, s.colors, s.materials, s.fuzz)
+    fr = oracle.make_frame(view, spt.scene.DEFAULT_EYE, spt.INIT_COLOR, 1200, 800, 8, 50, 1)
+    for (y0, y1, x0, x1) in ((360, 400, 560, 680), (500, 540, 200, 260)):
+        g = np.zeros(1200 * 800 * 3, np.uint8)
+        got = ctx.render_segment(y0, y1, x0, x1, g_data=g, task=task)
+        gw = np.zeros_like(g)
+        want, _ = oracle.render_segment(osc, fr, y0, y1, x0, x1, rgb8=gw, task=task)
+        if task and (y1 - y0) != (x1 - x0):
+            same_bits_or_nan(got[:, :3], want[:, :3], f"500 spheres task {y0},{x0}")
+        else:
+            assert_bitwise(got[:, :3], want[:, :3], f"500 spheres {y0},{x0}")
+        assert np.array_equal(g, gw)

@@ -25,9 +25,10 @@ W, H, SPP, B = {"c1": (200, 100, 4, 8), "c2": (1200, 800, 100, 50), "c2x10": (12
                 "c2hi": (2400, 1600, 25, 50), "c3s": (3840, 2160, 16, 50),
                 "c5": (1920, 1080, 256, 50), "c5x2": (1920, 1080, 512, 50), "c2x2": (1200, 800, 200, 50),
                 "c5s": (1920, 1080, 4, 50), "s20k": (1920, 1080, 16, 50), "s30k": (1920, 1080, 16, 50), "s40k": (1920, 1080, 16, 50),
-                "s50k": (1920, 1080, 16, 50)}[args.config]
+                "s50k": (1920, 1080, 16, 50), "c2w": (1200, 800, 100, 50)}[args.config]
 scene = (spt.generate_stress(1, int(args.config[1:3]) * 1000) if args.config in ("s20k", "s30k", "s40k", "s50k") else spt.generate_stress(1, 10000) if args.config.startswith("c5")
-         else spt.cornell3() if args.config == "c1" else spt.generate_spheres(1))
+         else spt.cornell3() if args.config == "c1" else spt.generate_spheres(1, z_end=37.5) if args.config == "c2w"
+         else spt.generate_spheres(1))
 view = spt.camera_basis()
 P = ctypes.c_void_p
 ctxs = []

@@ -9,6 +9,11 @@
 //   frames > 0: render one untimed frame, then `frames` timed frames, and print
 //   "frames=K seconds=T" (wall clock of the K frames).  SPT_DEVICES=0,1,.. (shim)
 //   renders on a multi-device context.
+//   SPT_HARNESS_COLD=1: the reference app's own pattern -- MainLoop renders exactly one
+//   frame per process (Renderer.hpp:335-344) -- timed in its parts and printed as
+//   "cold ctx_ms=.. setup_ms=.. frame_ms=..": context creation (HIP runtime and device
+//   init, the library's buffers), the globals' upload (scene, traversal tables, primary-ray
+//   lists, g_data page-locking), and the first RenderImageParallelMain frame itself.
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
@@ -107,7 +112,25 @@ int main(int argc, char **argv)
             }
         cv.wait(lk, [&] { return free_threads.load() == (int)tc; });
     };
-    frame_once();
+    const bool cold = std::getenv("SPT_HARNESS_COLD") && std::atoi(std::getenv("SPT_HARNESS_COLD")) != 0;
+    if (cold && !noop) {
+        using clk = std::chrono::steady_clock;
+        auto ms = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+        const auto t0 = clk::now();
+        spt_shim::context();
+        const auto t1 = clk::now();
+        spt_shim::sync_globals();
+        const auto t2 = clk::now();
+        frame_once();
+        const auto t3 = clk::now();
+        spt_stats st{};
+        spt_get_stats(spt_shim::context(), &st);
+        printf("cold ctx_ms=%.3f setup_ms=%.3f frame_ms=%.3f accel_ms=%.3f prim_ms=%.3f batches=%llu calls=%llu\n",
+               ms(t0, t1), ms(t1, t2), ms(t2, t3), st.accel_build_ms, st.prim_list_build_ms,
+               (unsigned long long)st.batches, (unsigned long long)st.batched_calls);
+    } else {
+        frame_once();
+    }
     const int frames = argc > 8 ? atoi(argv[8]) : 0;
     if (frames > 0) {
         const auto t0 = std::chrono::steady_clock::now();

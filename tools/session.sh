@@ -91,6 +91,9 @@ for step in "$@"; do
     tdrop) run tdrop 200 bash tools/trace_dropin.sh ;;
     tdrop20) TDROP_FRAMES=20 run tdrop20 200 bash tools/trace_dropin.sh ;;
     ab:*) NAB=$((${NAB:-0} + 1)); run ab$NAB 600 python tools/ab.py ${step#ab:} ;;
+    pyt:*) NPY=$((${NPY:-0} + 1)); run pyt$NPY 400 $PYT -v -s ${step#pyt:} ;;
+    benchc:*) NBC=$((${NBC:-0} + 1)); run benchc$NBC 300 python bench.py --no-cpu-baseline --no-dropin --config ${step#benchc:} ;;
+    dropincold) run dropincold 300 python -c "import bench; print(bench.dropin_bench(1200, 800, 100, 50, 20, (4,)))" ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

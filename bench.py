@@ -546,7 +546,7 @@ def main():
                                         "page-locking) and that one frame, each timed (median of 3 processes). "
                                         f"segment_tc*/task_tc*: REPEATED frames, {args.dropin_frames} timed after "
                                         "an untimed one; a pattern the reference app never produces, served by "
-                                        "the shim's tiling read-ahead (spt_api.cpp SpecFrame: once a tiling has "
+                                        "the shim's tiling read-ahead (spt_batch.cpp SpecFrame: once a tiling has "
                                         "been called whole, the whole frame renders in 4 launches at its next "
                                         "first tile; SPT_READAHEAD=0 turns it off)"}
         print(json.dumps(out), flush=True)

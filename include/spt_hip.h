@@ -119,6 +119,8 @@ typedef struct spt_stats {
                                     accel tables, the camera or the frame size changed) */
     double accel_build_ms;       /* host time of the last traversal-table build + upload
                                     (spt_set_scene / cluster setters) */
+    uint64_t svc_inkernel_folds; /* service jobs folded inside the session by its fold waves
+                                    (the rest are fold launches on the caller's stream) */
 } spt_stats;
 
 SPT_API int spt_abi_version(void);

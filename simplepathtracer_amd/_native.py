@@ -60,6 +60,7 @@ class Stats(ctypes.Structure):
         ("prim_list_build_ms", ctypes.c_double),
         ("prim_list_builds", ctypes.c_uint64),
         ("accel_build_ms", ctypes.c_double),
+        ("svc_inkernel_folds", ctypes.c_uint64),
     ]
 
 

@@ -17,7 +17,7 @@
 // member's test or beat its current winner (spt_accel.cpp).
 // render_kernel_lds walks large trees from a per-block LDS copy of the node table;
 // the *_batch kernels render several host calls' rectangles in one launch
-// (spt_api.cpp render_batched).
+// (spt_batch.cpp render_batched).
 //
 // fold_kernel: RenderSegment's `pixelColor += sample` in sample order followed by
 // `*= 1/g_samples` (SingleThreadPathTracer.hpp:121-134) or RenderSegmentTask's
@@ -140,7 +140,7 @@ __device__ __forceinline__ void unpark_path(const uint32_t *q, uint32_t row, Pat
 // One kernel per traversal shape (flat list of 4- or 8-slot leaves, tree of
 // 8-slot leaves), each with its own register allocation; launch_render picks.
 // BATCH: the launch renders a.n_rects rectangles (a.rects, concurrent host calls
-// batched by spt_api.cpp); each refill then serves lanes from one claim only, and a
+// batched by spt_batch.cpp); each refill then serves lanes from one claim only, and a
 // claim's rectangle is looked up once per claim.
 // The next claim of a launch (lane 0).  Items come from a.n_queues counters,
 // one per XCD: queue k hands out [k * queue_items, (k + 1) * queue_items), so the
@@ -177,8 +177,15 @@ __device__ __forceinline__ uint32_t svc_reserve(uint32_t q, uint32_t lane, uint3
     return lane == 0 ? atomicAdd(h, 1u) : old;
 }
 // the wave's LDS words after its job record: published claims and jobs as last seen, the
-// current job and the first claim after it
+// current job and the first claim after it, the fold-ring entries it is done taking from
 constexpr uint32_t kSvcSt = 28;
+constexpr uint32_t kSvcRecWords = 40;  // LDS words per wave: job record (32) + state
+// the sample words a fold lane loads ahead (svc_fold_loop; sc1 loads: deep runs keep a fold
+// wave's loads in flight)
+#ifndef SPT_SVC_FOLD_RUN
+#define SPT_SVC_FOLD_RUN 8
+#endif
+constexpr int kSvcFoldRun = SPT_SVC_FOLD_RUN;
 
 // The published pair {claims, jobs} (one 64-bit sc1 load: the forwarder stores it after
 // its records, sc1, with its stores drained -- MI355X_MICROARCH.md, hand-off table)
@@ -206,7 +213,8 @@ __device__ __forceinline__ void svc_forward(uint32_t lane)
 {
     kargs_t &k = *kernarg_args();
     const gu32 *hw = (const gu32 *)k.svc_host;
-    uint32_t fwd = 0;  // records forwarded
+    uint32_t fwd = 0;    // records forwarded
+    uint32_t nfold = 0;  // lane 33: in-kernel-fold jobs among them
     for (uint32_t idle = 0;; ++idle) {
         const uint32_t st = lane == 0 ? __hip_atomic_load(hw + kSvcHostStop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0u;
         const bool stop = __builtin_amdgcn_readfirstlane(st) != 0u;
@@ -218,7 +226,9 @@ __device__ __forceinline__ void svc_forward(uint32_t lane)
         const uint32_t plo = __builtin_amdgcn_readfirstlane((uint32_t)pv);
         const uint32_t phi = __builtin_amdgcn_readfirstlane((uint32_t)(pv >> 32));
         if (phi > fwd) {
-            // records [fwd, phi): lanes 0-31 one record's words, lane 32 its first claim
+            // records [fwd, phi): lanes 0-31 one record's words, lane 32 its first claim,
+            // lane 33 the record's counter -> job entry (in-kernel folds) and the count of
+            // in-kernel-fold jobs, stored before the pair that publishes them
             const gu32 *hj = (const gu32 *)k.svc_host_jobs;
             const gu32 *hc = (const gu32 *)k.svc_host_job_claim;
             for (uint32_t j = fwd; j < phi; ++j) {
@@ -229,8 +239,19 @@ __device__ __forceinline__ void svc_forward(uint32_t lane)
                 } else if (lane == kSvcJobWords) {
                     const uint32_t c = __hip_atomic_load(hc + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                     __hip_atomic_store((gu32 *)(k.svc_job_claim + j), c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                } else if (lane == kSvcJobWords + 1u && k.svc_fold) {
+                    const uint32_t di = __hip_atomic_load(hj + (size_t)j * kSvcJobWords + 3u, __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_SYSTEM);
+                    const uint32_t fl = __hip_atomic_load(hj + (size_t)j * kSvcJobWords + kSvcJobFoldFlags,
+                                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    __hip_atomic_store((gu32 *)(k.svc_fold + 3u * k.svc_job_cap + di), j, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                    nfold += (fl & kSvcFoldInKernel) ? 1u : 0u;
                 }
             }
+            const uint32_t nf = __builtin_amdgcn_readlane(nfold, (int)kSvcJobWords + 1);
+            if (k.svc_fold && lane == 0)
+                __hip_atomic_store((gu32 *)(k.svc_ctl + kSvcFoldJobs), nf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             if (lane == 0)
                 __hip_atomic_store((gu64 *)(k.svc_ctl + kSvcPub), (unsigned long long)plo | ((unsigned long long)phi << 32),
@@ -281,6 +302,259 @@ __device__ __forceinline__ uint32_t svc_find_job(uint32_t nb, uint32_t cur, uint
     return __builtin_amdgcn_readfirstlane(cur);
 }
 
+// The colour of a sample word (code_word, spt_internal.h), with the render kernel's own
+// operations: the sky as SampleColorSkybox computes it (SingleThreadPathTracer.hpp:11-14),
+// a diffuse sample as the albedo * 0.5 (line 24) halved once more per further bounce
+// (line 31), bit for bit.  Halving is exact while the value stays normal, so j halvings
+// are one multiply by 2^-j when the result is normal (or 0 / inf / NaN); otherwise (a
+// denormal result: each halving may round) they are done one at a time.
+__device__ __forceinline__ float halve_n(float x, uint32_t j)
+{
+    if (j <= 126u) {
+        const float r = x * __uint_as_float((127u - j) << 23);
+        if (__builtin_fabsf(r) >= 0x1p-126f || x == 0.f || !__builtin_isfinite(x)) return r;
+    }
+    for (uint32_t i = 0; i < j; ++i) x = x * 0.5f;
+    return x;
+}
+__device__ __forceinline__ f3 decode_sample(const FoldArgs &a, uint32_t w)
+{
+    const uint32_t c = word_code(w);
+    if (c == 0u) {
+        const float k = __uint_as_float(w);
+        return mul(mk(a.sky[0] * k, a.sky[1] * k, a.sky[2] * k), 0.5f);
+    }
+    if (c == 1u) return mk(0.f, 0.f, 0.f);
+    uint32_t j, slot;
+    diffuse_decode(c, a.code_div, j, slot);
+    const float4 sh = a.shade[slot];
+    return mk(halve_n(sh.x * 0.5f, j), halve_n(sh.y * 0.5f, j), halve_n(sh.z * 0.5f, j));
+}
+
+// decode_sample for a run of words without branches around the loads: the shading-table
+// reads of all N words are issued together (slot 0 stands in for sky and zero words), the
+// colours selected afterwards; only denormal halvings (halve_n's slow path) branch.
+template <int N>
+__device__ __forceinline__ void decode_run(const FoldArgs &a, const uint32_t (&w)[N], f3 (&col)[N])
+{
+    uint32_t c[N], j[N];
+    float4 sh[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        c[i] = word_code(w[i]);
+        uint32_t slot;
+        diffuse_decode(c[i] >= 2u ? c[i] : 2u, a.code_div, j[i], slot);
+        sh[i] = a.shade[slot];
+    }
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        const float k = __uint_as_float(w[i]);
+        const f3 s = mul(mk(a.sky[0] * k, a.sky[1] * k, a.sky[2] * k), 0.5f);
+        const f3 d = mk(halve_n(sh[i].x * 0.5f, j[i]), halve_n(sh[i].y * 0.5f, j[i]), halve_n(sh[i].z * 0.5f, j[i]));
+        col[i] = c[i] == 0u ? s : c[i] == 1u ? mk(0.f, 0.f, 0.f) : d;
+    }
+}
+
+// words loaded ahead per thread in the fold (a multiple of 8): small folds (the drop-in's
+// batches of one or two tiles) have few threads, and each is bound by its loads' latency
+#ifndef SPT_FOLD_RUN
+#define SPT_FOLD_RUN 8
+#endif
+static_assert(SPT_FOLD_RUN % 8 == 0, "fold runs are decoded eight words at a time");
+
+// RenderSegmentTask's colorIndex aliasing (TaskBasedPathTracer.hpp:103,186,196-205) for
+// output index p of a W x H call: colors[p] collects every pixel (dx, dy) of the call with
+// dx + dy * H == p, and the resolve writes colors[p] to pixel (p % W, p / W).  Within a
+// sample the sources reach colors[p] in the order of their (key, pixel) (finish_step), so
+// each sample's sources are added in that order.  No source: 0 samples, and 0 * (1.f / 0)
+// is NaN, as in the reference.  The sources' slots are those of rows [row0, row0 + rows)
+// of the launch (the call's own rows, or a range of them: spt_render_frame).
+__device__ __forceinline__ void alias_accumulate(const FoldArgs &a, const uint32_t *samples, uint32_t p, uint32_t W,
+                                                 uint32_t H, uint32_t row0, uint32_t rows, uint32_t S, float4 &acc)
+{
+    const uint32_t dy_lo = p >= W ? (p - W + H) / H : 0u;
+    const uint32_t dy_hi = min(H - 1u, p / H);
+    const uint32_t ns = dy_hi + 1u - dy_lo;  // sources: pixels (p - dy H, dy)
+    const uint2 *s2 = (const uint2 *)samples;
+    auto add = [&](uint32_t w) {
+        const f3 c = decode_sample(a, w);
+        acc.x = acc.x + c.x;
+        acc.y = acc.y + c.y;
+        acc.z = acc.z + c.z;
+        acc.w = acc.w + 1.f;
+    };
+    constexpr uint32_t kSrc = 4;  // sources kept in registers (config 2's tiles: <= 2)
+    if (ns <= kSrc) {
+        // the sources' slot bases once; per sample their keys, added in (key, pixel)
+        // order (pixel order = dy order when W > H, reversed when W < H)
+        uint32_t sq[kSrc], sst[kSrc];
+#pragma unroll
+        for (uint32_t j = 0; j < kSrc; ++j) {
+            const uint32_t dy = j < ns ? dy_lo + j : dy_lo;
+            ts_slot_base(dy - row0, p - dy * H, W, rows, S, sq[j], sst[j]);
+        }
+        const bool rev = W < H;
+        for (uint32_t k = 0; k < S; ++k) {
+            uint2 v[kSrc];
+#pragma unroll
+            for (uint32_t j = 0; j < kSrc; ++j) v[j] = j < ns ? s2[sq[j] + k * sst[j]] : make_uint2(0u, 0u);
+            uint32_t done = 0;  // sources already added (bit j)
+            for (uint32_t t = 0; t < ns; ++t) {
+                uint32_t bj = kSrc, bk = 0, bw = 0;  // the next source: index, key, word
+#pragma unroll
+                for (uint32_t j = 0; j < kSrc; ++j) {
+                    const bool cand = j < ns && v[j].y != 0u && !((done >> j) & 1u);
+                    const bool before = bj == kSrc || v[j].y < bk || (v[j].y == bk && rev);
+                    if (cand && before) {
+                        bj = j;
+                        bk = v[j].y;
+                        bw = v[j].x;
+                    }
+                }
+                if (bj == kSrc) break;
+                done |= 1u << bj;
+                add(bw);
+            }
+        }
+    } else {
+        for (uint32_t k = 0; k < S; ++k) {
+            uint64_t prev = 0;  // (key << 32 | pixel) of the last source added
+            for (uint32_t t = dy_lo; t <= dy_hi; ++t) {
+                uint64_t best = ~0ull;
+                uint32_t best_slot = 0;
+                for (uint32_t dy = dy_lo; dy <= dy_hi; ++dy) {
+                    const uint32_t dx = p - dy * H;  // source pixel (dx, dy)
+                    uint32_t sq0, sst;
+                    ts_slot_base(dy - row0, dx, W, rows, S, sq0, sst);
+                    const uint32_t q = sq0 + k * sst;
+                    const uint32_t key = s2[q].y;
+                    const uint64_t kp = ((uint64_t)key << 32) | (dy * W + dx);
+                    if (key != 0u && kp > prev && kp < best) {
+                        best = kp;
+                        best_slot = q;
+                    }
+                }
+                if (best == ~0ull) break;
+                add(s2[best_slot].x);
+                prev = best;
+            }
+        }
+    }
+}
+
+// RenderSegment's / RenderSegmentTask's resolve of local pixel (lr, col) of a region
+// (map, `rows` rows, alias: task mode on a non-square tile) whose slots start at
+// `samples` (item order of a batch of a.spp_batch samples: ts_slot_base); local float4
+// output at out_rgba[lr * width + col].
+// SC1 (the render service's in-kernel fold): the sample words are loaded with sc1 loads
+// (another XCD's L2 may hold stale lines of the ring) and the outputs stored write-through
+// (sc1), so that the counter add after the wave's drain publishes them (MI355X_MICROARCH.md
+// hand-off table, R1).  Segment mode and square task tiles only (no aliasing).
+template <bool SC1 = false, int RUN = SPT_FOLD_RUN>
+__device__ __forceinline__ void fold_pixel(const FoldArgs &a, const uint32_t *samples, const RowMap &map,
+                                           uint32_t rows, int alias, uint32_t lr, uint32_t col, float4 *out_rgba,
+                                           uint8_t *out_rgb8)
+{
+    typedef __attribute__((address_space(1))) uint32_t g32;
+    typedef __attribute__((address_space(1))) unsigned long long g64;
+    typedef __attribute__((address_space(1))) uint8_t g8;
+    auto ldw = [&](const uint32_t *q) -> uint32_t {
+        return SC1 ? __hip_atomic_load((g32 *)q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : *q;
+    };
+    auto ldw2 = [&](const uint2 *q) -> uint2 {
+        if (!SC1) return *q;
+        const unsigned long long v = __hip_atomic_load((g64 *)q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return make_uint2((uint32_t)v, (uint32_t)(v >> 32));
+    };
+    const uint32_t W = map.width, S = a.spp_batch;
+    const uint32_t p = lr * W + col;
+    float4 acc = a.first ? make_float4(0.f, 0.f, 0.f, 0.f) : a.acc[p];
+    uint32_t q0, step;
+    ts_slot_base(lr, col, W, rows, S, q0, step);
+    if (a.mode == 0) {
+        // RenderSegment: one word per slot, every sample counts.  Runs of kFoldRun words
+        // are loaded before any is decoded (the loads of a run are in flight together),
+        // then decoded eight at a time
+        constexpr int kFoldRun = RUN;
+        uint32_t k = 0;
+        for (; k + kFoldRun <= S; k += kFoldRun) {
+            uint32_t w[kFoldRun];
+#pragma unroll
+            for (int i = 0; i < kFoldRun; ++i) w[i] = ldw(samples + q0 + (k + i) * step);
+#pragma unroll
+            for (int g = 0; g < kFoldRun; g += 8) {
+                uint32_t w8[8];
+#pragma unroll
+                for (int i = 0; i < 8; ++i) w8[i] = w[g + i];
+                f3 c[8];
+                decode_run<8>(a, w8, c);
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    acc.x = acc.x + c[i].x;
+                    acc.y = acc.y + c[i].y;
+                    acc.z = acc.z + c[i].z;
+                    acc.w = acc.w + 1.f;
+                }
+            }
+        }
+        for (; k < S; ++k) {
+            const f3 c = decode_sample(a, ldw(samples + q0 + k * step));
+            acc.x = acc.x + c.x;
+            acc.y = acc.y + c.y;
+            acc.z = acc.z + c.z;
+            acc.w = acc.w + 1.f;
+        }
+    } else if (!alias) {
+        // RenderSegmentTask on a square tile: pixel p is colors[p]; key 0 marks a dropped path
+        const uint2 *s2 = (const uint2 *)samples;
+        for (uint32_t k = 0; k < S; ++k) {
+            const uint2 v = ldw2(s2 + q0 + k * step);
+            if (v.y != 0u) {
+                const f3 c = decode_sample(a, v.x);
+                acc.x = acc.x + c.x;
+                acc.y = acc.y + c.y;
+                acc.z = acc.z + c.z;
+                acc.w = acc.w + 1.f;
+            }
+        }
+    } else if (!SC1) {
+        alias_accumulate(a, samples, p, W, rows, 0u, rows, S, acc);
+    }
+    if (!a.last) {
+        a.acc[p] = acc;
+        if (!a.preview) return;
+    }
+    // RenderSegment: *= (1.f / g_samples) (line 133); RenderSegmentTask: *= 1.f / samples[i]
+    // (line 198).  s_done == g_samples after the last batch; a progressive preview after
+    // s_done samples is the render at g_samples = s_done, bit for bit (keyed samples).
+    const float scale = a.mode == 0 ? 1.f / (float)a.s_done : 1.f / acc.w;
+    const float r = acc.x * scale, g = acc.y * scale, b = acc.z * scale;
+    if (out_rgba) {
+        if (SC1) {
+            g64 *o = (g64 *)(out_rgba + p);
+            __hip_atomic_store(o, (unsigned long long)__float_as_uint(r) | ((unsigned long long)__float_as_uint(g) << 32),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(o + 1, (unsigned long long)__float_as_uint(b), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            out_rgba[p] = make_float4(r, g, b, 0.f);
+        }
+    }
+    if (out_rgb8) {
+        const uint32_t x = map.x0 + col;
+        const uint32_t y = row_of(map, lr);
+        const size_t gi = (size_t)3 * ((size_t)(a.height - 1u - y) * a.width + x);
+        if (SC1) {
+            __hip_atomic_store((g8 *)(out_rgb8 + gi + 0), gamma_byte(r), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store((g8 *)(out_rgb8 + gi + 1), gamma_byte(g), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store((g8 *)(out_rgb8 + gi + 2), gamma_byte(b), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            out_rgb8[gi + 0] = gamma_byte(r);
+            out_rgb8[gi + 1] = gamma_byte(g);
+            out_rgb8[gi + 2] = gamma_byte(b);
+        }
+    }
+}
+
 // 1 (default): the service stores sample words write-through (sc1), and a completion
 // count needs only the wave's own drain; 0: plain stores and an agent release (buffer_wbl2,
 // a write-back of the XCD's whole L2) before every count
@@ -293,6 +567,10 @@ __device__ __forceinline__ uint32_t svc_find_job(uint32_t nb, uint32_t cur, uint
 // an agent release: the fold runs on any XCD) before the add (MI355X_MICROARCH.md
 // hand-off table, each storing wave signalling for itself; Compiler hazard: the asm wait
 // after the fence).
+//
+// In-kernel folds (SvcJob::fold_flags): the add that brings the counter to the job's
+// fold_target -- the job's last samples, whichever wave holds them -- publishes the job to
+// the session's fold ring (svc_fold_step then folds it, any wave, 64 pixels at a time).
 __device__ __forceinline__ void svc_flush(uint32_t idx, uint32_t cnt, uint32_t lane)
 {
     if (cnt == 0u) return;
@@ -302,8 +580,154 @@ __device__ __forceinline__ void svc_flush(uint32_t idx, uint32_t cnt, uint32_t l
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-    if (lane == 0) __hip_atomic_fetch_add((gu32 *)(k.svc_done + idx), cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t old = 0;
+    if (lane == 0) old = __hip_atomic_fetch_add((gu32 *)(k.svc_done + idx), cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (k.svc_trace && lane == 0) atomicMax(k.svc_trace + 4u * idx + 2u, __builtin_amdgcn_s_memrealtime());
+    if (k.svc_fold) {
+        uint32_t *const fb = k.svc_fold;
+        const uint32_t j = __builtin_amdgcn_readfirstlane(
+            lane == 0 ? __hip_atomic_load((gu32 *)(fb + 3u * k.svc_job_cap + idx), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                      : 0u);
+        const gu32 *jr = (const gu32 *)(k.svc_jobs + j);
+        const uint32_t w = lane == 0   ? __hip_atomic_load(jr + kSvcJobFoldTarget, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                           : lane == 1 ? __hip_atomic_load(jr + kSvcJobFoldFlags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                       : 0u;
+        const uint32_t target = __builtin_amdgcn_readlane(w, 0), flags = __builtin_amdgcn_readlane(w, 1);
+        if ((flags & kSvcFoldInKernel) && __builtin_amdgcn_readfirstlane(old) + cnt == target) {
+            uint32_t e = 0;
+            if (lane == 0) e = __hip_atomic_fetch_add((gu32 *)(k.svc_ctl + kSvcFoldTail), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            e = __builtin_amdgcn_readfirstlane(e);
+            if (lane == 0) __hip_atomic_store((gu32 *)(fb + e), j + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
+// One chunk of in-kernel fold work (64 pixels of one job) for a fold wave (svc_fold_loop):
+// the first fold-ring entry from the wave's position st[4] whose chunks are not all taken;
+// false when there is none.  Ring entries are written right after their slot is taken; an entry not written
+// yet is left for the next visit.  The chunk's samples are loaded after this wave's own sc1
+// poll of the job's completion counter has matched (R1: every storing wave drained its
+// write-through sample stores before its add), its outputs stored write-through and
+// drained before the chunk is counted; the wave that finishes a job's last chunk adds the
+// job's samples to the counter's folded total, the value the caller's stream waits for.
+// Wave-uniform; `tail` = published ring entries as last read.
+// k: the kernel's arguments (passed in: svc_fold_loop is a real call, and a callee's
+// kernarg segment pointer is null)
+__device__ __forceinline__ bool svc_fold_step(kargs_t &k, uint32_t lane, uint32_t *st, uint32_t tail)
+{
+    uint32_t *const ring = k.svc_fold;
+    const uint32_t jc = k.svc_job_cap;
+    uint32_t seen = __builtin_amdgcn_readfirstlane(st[4]);
+    while (seen < tail) {
+        const uint32_t j1 = __builtin_amdgcn_readfirstlane(
+            lane == 0 ? __hip_atomic_load((gu32 *)(ring + seen), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u);
+        if (j1 == 0u) return false;
+        const uint32_t j = j1 - 1u;
+        const uint32_t w = lane < kSvcJobWords
+                               ? __hip_atomic_load((const gu32 *)(k.svc_jobs + j) + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                               : 0u;
+        auto f = [&](int i) -> uint32_t { return __builtin_amdgcn_readlane(w, i); };
+        const RowMap map{f(8), f(9), f(10), f(11), f(12), f(13), f(14)};
+        const uint32_t rows = f(4), S = f(5), idx = f(3), npix = rows * map.width;
+        const uint32_t nch = (npix + 63u) / 64u;
+        uint32_t c = 0;
+        if (lane == 0) c = __hip_atomic_fetch_add((gu32 *)(ring + jc + j), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        c = __builtin_amdgcn_readfirstlane(c);
+        if (c >= nch) {
+            // every chunk of this entry is taken: move on
+            ++seen;
+            if (lane == 0) st[4] = seen;
+            continue;
+        }
+        const uint32_t target = f(kSvcJobFoldTarget);
+        for (;;) {
+            const uint32_t v = __builtin_amdgcn_readfirstlane(
+                lane == 0 ? __hip_atomic_load((gu32 *)(k.svc_done + idx), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u);
+            if ((int32_t)(v - target) >= 0) break;
+            __builtin_amdgcn_s_sleep(1);
+        }
+        FoldArgs fa{};
+        fa.slot_words = k.mode == 0u ? 1u : 2u;
+        fa.samples = k.samples + (size_t)fa.slot_words * f(2);
+        fa.shade = k.scene.shade;
+        fa.sky[0] = k.cam.sky[0];
+        fa.sky[1] = k.cam.sky[1];
+        fa.sky[2] = k.cam.sky[2];
+        fa.code_div = FastDiv{k.fold_code_div.d, k.fold_code_div.m, k.fold_code_div.s};
+        fa.map = map;
+        fa.width = k.width;
+        fa.height = k.height;
+        fa.npix = npix;
+        fa.spp_batch = fa.spp_total = fa.s_done = S;
+        fa.first = fa.last = 1;
+        fa.mode = (int)k.mode;
+        float4 *const rgba = (float4 *)((unsigned long long)f(kSvcJobFoldRgba) | ((unsigned long long)f(kSvcJobFoldRgba + 1) << 32));
+        uint8_t *const rgb8 = (uint8_t *)((unsigned long long)f(kSvcJobFoldRgb8) | ((unsigned long long)f(kSvcJobFoldRgb8 + 1) << 32));
+        const uint32_t i = c * 64u + lane;
+        if (i < npix) {
+            uint32_t lr, col;
+            tile_pixel(i, map.width, rows, lr, col);
+            fold_pixel<true, kSvcFoldRun>(fa, fa.samples, map, rows, 0, lr, col, rgba, rgb8);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        uint32_t fin = 0;
+        if (lane == 0) fin = __hip_atomic_fetch_add((gu32 *)(ring + 2u * jc + j), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (__builtin_amdgcn_readfirstlane(fin) + 1u == nch && lane == 0) {
+            __hip_atomic_fetch_add((gu32 *)(ring + 3u * jc + k.svc_done_cap + idx), f(1) - f(0), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add((gu32 *)(k.svc_ctl + kSvcFoldsDone), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        return true;
+    }
+    return false;
+}
+
+// The session's fold-ring tail (lane 0; 0 when the session has no fold block)
+__device__ __forceinline__ uint32_t svc_fold_tail(kargs_t &k, uint32_t lane)
+{
+    return k.svc_fold && lane == 0 ? __hip_atomic_load((gu32 *)(k.svc_ctl + kSvcFoldTail), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                   : 0u;
+}
+
+// Every in-kernel fold of the session finished (read after the stop flag or with no render
+// wave left: the forwarder stored the fold-job count before the pair that published them)
+__device__ __forceinline__ bool svc_folds_done(kargs_t &k, uint32_t lane)
+{
+    const uint32_t v = lane == 0 ? __hip_atomic_load((gu32 *)(k.svc_ctl + kSvcFoldJobs), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                     : lane == 1 ? __hip_atomic_load((gu32 *)(k.svc_ctl + kSvcFoldsDone), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                 : 0u;
+    return __builtin_amdgcn_readlane(v, 1) >= __builtin_amdgcn_readlane(v, 0);
+}
+
+// A fold wave of the session (waves of blocks < svc_fold_blocks but the forwarder): folds
+// published jobs chunk by chunk; leaves once the stop flag is seen or no render wave is
+// left, and every in-kernel fold of the session has finished (the render waves' last
+// flushes publish the last folds before those waves leave).  Dedicated waves keep the fold
+// code out of the render loop's registers; 31 of them fold a config-2 frame's 384 MB of
+// sample words at well above a frame's rate.
+__device__ __attribute__((noinline)) void svc_fold_loop(kargs_t *kp, uint32_t lane, uint32_t *st)
+{
+    kargs_t &k = *kp;
+    for (uint32_t idle = 0;; ++idle) {
+        const uint32_t tail = __builtin_amdgcn_readfirstlane(svc_fold_tail(k, lane));
+        if (tail > __builtin_amdgcn_readfirstlane(st[4]) && svc_fold_step(k, lane, st, tail)) {
+            idle = 0;
+            continue;
+        }
+        const bool stop =
+            __hip_atomic_load((gu32 *)(k.svc_ctl + kSvcStop), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+        const uint32_t live = __builtin_amdgcn_readfirstlane(
+            lane == 0 ? __hip_atomic_load((gu32 *)(k.svc_ctl + kSvcLive), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 1u);
+        if (stop || live == 0u) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (svc_folds_done(k, lane)) return;
+        }
+        // ~0.1 us between polls while folds arrive, ~3 us once idle for a while
+        if (idle < 256u)
+            __builtin_amdgcn_s_sleep(2);
+        else
+            __builtin_amdgcn_s_sleep(127);
+    }
 }
 
 template <bool TREE, int LEAF, bool LDSN, uint32_t BLOCK, bool BATCH = false, bool GLANE = false, bool SVC = false>
@@ -332,12 +756,17 @@ __device__ __forceinline__ void render_body(const RenderArgs &a)
     uint32_t *const park = s_park + (PRIM ? (threadIdx.x >> 6) * PW * 64u : 0u);
     // SVC: the wave's copy of its current job's record (svc_find_job, words 0-23) and its
     // claim state (words kSvcSt..31: kept in LDS, not SGPRs, since only claims read them)
-    __shared__ uint32_t s_rec[SVC ? (BLOCK / 64u) * kSvcJobWords : 1];
-    uint32_t *const rec = s_rec + (SVC ? (threadIdx.x >> 6) * kSvcJobWords : 0u);
-    if (SVC && lane < 4u) rec[kSvcSt + lane] = 0u;
-    // the session's forwarder: wave 0 of block 0 (before any claim is reserved)
+    __shared__ uint32_t s_rec[SVC ? (BLOCK / 64u) * kSvcRecWords : 1];
+    uint32_t *const rec = s_rec + (SVC ? (threadIdx.x >> 6) * kSvcRecWords : 0u);
+    if (SVC && lane < kSvcRecWords - kSvcSt) rec[kSvcSt + lane] = 0u;
+    // the session's forwarder: wave 0 of block 0 (before any claim is reserved); the other
+    // waves of the first svc_fold_blocks blocks are its fold waves (in-kernel folds)
     if (SVC && blockIdx.x == 0u && (threadIdx.x >> 6) == 0u) {
         svc_forward(lane);
+        return;
+    }
+    if (SVC && kernarg_args()->svc_fold && blockIdx.x < kernarg_args()->svc_fold_blocks) {
+        svc_fold_loop(kernarg_args(), lane, rec + kSvcSt);
         return;
     }
     uint32_t q_n = 0, q_pos = 0;  // the wave's queue: rows [q_pos, q_n) hold parked paths
@@ -865,228 +1294,6 @@ __global__ __launch_bounds__(kLdsBlock)
     __attribute__((amdgpu_num_sgpr(SPT_LDS_NUM_SGPR), amdgpu_waves_per_eu(2 * kLdsBlock / 256))) void render_kernel_lds_batch(RenderArgs a)
 {
     render_body<true, (int)kClusterSlots, true, kLdsBlock, true>(a);
-}
-
-// The colour of a sample word (code_word, spt_internal.h), with the render kernel's own
-// operations: the sky as SampleColorSkybox computes it (SingleThreadPathTracer.hpp:11-14),
-// a diffuse sample as the albedo * 0.5 (line 24) halved once more per further bounce
-// (line 31), bit for bit.  Halving is exact while the value stays normal, so j halvings
-// are one multiply by 2^-j when the result is normal (or 0 / inf / NaN); otherwise (a
-// denormal result: each halving may round) they are done one at a time.
-__device__ __forceinline__ float halve_n(float x, uint32_t j)
-{
-    if (j <= 126u) {
-        const float r = x * __uint_as_float((127u - j) << 23);
-        if (__builtin_fabsf(r) >= 0x1p-126f || x == 0.f || !__builtin_isfinite(x)) return r;
-    }
-    for (uint32_t i = 0; i < j; ++i) x = x * 0.5f;
-    return x;
-}
-__device__ __forceinline__ f3 decode_sample(const FoldArgs &a, uint32_t w)
-{
-    const uint32_t c = word_code(w);
-    if (c == 0u) {
-        const float k = __uint_as_float(w);
-        return mul(mk(a.sky[0] * k, a.sky[1] * k, a.sky[2] * k), 0.5f);
-    }
-    if (c == 1u) return mk(0.f, 0.f, 0.f);
-    uint32_t j, slot;
-    diffuse_decode(c, a.code_div, j, slot);
-    const float4 sh = a.shade[slot];
-    return mk(halve_n(sh.x * 0.5f, j), halve_n(sh.y * 0.5f, j), halve_n(sh.z * 0.5f, j));
-}
-
-// decode_sample for a run of words without branches around the loads: the shading-table
-// reads of all N words are issued together (slot 0 stands in for sky and zero words), the
-// colours selected afterwards; only denormal halvings (halve_n's slow path) branch.
-template <int N>
-__device__ __forceinline__ void decode_run(const FoldArgs &a, const uint32_t (&w)[N], f3 (&col)[N])
-{
-    uint32_t c[N], j[N];
-    float4 sh[N];
-#pragma unroll
-    for (int i = 0; i < N; ++i) {
-        c[i] = word_code(w[i]);
-        uint32_t slot;
-        diffuse_decode(c[i] >= 2u ? c[i] : 2u, a.code_div, j[i], slot);
-        sh[i] = a.shade[slot];
-    }
-#pragma unroll
-    for (int i = 0; i < N; ++i) {
-        const float k = __uint_as_float(w[i]);
-        const f3 s = mul(mk(a.sky[0] * k, a.sky[1] * k, a.sky[2] * k), 0.5f);
-        const f3 d = mk(halve_n(sh[i].x * 0.5f, j[i]), halve_n(sh[i].y * 0.5f, j[i]), halve_n(sh[i].z * 0.5f, j[i]));
-        col[i] = c[i] == 0u ? s : c[i] == 1u ? mk(0.f, 0.f, 0.f) : d;
-    }
-}
-
-// words loaded ahead per thread in the fold (a multiple of 8): small folds (the drop-in's
-// batches of one or two tiles) have few threads, and each is bound by its loads' latency
-#ifndef SPT_FOLD_RUN
-#define SPT_FOLD_RUN 8
-#endif
-static_assert(SPT_FOLD_RUN % 8 == 0, "fold runs are decoded eight words at a time");
-
-// RenderSegmentTask's colorIndex aliasing (TaskBasedPathTracer.hpp:103,186,196-205) for
-// output index p of a W x H call: colors[p] collects every pixel (dx, dy) of the call with
-// dx + dy * H == p, and the resolve writes colors[p] to pixel (p % W, p / W).  Within a
-// sample the sources reach colors[p] in the order of their (key, pixel) (finish_step), so
-// each sample's sources are added in that order.  No source: 0 samples, and 0 * (1.f / 0)
-// is NaN, as in the reference.  The sources' slots are those of rows [row0, row0 + rows)
-// of the launch (the call's own rows, or a range of them: spt_render_frame).
-__device__ __forceinline__ void alias_accumulate(const FoldArgs &a, const uint32_t *samples, uint32_t p, uint32_t W,
-                                                 uint32_t H, uint32_t row0, uint32_t rows, uint32_t S, float4 &acc)
-{
-    const uint32_t dy_lo = p >= W ? (p - W + H) / H : 0u;
-    const uint32_t dy_hi = min(H - 1u, p / H);
-    const uint32_t ns = dy_hi + 1u - dy_lo;  // sources: pixels (p - dy H, dy)
-    const uint2 *s2 = (const uint2 *)samples;
-    auto add = [&](uint32_t w) {
-        const f3 c = decode_sample(a, w);
-        acc.x = acc.x + c.x;
-        acc.y = acc.y + c.y;
-        acc.z = acc.z + c.z;
-        acc.w = acc.w + 1.f;
-    };
-    constexpr uint32_t kSrc = 4;  // sources kept in registers (config 2's tiles: <= 2)
-    if (ns <= kSrc) {
-        // the sources' slot bases once; per sample their keys, added in (key, pixel)
-        // order (pixel order = dy order when W > H, reversed when W < H)
-        uint32_t sq[kSrc], sst[kSrc];
-#pragma unroll
-        for (uint32_t j = 0; j < kSrc; ++j) {
-            const uint32_t dy = j < ns ? dy_lo + j : dy_lo;
-            ts_slot_base(dy - row0, p - dy * H, W, rows, S, sq[j], sst[j]);
-        }
-        const bool rev = W < H;
-        for (uint32_t k = 0; k < S; ++k) {
-            uint2 v[kSrc];
-#pragma unroll
-            for (uint32_t j = 0; j < kSrc; ++j) v[j] = j < ns ? s2[sq[j] + k * sst[j]] : make_uint2(0u, 0u);
-            uint32_t done = 0;  // sources already added (bit j)
-            for (uint32_t t = 0; t < ns; ++t) {
-                uint32_t bj = kSrc, bk = 0, bw = 0;  // the next source: index, key, word
-#pragma unroll
-                for (uint32_t j = 0; j < kSrc; ++j) {
-                    const bool cand = j < ns && v[j].y != 0u && !((done >> j) & 1u);
-                    const bool before = bj == kSrc || v[j].y < bk || (v[j].y == bk && rev);
-                    if (cand && before) {
-                        bj = j;
-                        bk = v[j].y;
-                        bw = v[j].x;
-                    }
-                }
-                if (bj == kSrc) break;
-                done |= 1u << bj;
-                add(bw);
-            }
-        }
-    } else {
-        for (uint32_t k = 0; k < S; ++k) {
-            uint64_t prev = 0;  // (key << 32 | pixel) of the last source added
-            for (uint32_t t = dy_lo; t <= dy_hi; ++t) {
-                uint64_t best = ~0ull;
-                uint32_t best_slot = 0;
-                for (uint32_t dy = dy_lo; dy <= dy_hi; ++dy) {
-                    const uint32_t dx = p - dy * H;  // source pixel (dx, dy)
-                    uint32_t sq0, sst;
-                    ts_slot_base(dy - row0, dx, W, rows, S, sq0, sst);
-                    const uint32_t q = sq0 + k * sst;
-                    const uint32_t key = s2[q].y;
-                    const uint64_t kp = ((uint64_t)key << 32) | (dy * W + dx);
-                    if (key != 0u && kp > prev && kp < best) {
-                        best = kp;
-                        best_slot = q;
-                    }
-                }
-                if (best == ~0ull) break;
-                add(s2[best_slot].x);
-                prev = best;
-            }
-        }
-    }
-}
-
-// RenderSegment's / RenderSegmentTask's resolve of local pixel (lr, col) of a region
-// (map, `rows` rows, alias: task mode on a non-square tile) whose slots start at
-// `samples` (item order of a batch of a.spp_batch samples: ts_slot_base); local float4
-// output at out_rgba[lr * width + col].
-__device__ __forceinline__ void fold_pixel(const FoldArgs &a, const uint32_t *samples, const RowMap &map,
-                                           uint32_t rows, int alias, uint32_t lr, uint32_t col, float4 *out_rgba,
-                                           uint8_t *out_rgb8)
-{
-    const uint32_t W = map.width, S = a.spp_batch;
-    const uint32_t p = lr * W + col;
-    float4 acc = a.first ? make_float4(0.f, 0.f, 0.f, 0.f) : a.acc[p];
-    uint32_t q0, step;
-    ts_slot_base(lr, col, W, rows, S, q0, step);
-    if (a.mode == 0) {
-        // RenderSegment: one word per slot, every sample counts.  Runs of kFoldRun words
-        // are loaded before any is decoded (the loads of a run are in flight together),
-        // then decoded eight at a time
-        constexpr int kFoldRun = SPT_FOLD_RUN;
-        uint32_t k = 0;
-        for (; k + kFoldRun <= S; k += kFoldRun) {
-            uint32_t w[kFoldRun];
-#pragma unroll
-            for (int i = 0; i < kFoldRun; ++i) w[i] = samples[q0 + (k + i) * step];
-#pragma unroll
-            for (int g = 0; g < kFoldRun; g += 8) {
-                uint32_t w8[8];
-#pragma unroll
-                for (int i = 0; i < 8; ++i) w8[i] = w[g + i];
-                f3 c[8];
-                decode_run<8>(a, w8, c);
-#pragma unroll
-                for (int i = 0; i < 8; ++i) {
-                    acc.x = acc.x + c[i].x;
-                    acc.y = acc.y + c[i].y;
-                    acc.z = acc.z + c[i].z;
-                    acc.w = acc.w + 1.f;
-                }
-            }
-        }
-        for (; k < S; ++k) {
-            const f3 c = decode_sample(a, samples[q0 + k * step]);
-            acc.x = acc.x + c.x;
-            acc.y = acc.y + c.y;
-            acc.z = acc.z + c.z;
-            acc.w = acc.w + 1.f;
-        }
-    } else if (!alias) {
-        // RenderSegmentTask on a square tile: pixel p is colors[p]; key 0 marks a dropped path
-        const uint2 *s2 = (const uint2 *)samples;
-        for (uint32_t k = 0; k < S; ++k) {
-            const uint2 v = s2[q0 + k * step];
-            if (v.y != 0u) {
-                const f3 c = decode_sample(a, v.x);
-                acc.x = acc.x + c.x;
-                acc.y = acc.y + c.y;
-                acc.z = acc.z + c.z;
-                acc.w = acc.w + 1.f;
-            }
-        }
-    } else {
-        alias_accumulate(a, samples, p, W, rows, 0u, rows, S, acc);
-    }
-    if (!a.last) {
-        a.acc[p] = acc;
-        if (!a.preview) return;
-    }
-    // RenderSegment: *= (1.f / g_samples) (line 133); RenderSegmentTask: *= 1.f / samples[i]
-    // (line 198).  s_done == g_samples after the last batch; a progressive preview after
-    // s_done samples is the render at g_samples = s_done, bit for bit (keyed samples).
-    const float scale = a.mode == 0 ? 1.f / (float)a.s_done : 1.f / acc.w;
-    const float r = acc.x * scale, g = acc.y * scale, b = acc.z * scale;
-    if (out_rgba) out_rgba[p] = make_float4(r, g, b, 0.f);
-    if (out_rgb8) {
-        const uint32_t x = map.x0 + col;
-        const uint32_t y = row_of(map, lr);
-        const size_t gi = (size_t)3 * ((size_t)(a.height - 1u - y) * a.width + x);
-        out_rgb8[gi + 0] = gamma_byte(r);
-        out_rgb8[gi + 1] = gamma_byte(g);
-        out_rgb8[gi + 2] = gamma_byte(b);
-    }
 }
 
 // Threads take the region's pixels in 8x8-tile order (tile_pixel), so the 64 lanes of

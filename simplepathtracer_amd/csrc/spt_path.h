@@ -30,6 +30,11 @@
 #ifndef SPT_DUP
 #define SPT_DUP 0
 #endif
+// the cube-minus-ball sampler skips its one-trial-per-lane round 0 when at most 32 lanes
+// need a vector (coop_ball_vector)
+#ifndef SPT_SAMPLER_SKIP0
+#define SPT_SAMPLER_SKIP0 1
+#endif
 // wave walk: leaves entered by at most 8 lanes are tested as dealt (lane, member) pairs
 // (test_leaf_pairs); 2: also those entered by 9-16 lanes, two members per lane
 #ifndef SPT_LEAF_PAIRS
@@ -936,14 +941,25 @@ __device__ __forceinline__ f3 coop_ball_vector(uint64_t &st, bool need, uint32_t
 {
     const uint32_t lane = __lane_id();
     const uint64_t st0 = st;
-    uint64_t t = st0;
     f3 r;
-    r.x = uniform(t, -0.5f, 0.5f);
-    r.y = uniform(t, -0.5f, 0.5f);
-    r.z = uniform(t, -0.5f, 0.5f);
     uint32_t jacc = 0;
-    unsigned long long pend = __ballot(need && lensq(r) < 0.25f);
-    uint32_t jb = 1;
+    unsigned long long pend;
+    uint32_t jb;
+    const unsigned long long needm = __ballot(need);
+    if (SPT_SAMPLER_SKIP0 && __popcll(needm) <= 32) {
+        // at most 32 lanes need a vector: every one gets two or more helpers from trial 0 on
+        // (round 0 would run one trial per lane for all 64, half of them for nothing)
+        r = mk(0.f, 0.f, 0.f);
+        pend = needm;
+        jb = 0;
+    } else {
+        uint64_t t = st0;
+        r.x = uniform(t, -0.5f, 0.5f);
+        r.y = uniform(t, -0.5f, 0.5f);
+        r.z = uniform(t, -0.5f, 0.5f);
+        pend = __ballot(need && lensq(r) < 0.25f);
+        jb = 1;
+    }
     const uint32_t s_lo = (uint32_t)st0, s_hi = (uint32_t)(st0 >> 32);
     if (SPT_DIAG && rounds) rounds[0] += 1;  // calls (round 0 for every lane)
 #if SPT_DIAG

@@ -87,7 +87,7 @@ extern "C" __attribute__((visibility("default"))) int spt_test_stamp(void *strea
     return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 
-// A stream whose CU mask holds the low `keep` of `total` bits (the layout spt_api.cpp's
+// A stream whose CU mask holds the low `keep` of `total` bits (the layout spt_ctx.cpp's
 // masked_for uses); *out receives the hipStream_t.
 extern "C" __attribute__((visibility("default"))) int spt_test_masked_stream(uint32_t keep, uint32_t total, void **out)
 {

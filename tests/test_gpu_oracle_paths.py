@@ -1,6 +1,6 @@
 """Paths added in rounds 4 and 5, checked against the oracle directly and not only
 against the launched path: regions rendered as jobs of the resident
-render service, the drop-in's tiling read-ahead (spt_api.cpp SpecFrame,
+render service, the drop-in's tiling read-ahead (spt_batch.cpp SpecFrame,
 DESIGN.md §5) and launches on CU-masked streams (spt_set_reserved_cus), each compared bit
 for bit with the CPU restatement (oracle/: RenderSegment / RenderSegmentTask,
 SingleThreadPathTracer.hpp:118-136 / TaskBasedPathTracer.hpp:61-210, and

@@ -907,7 +907,7 @@ def test_concurrent_tiles_overlap_and_match(spt, ctx, golden_scenes):
 @pytest.mark.parametrize("task", [False, True])
 def test_batched_calls_match_single_calls(spt, golden_scenes, monkeypatch, task):
     """Concurrent spt_render_segment[_task] calls are rendered in batches (one render
-    and one fold launch over a table of rectangles, spt_api.cpp render_batched): float
+    and one fold launch over a table of rectangles, spt_batch.cpp render_batched): float
     pixels and g_data bytes of every tile equal the same calls rendered one by one
     without batching (SPT_BATCH=0), for square and non-square tiles (task mode: the
     colorIndex aliasing per tile) and ragged sizes; the stats count every call."""
@@ -1146,7 +1146,7 @@ def test_claim_queues_render_the_same(spt, golden_scenes, monkeypatch, task):
 
 def test_small_launches_on_two_streams_render_the_same(spt, ctx, golden_scenes):
     """Frames in flight on two streams (the bench's rank shares): a launch of under 3 Ki
-    items per wave takes the smaller grid (spt_api.cpp render_grid, grid_small).  The
+    items per wave takes the smaller grid (spt_ctx.cpp render_grid, grid_small).  The
     strips of an 8-way split rendered alternately on two streams, the same strips on the
     caller's stream alone, and the whole frame assembled from either, are bit-identical."""
     import torch

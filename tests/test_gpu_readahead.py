@@ -1,4 +1,4 @@
-"""GPU tests of the drop-in's tiling read-ahead (spt_api.cpp SpecFrame):
+"""GPU tests of the drop-in's tiling read-ahead (spt_batch.cpp SpecFrame):
 RenderSegment / RenderSegmentTask calls over the reference's tc x tc tiling
 (Renderer.hpp:264-273, MakeRenderSegmentData), g_data only, are served from one
 read-ahead render of the whole tiling, once the caller has called every tile of that

@@ -80,20 +80,26 @@ int main(int argc, char **argv)
     // and the slot is returned under the mutex (the reference's unlocked fetch_add +
     // notify can be lost and leave the final wait asleep).  `alive` lets main return only
     // after every detached thread has finished touching them.
+    // SPT_HARNESS_COLD=2 also prints every tile's RenderJob span (ms from the frame's start)
+    static std::vector<std::pair<double, double>> spans((size_t)tc * tc);
+    static std::chrono::steady_clock::time_point frame_t0;
     static std::atomic<int> free_threads, alive{0};
     static std::condition_variable cv;
     static std::mutex mu;
     auto frame_once = [&]() {
         const uint32_t sw = g_width / tc, sh = g_height / tc;
         free_threads = (int)tc;
+        frame_t0 = std::chrono::steady_clock::now();
         std::unique_lock<std::mutex> lk(mu);
         for (uint32_t j = 0; j < tc; ++j)
             for (uint32_t i = 0; i < tc; ++i) {
                 RenderSegmentData seg{sh * j, sh * j + sh > g_height ? g_height : sh * j + sh, sw * i,
                                       sw * i + sw > g_width ? g_width : sw * i + sw};
                 alive.fetch_add(1);
-                std::thread thread([seg, task, noop] {
+                const size_t k = (size_t)j * tc + i;
+                std::thread thread([seg, task, noop, k] {
                     free_threads.fetch_sub(1);
+                    const auto ts = std::chrono::steady_clock::now();
                     if (noop) {
                     } else if (task) {
                         RenderSegmentTask(seg);
@@ -102,6 +108,9 @@ int main(int argc, char **argv)
                     }
                     {
                         std::lock_guard<std::mutex> g(mu);
+                        const auto te = std::chrono::steady_clock::now();
+                        spans[k] = {std::chrono::duration<double, std::milli>(ts - frame_t0).count(),
+                                    std::chrono::duration<double, std::milli>(te - frame_t0).count()};
                         free_threads.fetch_add(1);
                     }
                     cv.notify_one();
@@ -125,6 +134,8 @@ int main(int argc, char **argv)
         const auto t3 = clk::now();
         spt_stats st{};
         spt_get_stats(spt_shim::context(), &st);
+        if (std::atoi(std::getenv("SPT_HARNESS_COLD")) == 2)
+            for (size_t k = 0; k < spans.size(); ++k) printf("tile %zu: %.3f .. %.3f ms\n", k, spans[k].first, spans[k].second);
         printf("cold ctx_ms=%.3f setup_ms=%.3f frame_ms=%.3f accel_ms=%.3f prim_ms=%.3f batches=%llu calls=%llu\n",
                ms(t0, t1), ms(t1, t2), ms(t2, t3), st.accel_build_ms, st.prim_list_build_ms,
                (unsigned long long)st.batches, (unsigned long long)st.batched_calls);

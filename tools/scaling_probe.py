@@ -32,6 +32,9 @@ ap.add_argument("--reserve", type=int, default=0, help="CUs kept free of launche
 ap.add_argument("--blocker", type=int, default=0,
                 help="after each frame, a collective stand-in of this many us (tests/cpp/spt_testhooks.hip's "
                      "blocker: 8 blocks of 256-VGPR waves, like RCCL's gather kernel) on a third stream")
+ap.add_argument("--sdma", type=int, default=0,
+                help="after each frame, copy its tile to page-locked host memory on a third stream (a copy-engine "
+                     "transfer that needs no CU: the stand-in for a peer copy over xGMI); the frame after next waits")
 args = ap.parse_args()
 W, H, SPP, B = {"c2": (1200, 800, 100, 50), "c3": (3840, 2160, 1024, 50)}[args.config]
 ctx = spt.Context(0)
@@ -51,6 +54,7 @@ lines = []
 for n in [int(x) for x in args.ns.split(",")]:
     split = FrameSplit(W, H, n, args.strip or even_strip(H, n))
     tiles = [torch.zeros((split.tile_pixels(), 4), dtype=torch.float32, device="cuda") for _ in streams]
+    hosts = [torch.zeros((split.tile_pixels(), 4), dtype=torch.float32).pin_memory() for _ in streams] if args.sdma else []
 
     def frame(k):
         ctx.render_rows_async(spt.MODE_SEGMENT, 0, H, split.strip if n > 1 else 1, n, 0, 0, W,
@@ -61,6 +65,12 @@ for n in [int(x) for x in args.ns.split(",")]:
             s = streams[k % len(streams)]
             comm.wait_stream(s)
             assert hooks.spt_test_blocker(ctypes.c_void_p(comm.cuda_stream), args.blocker, 8, None) == 0
+            s.wait_stream(comm)
+        if args.sdma:
+            s = streams[k % len(streams)]
+            comm.wait_stream(s)
+            with torch.cuda.stream(comm):
+                hosts[k % len(streams)].copy_(tiles[k % len(streams)], non_blocking=True)
             s.wait_stream(comm)
 
     ts = []
@@ -99,7 +109,8 @@ if args.record:
                       "libspt_hip.so")
     with open(args.record, "w") as f:
         f.write(f"# tools/scaling_probe.py --config {args.config} --streams {args.streams} --frames {args.frames} "
-                f"--reps {args.reps} --service {args.service} --reserve {args.reserve} --blocker {args.blocker}\n")
+                f"--reps {args.reps} --service {args.service} --reserve {args.reserve} --blocker {args.blocker} "
+                f"--sdma {args.sdma}\n")
         f.write(f"# {datetime.datetime.now().isoformat(timespec='seconds')}, git {head}, libspt_hip.so mtime "
                 f"{datetime.datetime.fromtimestamp(os.path.getmtime(so)).isoformat(timespec='seconds')}, "
                 f"env SPT_*: {' '.join(f'{k}={v}' for k, v in sorted(os.environ.items()) if k.startswith('SPT_')) or '-'}\n")

@@ -91,8 +91,12 @@ for step in "$@"; do
     tdrop) run tdrop 200 bash tools/trace_dropin.sh ;;
     tdrop20) TDROP_FRAMES=20 run tdrop20 200 bash tools/trace_dropin.sh ;;
     ab:*) NAB=$((${NAB:-0} + 1)); run ab$NAB 600 python tools/ab.py ${step#ab:} ;;
+    probe:*) NPR=$((${NPR:-0} + 1)); spec=${step#probe:}; envs=${spec%%|*}; pargs=${spec#*|}
+             run probe$NPR 400 env $(echo "$envs" | tr ',' ' ') python tools/scaling_probe.py --streams 2 --reps 3 $pargs \
+                 --record "gpurun_out/${TAG}_probe$NPR.txt" ;;
     pyt:*) NPY=$((${NPY:-0} + 1)); run pyt$NPY 400 $PYT -v -s ${step#pyt:} ;;
     benchc:*) NBC=$((${NBC:-0} + 1)); run benchc$NBC 300 python bench.py --no-cpu-baseline --no-dropin --config ${step#benchc:} ;;
+    coldtrace) SPT_HOST_TRACE=1 SPT_HARNESS_COLD=2 run coldtrace 120 simplepathtracer_amd/lib/spt_dropin_harness /dev/null 1200 800 100 50 4 0 0 ;;
     dropincold) run dropincold 300 python -c "import bench; print(bench.dropin_bench(1200, 800, 100, 50, 20, (4,)))" ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac

@@ -69,6 +69,9 @@ inline spt_ctx *context()
         // launch per batch of tiles); its session idles out by itself between frames
         const char *svc = std::getenv("SPT_SERVICE");
         if (svc && std::atoi(svc) != 0) check(c, spt_service_start(c), "spt_service_start");
+        // the batch and read-ahead streams, created with the context so that the first
+        // frame does not pay for them
+        check(c, spt_prepare_dropin(c), "spt_prepare_dropin");
         return c;
     }();
     return ctx;

@@ -185,6 +185,12 @@ SPT_API int spt_set_cluster_tree(spt_ctx *ctx, uint32_t branching);
  * engine (DESIGN.md §5 "Reserved CUs": 3.1 ms vs 18.5 ms into a 19 ms render at n = 32;
  * not bench.py's default -- the multi-rank bench is faster with the render service).
  * Results are identical for any n; the render service ignores it.  n < the CU count. */
+/* The drop-in's warm-up (the C++ shim calls it once, right after creating its
+ * context): creates the streams of the second batch set and of the tiling read-ahead
+ * now, so that the first frame does not pay for them (a HIP stream costs ~9.5 ms to
+ * create on MI355X and stalls the device's other queues meanwhile).  Results unchanged;
+ * optional. */
+SPT_API int spt_prepare_dropin(spt_ctx *ctx);
 SPT_API int spt_set_reserved_cus(spt_ctx *ctx, uint32_t n);
 /* Host-only check (no device needed): build the traversal tables for a scene and
  * verify the properties exactness rests on (every sphere once, preorder/skip

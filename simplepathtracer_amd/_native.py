@@ -107,6 +107,7 @@ def lib() -> ctypes.CDLL:
         "spt_set_cluster_size": ([P, u32], I),
         "spt_set_cluster_tree": ([P, u32], I),
         "spt_set_reserved_cus": ([P, u32], I),
+        "spt_prepare_dropin": ([P], I),
         "spt_set_engine": ([P, I], I),
         "spt_accel_check": ([P, P, u32, u32, u32, P], I),
         "spt_prim_lists_check": ([P, P, u32, P, P, u32, u32, u32, P, P, P, P, u32, P], I),

@@ -280,6 +280,7 @@ int render_batched(spt_ctx *ctx, std::unique_lock<std::mutex> &lk, int mode, uin
         bs->busy = true;
         ctx->batch_leader = false;
         ctx->batch_cv.notify_all();  // the next caller may assemble the next batch
+        if (!bs->stream && bs == &ctx->bsets[1]) bs->stream = warm_take(ctx, 0);  // created while set 0 rendered
         if (!bs->stream && hipStreamCreateWithFlags(&bs->stream, hipStreamNonBlocking) != hipSuccess) bs->stream = nullptr;
         int rc = bs->stream ? launch_batch(ctx, bs, batch) : fail(ctx, SPT_ERR_HIP, "stream creation failed");
         if (rc == SPT_OK) {
@@ -327,6 +328,7 @@ int spec_stream(spt_ctx *ctx, int p)
 {
     SpecFrame &sp = ctx->spec;
     BatchSet *bs = &sp.bs[p];
+    if (!bs->stream) bs->stream = warm_take(ctx, 1 + p);
     if (!bs->stream) {
         int lo = 0, hi = 0;
         HIP_TRY(ctx, hipDeviceGetStreamPriorityRange(&lo, &hi));
@@ -350,15 +352,16 @@ int spec_prepare(spt_ctx *ctx, std::unique_lock<std::mutex> &lk, int mode, uint3
     SpecFrame &sp = ctx->spec;
     sp.readers_cv.wait(lk, [&] { return sp.readers == 0; });
     host_trace("spec_prepare begin");
-    const uint32_t W = ctx->W, H = ctx->H, sw = W / tc, sh = H / tc;
-    const uint32_t slot_words = mode == SPT_MODE_SEGMENT ? 1u : 2u;
+    (void)mode;
+    const uint32_t W = ctx->W, H = ctx->H;
     int rc = ensure(ctx, &sp.d8, &sp.d8_cap, (size_t)W * H * 3);
     host_trace("spec_prepare d8");
     if (rc) return rc;
     const uint32_t np = std::min(sp.parts, tc), rpp = (tc + np - 1) / np;
+    // the parts' streams and sample workspaces come with the first read-ahead (spec_launch):
+    // a one-frame caller (the reference's MainLoop renders one frame per process) never
+    // pays for them
     for (uint32_t p = 0; p * rpp < tc; ++p) {
-        if ((rc = spec_stream(ctx, (int)p))) return rc;
-        host_trace("spec_prepare stream", (void *)(uintptr_t)p);
         BatchSet *bs = &sp.bs[p];
         const size_t tiles = (size_t)(std::min(tc, (p + 1) * rpp) - p * rpp) * tc;
         if (bs->h_rects_cap < tiles) {
@@ -372,10 +375,6 @@ int spec_prepare(spt_ctx *ctx, std::unique_lock<std::mutex> &lk, int mode, uint3
         }
         host_trace("spec_prepare host rects", (void *)(uintptr_t)p);
         if ((rc = ensure(ctx, &bs->d_rects, &bs->rects_cap, tiles))) return rc;
-        Workspace *w = workspace_for(ctx, bs->stream);
-        if (!w) return SPT_ERR_STATE;
-        if ((rc = ensure(ctx, &w->d_samples, &w->samples_cap, tiles * sw * sh * ctx->spp * slot_words))) return rc;
-        host_trace("spec_prepare samples", (void *)(uintptr_t)p);
     }
     return SPT_OK;
 }

@@ -28,6 +28,46 @@ void host_trace(const char *what, const void *arg)
     std::fprintf(stderr, "[spt %9.3f ms] %s %p\n", ms, what, arg);
 }
 
+// ---- stream warm-up (spt_prepare_dropin) ----------------------------------------------
+// Creates the second batch set's stream and the read-ahead parts' streams now, in the
+// caller, so that no frame pays for them.  Creating a stream adds a hardware queue, and
+// on the box that stalls every queue of the device for ~9.5 ms (the scheduler's queue
+// map is rewritten): done while the first frame renders (a helper thread, measured
+// round 6) it stretched that frame by the same ~45 ms it took off it
+void warm_start(spt_ctx *ctx)
+{
+    spt_ctx::Warm &w = ctx->warm;
+    if (w.started) return;
+    w.started = true;
+    int lo = 0, hi = 0;
+    (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
+    int prio = lo;  // the read-ahead parts' priority (spec_stream)
+    if (const char *e = env_var("SPT_READAHEAD_PRIO")) prio = std::atoi(e);
+    for (int i = 0; i < 1 + SpecFrame::kParts; ++i) {
+        hipStream_t s = nullptr;
+        const hipError_t e = i == 0 ? hipStreamCreateWithFlags(&s, hipStreamNonBlocking)
+                                    : hipStreamCreateWithPriority(&s, hipStreamNonBlocking, prio);
+        w.s[i] = e == hipSuccess ? s : nullptr;  // null: the taker creates its own
+    }
+}
+
+// Warm stream i, or nullptr without a warm-up (or once taken)
+hipStream_t warm_take(spt_ctx *ctx, int i)
+{
+    hipStream_t s = ctx->warm.s[i];
+    ctx->warm.s[i] = nullptr;
+    return s;
+}
+
+void warm_join(spt_ctx *ctx)
+{
+    for (hipStream_t &s : ctx->warm.s)
+        if (s) {
+            (void)hipStreamDestroy(s);
+            s = nullptr;
+        }
+}
+
 int check_on_device(spt_ctx *ctx, const void *p, const char *what)
 {
     hipPointerAttribute_t at{};
@@ -769,6 +809,7 @@ void spt_ctx_destroy(spt_ctx *ctx)
 {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
+    warm_join(ctx);
     (void)svc_end(ctx);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     for (auto *vec : {&ctx->pending_render, &ctx->pending_fold, &ctx->pool})
@@ -870,6 +911,15 @@ int spt_set_cluster_size(spt_ctx *ctx, uint32_t k)
 int spt_set_cluster_tree(spt_ctx *ctx, uint32_t branching)
 {
     return for_members(ctx, [&](spt_ctx *c) { return spt_set_cluster_tree_one(c, branching); });
+}
+
+int spt_prepare_dropin(spt_ctx *ctx)
+{
+    return for_members(ctx, [](spt_ctx *c) {
+        std::lock_guard<std::mutex> lk(c->mu);
+        warm_start(c);
+        return SPT_OK;
+    });
 }
 
 int spt_set_reserved_cus(spt_ctx *ctx, uint32_t n)

@@ -397,6 +397,14 @@ struct spt_ctx {
     uint64_t launches = 0;
 
     Service svc;
+
+    // Stream warm-up for the drop-in (spt_prepare_dropin, spt_ctx.cpp): the second batch
+    // set's stream (s[0]) and the read-ahead parts' streams (s[1 + p]), created up front
+    // and taken by the first call that needs each (warm_take)
+    struct Warm {
+        hipStream_t s[1 + SpecFrame::kParts] = {};
+        bool started = false;
+    } warm;
 };
 
 namespace spt_api {
@@ -455,6 +463,9 @@ bool svc_eligible(const spt_ctx *ctx, uint64_t words, bool keep_samples);
 // SPT_HOST_TRACE=1: a line on stderr with the ms since the process's first trace point
 // (where host time goes in a cold frame: allocations, stream creation, first launches)
 void host_trace(const char *what, const void *arg = nullptr);
+void warm_start(spt_ctx *ctx);
+hipStream_t warm_take(spt_ctx *ctx, int i);
+void warm_join(spt_ctx *ctx);
 bool svc_folds_in_kernel(const spt_ctx *ctx);
 int svc_begin(spt_ctx *ctx, int mode, const std::vector<hipEvent_t> &waits, int64_t reset_idx, hipStream_t s);
 int svc_end(spt_ctx *ctx);

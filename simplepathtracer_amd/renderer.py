@@ -101,6 +101,11 @@ class Context:
         _native.TREE_AUTO = default heuristic); results identical."""
         self._check(_native.lib().spt_set_cluster_tree(self._h, int(branching)))
 
+    def prepare_dropin(self) -> None:
+        """spt_prepare_dropin: create the drop-in's batch and read-ahead streams on a helper
+        thread (what the C++ shim does once after creating its context)."""
+        self._check(_native.lib().spt_prepare_dropin(self._h))
+
     def set_reserved_cus(self, n: int) -> None:
         """Keep n CUs free of launched renders (spt_set_reserved_cus: 32 = one per shader
         engine lets a whole-CU kernel on another stream start beside a render); results

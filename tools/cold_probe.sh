@@ -5,10 +5,10 @@
 # Usage (GPU box): bash tools/cold_probe.sh <out_dir>
 set -o pipefail
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
-OUT=${1:-$R/gpurun_out/cold}
+OUT=$R/${1:-gpurun_out/cold}
 mkdir -p "$OUT"
 H="$R/simplepathtracer_amd/lib/spt_dropin_harness"
-for v in default SPT_READAHEAD=0 SPT_BATCH=0; do
+for v in default SPT_BATCH_SETS=1 SPT_BATCH=0; do
   for rep in 1 2; do
     echo "== $v rep $rep"
     if [ "$v" = default ]; then

@@ -269,6 +269,11 @@ def main():
                          "-1 (default): the service for the rank shares of N > 1 ranks, launches at N = 1 "
                          "(profiles/svc_timeline_r04.txt: 20 config-2 frames, 1/8 shares 13.4 vs 14.4 ms, "
                          "whole frames 95.0 vs 92.9 ms)")
+    ap.add_argument("--transport", default="rccl", choices=["rccl", "ipc"],
+                    help="N > 1: how the rank tiles reach rank 0: one RCCL gather per frame (default, north_star), "
+                         "or the copy-engine transport (distributed.TileTransport: peer copies from IPC handles "
+                         "ordered by stream wait/write-value packets, no collective kernel; the session then "
+                         "keeps one block slot per CU free for the folds and assembles: DESIGN.md §5 Round 6)")
     ap.add_argument("--cpu-spp", type=int, default=0,
                     help="spp of the CPU-baseline sample (0: the config's own spp on config 2, scaled down on others)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -318,7 +323,8 @@ def main():
     # share; whole frames 4.46 vs 4.67 ms)
     auto_svc = world > 1 and world <= torch.cuda.device_count()
     use_svc = (args.service if args.service >= 0 else auto_svc) and args.engine == "megakernel"
-    if use_svc:
+    ipc = world > 1 and args.transport == "ipc"
+    if use_svc and not ipc:
         os.environ.setdefault("SPT_SVC_FULL_GRID", "1")
     scene_name, W, H, spp, bounces = CONFIGS[args.config]
     scene = make_scene(spt, scene_name)
@@ -351,15 +357,21 @@ def main():
              "local": None, "gathered": None}
         if world > 1:
             b["local"] = torch.zeros((split.tile_pixels(), 4), dtype=torch.float32, device=dev)
-            if rank == 0:
+            if rank == 0 and not ipc:
                 b["gathered"] = torch.zeros((world * split.tile_pixels(), 4), dtype=torch.float32, device=dev)
         bufs.append(b)
+    transport = None
+    if ipc:
+        from simplepathtracer_amd.distributed import TileTransport
+        # one gathered buffer per stream: frames f and f + nst share a stream (step below)
+        transport = TileTransport(ctx, split, rank, nbuf=nst)
     counter = [0]
     # gather timing of the timed steps (N > 1): events around each step's gather
     gev = []
 
     def step(timed=False):
-        k = counter[0] % nst
+        f = counter[0]
+        k = f % nst
         counter[0] += 1
         b = bufs[k]
         ev = None
@@ -368,7 +380,7 @@ def main():
             gev.append(ev)
         with torch.cuda.stream(streams[k]):  # RCCL collectives follow the current stream
             render_frame(ctx, split, rank, mode, b["local"], b["gathered"], b["frame"], b["g_data"],
-                         streams[k].cuda_stream, gather_events=ev)
+                         streams[k].cuda_stream, gather_events=ev, transport=transport, frame_no=f)
 
     if use_svc:
         ctx.service_start()
@@ -455,6 +467,7 @@ def main():
                        "width": W, "height": H, "spp": spp, "bounces": bounces, "spheres": scene.n,
                        "parallelism": f"row-strips{split.strip}x{world}" if world > 1 else "1 GPU",
                        "frames_in_flight": nst, "render_service": bool(use_svc),
+                       "transport": (args.transport if world > 1 else None),
                        "service_full_grid": bool(use_svc) and os.environ.get("SPT_SVC_FULL_GRID", "0") != "0"},
             # contract form: the render kernel against HBM with SURVEY §8(d)'s algorithmic
             # bytes; HBM does not bind this kernel (VALU issue + latency do: roofline_valu)
@@ -496,8 +509,9 @@ def main():
             out["ranks"] = {"render_ms": [round(v, 4) for v in per_rank[0]],
                             "gather_ms": [round(v, 4) for v in per_rank[1]],
                             "def": "per rank and step: render device time (union of its render launches' HIP-event "
-                                   "intervals) and the gather (HIP events on the step's stream around dist.gather; "
-                                   "includes waiting for the slowest rank)"}
+                                   "intervals) and the gather (HIP events on the step's stream around dist.gather, "
+                                   "or around the transport's send / receive packets; includes waiting for the "
+                                   "slowest rank)"}
         if prof and "SQ_INSTS_VALU" in rk:
             # the binding resource: VALU issue.  Wave-instructions per launch from the PMC
             # pass over this same command, against 1024 SIMDs x 2.4 GHz / 2 cycles per
@@ -553,6 +567,8 @@ def main():
         if args.dump:
             torch.cuda.synchronize(dev)
             bufs[(counter[0] - 1) % nst]["g_data"].cpu().numpy().tofile(args.dump)
+    if transport is not None:
+        transport.close()
     ctx.close()
     if world > 1:
         dist.destroy_process_group()

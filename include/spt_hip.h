@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define SPT_ABI_VERSION 9
+#define SPT_ABI_VERSION 10
 
 /* Only the functions below are exported from libspt_hip.so (built with
  * -fvisibility=hidden), so several builds can be loaded side by side. */
@@ -312,6 +312,36 @@ SPT_API int spt_assemble_rows_async(spt_ctx *ctx, const void *d_tiles, uint32_t 
                             uint32_t strip, uint32_t parts, uint32_t xBegin, uint32_t xEnd, void *d_frame_rgba,
                             void *d_rgb8, void *stream);
 SPT_API int spt_synchronize(spt_ctx *ctx);
+
+/* ---- copy-engine tile transport (one process per GPU, ranks of one node) -------------
+ * The alternative to distributed.py's RCCL gather of the rank tiles (Renderer.hpp:257-302's
+ * tile split; DESIGN.md §5 "Round 6"): rank 0 holds nbuf gathered buffers of world tiles
+ * (tile_bytes each, rank-major, the layout spt_assemble_rows_async reads) in one device
+ * allocation it exports by IPC handle; rank r > 0 copies its tile into slot r of the
+ * frame's buffer with an asynchronous device-to-device copy on its own stream (peer
+ * memory over xGMI) and then raises its ready word; rank 0's stream waits for every ready
+ * word before its assemble and raises the buffer's consumed word after it, which a
+ * rank's copy into the same buffer nbuf frames later waits for.  The words live in a
+ * POSIX shared-memory segment (/dev/shm) page-locked in every process: stream
+ * wait/write-value packets, no host thread and no collective kernel on the path.
+ * Frames are numbered 0, 1, ... identically on every rank; frame f uses buffer f % nbuf.
+ * Setup: rank 0 calls spt_tiles_create(name) first; after a barrier every other rank
+ * calls it with the same name, then spt_tiles_attach with rank 0's spt_tiles_handle;
+ * after another barrier rank 0 may spt_tiles_unlink the name (the mappings stay).
+ * Rank 0 renders its own tile into slot 0 of spt_tiles_buffer(frame) on a stream ordered
+ * after its spt_tiles_release_async(frame - nbuf).  Errors: SPT_ERR_ARG (bad sizes, a
+ * segment name in use), SPT_ERR_STATE (a call for the other side), SPT_ERR_HIP. */
+typedef struct spt_tiles spt_tiles;
+SPT_API int spt_tiles_create(spt_ctx *ctx, const char *name, uint32_t rank, uint32_t world, uint64_t tile_bytes,
+                             uint32_t nbuf, spt_tiles **out);
+SPT_API int spt_tiles_handle(spt_tiles *t, uint8_t handle[64]);
+SPT_API int spt_tiles_attach(spt_tiles *t, const uint8_t handle[64]);
+SPT_API int spt_tiles_unlink(spt_tiles *t);
+SPT_API int spt_tiles_buffer(spt_tiles *t, uint64_t frame, void **d_buffer);
+SPT_API int spt_tiles_send_async(spt_tiles *t, uint64_t frame, const void *d_tile, void *stream);
+SPT_API int spt_tiles_recv_async(spt_tiles *t, uint64_t frame, void *stream);
+SPT_API int spt_tiles_release_async(spt_tiles *t, uint64_t frame, void *stream);
+SPT_API void spt_tiles_destroy(spt_tiles *t);
 
 /* Per-(pixel, sample) colors of a rectangle, host memory: out[(p*spp + s)*4 + c]
  * with p the region-local pixel.  w = 1 if the sample counts, 0 if dropped

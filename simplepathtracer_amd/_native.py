@@ -15,7 +15,7 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG_DIR, "lib", os.environ.get("SPT_LIB", "libspt_hip.so"))
 HEADER_PATH = os.path.join(os.path.dirname(PKG_DIR), "include", "spt_hip.h")
 
-ABI_VERSION = 9  # SPT_ABI_VERSION of include/spt_hip.h
+ABI_VERSION = 10  # SPT_ABI_VERSION of include/spt_hip.h
 SPT_OK = 0
 STATUS_NAMES = {0: "SPT_OK", 1: "SPT_ERR_ARG", 2: "SPT_ERR_STATE", 3: "SPT_ERR_HIP", 4: "SPT_ERR_NOMEM",
                 5: "SPT_ERR_NODEVICE", 6: "SPT_ERR_TIMEOUT"}
@@ -132,6 +132,15 @@ def lib() -> ctypes.CDLL:
         "spt_selftest_numerics": ([P, P, P, P, u32, P], I),
         "spt_service_start": ([P], I),
         "spt_service_stop": ([P], I),
+        "spt_tiles_create": ([P, ctypes.c_char_p, u32, u32, u64, u32, P], I),
+        "spt_tiles_handle": ([P, P], I),
+        "spt_tiles_attach": ([P, P], I),
+        "spt_tiles_unlink": ([P], I),
+        "spt_tiles_buffer": ([P, u64, P], I),
+        "spt_tiles_send_async": ([P, u64, P, P], I),
+        "spt_tiles_recv_async": ([P, u64, P], I),
+        "spt_tiles_release_async": ([P, u64, P], I),
+        "spt_tiles_destroy": ([P], None),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

@@ -4,7 +4,8 @@ with an RCCL gather of the per-tile framebuffers).
 One process per GPU.  The frame's rows are dealt in interleaved `strip`-row
 strips: rank r owns strips r, r+N, r+2N, ...  Each rank renders its rows into a
 compact float4 tile (spt_render_rows_async); one gather over RCCL/xGMI brings
-every tile to rank 0, which scatters them into the frame
+every tile to rank 0 (or the copy-engine TileTransport: peer copies from IPC
+handles, ordered by stream wait/write-value packets), which scatters them into the frame
 and the RGB8 g_data buffer (spt_assemble_rows_async).  Per-pixel results do not
 depend on the split (keyed per-(pixel, sample) RNG), so any N gives the 1-GPU frame.
 """
@@ -73,17 +74,114 @@ def gather_tiles(local_tile, gathered, group=None) -> None:
     dist.gather(local_tile, parts, dst=dst, group=group)
 
 
+class TileTransport:
+    """The copy-engine tile transport (spt_tiles_*, include/spt_hip.h): the alternative to
+    gather_tiles' RCCL gather.  Rank 0 owns `nbuf` gathered buffers in one device
+    allocation exported by IPC handle; every other rank copies its tile into its slot of
+    the frame's buffer on its own stream (a device-to-device copy into peer memory, no
+    collective kernel), and stream wait/write-value packets on words in a shared host
+    segment order the copies, rank 0's assemble and the buffers' reuse.  Frames are
+    numbered identically on every rank; frame f uses buffer f % nbuf.  Collective setup
+    over `torch.distributed` (any backend: only the segment name and the 64-byte handle
+    travel through it)."""
+
+    def __init__(self, ctx, split: FrameSplit, rank: int, nbuf: int = 2, group=None):
+        import ctypes
+        import os
+        import secrets
+        import torch.distributed as dist
+        from . import _native
+        self._lib = _native.lib()
+        self._ctx = ctx
+        self.rank, self.world, self.nbuf = rank, split.world, nbuf
+        self.tile_bytes = split.tile_pixels() * 16  # float4
+        src = dist.get_global_rank(group, 0) if group is not None else 0
+        name = [f"{os.getpid()}_{secrets.token_hex(6)}" if rank == 0 else None]
+        dist.broadcast_object_list(name, src=src, group=group)
+        self._h = ctypes.c_void_p()
+
+        def create():
+            _native.check(self._lib.spt_tiles_create(ctx.handle, name[0].encode(), rank, self.world,
+                                                     self.tile_bytes, nbuf, ctypes.byref(self._h)), ctx.handle)
+
+        if rank == 0:
+            create()  # the segment exists before the others open it
+        dist.barrier(group=group)
+        if rank != 0:
+            create()
+        handle = [None]
+        if rank == 0:
+            buf = (ctypes.c_uint8 * 64)()
+            self._check(self._lib.spt_tiles_handle(self._h, buf))
+            handle[0] = bytes(buf)
+        dist.broadcast_object_list(handle, src=src, group=group)
+        if rank != 0:
+            self._check(self._lib.spt_tiles_attach(self._h, (ctypes.c_uint8 * 64).from_buffer_copy(handle[0])))
+        dist.barrier(group=group)
+        if rank == 0:
+            self._check(self._lib.spt_tiles_unlink(self._h))
+
+    def _check(self, code: int) -> None:
+        from . import _native
+        _native.check(code, self._ctx.handle)
+
+    def buffer(self, frame: int) -> int:
+        """Rank 0: device address of frame's gathered buffer (its own tile is slot 0)."""
+        import ctypes
+        p = ctypes.c_void_p()
+        self._check(self._lib.spt_tiles_buffer(self._h, frame, ctypes.byref(p)))
+        return p.value
+
+    def send(self, frame: int, d_tile: int, stream) -> None:
+        import ctypes
+        self._check(self._lib.spt_tiles_send_async(self._h, frame, ctypes.c_void_p(d_tile), ctypes.c_void_p(stream)))
+
+    def recv(self, frame: int, stream) -> None:
+        import ctypes
+        self._check(self._lib.spt_tiles_recv_async(self._h, frame, ctypes.c_void_p(stream)))
+
+    def release(self, frame: int, stream) -> None:
+        import ctypes
+        self._check(self._lib.spt_tiles_release_async(self._h, frame, ctypes.c_void_p(stream)))
+
+    def close(self) -> None:
+        if self._h.value:
+            self._lib.spt_tiles_destroy(self._h)
+            self._h = type(self._h)()
+
+
 def render_frame(ctx, split: FrameSplit, rank: int, mode: int, local_tile, gathered=None, frame=None,
-                 g_data=None, stream=0, group=None, gather_events=None) -> None:
+                 g_data=None, stream=0, group=None, gather_events=None, transport: TileTransport | None = None,
+                 frame_no: int = 0) -> None:
     """One distributed frame: render own rows, gather, assemble on rank 0.
     Tensors are device tensors; `stream` is the hipStream_t the launches use (the
     current torch stream: the collective follows it).  gather_events: an optional
     pair of torch.cuda.Event recorded on that stream around the gather (its time
-    includes waiting for the slowest rank's render)."""
+    includes waiting for the slowest rank's render).  transport: the copy-engine
+    transport instead of the RCCL gather (frame_no: the frame's number, the same on
+    every rank; rank 0 renders into its slot of the frame's buffer, `gathered` unused;
+    with nbuf buffers, frames f and f + nbuf must use the same stream)."""
     if split.world == 1:
         ctx.render_rows_async(mode, 0, split.height, 1, 1, 0, 0, split.width,
                               frame.data_ptr() if frame is not None else 0,
                               g_data.data_ptr() if g_data is not None else 0, stream)
+        return
+    if transport is not None:
+        dst = transport.buffer(frame_no) if rank == 0 else local_tile.data_ptr()
+        ctx.render_rows_async(mode, 0, split.height, split.strip, split.world, rank, 0, split.width, dst, 0, stream)
+        if gather_events is not None:
+            gather_events[0].record()
+        if rank == 0:
+            transport.recv(frame_no, stream)
+        else:
+            transport.send(frame_no, dst, stream)
+        if gather_events is not None:
+            gather_events[1].record()
+        if rank == 0:
+            ctx.assemble_rows_async(dst, split.max_rows, 0, split.height, split.strip, split.world, 0, split.width,
+                                    frame.data_ptr() if frame is not None else 0,
+                                    g_data.data_ptr() if g_data is not None else 0, stream)
+            transport.release(frame_no, stream)
         return
     ctx.render_rows_async(mode, 0, split.height, split.strip, split.world, rank, 0, split.width,
                           local_tile.data_ptr(), 0, stream)

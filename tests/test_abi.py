@@ -12,7 +12,7 @@ def test_library_exports_every_declared_symbol(native):
     L = native.lib()
     missing = [n for n in names if not hasattr(L, n)]
     assert not missing, missing
-    assert L.spt_abi_version() == native.ABI_VERSION == 9
+    assert L.spt_abi_version() == native.ABI_VERSION == 10
 
 
 def test_ctx_create_reports_no_device_without_gpu(native):
@@ -30,6 +30,23 @@ def test_null_context_is_an_argument_error(native):
     L = native.lib()
     assert L.spt_set_params(None, 10, 10, 1, 1, 1) == 1
     assert L.spt_render_segment(None, 0, 1, 0, 1, None, None) == 1
+    assert b"null" in L.spt_last_error(None)
+
+
+def test_tile_transport_validates_arguments(native):
+    """spt_tiles_* (the copy-engine tile transport) reject a null context or transport
+    before touching a device, and destroying a null transport is a no-op.  (The size,
+    rank and side checks need a context, i.e. a GPU: tests/test_gpu_parity.py.)"""
+    L = native.lib()
+    h = ctypes.c_void_p()
+    assert L.spt_tiles_create(None, b"x", 0, 2, 16, 2, ctypes.byref(h)) == 1
+    assert not h.value
+    assert L.spt_tiles_buffer(None, 0, ctypes.byref(h)) == 1
+    assert L.spt_tiles_send_async(None, 0, None, None) == 1
+    assert L.spt_tiles_recv_async(None, 0, None) == 1
+    assert L.spt_tiles_release_async(None, 0, None) == 1
+    assert L.spt_tiles_attach(None, None) == 1
+    L.spt_tiles_destroy(None)
     assert b"null" in L.spt_last_error(None)
 
 

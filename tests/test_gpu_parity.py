@@ -537,15 +537,18 @@ def test_cpp_dropin_shim_renders_like_the_context(spt, golden_scenes, tmp_path, 
     assert bad.size == 0, f"{bad.size} bytes differ in tiles (row, col) {tiles[:24]} (of {len(tiles)})"
 
 
-@pytest.mark.parametrize("service", [0, 1])
-def test_bench_two_ranks_on_one_gpu_matches_one_rank(spt, tmp_path, service):
+@pytest.mark.parametrize("service,transport", [(0, "rccl"), (1, "rccl"), (0, "ipc"), (1, "ipc")])
+def test_bench_two_ranks_on_one_gpu_matches_one_rank(spt, tmp_path, service, transport):
     """bench.py's N>1 flow (strip split, gather to rank 0, rank-0 assemble)
     rehearsed with two gloo ranks sharing cuda:0, launched by bench.py itself
     (`--gpus 2`, no torchrun): the line says 2 ranks and g_data equals N=1's.
     service=1 runs the N>1 default of a real node -- every rank share a job of the
     rank's resident render service, gathered per frame (bench.py `use_svc`) -- with each
     rank's session on half its grid (SPT_SVC_GRID_DIV=2) so both ranks' sessions are
-    resident on the one GPU."""
+    resident on the one GPU.  transport="ipc": the copy-engine TileTransport instead of
+    the gather (rank 1's copies into rank 0's IPC-exported buffers, stream wait/write
+    packets on shared host words), over enough frames that each of the two gathered
+    buffers is reused (its consumed word gates the next copy)."""
     import json
     import os
     import subprocess
@@ -561,11 +564,14 @@ def test_bench_two_ranks_on_one_gpu_matches_one_rank(spt, tmp_path, service):
     if service:
         env["SPT_SVC_GRID_DIV"] = "2"
         extra = ["--service", "1", "--steps", "3", "--warmup", "1"]
+    if transport == "ipc":
+        extra = ["--service", str(service), "--steps", "5", "--warmup", "2", "--transport", "ipc"]
     r = subprocess.run(base + ["--gpus", "2", "--dump", str(two)] + extra, check=True, timeout=300, cwd=root, env=env,
                        capture_output=True, text=True)
     line = json.loads([s for s in r.stdout.splitlines() if s.startswith("{")][-1])
     assert line["n_gpus"] == 2 and line["world_size"] == 2 and line["backend"] == "gloo"
     assert line["config"]["render_service"] == bool(service)
+    assert line["config"]["transport"] == transport
     assert len(line["ranks"]["render_ms"]) == 2 and min(line["ranks"]["render_ms"]) > 0
     a, b = np.fromfile(one, np.uint8), np.fromfile(two, np.uint8)
     assert a.size == b.size == 1200 * 800 * 3

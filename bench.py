@@ -99,6 +99,15 @@ def tiled_pixels(w, h, tc):
     return (w // tc) * tc * (h // tc) * tc
 
 
+_T_START = time.perf_counter()
+
+
+def progress(msg: str) -> None:
+    """A progress line on stderr (the JSON line stays the only stdout line): a long
+    default run -- CPU baseline, drop-in processes -- keeps showing it is alive."""
+    print(f"[bench {time.perf_counter() - _T_START:7.1f} s] {msg}", file=sys.stderr, flush=True)
+
+
 def cpu_baseline(scene, view, w, h, spp_sample, bounces):
     """The CPU restatement (oracle/, "port", gcc -O2 -msse4.1) timed with the
     reference's RenderImageParallelMain tiling (Renderer.hpp:257-302: tc x tc tiles,
@@ -120,6 +129,7 @@ def cpu_baseline(scene, view, w, h, spp_sample, bounces):
             t0 = time.perf_counter()
             pyoracle.render_image_parallel(osc, fr, threads, mode=mode, want_rgba=False)
             dt = time.perf_counter() - t0
+            progress(f"cpu baseline {name} tc={threads}: {dt:.1f} s")
             wall += dt
             res[(name, threads)] = round(tiled_pixels(w, h, threads) * spp_sample / dt / 1e6, 4)
     return {"value": res[("task", tc)], "unit": "Msamples/s", "cores": cores, "kind": "port",
@@ -157,6 +167,7 @@ def dropin_bench(w, h, spp, bounces, frames, tcs, env=None):
             if r.returncode != 0:
                 raise RuntimeError(f"dropin harness (cold) failed: {r.stderr[-400:]}")
             line = r.stdout.split("cold ", 1)[1].split("\n")[0]
+            progress(f"drop-in cold {'task' if task else 'segment'} tc={tc}: {line}")
             runs.append({k: float(v) for k, v in (kv.split("=") for kv in line.split())})
         med = {k: float(np.median([x[k] for x in runs])) for k in ("ctx_ms", "setup_ms", "frame_ms", "accel_ms", "prim_ms")}
         key = f"cold_{'task' if task else 'segment'}_tc{tc}"
@@ -177,6 +188,7 @@ def dropin_bench(w, h, spp, bounces, frames, tcs, env=None):
                 raise RuntimeError(f"dropin harness failed: {r.stderr[-400:]}")
             sec = float(r.stdout.split("seconds=")[1].split()[0])
             key = f"{'task' if task else 'segment'}_tc{tc}"
+            progress(f"drop-in {key}: {frames} frames in {sec:.2f} s")
             out[key] = round(tiled_pixels(w, h, tc) * spp * frames / sec / 1e6, 3)
             if "batches=" in r.stdout:  # calls per batched launch, over all frames run
                 calls = int(r.stdout.split("calls=")[1].split()[0])
@@ -393,6 +405,7 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
+    progress(f"rank {rank}: warm-up done, timing {args.steps} steps")
     t0 = time.perf_counter()
     if use_svc:
         ctx.service_start()
@@ -545,9 +558,11 @@ def main():
             # spheres are scanned brute force by the reference's loop)
             cpu_spp = args.cpu_spp or (spp if args.config == "c2" else max(1, round(100 * 149 / scene.n)))
             cw, ch = (W, H) if args.config in ("c1", "c2") else (1200, 800)
+            progress("timed region done; CPU baseline")
             out["cpu_baseline"] = cpu_baseline(scene, view, cw, ch, cpu_spp, bounces)
         if world == 1 and args.config == "c2" and not args.no_dropin and args.engine == "megakernel":
             # the drop-in boundary itself: RenderSegment/RenderSegmentTask from RenderJob threads
+            progress("C++ drop-in legs")
             d = dropin_bench(W, H, spp, bounces, args.dropin_frames, (4, 2 * host_cores()))
             if d:
                 out["dropin"] = {"unit": "Msamples/s", **d,

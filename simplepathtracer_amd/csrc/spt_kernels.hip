@@ -571,6 +571,7 @@ __device__ __forceinline__ void fold_pixel(const FoldArgs &a, const uint32_t *sa
 // In-kernel folds (SvcJob::fold_flags): the add that brings the counter to the job's
 // fold_target -- the job's last samples, whichever wave holds them -- publishes the job to
 // the session's fold ring (svc_fold_step then folds it, any wave, 64 pixels at a time).
+template <bool FOLD>
 __device__ __forceinline__ void svc_flush(uint32_t idx, uint32_t cnt, uint32_t lane)
 {
     if (cnt == 0u) return;
@@ -583,7 +584,7 @@ __device__ __forceinline__ void svc_flush(uint32_t idx, uint32_t cnt, uint32_t l
     uint32_t old = 0;
     if (lane == 0) old = __hip_atomic_fetch_add((gu32 *)(k.svc_done + idx), cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (k.svc_trace && lane == 0) atomicMax(k.svc_trace + 4u * idx + 2u, __builtin_amdgcn_s_memrealtime());
-    if (k.svc_fold) {
+    if (FOLD && k.svc_fold) {
         uint32_t *const fb = k.svc_fold;
         const uint32_t j = __builtin_amdgcn_readfirstlane(
             lane == 0 ? __hip_atomic_load((gu32 *)(fb + 3u * k.svc_job_cap + idx), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
@@ -730,7 +731,10 @@ __device__ __attribute__((noinline)) void svc_fold_loop(kargs_t *kp, uint32_t la
     }
 }
 
-template <bool TREE, int LEAF, bool LDSN, uint32_t BLOCK, bool BATCH = false, bool GLANE = false, bool SVC = false>
+// SVCF: the session may fold jobs in-kernel (SPT_SVC_FOLD; its own instantiation, so that
+// the default session kernel keeps round 5's register allocation)
+template <bool TREE, int LEAF, bool LDSN, uint32_t BLOCK, bool BATCH = false, bool GLANE = false, bool SVC = false,
+          bool SVCF = false>
 __device__ __forceinline__ void render_body(const RenderArgs &a)
 {
     static_assert(!SVC || (SPT_PRIM && !LDSN && !GLANE && !BATCH), "the render service runs the wave-walk kernel");
@@ -765,7 +769,7 @@ __device__ __forceinline__ void render_body(const RenderArgs &a)
         svc_forward(lane);
         return;
     }
-    if (SVC && kernarg_args()->svc_fold && blockIdx.x < kernarg_args()->svc_fold_blocks) {
+    if (SVCF && kernarg_args()->svc_fold && blockIdx.x < kernarg_args()->svc_fold_blocks) {
         svc_fold_loop(kernarg_args(), lane, rec + kSvcSt);
         return;
     }
@@ -1010,7 +1014,7 @@ __device__ __forceinline__ void render_body(const RenderArgs &a)
                 // published pair: jobs are published before the stop).  After kSvcIdleTicks
                 // without work the wave may leave through the closing handshake with the
                 // host (spt_internal.h kSvcIdleTicks), then the watchdog word tells the host.
-                svc_flush(acc_idx, acc_cnt, lane);
+                svc_flush<SVCF>(acc_idx, acc_cnt, lane);
                 acc_cnt = 0;
                 unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
                 bool leave = false;
@@ -1174,7 +1178,7 @@ __device__ __forceinline__ void render_body(const RenderArgs &a)
                 const uint32_t j = __builtin_amdgcn_readlane(ps.job, (int)__builtin_ctzll(fm));
                 const unsigned long long m = __ballot(fin && ps.job == j);
                 if (j != acc_idx) {
-                    svc_flush(acc_idx, acc_cnt, lane);
+                    svc_flush<SVCF>(acc_idx, acc_cnt, lane);
                     acc_idx = j;
                     acc_cnt = 0;
                 }
@@ -1199,7 +1203,7 @@ __device__ __forceinline__ void render_body(const RenderArgs &a)
     }
 
     if (SVC) {
-        svc_flush(acc_idx, acc_cnt, lane);
+        svc_flush<SVCF>(acc_idx, acc_cnt, lane);
         // one render wave fewer (the forwarder leaves when none is left)
         kargs_t &k = *kernarg_args();
         if (lane == 0) __hip_atomic_fetch_add((gu32 *)(k.svc_ctl + kSvcLive), 0xFFFFFFFFu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1264,10 +1268,10 @@ __global__ __launch_bounds__(kRenderBlock) SPT_RENDER_ATTR void render_kernel_ba
 
 // the render service: one resident launch over a stream of published jobs (RenderArgs
 // svc_*)
-template <bool TREE, int LEAF>
+template <bool TREE, int LEAF, bool FOLD>
 __global__ __launch_bounds__(kRenderBlock) SPT_RENDER_ATTR void render_kernel_svc(RenderArgs a)
 {
-    render_body<TREE, LEAF, false, kRenderBlock, false, false, true>(a);
+    render_body<TREE, LEAF, false, kRenderBlock, false, false, true, FOLD>(a);
 }
 
 // trees of kLdsNodeRecords to kGlaneMaxNodes nodes: the lane walk reading layout 0 from
@@ -1517,12 +1521,23 @@ bool svc_supported(const AccelView &ac)
 hipError_t launch_render_svc(const RenderArgs &a, uint32_t grid, hipStream_t s)
 {
     if (!svc_supported(a.scene.accel) || !a.svc_host) return hipErrorInvalidValue;
-    if (a.scene.accel.tree)
-        hipLaunchKernelGGL((render_kernel_svc<true, (int)kClusterSlots>), dim3(grid), dim3(kRenderBlock), 0, s, a);
-    else if (a.scene.accel.leaf_slots == kFlatLeafSlots)
-        hipLaunchKernelGGL((render_kernel_svc<false, (int)kFlatLeafSlots>), dim3(grid), dim3(kRenderBlock), 0, s, a);
-    else
-        hipLaunchKernelGGL((render_kernel_svc<false, (int)kClusterSlots>), dim3(grid), dim3(kRenderBlock), 0, s, a);
+    // sessions that fold in-kernel (a.svc_fold) run the kernel built with the fold waves
+    if (a.scene.accel.tree) {
+        if (a.svc_fold)
+            hipLaunchKernelGGL((render_kernel_svc<true, (int)kClusterSlots, true>), dim3(grid), dim3(kRenderBlock), 0, s, a);
+        else
+            hipLaunchKernelGGL((render_kernel_svc<true, (int)kClusterSlots, false>), dim3(grid), dim3(kRenderBlock), 0, s, a);
+    } else if (a.scene.accel.leaf_slots == kFlatLeafSlots) {
+        if (a.svc_fold)
+            hipLaunchKernelGGL((render_kernel_svc<false, (int)kFlatLeafSlots, true>), dim3(grid), dim3(kRenderBlock), 0, s, a);
+        else
+            hipLaunchKernelGGL((render_kernel_svc<false, (int)kFlatLeafSlots, false>), dim3(grid), dim3(kRenderBlock), 0, s, a);
+    } else {
+        if (a.svc_fold)
+            hipLaunchKernelGGL((render_kernel_svc<false, (int)kClusterSlots, true>), dim3(grid), dim3(kRenderBlock), 0, s, a);
+        else
+            hipLaunchKernelGGL((render_kernel_svc<false, (int)kClusterSlots, false>), dim3(grid), dim3(kRenderBlock), 0, s, a);
+    }
     return hipGetLastError();
 }
 

@@ -618,7 +618,7 @@ int stats_one(spt_ctx *ctx, spt_stats *out)
     out->svc_watchdog_exits = ctx->svc.watchdog_exits;
     out->svc_kernel_ms = ctx->svc.kernel_ms;
     out->svc_running = ctx->svc.running ? 1u : 0u;
-    out->svc_grid_blocks = std::max<uint32_t>(1u, ctx->svc_grid / ctx->svc.grid_div);
+    out->svc_grid_blocks = svc_session_grid(ctx);
     out->svc_flow_restarts = ctx->svc.flow_restarts;
     out->svc_closing_restarts = ctx->svc.closing_restarts;
     out->prim_list_blocks = ctx->prim_blocks;
@@ -696,7 +696,10 @@ int spt_ctx_create(int device, spt_ctx **out)
     // kernels then wait for the session's end; for pipelines that end their sessions
     // themselves, like bench.py's timed regions: DESIGN.md §5)
     if (const char *e = env_var("SPT_SVC_FULL_GRID"))
-        if (std::atoi(e) != 0) ctx->svc_grid = (uint32_t)(per_cu * ctx->num_cu);
+        if (std::atoi(e) != 0) {
+            ctx->svc_grid = (uint32_t)(per_cu * ctx->num_cu);
+            ctx->svc_full = true;
+        }
     // launch_bounds / occupancy API may over-report by one block per CU for SGPR-heavy
     // kernels (MI355X_MICROARCH.md, Residency): the kernel needs no co-residency, so
     // extra blocks only queue.  SPT_BLOCKS_PER_CU overrides for tuning.
@@ -724,6 +727,7 @@ int spt_ctx_create(int device, spt_ctx **out)
     if (const char *e = env_var("SPT_SERVICE")) ctx->svc.enabled = std::atoi(e) != 0;
     if (const char *e = env_var("SPT_SVC_CLAIM")) ctx->svc.claim = (uint32_t)std::max(64, std::atoi(e) / 64 * 64);
     if (const char *e = env_var("SPT_SVC_FOLD")) ctx->svc.fold_inkernel = std::atoi(e) != 0;
+    if (const char *e = env_var("SPT_SVC_LDS")) ctx->svc.lds = std::atoi(e) != 0;
     if (const char *e = env_var("SPT_SVC_FOLD_BLOCKS")) ctx->svc.fold_blocks = (uint32_t)std::max(1, std::atoi(e));
     if (const char *e = env_var("SPT_SVC_QUEUES"))
         ctx->svc.queues = (uint32_t)std::min<int>((int)spt::kMaxQueues, std::max(1, std::atoi(e)));

@@ -159,6 +159,9 @@ struct Service {
     // svc_fold_words).  Off by default: measured slower than fold launches
     uint32_t *d_fold = nullptr;
     bool fold_inkernel = false;
+    // SPT_SVC_LDS=1: scenes whose tree takes the LDS lane walk run LDS-tree sessions
+    // (render_kernel_svc_lds); off by default: measured slower than launches (§4.7)
+    bool lds = false;
     bool fold_session = false;  // the running session has fold waves
     uint32_t fold_blocks = 64;  // SPT_SVC_FOLD_BLOCKS: blocks of fold waves per session
     uint64_t inkernel_folds = 0;  // jobs published with an in-kernel fold
@@ -258,6 +261,7 @@ struct spt_ctx {
     // the render service's grid: the occupancy's blocks per CU minus one, always (its
     // folds, publish launches and other streams' kernels need the free slot)
     uint32_t svc_grid = 0;
+    bool svc_full = false;  // SPT_SVC_FULL_GRID: sessions take every block slot (LDS-tree sessions too)
     uint32_t last_grid = 0, last_block = 0;  // shape of the most recent render launch
 
     // scene (Globals.hpp:31-37)
@@ -467,6 +471,7 @@ void warm_start(spt_ctx *ctx);
 hipStream_t warm_take(spt_ctx *ctx, int i);
 void warm_join(spt_ctx *ctx);
 bool svc_folds_in_kernel(const spt_ctx *ctx);
+uint32_t svc_session_grid(const spt_ctx *ctx);
 int svc_begin(spt_ctx *ctx, int mode, const std::vector<hipEvent_t> &waits, int64_t reset_idx, hipStream_t s);
 int svc_end(spt_ctx *ctx);
 int svc_wait(spt_ctx *ctx, hipEvent_t e, const char *what);

@@ -440,10 +440,19 @@ constexpr unsigned long long kSvcIdleTicks = 50000000ull;
 constexpr uint32_t kSvcHostCommitted = 0, kSvcHostClosing = 32, kSvcHostPub = 64, kSvcHostStop = 96,
                    kSvcHostWatchdog = 128, kSvcHostWords = 160;
 constexpr uint32_t kSvcTraceClaims = 1u << 21;  // SPT_SVC_TRACE: claims with a take time
+// grid: blocks of the session kernel's shape (svc_grid: 256-thread blocks, or the LDS-tree
+// kernel's 1 024-thread blocks when the scene's tree takes the LDS lane walk)
 hipError_t launch_render_svc(const RenderArgs &a, uint32_t grid, hipStream_t s);
-// the service covers the wave-walk kernels (render_kernel's shapes); the lane-walk
-// trees (LDS / global-memory node tables) keep their own launches
+// the service covers the wave-walk kernels (render_kernel's shapes) and the LDS lane walk
+// (render_kernel_lds's shape, round 6); trees walked from global memory keep their launches
 bool svc_supported(const AccelView &ac);
+// does the scene's session run the LDS-tree kernel (1 024-thread blocks)?
+bool svc_lds(const AccelView &ac);
+// the LDS-tree session's grid: every block slot (full) or one per CU fewer, at least one
+// per CU; 0 when the LDS-tree kernel cannot run on this device
+uint32_t svc_lds_grid(bool full);
+// threads per block of the session kernel for this scene
+uint32_t svc_block(const AccelView &ac);
 
 struct FoldArgs {
     const uint32_t *samples;  // slot_words per slot, in item order (ts_slot_base)

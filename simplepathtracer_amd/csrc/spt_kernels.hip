@@ -64,6 +64,10 @@ constexpr uint32_t kLdsBlock = SPT_LDS_BLOCK;
 #define SPT_LDS_NODES 2432
 #endif
 constexpr uint32_t kLdsNodeRecords = SPT_LDS_NODES;
+// the LDS-tree session kernel (render_kernel_svc_lds) also holds its waves' job records
+// (16 x kSvcRecWords words = 80 records' worth): its table is that much shorter, so that
+// two blocks still fit a CU (at 81 920 B the compiler keeps 64 VGPRs, 8 waves per SIMD)
+constexpr uint32_t kLdsSvcNodeRecords = kLdsNodeRecords - 80u;
 // smallest tree walked from LDS: below it the 8 octant layouts (64 nodes: 16 KiB) fit
 // the scalar cache
 #ifndef SPT_LDS_MIN_NODES
@@ -737,12 +741,14 @@ template <bool TREE, int LEAF, bool LDSN, uint32_t BLOCK, bool BATCH = false, bo
           bool SVCF = false>
 __device__ __forceinline__ void render_body(const RenderArgs &a)
 {
-    static_assert(!SVC || (SPT_PRIM && !LDSN && !GLANE && !BATCH), "the render service runs the wave-walk kernel");
+    static_assert(!SVC || (!GLANE && !BATCH && (LDSN || SPT_PRIM)),
+                  "the render service runs the wave-walk kernel or the LDS lane walk");
+    static_assert(!SVCF || (SVC && !LDSN), "in-kernel folds: the wave-walk session only");
     const uint32_t lane = __lane_id();
     const uint32_t rows = SVC ? 0u : a.npix / a.map.width;  // region rows (uniform; SVC: per job)
 
     __shared__ uint32_t s_lds[BLOCK];  // wave-private scratch of the cooperative sampler
-    __shared__ uint4 s_nodes[LDSN ? 2 * kLdsNodeRecords : 1];
+    __shared__ uint4 s_nodes[LDSN ? 2 * (SVC ? kLdsSvcNodeRecords : kLdsNodeRecords) : 1];
     // the LDS copy holds byte-offset skip links when only lane_cast walks it
     constexpr bool LDS_BYTES = LDSN && SPT_LANE_WALK && SPT_LANE_BUDGET > 0;
     // Primary batches (SPT_PRIM; the wave-walk kernels): when idle lanes want
@@ -764,8 +770,9 @@ __device__ __forceinline__ void render_body(const RenderArgs &a)
     uint32_t *const rec = s_rec + (SVC ? (threadIdx.x >> 6) * kSvcRecWords : 0u);
     if (SVC && lane < kSvcRecWords - kSvcSt) rec[kSvcSt + lane] = 0u;
     // the session's forwarder: wave 0 of block 0 (before any claim is reserved); the other
-    // waves of the first svc_fold_blocks blocks are its fold waves (in-kernel folds)
-    if (SVC && blockIdx.x == 0u && (threadIdx.x >> 6) == 0u) {
+    // waves of the first svc_fold_blocks blocks are its fold waves (in-kernel folds).  The
+    // LDS-tree session's forwarder first joins its block's node-table copy (its barrier)
+    if (SVC && !LDSN && blockIdx.x == 0u && (threadIdx.x >> 6) == 0u) {
         svc_forward(lane);
         return;
     }
@@ -785,6 +792,10 @@ __device__ __forceinline__ void render_body(const RenderArgs &a)
             s_nodes[k] = v;
         }
         __syncthreads();
+        if (SVC && blockIdx.x == 0u && (threadIdx.x >> 6) == 0u) {
+            svc_forward(lane);
+            return;
+        }
     }
     Path ps;
     ps.phase = PH_IDLE;
@@ -984,6 +995,18 @@ __device__ __forceinline__ void render_body(const RenderArgs &a)
                     }
                     prim_iter = true;
                 }
+            }
+        } else if (SVC && !PRIM && need != 0ull) {
+            // the LDS-tree session: idle lanes take items of the current claim, then of the
+            // next published one (a claim never spans two jobs: each lane starts from the
+            // job record current when it takes its item)
+            // (one claim per refill: lanes left over take the next claim next iteration)
+            if (blk_cur == blk_end) next_claim_svc();
+            if (blk_cur < blk_end) {
+                const uint32_t take = min((uint32_t)__popcll(need), blk_end - blk_cur);
+                const uint32_t rank = lane_rank(need);
+                if (__builtin_amdgcn_inverse_ballot_w64(need) && rank < take) start_path_svc(blk_cur + rank, rec, ps);
+                blk_cur += take;
             }
         } else if (BATCH && need != 0ull && !exhausted) {
             if (blk_cur == blk_end) next_claim();
@@ -1300,6 +1323,14 @@ __global__ __launch_bounds__(kLdsBlock)
     render_body<true, (int)kClusterSlots, true, kLdsBlock, true>(a);
 }
 
+// the render service over the LDS lane walk (config 5's trees): one resident launch of
+// render_kernel_lds's shape over the published jobs (DESIGN.md §4.7 "LDS-tree sessions")
+__global__ __launch_bounds__(kLdsBlock)
+    __attribute__((amdgpu_num_sgpr(SPT_LDS_NUM_SGPR), amdgpu_waves_per_eu(2 * kLdsBlock / 256))) void render_kernel_svc_lds(RenderArgs a)
+{
+    render_body<true, (int)kClusterSlots, true, kLdsBlock, false, false, true, false>(a);
+}
+
 // Threads take the region's pixels in 8x8-tile order (tile_pixel), so the 64 lanes of
 // a wave read 64 consecutive slots per sample.
 __global__ __launch_bounds__(256) void fold_kernel(FoldArgs a)
@@ -1461,6 +1492,14 @@ static void lds_tree_shape(int *per_cu, int *num_cu)
     *num_cu = nc[dev];
 }
 
+uint32_t svc_lds_grid(bool full)
+{
+    int per_cu = 0, num_cu = 0;
+    lds_tree_shape(&per_cu, &num_cu);
+    if (per_cu <= 0 || num_cu <= 0) return 0u;
+    return (uint32_t)((full ? per_cu : std::max(1, per_cu - 1)) * num_cu);
+}
+
 hipError_t launch_render(const RenderArgs &a, LaunchShape &sh, hipStream_t s)
 {
     const uint32_t div = sh.div ? sh.div : 1u;
@@ -1513,14 +1552,26 @@ hipError_t launch_render(const RenderArgs &a, LaunchShape &sh, hipStream_t s)
     return hipGetLastError();
 }
 
+bool svc_lds(const AccelView &ac)
+{
+    return ac.tree && ac.n_nodes >= kLdsMinNodes && ac.n_nodes + 1u <= kLdsSvcNodeRecords;
+}
+
 bool svc_supported(const AccelView &ac)
 {
-    return !(ac.tree && ac.n_nodes >= kLdsMinNodes && ac.n_nodes <= kGlaneMaxNodes);
+    return !(ac.tree && ac.n_nodes >= kLdsMinNodes && ac.n_nodes <= kGlaneMaxNodes) || svc_lds(ac);
 }
+
+uint32_t svc_block(const AccelView &ac) { return svc_lds(ac) ? kLdsBlock : kRenderBlock; }
 
 hipError_t launch_render_svc(const RenderArgs &a, uint32_t grid, hipStream_t s)
 {
     if (!svc_supported(a.scene.accel) || !a.svc_host) return hipErrorInvalidValue;
+    if (svc_lds(a.scene.accel)) {
+        if (a.svc_fold) return hipErrorInvalidValue;  // no fold waves in the LDS-tree session
+        hipLaunchKernelGGL(render_kernel_svc_lds, dim3(grid), dim3(kLdsBlock), 0, s, a);
+        return hipGetLastError();
+    }
     // sessions that fold in-kernel (a.svc_fold) run the kernel built with the fold waves
     if (a.scene.accel.tree) {
         if (a.svc_fold)

@@ -178,7 +178,7 @@ int svc_begin(spt_ctx *ctx, int mode, const std::vector<hipEvent_t> &waits, int6
         // the folded totals (the block's last done_cap words), like the completion counters
         HIP_TRY(ctx, hipMemsetAsync(v.d_fold + 3u * v.job_cap + v.done_cap, 0, (size_t)v.done_cap * sizeof(uint32_t), v.stream));
     }
-    const uint32_t grid = std::max<uint32_t>(1u, ctx->svc_grid / v.grid_div);
+    const uint32_t grid = svc_session_grid(ctx);
     v.fold_session = svc_folds_in_kernel(ctx);
     spt::RenderArgs ra{};
     ra.scene = device_scene(ctx);
@@ -227,8 +227,9 @@ int svc_begin(spt_ctx *ctx, int mode, const std::vector<hipEvent_t> &waits, int6
     // control words zeroed, the render-wave count set (every wave but the forwarder and the
     // fold waves), before the kernel; the fold ring and its chunk counters zeroed
     HIP_TRY(ctx, hipMemsetAsync(v.d_ctl, 0, spt::kSvcCtlWords * sizeof(uint32_t), v.stream));
-    const uint32_t waves = grid * (spt::kRenderBlock / 64u);
-    const uint32_t render_waves = v.fold_session ? waves - v.fold_blocks * (spt::kRenderBlock / 64u) : waves - 1u;
+    const uint32_t bw = spt::svc_block(ctx->accel) / 64u;  // waves per block of the session kernel
+    const uint32_t waves = grid * bw;
+    const uint32_t render_waves = v.fold_session ? waves - v.fold_blocks * bw : waves - 1u;
     HIP_TRY(ctx, hipMemsetD32Async((hipDeviceptr_t)(v.d_ctl + spt::kSvcLive), (int)render_waves, 1, v.stream));
     if (v.fold_session)
         HIP_TRY(ctx, hipMemsetAsync(v.d_fold, 0, (size_t)(3u * v.job_cap + v.done_cap) * sizeof(uint32_t), v.stream));
@@ -259,7 +260,16 @@ int svc_begin(spt_ctx *ctx, int mode, const std::vector<hipEvent_t> &waits, int6
 bool svc_folds_in_kernel(const spt_ctx *ctx)
 {
     const Service &v = ctx->svc;
-    return v.fold_inkernel && std::max<uint32_t>(1u, ctx->svc_grid / v.grid_div) > 2u * v.fold_blocks;
+    return v.fold_inkernel && !spt::svc_lds(ctx->accel) && svc_session_grid(ctx) > 2u * v.fold_blocks;
+}
+
+// Blocks of a session over the context's scene: the wave-walk kernel's svc_grid, or the
+// LDS-tree kernel's (1 024-thread blocks: every slot with SPT_SVC_FULL_GRID, else one per
+// CU fewer, so that folds and other kernels find room), divided by SPT_SVC_GRID_DIV
+uint32_t svc_session_grid(const spt_ctx *ctx)
+{
+    const uint32_t g = spt::svc_lds(ctx->accel) ? spt::svc_lds_grid(ctx->svc_full) : ctx->svc_grid;
+    return std::max<uint32_t>(1u, g / ctx->svc.grid_div);
 }
 
 // Can render_impl hand a launch of `words` sample words to the service?
@@ -267,7 +277,7 @@ bool svc_eligible(const spt_ctx *ctx, uint64_t words, bool keep_samples)
 {
     const Service &v = ctx->svc;
     return v.enabled && !keep_samples && ctx->engine == SPT_ENGINE_MEGAKERNEL && spt::svc_supported(ctx->accel) &&
-           words <= v.ring_bytes / sizeof(uint32_t) / 2;
+           (v.lds || !spt::svc_lds(ctx->accel)) && words <= v.ring_bytes / sizeof(uint32_t) / 2;
 }
 
 // Publish jobs sharing one completion counter (a render_impl batch: one job; a batched

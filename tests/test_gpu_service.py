@@ -99,6 +99,40 @@ def test_service_frames_equal_launched_frames(spt, golden_scenes, monkeypatch, m
     assert st["svc_inkernel_folds"] == (len(jobs) if fold and mode == 0 else 0)
 
 
+@pytest.mark.parametrize("full", [0, 1])
+@pytest.mark.parametrize("mode", [0, 1])
+def test_service_lds_tree_sessions_equal_launched_frames(spt, monkeypatch, mode, full):
+    """A 10 000-sphere stress scene (config 5's generator; its 2 026-node tree takes the
+    LDS lane walk) through the service (SPT_SVC_LDS=1, opt-in): the session runs
+    render_kernel_svc_lds (1 024-
+    thread blocks, the node table in LDS, the resumable lane walk; at most 2 blocks per CU)
+    and every frame and rank share equals its launched render bit for bit -- the launched
+    LDS kernel is pinned against brute force and the oracle by test_gpu_parity.py."""
+    import torch
+    monkeypatch.setenv("SPT_SVC_FULL_GRID", str(full))
+    monkeypatch.setenv("SPT_SVC_LDS", "1")
+    W, H = 320, 180
+    ctx = spt.Context(0)
+    ctx.set_scene(spt.generate_stress(5, 10000))
+    ctx.set_camera(spt.camera_basis(EYE, LOOK, UP), EYE, SKY)
+    ctx.set_params(W, H, 8, 50, 11)
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    jobs = [(0, H, 1, 1, 0, 0, W)] * 3 + [(0, H, 4, 3, p, 0, W) for p in range(3)] + [(5, 61, 1, 1, 0, 17, 250)]
+    ref = render_frames(ctx, jobs, W, H, mode, streams, service=False)
+    ctx.reset_stats()
+    got = render_frames(ctx, jobs, W, H, mode, streams, service=True)
+    st = ctx.stats()
+    ctx.close()
+    for k, ((a, b), (ra, rb)) in enumerate(zip(got, ref)):
+        assert_bitwise(a[:, :3], ra[:, :3], f"job {k} {jobs[k]} rgba")
+        assert np.array_equal(b, rb), f"job {k} {jobs[k]} g_data"
+    assert st["svc_jobs"] == len(jobs) and st["svc_sessions"] >= 1 and st["svc_running"] == 0
+    assert st["svc_watchdog_exits"] == 0
+    n_cu = torch.cuda.get_device_properties(0).multi_processor_count
+    # the LDS-tree session's grid: 1 024-thread blocks, one per CU (two with the full grid)
+    assert st["svc_grid_blocks"] == (2 if full else 1) * n_cu
+
+
 @pytest.mark.parametrize("fold", [1, 0])
 def test_service_rank_shares_and_regions(spt, golden_scenes, monkeypatch, fold):
     """Interleaved strips (the bench's rank shares), odd rectangles and tiny regions, many

@@ -36,9 +36,10 @@ ap.add_argument("--sdma", type=int, default=0,
                 help="after each frame, copy its tile to page-locked host memory on a third stream (a copy-engine "
                      "transfer that needs no CU: the stand-in for a peer copy over xGMI); the frame after next waits")
 args = ap.parse_args()
-W, H, SPP, B = {"c2": (1200, 800, 100, 50), "c3": (3840, 2160, 1024, 50)}[args.config]
+W, H, SPP, B = {"c2": (1200, 800, 100, 50), "c3": (3840, 2160, 1024, 50), "c5": (1920, 1080, 256, 50)}[args.config]
 ctx = spt.Context(0)
-ctx.set_scene(spt.generate_spheres(1))
+# config 5: the 10 000-sphere stress scene (bench.py make_scene "stress10k"; LDS lane walk)
+ctx.set_scene(spt.generate_stress(1, 10000) if args.config == "c5" else spt.generate_spheres(1))
 ctx.set_camera(spt.camera_basis(), spt.scene.DEFAULT_EYE, spt.INIT_COLOR)
 ctx.set_params(W, H, SPP, B, 1)
 ctx.set_reserved_cus(args.reserve)

@@ -124,7 +124,17 @@ int spt_tiles_create(spt_ctx *ctx, const char *name, uint32_t rank, uint32_t wor
     e = hipHostGetDevicePointer((void **)&t->words, t->host, 0);
     if (e != hipSuccess) return hip_fail(e, "hipHostGetDevicePointer");
     if (t->owner) {
-        e = hipMalloc((void **)&t->buf, (size_t)nbuf * world * tile_bytes);
+        // uncached device memory: the other ranks' copy engines write it over xGMI, which no
+        // L2 of this device observes, and the assemble reads each buffer again nbuf frames
+        // later -- an uncached line cannot be stale.  (The assemble reads it once per frame:
+        // 1/8 frame x 8 ranks of float4, no reuse to lose.)  Plain hipMalloc if refused.
+        const size_t bytes = (size_t)nbuf * world * tile_bytes;
+        e = hipExtMallocWithFlags((void **)&t->buf, bytes, hipDeviceMallocUncached);
+        if (e != hipSuccess) {
+            (void)hipGetLastError();
+            t->buf = nullptr;
+            e = hipMalloc((void **)&t->buf, bytes);
+        }
         if (e != hipSuccess) return hip_fail(e, "hipMalloc of the gathered buffers");
     }
     *out = t;
@@ -140,8 +150,6 @@ int spt_tiles_handle(spt_tiles *t, uint8_t handle[64])
     const hipError_t e = hipIpcGetMemHandle(&h, t->buf);
     if (e != hipSuccess) return fail(t->ctx, SPT_ERR_HIP, "tiles: hipIpcGetMemHandle: %s", hipGetErrorString(e));
     std::memcpy(handle, &h, 64);
-    // every rank has opened the segment once rank 0 exports (the caller's barrier came
-    // before): the name can go, the mappings stay
     return SPT_OK;
 }
 

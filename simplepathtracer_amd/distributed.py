@@ -11,6 +11,7 @@ depend on the split (keyed per-(pixel, sample) RNG), so any N gives the 1-GPU fr
 """
 from __future__ import annotations
 
+import ctypes
 from dataclasses import dataclass
 
 import numpy as np
@@ -86,7 +87,6 @@ class TileTransport:
     travel through it)."""
 
     def __init__(self, ctx, split: FrameSplit, rank: int, nbuf: int = 2, group=None):
-        import ctypes
         import os
         import secrets
         import torch.distributed as dist
@@ -127,21 +127,20 @@ class TileTransport:
 
     def buffer(self, frame: int) -> int:
         """Rank 0: device address of frame's gathered buffer (its own tile is slot 0)."""
-        import ctypes
         p = ctypes.c_void_p()
         self._check(self._lib.spt_tiles_buffer(self._h, frame, ctypes.byref(p)))
         return p.value
 
     def send(self, frame: int, d_tile: int, stream) -> None:
-        import ctypes
+        """Ranks > 0: the tile at d_tile into the frame's buffer, then the ready word."""
         self._check(self._lib.spt_tiles_send_async(self._h, frame, ctypes.c_void_p(d_tile), ctypes.c_void_p(stream)))
 
     def recv(self, frame: int, stream) -> None:
-        import ctypes
+        """Rank 0: `stream` waits for every rank's ready word of the frame."""
         self._check(self._lib.spt_tiles_recv_async(self._h, frame, ctypes.c_void_p(stream)))
 
     def release(self, frame: int, stream) -> None:
-        import ctypes
+        """Rank 0, after its reads of the frame's buffer: the buffer's consumed word."""
         self._check(self._lib.spt_tiles_release_async(self._h, frame, ctypes.c_void_p(stream)))
 
     def close(self) -> None:

@@ -394,6 +394,8 @@ def main():
             render_frame(ctx, split, rank, mode, b["local"], b["gathered"], b["frame"], b["g_data"],
                          streams[k].cuda_stream, gather_events=ev, transport=transport, frame_no=f)
 
+    progress(f"rank {rank}: {args.config} ready (setup {ctx.stats()['prim_list_build_ms']:.1f} ms of lists), "
+             f"{args.warmup} warm-up steps")
     if use_svc:
         ctx.service_start()
     for _ in range(args.warmup):

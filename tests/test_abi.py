@@ -77,6 +77,33 @@ def test_scene_generators_validate_arguments(native):
     assert c.n == 4 and list(c.materials) == [3, 3, 1, 2]
 
 
+def test_wider_random_scene_extends_the_reference_rows(native):
+    """spt_scene_generate_random_rows (BASELINE.json's "~500-sphere" scene): GenerateSpheres'
+    row loop (SceneGenerators.hpp:32-53) run to z < 37.5 instead of 20 draws the same
+    stream, so its first spheres are the reference-sized scene's, in order; every added
+    sphere lies in the added rows; z_end 20 is spt_scene_generate_random itself; a bad
+    z_end or a capacity below the scene is an argument error.  (Fuzz is drawn after the
+    rows, so it differs.)"""
+    import simplepathtracer_amd as spt
+    a, b = spt.generate_spheres(1), spt.generate_spheres(1, z_end=37.5)
+    assert a.n == 149 and 480 <= b.n <= 520
+    for k in ("centers", "radii", "colors", "materials"):
+        assert np.array_equal(getattr(b, k)[:a.n], getattr(a, k)), k
+    assert (b.centers[a.n:, 2] >= 20.0).all() and (b.centers[a.n:, 2] < 37.5 + 0.3).all()
+    c = spt.generate_spheres(1, z_end=20.0)
+    for k in ("centers", "radii", "colors", "materials", "fuzz"):
+        assert np.array_equal(getattr(c, k), getattr(a, k)), k
+    L = native.lib()
+    buf = [np.zeros(4 * 600, np.float32), np.zeros(600, np.float32), np.zeros(4 * 600, np.float32),
+           np.zeros(600, np.uint8), np.zeros(600, np.float32)]
+    n = ctypes.c_uint32()
+    ptrs = [x.ctypes.data for x in buf]
+    assert L.spt_scene_generate_random_rows(1, ctypes.c_float(-1.0), 600, *ptrs, ctypes.byref(n)) == 1
+    assert L.spt_scene_generate_random_rows(1, ctypes.c_float(37.5), 300, *ptrs, ctypes.byref(n)) == 1
+    assert L.spt_scene_generate_random_rows(1, ctypes.c_float(37.5), 600, *ptrs, ctypes.byref(n)) == 0
+    assert n.value == b.n
+
+
 def _build_shim_harness(tmp_path):
     import os
     import subprocess

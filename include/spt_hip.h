@@ -329,8 +329,10 @@ SPT_API int spt_synchronize(spt_ctx *ctx);
  * calls it with the same name, then spt_tiles_attach with rank 0's spt_tiles_handle;
  * after another barrier rank 0 may spt_tiles_unlink the name (the mappings stay).
  * Rank 0 renders its own tile into slot 0 of spt_tiles_buffer(frame) on a stream ordered
- * after its spt_tiles_release_async(frame - nbuf).  Errors: SPT_ERR_ARG (bad sizes, a
- * segment name in use), SPT_ERR_STATE (a call for the other side), SPT_ERR_HIP. */
+ * after its spt_tiles_release_async(frame - nbuf).  spt_tiles_destroy synchronizes the
+ * device (stop the render service first: a resident session would hold it up to its idle
+ * exit).  Errors: SPT_ERR_ARG (bad sizes, a segment name in use), SPT_ERR_STATE (a call for
+ * the other side), SPT_ERR_HIP. */
 typedef struct spt_tiles spt_tiles;
 SPT_API int spt_tiles_create(spt_ctx *ctx, const char *name, uint32_t rank, uint32_t world, uint64_t tile_bytes,
                              uint32_t nbuf, spt_tiles **out);

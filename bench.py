@@ -386,15 +386,15 @@ def main():
              "g_data": torch.zeros(W * H * 3, dtype=torch.uint8, device=dev) if rank == 0 else None,
              "local": None, "gathered": None}
         if world > 1:
-            b["local"] = torch.zeros((split.tile_pixels(), 4), dtype=torch.float32, device=dev)
+            b["local"] = torch.zeros((split.slot_pixels(mode), 4), dtype=torch.float32, device=dev)
             if rank == 0 and not ipc:
-                b["gathered"] = torch.zeros((world * split.tile_pixels(), 4), dtype=torch.float32, device=dev)
+                b["gathered"] = torch.zeros((world * split.slot_pixels(mode), 4), dtype=torch.float32, device=dev)
         bufs.append(b)
     transport = None
     if ipc:
         from simplepathtracer_amd.distributed import TileTransport
         # one gathered buffer per stream: frames f and f + nst share a stream (step below)
-        transport = TileTransport(ctx, split, rank, nbuf=nst)
+        transport = TileTransport(ctx, split, rank, nbuf=nst, mode=mode)
     counter = [0]
     # gather timing of the timed steps (N > 1): events around each step's gather
     gev = []

@@ -312,6 +312,19 @@ SPT_API int spt_assemble_rows_async(spt_ctx *ctx, const void *d_tiles, uint32_t 
                             uint32_t strip, uint32_t parts, uint32_t xBegin, uint32_t xEnd, void *d_frame_rgba,
                             void *d_rgb8, void *stream);
 SPT_API int spt_synchronize(spt_ctx *ctx);
+/* The rank-share form of RenderImage's RenderSegmentTask({0, H, 0, W}) on a NON-SQUARE
+ * frame (mode TASK, W != H).  There the reference strides its colour accumulator by the
+ * tile height (TaskBasedPathTracer.hpp:103,186,196-205), so pixels alias across rows and a
+ * row-strip split cannot resolve them locally; the frame is split by output index instead.
+ * spt_task_range: part `part` of `parts`'s outputs [i0, i1) of the frame's row-major order
+ * (outputs with sources dealt evenly; the last part also takes the source-less tail,
+ * which resolves to NaN / bytes 0).  spt_render_task_range_async: renders the rows
+ * holding those outputs' sources and writes outputs [i0, i1) to d_rgba[0, i1 - i0)
+ * (float4, device) on `stream`.  The parts' outputs end to end are the frame, which
+ * spt_assemble_rows_async turns into RGBA / g_data with max_rows = H, strip 1, parts 1.
+ * (spt_render_frame does the same over a multi-device context.) */
+SPT_API int spt_task_range(uint32_t width, uint32_t height, uint32_t parts, uint32_t part, uint32_t *i0, uint32_t *i1);
+SPT_API int spt_render_task_range_async(spt_ctx *ctx, uint32_t i0, uint32_t i1, void *d_rgba, void *stream);
 
 /* ---- copy-engine tile transport (one process per GPU, ranks of one node) -------------
  * The alternative to distributed.py's RCCL gather of the rank tiles (Renderer.hpp:257-302's
@@ -341,6 +354,10 @@ SPT_API int spt_tiles_attach(spt_tiles *t, const uint8_t handle[64]);
 SPT_API int spt_tiles_unlink(spt_tiles *t);
 SPT_API int spt_tiles_buffer(spt_tiles *t, uint64_t frame, void **d_buffer);
 SPT_API int spt_tiles_send_async(spt_tiles *t, uint64_t frame, const void *d_tile, void *stream);
+/* The same for `bytes` at byte `offset` of the frame's buffer instead of slot `rank` (the
+ * task-range split, spt_task_range: each part's outputs at their place in the frame) */
+SPT_API int spt_tiles_send_range_async(spt_tiles *t, uint64_t frame, const void *d_src, uint64_t offset,
+                                       uint64_t bytes, void *stream);
 SPT_API int spt_tiles_recv_async(spt_tiles *t, uint64_t frame, void *stream);
 SPT_API int spt_tiles_release_async(spt_tiles *t, uint64_t frame, void *stream);
 SPT_API void spt_tiles_destroy(spt_tiles *t);

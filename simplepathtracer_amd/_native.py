@@ -138,6 +138,9 @@ def lib() -> ctypes.CDLL:
         "spt_tiles_unlink": ([P], I),
         "spt_tiles_buffer": ([P, u64, P], I),
         "spt_tiles_send_async": ([P, u64, P, P], I),
+        "spt_tiles_send_range_async": ([P, u64, P, u64, u64, P], I),
+        "spt_task_range": ([u32, u32, u32, u32, P, P], I),
+        "spt_render_task_range_async": ([P, u32, u32, P, P], I),
         "spt_tiles_recv_async": ([P, u64, P], I),
         "spt_tiles_release_async": ([P, u64, P], I),
         "spt_tiles_destroy": ([P], None),

@@ -482,6 +482,7 @@ void release_slot(spt_ctx *ctx, HostSlot *h);
 HostSlot * acquire_slot(spt_ctx *ctx, std::unique_lock<std::mutex> &lk);
 int check_region(spt_ctx *ctx, uint32_t yB, uint32_t yE, uint32_t xB, uint32_t xE);
 int render_impl(spt_ctx *ctx, int mode, const spt::RowMap &map, float4 *d_rgba, uint8_t *d_rgb8, hipStream_t s, bool keep_samples, const Progress *pg = nullptr, uint32_t grid_div = 1, const AliasRange *ar = nullptr);
+int render_task_range(spt_ctx *ctx, uint32_t i0, uint32_t i1, float4 *d_out, hipStream_t s);
 spt::FoldArgs fold_args(const spt_ctx *ctx, const uint32_t *samples, uint32_t slot_words);
 int spec_serve(spt_ctx *ctx, std::unique_lock<std::mutex> &lk, int mode, uint32_t yB, uint32_t yE, uint32_t xB, uint32_t xE, uint8_t *g_data);
 int spec_launch(spt_ctx *ctx, std::unique_lock<std::mutex> &lk, int mode, uint32_t tc);

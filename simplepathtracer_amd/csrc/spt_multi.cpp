@@ -2,8 +2,56 @@
 // assemble) and page-locked g_data (spt_pin_host; spt_host.h).
 #include "spt_host.h"
 
+// Outputs [i0, i1) of RenderSegmentTask({0, H, 0, W}) on a non-square frame (the
+// context's frame; RenderImage's aliasing, TaskBasedPathTracer.hpp:103,186,196-205) into
+// d_out[0, i1 - i0) on stream s: the rows holding the range's sources (dx + dy H in
+// [i0, i1), 0 <= dx < W; none when i0 >= (W - 1) + (H - 1) H + 1: NaN outputs) rendered,
+// the range folded.  Called with ctx->mu held.
+namespace spt_api {
+
+int render_task_range(spt_ctx *ctx, uint32_t i0, uint32_t i1, float4 *d_out, hipStream_t s)
+{
+    const uint32_t W = ctx->W, H = ctx->H;
+    if (i1 <= i0) return SPT_OK;
+    const uint32_t dy_lo = i0 >= W ? (i0 - W + H) / H : 0u, dy_hi = std::min(H - 1u, (i1 - 1u) / H);
+    const spt::RowMap map{std::min(dy_lo, H), std::max(std::min(dy_lo, H), dy_hi + 1u), 1u, 1u, 0u, 0u, W};
+    const AliasRange ar{i0, i1 - i0, H};
+    return render_impl(ctx, SPT_MODE_TASK, map, d_out, nullptr, s, false, nullptr, 1, &ar);
+}
+
+}  // namespace spt_api
+
 
 extern "C" {
+
+int spt_task_range(uint32_t width, uint32_t height, uint32_t parts, uint32_t part, uint32_t *i0, uint32_t *i1)
+{
+    if (!i0 || !i1 || width == 0 || height == 0 || parts == 0 || part >= parts)
+        return fail(nullptr, SPT_ERR_ARG, "bad task range arguments");
+    // outputs [0, n_src) have sources (p_max + 1 = W + (H - 1) H, at most W H): dealt evenly,
+    // the last part also takes the source-less tail (every part renders about the same rows)
+    const uint64_t total = (uint64_t)width * height;
+    const uint64_t n_src = std::min<uint64_t>(total, (uint64_t)width + (uint64_t)(height - 1u) * height);
+    const uint64_t L = (n_src + parts - 1) / parts;
+    const uint64_t a = std::min<uint64_t>((uint64_t)part * L, n_src);
+    const uint64_t b = part + 1 == parts ? total : std::min<uint64_t>(a + L, n_src);
+    if (total > 0xFFFFFFFFull) return fail(nullptr, SPT_ERR_ARG, "frame too large");
+    *i0 = (uint32_t)a;
+    *i1 = (uint32_t)b;
+    return SPT_OK;
+}
+
+int spt_render_task_range_async(spt_ctx *ctx, uint32_t i0, uint32_t i1, void *d_rgba, void *stream)
+{
+    if (!ctx) return fail(nullptr, SPT_ERR_ARG, "null context");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    int rc = check_ready(ctx);
+    if (rc) return rc;
+    if (i0 > i1 || (uint64_t)i1 > (uint64_t)ctx->W * ctx->H || (i1 > i0 && !d_rgba))
+        return fail(ctx, SPT_ERR_ARG, "bad task range [%u, %u) of a %ux%u frame", i0, i1, ctx->W, ctx->H);
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    return render_task_range(ctx, i0, i1, (float4 *)d_rgba, (hipStream_t)stream);
+}
 
 int spt_pin_host(spt_ctx *ctx, void *ptr, size_t bytes)
 {
@@ -107,15 +155,12 @@ int spt_render_frame(spt_ctx *ctx, int mode, float *rgba_out, uint8_t *g_data)
     const uint32_t strip = even_strip(H, parts);
     const bool alias = mode == SPT_MODE_TASK && W != H;
     const uint64_t total = (uint64_t)W * H;
-    // alias: outputs [0, n_src) have sources (p_max + 1 = W + (H - 1) H, at most W H)
-    const uint64_t n_src = std::min<uint64_t>(total, (uint64_t)W + (uint64_t)(H - 1u) * H);
-    const uint64_t L = (n_src + parts - 1) / parts;  // source-holding outputs per member (alias)
     uint32_t max_rows = 0;
     for (uint32_t r = 0; r < parts; ++r) max_rows = std::max(max_rows, spt::rows_owned(spt::RowMap{0, H, strip, parts, r, 0, W}));
     auto range_of = [&](uint32_t r) {
-        const uint64_t i0 = std::min<uint64_t>((uint64_t)r * L, n_src);
-        const uint64_t i1 = r + 1 == parts ? total : std::min<uint64_t>(i0 + L, n_src);
-        return std::make_pair((uint32_t)i0, (uint32_t)i1);
+        uint32_t i0 = 0, i1 = 0;
+        (void)spt_task_range(W, H, parts, r, &i0, &i1);
+        return std::make_pair(i0, i1);
     };
     // a member's tile: its strips, or its colorIndex range (the largest: the last member's,
     // with the source-less tail); member 0 stacks the tiles (alias: the whole frame)
@@ -139,15 +184,8 @@ int spt_render_frame(spt_ctx *ctx, int mode, float *rgba_out, uint8_t *g_data)
         float4 *dst = r == 0 ? ctx->d_tile : c->d_tile;
         if (alias) {
             const auto [i0, i1] = range_of(r);
-            if (i1 > i0) {
-                // the rows holding the range's sources: dx + dy H in [i0, i1), 0 <= dx < W
-                // (none when i0 >= (W - 1) + (H - 1) H + 1: an empty map, NaN outputs)
-                const uint32_t dy_lo = i0 >= W ? (i0 - W + H) / H : 0u, dy_hi = std::min(H - 1u, (i1 - 1u) / H);
-                const spt::RowMap map{std::min(dy_lo, H), std::max(std::min(dy_lo, H), dy_hi + 1u), 1u, 1u, 0u, 0u, W};
-                const AliasRange ar{i0, i1 - i0, H};
-                if ((rc = render_impl(c, mode, map, dst, nullptr, c->stream, false, nullptr, 1, &ar)))
-                    return r == 0 ? rc : fail(ctx, rc, "member device %d: %s", c->device, c->err.c_str());
-            }
+            if ((rc = render_task_range(c, i0, i1, dst, c->stream)))
+                return r == 0 ? rc : fail(ctx, rc, "member device %d: %s", c->device, c->err.c_str());
         } else {
             spt::RowMap map{0, H, strip, parts, r, 0, W};
             if ((rc = render_impl(c, mode, map, dst, nullptr, c->stream, false)))

@@ -188,21 +188,32 @@ int spt_tiles_buffer(spt_tiles *t, uint64_t frame, void **d_buffer)
     return SPT_OK;
 }
 
-int spt_tiles_send_async(spt_tiles *t, uint64_t frame, const void *d_tile, void *stream)
+int spt_tiles_send_range_async(spt_tiles *t, uint64_t frame, const void *d_src, uint64_t offset, uint64_t bytes,
+                               void *stream)
 {
-    if (!t || !d_tile) return tiles_fail(t, SPT_ERR_ARG, "null tiles or tile");
+    if (!t || (!d_src && bytes)) return tiles_fail(t, SPT_ERR_ARG, "null tiles or source");
     if (t->owner) return tiles_fail(t, SPT_ERR_STATE, "tiles: rank 0 renders into its slot (spt_tiles_buffer)");
     if (!t->buf) return tiles_fail(t, SPT_ERR_STATE, "tiles: not attached");
+    const uint64_t cap = (uint64_t)t->world * t->tile_bytes;
+    if (offset > cap || bytes > cap - offset) return tiles_fail(t, SPT_ERR_ARG, "tiles: range outside the buffer");
     spt_ctx *ctx = t->ctx;
     const hipStream_t s = (hipStream_t)stream;
     const uint32_t b = (uint32_t)(frame % t->nbuf), gen = generation(t, frame);
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     // the buffer's previous use (frame - nbuf) must be assembled before this copy lands
     if (gen > 1u) HIP_TRY(ctx, hipStreamWaitValue32(s, word(t, 0, b), gen - 1u, hipStreamWaitValueGte, 0xFFFFFFFFu));
-    uint8_t *dst = t->buf + ((size_t)b * t->world + t->rank) * t->tile_bytes;
-    HIP_TRY(ctx, hipMemcpyAsync(dst, d_tile, t->tile_bytes, hipMemcpyDeviceToDevice, s));
+    if (bytes) {
+        uint8_t *dst = t->buf + (size_t)b * cap + offset;
+        HIP_TRY(ctx, hipMemcpyAsync(dst, d_src, bytes, hipMemcpyDeviceToDevice, s));
+    }
     HIP_TRY(ctx, hipStreamWriteValue32(s, word(t, t->rank, b), gen, 0));
     return SPT_OK;
+}
+
+int spt_tiles_send_async(spt_tiles *t, uint64_t frame, const void *d_tile, void *stream)
+{
+    if (!t || !d_tile) return tiles_fail(t, SPT_ERR_ARG, "null tiles or tile");
+    return spt_tiles_send_range_async(t, frame, d_tile, (uint64_t)t->rank * t->tile_bytes, t->tile_bytes, stream);
 }
 
 int spt_tiles_recv_async(spt_tiles *t, uint64_t frame, void *stream)

@@ -16,7 +16,9 @@ from dataclasses import dataclass
 
 import numpy as np
 
-from .renderer import rows_count
+from .renderer import rows_count, task_range
+
+MODE_TASK = 1  # spt_hip.h SPT_MODE_TASK
 
 
 def even_strip(height: int, world: int) -> int:
@@ -53,6 +55,21 @@ class FrameSplit:
     def tile_pixels(self) -> int:
         return self.max_rows * self.width
 
+    def aliased(self, mode: int) -> bool:
+        """RenderImage's RenderSegmentTask({0, H, 0, W}) on a non-square frame aliases pixels
+        across rows (TaskBasedPathTracer.hpp:103,186): the frame is then split by output
+        ranges (spt_task_range) instead of row strips."""
+        return mode == MODE_TASK and self.width != self.height and self.world > 1
+
+    def task_ranges(self) -> list[tuple[int, int]]:
+        return [task_range(self.width, self.height, self.world, r) for r in range(self.world)]
+
+    def slot_pixels(self, mode: int) -> int:
+        """Pixels of one rank's tile slot: its strips' rows, or its longest output range."""
+        if self.aliased(mode):
+            return max(b - a for a, b in self.task_ranges())
+        return self.tile_pixels()
+
 
 def gather_tiles(local_tile, gathered, group=None) -> None:
     """Every rank's tile -> rank 0's gathered[world*max_rows*width, 4], rank-major: one
@@ -86,7 +103,7 @@ class TileTransport:
     over `torch.distributed` (any backend: only the segment name and the 64-byte handle
     travel through it)."""
 
-    def __init__(self, ctx, split: FrameSplit, rank: int, nbuf: int = 2, group=None):
+    def __init__(self, ctx, split: FrameSplit, rank: int, nbuf: int = 2, group=None, mode: int = 0):
         import os
         import secrets
         import torch.distributed as dist
@@ -94,7 +111,7 @@ class TileTransport:
         self._lib = _native.lib()
         self._ctx = ctx
         self.rank, self.world, self.nbuf = rank, split.world, nbuf
-        self.tile_bytes = split.tile_pixels() * 16  # float4
+        self.tile_bytes = split.slot_pixels(mode) * 16  # float4
         src = dist.get_global_rank(group, 0) if group is not None else 0
         name = [f"{os.getpid()}_{secrets.token_hex(6)}" if rank == 0 else None]
         dist.broadcast_object_list(name, src=src, group=group)
@@ -135,6 +152,11 @@ class TileTransport:
         """Ranks > 0: the tile at d_tile into the frame's buffer, then the ready word."""
         self._check(self._lib.spt_tiles_send_async(self._h, frame, ctypes.c_void_p(d_tile), ctypes.c_void_p(stream)))
 
+    def send_range(self, frame: int, d_src: int, offset: int, nbytes: int, stream) -> None:
+        """Ranks > 0: nbytes at d_src to byte `offset` of the frame's buffer, then the ready word."""
+        self._check(self._lib.spt_tiles_send_range_async(self._h, frame, ctypes.c_void_p(d_src), offset, nbytes,
+                                                         ctypes.c_void_p(stream)))
+
     def recv(self, frame: int, stream) -> None:
         """Rank 0: `stream` waits for every rank's ready word of the frame."""
         self._check(self._lib.spt_tiles_recv_async(self._h, frame, ctypes.c_void_p(stream)))
@@ -165,6 +187,10 @@ def render_frame(ctx, split: FrameSplit, rank: int, mode: int, local_tile, gathe
                               frame.data_ptr() if frame is not None else 0,
                               g_data.data_ptr() if g_data is not None else 0, stream)
         return
+    if split.aliased(mode):
+        _render_frame_ranges(ctx, split, rank, local_tile, gathered, frame, g_data, stream, group, gather_events,
+                             transport, frame_no)
+        return
     if transport is not None:
         dst = transport.buffer(frame_no) if rank == 0 else local_tile.data_ptr()
         ctx.render_rows_async(mode, 0, split.height, split.strip, split.world, rank, 0, split.width, dst, 0, stream)
@@ -193,3 +219,52 @@ def render_frame(ctx, split: FrameSplit, rank: int, mode: int, local_tile, gathe
         ctx.assemble_rows_async(gathered.data_ptr(), split.max_rows, 0, split.height, split.strip, split.world, 0,
                                 split.width, frame.data_ptr() if frame is not None else 0,
                                 g_data.data_ptr() if g_data is not None else 0, stream)
+
+
+def _render_frame_ranges(ctx, split: FrameSplit, rank, local_tile, gathered, frame, g_data, stream, group,
+                         gather_events, transport, frame_no) -> None:
+    """render_frame for a non-square task-mode frame: rank r renders outputs [i0_r, i1_r)
+    of the frame's row-major order (spt_render_task_range_async, the split spt_render_frame
+    uses over a multi-device context); rank 0 places each range at its first output -- the
+    ranges end to end are the frame -- and assembles it as one part of H rows."""
+    import torch
+    ranges = split.task_ranges()
+    i0, i1 = ranges[rank]
+    W, H = split.width, split.height
+
+    def assemble(d_stack):
+        ctx.assemble_rows_async(d_stack, H, 0, H, 1, 1, 0, W, frame.data_ptr() if frame is not None else 0,
+                                g_data.data_ptr() if g_data is not None else 0, stream)
+
+    if transport is not None:
+        # the transport's buffer is the frame: rank 0 renders its range in place, the
+        # others copy theirs to its offset
+        dst = transport.buffer(frame_no) + 16 * i0 if rank == 0 else local_tile.data_ptr()
+        ctx.render_task_range_async(i0, i1, dst, stream)
+        if gather_events is not None:
+            gather_events[0].record()
+        if rank == 0:
+            transport.recv(frame_no, stream)
+        else:
+            transport.send_range(frame_no, dst, 16 * i0, 16 * (i1 - i0), stream)
+        if gather_events is not None:
+            gather_events[1].record()
+        if rank == 0:
+            assemble(transport.buffer(frame_no))
+            transport.release(frame_no, stream)
+        return
+    ctx.render_task_range_async(i0, i1, local_tile.data_ptr(), stream)
+    if gather_events is not None:
+        gather_events[0].record()
+    gather_tiles(local_tile, gathered, group)
+    if gather_events is not None:
+        gather_events[1].record()
+    if rank == 0:
+        # slot r of the gathered stack holds range r from its start (torch's current
+        # stream: the caller's, as for the gather)
+        slot = local_tile.shape[0]
+        stack = torch.empty((W * H, 4), dtype=torch.float32, device=gathered.device)
+        for r, (a, b) in enumerate(ranges):
+            if b > a:
+                stack[a:b].copy_(gathered[r * slot:r * slot + (b - a)])
+        assemble(stack.data_ptr())

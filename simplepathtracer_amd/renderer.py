@@ -201,6 +201,12 @@ class Context:
                                                           ctypes.c_void_p(d_rgb8 or None),
                                                           ctypes.c_void_p(stream or None)))
 
+    def render_task_range_async(self, i0, i1, d_rgba, stream=0) -> None:
+        """Outputs [i0, i1) of RenderSegmentTask({0, H, 0, W}) on a non-square frame into
+        d_rgba (spt_render_task_range_async: the rank-share form of its aliasing)."""
+        self._check(_native.lib().spt_render_task_range_async(self._h, i0, i1, ctypes.c_void_p(d_rgba or None),
+                                                              ctypes.c_void_p(stream or None)))
+
     def synchronize(self) -> None:
         self._check(_native.lib().spt_synchronize(self._h))
 
@@ -230,6 +236,13 @@ class Context:
         out = np.zeros((len(a), _native.SELFTEST_COLS), np.float32)
         self._check(_native.lib().spt_selftest_numerics(self._h, _p(a), _p(b), _p(bits), len(a), _p(out)))
         return out
+
+
+def task_range(width, height, parts, part) -> tuple[int, int]:
+    """Part `part` of `parts`'s outputs [i0, i1) of a non-square task-mode frame (spt_task_range)."""
+    a, b = ctypes.c_uint32(), ctypes.c_uint32()
+    _native.check(_native.lib().spt_task_range(width, height, parts, part, ctypes.byref(a), ctypes.byref(b)))
+    return a.value, b.value
 
 
 def rows_count(yB, yE, strip, parts, part) -> int:

@@ -77,6 +77,26 @@ def test_scene_generators_validate_arguments(native):
     assert c.n == 4 and list(c.materials) == [3, 3, 1, 2]
 
 
+@pytest.mark.parametrize("w,h,parts", [(1200, 800, 8), (1200, 800, 3), (800, 1200, 5), (64, 8, 7), (3, 900, 4),
+                                        (7, 5, 1)])
+def test_task_ranges_partition_the_frame(native, w, h, parts):
+    """spt_task_range (the rank-share split of a non-square task-mode frame): the parts'
+    output ranges are contiguous and cover [0, W H) in order; the outputs that have sources
+    (below W + (H - 1) H) are dealt evenly, the last part also takes the source-less tail."""
+    from simplepathtracer_amd.renderer import task_range
+    rs = [task_range(w, h, parts, r) for r in range(parts)]
+    assert rs[0][0] == 0 and rs[-1][1] == w * h
+    assert all(rs[k][1] == rs[k + 1][0] for k in range(parts - 1))
+    n_src = min(w * h, w + (h - 1) * h)
+    L = -(-n_src // parts)
+    for r, (a, b) in enumerate(rs[:-1]):
+        assert b - a == max(0, min(L, n_src - a)), (r, a, b)
+    L_ = native.lib()
+    x, y = ctypes.c_uint32(), ctypes.c_uint32()
+    assert L_.spt_task_range(w, h, parts, parts, ctypes.byref(x), ctypes.byref(y)) == 1
+    assert L_.spt_render_task_range_async(None, 0, 1, None, None) == 1
+
+
 def test_wider_random_scene_extends_the_reference_rows(native):
     """spt_scene_generate_random_rows (BASELINE.json's "~500-sphere" scene): GenerateSpheres'
     row loop (SceneGenerators.hpp:32-53) run to z < 37.5 instead of 20 draws the same

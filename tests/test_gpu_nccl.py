@@ -1,4 +1,4 @@
-"""GPU test of the N > 1 frame path's collective branch: gather_tiles with
+"""GPU tests of the N > 1 frame path: the collective branch: gather_tiles with
 device tensors over the nccl (= RCCL) backend -- the branch bench.py takes at N > 1 on
 a node, `dist.gather` of device tiles (simplepathtracer_amd/distributed.py) -- at world
 size 1 (one GPU per box), followed by rank 0's assemble kernel.  The frame and g_data
@@ -72,3 +72,42 @@ def test_nccl_gather_then_assemble_equals_one_launch(mode):
     finally:
         if own:
             dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("parts", [2, 3, 8])
+def test_task_ranges_assembled_equal_one_launch(parts):
+    """The rank-share form of RenderSegmentTask({0, H, 0, W}) on a non-square frame
+    (spt_task_range / spt_render_task_range_async, distributed.render_frame's split for it):
+    each part's output range rendered alone, placed at its first output and assembled as
+    one part of H rows equals the one-launch frame bit for bit, NaN outputs (bytes 0)
+    included."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import simplepathtracer_amd as spt
+    from simplepathtracer_amd.renderer import task_range
+    torch.cuda.set_device(0)
+    W, H, spp = 360, 200, 8
+    ctx = spt.Context(0)
+    ctx.set_scene(spt.generate_spheres(1))
+    ctx.set_camera(spt.camera_basis(), spt.scene.DEFAULT_EYE, spt.INIT_COLOR)
+    ctx.set_params(W, H, spp, 50, 1)
+    stream = torch.cuda.current_stream().cuda_stream
+    want = torch.zeros((W * H, 4), dtype=torch.float32, device="cuda")
+    want8 = torch.zeros(W * H * 3, dtype=torch.uint8, device="cuda")
+    ctx.render_rows_async(1, 0, H, 1, 1, 0, 0, W, want.data_ptr(), want8.data_ptr(), stream)
+    stack = torch.full((W * H, 4), -7.0, dtype=torch.float32, device="cuda")
+    for r in range(parts):
+        a, b = task_range(W, H, parts, r)
+        part = torch.full((max(b - a, 1), 4), -5.0, dtype=torch.float32, device="cuda")
+        ctx.render_task_range_async(a, b, part.data_ptr(), stream)
+        if b > a:
+            stack[a:b].copy_(part[:b - a])
+    frame = torch.zeros((W * H, 4), dtype=torch.float32, device="cuda")
+    g8 = torch.zeros(W * H * 3, dtype=torch.uint8, device="cuda")
+    ctx.assemble_rows_async(stack.data_ptr(), H, 0, H, 1, 1, 0, W, frame.data_ptr(), g8.data_ptr(), stream)
+    torch.cuda.synchronize()
+    assert torch.equal(frame[:, :3].contiguous().view(torch.int32), want[:, :3].contiguous().view(torch.int32))
+    assert torch.equal(g8, want8)
+    ctx.close()
+

@@ -537,8 +537,10 @@ def test_cpp_dropin_shim_renders_like_the_context(spt, golden_scenes, tmp_path, 
     assert bad.size == 0, f"{bad.size} bytes differ in tiles (row, col) {tiles[:24]} (of {len(tiles)})"
 
 
-@pytest.mark.parametrize("service,transport", [(0, "rccl"), (1, "rccl"), (0, "ipc"), (1, "ipc")])
-def test_bench_two_ranks_on_one_gpu_matches_one_rank(spt, tmp_path, service, transport):
+@pytest.mark.parametrize("service,transport,world,mode", [(0, "rccl", 2, "segment"), (1, "rccl", 2, "segment"),
+                                                         (0, "ipc", 2, "segment"), (1, "ipc", 2, "segment"),
+                                                         (0, "rccl", 3, "task"), (0, "ipc", 3, "task")])
+def test_bench_two_ranks_on_one_gpu_matches_one_rank(spt, tmp_path, service, transport, world, mode):
     """bench.py's N>1 flow (strip split, gather to rank 0, rank-0 assemble)
     rehearsed with two gloo ranks sharing cuda:0, launched by bench.py itself
     (`--gpus 2`, no torchrun): the line says 2 ranks and g_data equals N=1's.
@@ -548,7 +550,9 @@ def test_bench_two_ranks_on_one_gpu_matches_one_rank(spt, tmp_path, service, tra
     resident on the one GPU.  transport="ipc": the copy-engine TileTransport instead of
     the gather (rank 1's copies into rank 0's IPC-exported buffers, stream wait/write
     packets on shared host words), over enough frames that each of the two gathered
-    buffers is reused (its consumed word gates the next copy)."""
+    buffers is reused (its consumed word gates the next copy); also three ranks in task
+    mode, whose non-square frame aliases pixels across rows (TaskBasedPathTracer.hpp:103,
+    186): split by output ranges (spt_task_range), gathered and placed end to end.""" 
     import json
     import os
     import subprocess
@@ -556,7 +560,7 @@ def test_bench_two_ranks_on_one_gpu_matches_one_rank(spt, tmp_path, service, tra
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     one, two = tmp_path / "one.bin", tmp_path / "two.bin"
     base = [sys.executable, os.path.join(root, "bench.py"), "--steps", "1", "--warmup", "0", "--no-cpu-baseline",
-            "--no-dropin"]
+            "--no-dropin", "--mode", mode]
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     subprocess.run(base + ["--dump", str(one)], check=True, timeout=300, cwd=root, env=env)
     env["SPT_DIST_BACKEND"] = "gloo"
@@ -566,13 +570,13 @@ def test_bench_two_ranks_on_one_gpu_matches_one_rank(spt, tmp_path, service, tra
         extra = ["--service", "1", "--steps", "3", "--warmup", "1"]
     if transport == "ipc":
         extra = ["--service", str(service), "--steps", "5", "--warmup", "2", "--transport", "ipc"]
-    r = subprocess.run(base + ["--gpus", "2", "--dump", str(two)] + extra, check=True, timeout=300, cwd=root, env=env,
-                       capture_output=True, text=True)
+    r = subprocess.run(base + ["--gpus", str(world), "--dump", str(two)] + extra, check=True, timeout=300, cwd=root,
+                       env=env, capture_output=True, text=True)
     line = json.loads([s for s in r.stdout.splitlines() if s.startswith("{")][-1])
-    assert line["n_gpus"] == 2 and line["world_size"] == 2 and line["backend"] == "gloo"
+    assert line["n_gpus"] == world and line["world_size"] == world and line["backend"] == "gloo"
     assert line["config"]["render_service"] == bool(service)
     assert line["config"]["transport"] == transport
-    assert len(line["ranks"]["render_ms"]) == 2 and min(line["ranks"]["render_ms"]) > 0
+    assert len(line["ranks"]["render_ms"]) == world and min(line["ranks"]["render_ms"]) > 0
     a, b = np.fromfile(one, np.uint8), np.fromfile(two, np.uint8)
     assert a.size == b.size == 1200 * 800 * 3
     bad = np.nonzero(a != b)[0]

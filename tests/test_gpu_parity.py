@@ -539,7 +539,8 @@ def test_cpp_dropin_shim_renders_like_the_context(spt, golden_scenes, tmp_path, 
 
 @pytest.mark.parametrize("service,transport,world,mode", [(0, "rccl", 2, "segment"), (1, "rccl", 2, "segment"),
                                                          (0, "ipc", 2, "segment"), (1, "ipc", 2, "segment"),
-                                                         (0, "rccl", 3, "task"), (0, "ipc", 3, "task")])
+                                                         (0, "rccl", 3, "task"), (0, "ipc", 3, "task"),
+                                                         (1, "rccl", 3, "task"), (1, "ipc", 3, "task")])
 def test_bench_two_ranks_on_one_gpu_matches_one_rank(spt, tmp_path, service, transport, world, mode):
     """bench.py's N>1 flow (strip split, gather to rank 0, rank-0 assemble)
     rehearsed with two gloo ranks sharing cuda:0, launched by bench.py itself
@@ -566,7 +567,7 @@ def test_bench_two_ranks_on_one_gpu_matches_one_rank(spt, tmp_path, service, tra
     env["SPT_DIST_BACKEND"] = "gloo"
     extra = []
     if service:
-        env["SPT_SVC_GRID_DIV"] = "2"
+        env["SPT_SVC_GRID_DIV"] = str(world)
         extra = ["--service", "1", "--steps", "3", "--warmup", "1"]
     if transport == "ipc":
         extra = ["--service", str(service), "--steps", "5", "--warmup", "2", "--transport", "ipc"]

@@ -537,11 +537,11 @@ def test_cpp_dropin_shim_renders_like_the_context(spt, golden_scenes, tmp_path, 
     assert bad.size == 0, f"{bad.size} bytes differ in tiles (row, col) {tiles[:24]} (of {len(tiles)})"
 
 
-@pytest.mark.parametrize("service,transport,world,mode", [(0, "rccl", 2, "segment"), (1, "rccl", 2, "segment"),
-                                                         (0, "ipc", 2, "segment"), (1, "ipc", 2, "segment"),
-                                                         (0, "rccl", 3, "task"), (0, "ipc", 3, "task"),
-                                                         (1, "rccl", 3, "task"), (1, "ipc", 3, "task")])
-def test_bench_two_ranks_on_one_gpu_matches_one_rank(spt, tmp_path, service, transport, world, mode):
+@pytest.mark.parametrize("service,transport,world,mode,config", [
+    (0, "rccl", 2, "segment", "c2"), (1, "rccl", 2, "segment", "c2"), (0, "ipc", 2, "segment", "c2"),
+    (1, "ipc", 2, "segment", "c2"), (0, "rccl", 3, "task", "c2"), (0, "ipc", 3, "task", "c2"),
+    (1, "rccl", 3, "task", "c2"), (1, "ipc", 3, "task", "c2"), (0, "ipc", 2, "segment", "c5")])
+def test_bench_two_ranks_on_one_gpu_matches_one_rank(spt, tmp_path, service, transport, world, mode, config):
     """bench.py's N>1 flow (strip split, gather to rank 0, rank-0 assemble)
     rehearsed with two gloo ranks sharing cuda:0, launched by bench.py itself
     (`--gpus 2`, no torchrun): the line says 2 ranks and g_data equals N=1's.
@@ -553,7 +553,8 @@ def test_bench_two_ranks_on_one_gpu_matches_one_rank(spt, tmp_path, service, tra
     packets on shared host words), over enough frames that each of the two gathered
     buffers is reused (its consumed word gates the next copy); also three ranks in task
     mode, whose non-square frame aliases pixels across rows (TaskBasedPathTracer.hpp:103,
-    186): split by output ranges (spt_task_range), gathered and placed end to end.""" 
+    186): split by output ranges (spt_task_range), gathered and placed end to end; and
+    config 5's LDS-tree scene (1920 x 1080 x 256 spp) over the transport."""
     import json
     import os
     import subprocess
@@ -561,7 +562,7 @@ def test_bench_two_ranks_on_one_gpu_matches_one_rank(spt, tmp_path, service, tra
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     one, two = tmp_path / "one.bin", tmp_path / "two.bin"
     base = [sys.executable, os.path.join(root, "bench.py"), "--steps", "1", "--warmup", "0", "--no-cpu-baseline",
-            "--no-dropin", "--mode", mode]
+            "--no-dropin", "--mode", mode, "--config", config]
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     subprocess.run(base + ["--dump", str(one)], check=True, timeout=300, cwd=root, env=env)
     env["SPT_DIST_BACKEND"] = "gloo"
@@ -579,9 +580,10 @@ def test_bench_two_ranks_on_one_gpu_matches_one_rank(spt, tmp_path, service, tra
     assert line["config"]["transport"] == transport
     assert len(line["ranks"]["render_ms"]) == world and min(line["ranks"]["render_ms"]) > 0
     a, b = np.fromfile(one, np.uint8), np.fromfile(two, np.uint8)
-    assert a.size == b.size == 1200 * 800 * 3
+    W, H = (1920, 1080) if config == "c5" else (1200, 800)
+    assert a.size == b.size == W * H * 3
     bad = np.nonzero(a != b)[0]
-    rows = np.unique(799 - (bad // 3) // 1200)  # g_data row r holds image row y = H-1-r
+    rows = np.unique(H - 1 - (bad // 3) // W)  # g_data row r holds image row y = H-1-r
     assert bad.size == 0, f"{bad.size} bytes differ in {rows.size} rows, first rows {rows[:16]}, a={a[bad[:6]]} b={b[bad[:6]]}"
 
 

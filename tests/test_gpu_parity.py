@@ -540,7 +540,8 @@ def test_cpp_dropin_shim_renders_like_the_context(spt, golden_scenes, tmp_path, 
 @pytest.mark.parametrize("service,transport,world,mode,config", [
     (0, "rccl", 2, "segment", "c2"), (1, "rccl", 2, "segment", "c2"), (0, "ipc", 2, "segment", "c2"),
     (1, "ipc", 2, "segment", "c2"), (0, "rccl", 3, "task", "c2"), (0, "ipc", 3, "task", "c2"),
-    (1, "rccl", 3, "task", "c2"), (1, "ipc", 3, "task", "c2"), (0, "ipc", 2, "segment", "c5")])
+    (1, "rccl", 3, "task", "c2"), (1, "ipc", 3, "task", "c2"), (0, "ipc", 2, "segment", "c5"),
+    (0, "rccl", 2, "task", "c2w")])
 def test_bench_two_ranks_on_one_gpu_matches_one_rank(spt, tmp_path, service, transport, world, mode, config):
     """bench.py's N>1 flow (strip split, gather to rank 0, rank-0 assemble)
     rehearsed with two gloo ranks sharing cuda:0, launched by bench.py itself
@@ -554,7 +555,8 @@ def test_bench_two_ranks_on_one_gpu_matches_one_rank(spt, tmp_path, service, tra
     buffers is reused (its consumed word gates the next copy); also three ranks in task
     mode, whose non-square frame aliases pixels across rows (TaskBasedPathTracer.hpp:103,
     186): split by output ranges (spt_task_range), gathered and placed end to end; and
-    config 5's LDS-tree scene (1920 x 1080 x 256 spp) over the transport."""
+    config 5's LDS-tree scene (1920 x 1080 x 256 spp) over the transport, and the
+    ~500-sphere scene (its 89-node tree takes the LDS lane walk) in task mode."""
     import json
     import os
     import subprocess

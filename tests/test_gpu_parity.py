@@ -505,23 +505,32 @@ def test_concurrent_render_jobs_share_a_context(spt, golden_scenes):
 
 @pytest.mark.parametrize("w,h,tc,task,devices", [(1200, 800, 4, 0, None), (1200, 800, 4, 1, None),
                                                   (1200, 800, 8, 0, "0,0"), (320, 160, 16, 0, None),
-                                                  (320, 160, 16, 1, None)])
+                                                  (320, 160, 16, 1, None), (1200, 800, 4, 0, "svc"),
+                                                  (1200, 800, 4, 1, "svc")])
 def test_cpp_dropin_shim_renders_like_the_context(spt, golden_scenes, tmp_path, w, h, tc, task, devices):
     """The C++ RenderSegment/RenderSegmentTask shim, driven by RenderJob-style
     concurrent threads over a tc x tc tile grid (config 2's 300x200 tiles at tc = 4,
     non-square: task mode aliases; 256 tiles of 20x10 at tc = 16, batched many to a
     launch), writes the same g_data bytes as tile renders through the context (its
     page-locked g_data written in place by the batched fold); SPT_DEVICES spreads the
-    tiles over a multi-device context."""
+    tiles over a multi-device context; SPT_SERVICE=1 makes them service jobs (with repeated
+    frames, so the read-ahead serves them too)."""
     import os
     import subprocess
     from test_abi import _build_shim_harness
     exe = _build_shim_harness(tmp_path)
     out = tmp_path / "g_data.bin"
     env = dict(os.environ)
-    if devices:
+    frames = []
+    if devices == "svc":
+        # the shim's calls as jobs of the render service (SPT_SERVICE=1), three more frames:
+        # the tiling read-ahead arms after the first and serves the others through it
+        env["SPT_SERVICE"] = "1"
+        frames = ["3"]
+    elif devices:
         env["SPT_DEVICES"] = devices
-    subprocess.run([exe, str(out), str(w), str(h), "6", "50", str(tc), str(task)], check=True, timeout=300, env=env)
+    subprocess.run([exe, str(out), str(w), str(h), "6", "50", str(tc), str(task)] + frames, check=True, timeout=300,
+                   env=env)
     got = np.fromfile(out, np.uint8)
     c = spt.Context(0)
     setup(c, scene_from(spt, golden_scenes, "random"), w, h, 6, 50)

@@ -550,7 +550,7 @@ def test_cpp_dropin_shim_renders_like_the_context(spt, golden_scenes, tmp_path, 
     (0, "rccl", 2, "segment", "c2"), (1, "rccl", 2, "segment", "c2"), (0, "ipc", 2, "segment", "c2"),
     (1, "ipc", 2, "segment", "c2"), (0, "rccl", 3, "task", "c2"), (0, "ipc", 3, "task", "c2"),
     (1, "rccl", 3, "task", "c2"), (1, "ipc", 3, "task", "c2"), (0, "ipc", 2, "segment", "c5"),
-    (0, "rccl", 2, "task", "c2w")])
+    (0, "rccl", 2, "task", "c2w"), (0, "ipc", 2, "segment", "c3")])
 def test_bench_two_ranks_on_one_gpu_matches_one_rank(spt, tmp_path, service, transport, world, mode, config):
     """bench.py's N>1 flow (strip split, gather to rank 0, rank-0 assemble)
     rehearsed with two gloo ranks sharing cuda:0, launched by bench.py itself
@@ -565,7 +565,8 @@ def test_bench_two_ranks_on_one_gpu_matches_one_rank(spt, tmp_path, service, tra
     mode, whose non-square frame aliases pixels across rows (TaskBasedPathTracer.hpp:103,
     186): split by output ranges (spt_task_range), gathered and placed end to end; and
     config 5's LDS-tree scene (1920 x 1080 x 256 spp) over the transport, and the
-    ~500-sphere scene (its 89-node tree takes the LDS lane walk) in task mode."""
+    ~500-sphere scene (its 89-node tree takes the LDS lane walk) in task mode, and config 3
+    (3840 x 2160 x 1024 spp: each rank share rendered in sample batches) over the transport."""
     import json
     import os
     import subprocess
@@ -591,7 +592,7 @@ def test_bench_two_ranks_on_one_gpu_matches_one_rank(spt, tmp_path, service, tra
     assert line["config"]["transport"] == transport
     assert len(line["ranks"]["render_ms"]) == world and min(line["ranks"]["render_ms"]) > 0
     a, b = np.fromfile(one, np.uint8), np.fromfile(two, np.uint8)
-    W, H = (1920, 1080) if config == "c5" else (1200, 800)
+    W, H = {"c5": (1920, 1080), "c3": (3840, 2160)}.get(config, (1200, 800))
     assert a.size == b.size == W * H * 3
     bad = np.nonzero(a != b)[0]
     rows = np.unique(H - 1 - (bad // 3) // W)  # g_data row r holds image row y = H-1-r

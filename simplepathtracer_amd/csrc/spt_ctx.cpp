@@ -39,6 +39,9 @@ void warm_start(spt_ctx *ctx)
     spt_ctx::Warm &w = ctx->warm;
     if (w.started) return;
     w.started = true;
+    // the member's own device (a multi-device context's members: the caller's current
+    // device is another member's)
+    if (hipSetDevice(ctx->device) != hipSuccess) return;  // no warm streams: created on first use
     int lo = 0, hi = 0;
     (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
     int prio = lo;  // the read-ahead parts' priority (spec_stream)

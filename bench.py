@@ -299,11 +299,13 @@ def main():
                          "-1 (default): the service for the rank shares of N > 1 ranks, launches at N = 1 "
                          "(profiles/svc_timeline_r04.txt: 20 config-2 frames, 1/8 shares 13.4 vs 14.4 ms, "
                          "whole frames 95.0 vs 92.9 ms)")
-    ap.add_argument("--transport", default="rccl", choices=["rccl", "ipc"],
-                    help="N > 1: how the rank tiles reach rank 0: one RCCL gather per frame (default, north_star), "
-                         "or the copy-engine transport (distributed.TileTransport: peer copies from IPC handles "
-                         "ordered by stream wait/write-value packets, no collective kernel; the session then "
-                         "keeps one block slot per CU free for the folds and assembles: DESIGN.md §5 Round 6)")
+    ap.add_argument("--transport", default="auto", choices=["auto", "rccl", "ipc"],
+                    help="N > 1: how the rank tiles reach rank 0: the copy-engine transport (distributed."
+                         "TileTransport: peer copies from IPC handles ordered by stream wait/write-value packets, "
+                         "no collective kernel; the session keeps one block slot per CU free for the folds and "
+                         "assembles: DESIGN.md §5 Round 6) when its setup check passes on every rank, else one "
+                         "RCCL gather per frame (auto, default); rccl / ipc force one (ipc: exit if the check "
+                         "fails)")
     ap.add_argument("--cpu-spp", type=int, default=0,
                     help="spp of the CPU-baseline sample (0: the config's own spp on config 2, scaled down on others)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -347,15 +349,16 @@ def main():
     # the render service (--service 1) is started around each timed region and stopped
     # (drained) inside it: a device-wide synchronisation must not wait for its resident kernel
     # (auto: rank shares of N > 1 ranks, each on a GPU of its own -- ranks rehearsed on a
-    # shared GPU would hold each other's resident kernels off the CUs).  The session takes
-    # every block slot (SPT_SVC_FULL_GRID): the folds and gathers of a region's frames run
-    # after its session ends (N = 8 shares with a gather stand-in: 0.740 vs 0.756 ms per
-    # share; whole frames 4.46 vs 4.67 ms)
+    # shared GPU would hold each other's resident kernels off the CUs).  With the RCCL gather
+    # the session takes every block slot (spt_service_set_full_grid): RCCL's kernel needs a
+    # whole CU, so the folds and gathers of a region's frames run after its session ends
+    # anyway (N = 8 shares with a gather stand-in: 0.740 vs 0.756 ms per share; DESIGN.md
+    # §5); with the copy-engine transport one slot per CU stays free for the folds, wait
+    # packets and assembles, which then overlap the session (0.847 vs 0.757 in the one-GPU
+    # rehearsal, profiles/scaling_r06.txt)
     auto_svc = world > 1 and world <= torch.cuda.device_count()
     use_svc = (args.service if args.service >= 0 else auto_svc) and args.engine == "megakernel"
-    ipc = world > 1 and args.transport == "ipc"
-    if use_svc and not ipc:
-        os.environ.setdefault("SPT_SVC_FULL_GRID", "1")
+    try_ipc = world > 1 and args.transport in ("auto", "ipc")
     scene_name, W, H, spp, bounces = CONFIGS[args.config]
     scene = make_scene(spt, scene_name)
     view = spt.camera_basis()
@@ -387,14 +390,31 @@ def main():
              "local": None, "gathered": None}
         if world > 1:
             b["local"] = torch.zeros((split.slot_pixels(mode), 4), dtype=torch.float32, device=dev)
-            if rank == 0 and not ipc:
-                b["gathered"] = torch.zeros((world * split.slot_pixels(mode), 4), dtype=torch.float32, device=dev)
         bufs.append(b)
-    transport = None
-    if ipc:
+    transport, transport_check = None, None
+    if try_ipc:
         from simplepathtracer_amd.distributed import TileTransport
-        # one gathered buffer per stream: frames f and f + nst share a stream (step below)
-        transport = TileTransport(ctx, split, rank, nbuf=nst, mode=mode)
+        # one gathered buffer per stream: frames f and f + nst share a stream (step below);
+        # kept only if its setup check passes on every rank (else the RCCL gather)
+        try:
+            transport = TileTransport(ctx, split, rank, nbuf=nst, mode=mode)
+            ok = transport.verify(bufs[0]["local"], streams[0])
+        except RuntimeError as e:  # the setup failed on some rank: every rank raises it
+            progress(f"rank {rank}: copy-engine transport setup failed: {e}")
+            transport, ok = None, False
+        transport_check = "passed" if ok else "failed"
+        if not ok:
+            if transport is not None:
+                transport.close()
+            transport = None
+            if args.transport == "ipc":
+                raise SystemExit("bench.py: --transport ipc: the transport's setup check failed")
+        progress(f"rank {rank}: tile transport {'copy-engine (IPC)' if transport else 'RCCL gather'}")
+    if world > 1 and rank == 0 and transport is None:
+        for b in bufs:
+            b["gathered"] = torch.zeros((world * split.slot_pixels(mode), 4), dtype=torch.float32, device=dev)
+    if use_svc and "SPT_SVC_FULL_GRID" not in os.environ:
+        ctx.service_set_full_grid(transport is None)
     counter = [0]
     # gather timing of the timed steps (N > 1): events around each step's gather
     gev = []
@@ -500,8 +520,11 @@ def main():
                        "width": W, "height": H, "spp": spp, "bounces": bounces, "spheres": scene.n,
                        "parallelism": f"row-strips{split.strip}x{world}" if world > 1 else "1 GPU",
                        "frames_in_flight": nst, "render_service": bool(use_svc),
-                       "transport": (args.transport if world > 1 else None),
-                       "service_full_grid": bool(use_svc) and os.environ.get("SPT_SVC_FULL_GRID", "0") != "0"},
+                       "transport": (("ipc" if transport is not None else "rccl") if world > 1 else None),
+                       "transport_check": transport_check,
+                       "service_full_grid": bool(use_svc) and (os.environ.get("SPT_SVC_FULL_GRID", "0") != "0"
+                                                               if "SPT_SVC_FULL_GRID" in os.environ
+                                                               else transport is None)},
             # contract form: the render kernel against HBM with SURVEY §8(d)'s algorithmic
             # bytes; HBM does not bind this kernel (VALU issue + latency do: roofline_valu)
             "roofline": {"bound": "hbm", "achieved": round(algo_bytes / t_launch / 1e9, 4),

@@ -301,6 +301,10 @@ SPT_API int spt_render_rows_async(spt_ctx *ctx, int mode, uint32_t yBegin, uint3
  * service off.  Every host wait for a session is bounded (SPT_SVC_TIMEOUT_MS, default
  * 30 s: SPT_ERR_TIMEOUT). */
 SPT_API int spt_service_start(spt_ctx *ctx);
+/* full != 0: sessions take every block slot (SPT_SVC_FULL_GRID's setting, for callers that
+ * end their sessions themselves and need no kernel of their own beside one); 0: one slot
+ * per CU left free (the default).  SPT_ERR_STATE while a session runs. */
+SPT_API int spt_service_set_full_grid(spt_ctx *ctx, uint32_t full);
 SPT_API int spt_service_stop(spt_ctx *ctx);
 
 /* Number of rows the (yBegin, yEnd, strip, parts, part) map owns. */
@@ -360,6 +364,10 @@ SPT_API int spt_tiles_send_range_async(spt_tiles *t, uint64_t frame, const void 
                                        uint64_t bytes, void *stream);
 SPT_API int spt_tiles_recv_async(spt_tiles *t, uint64_t frame, void *stream);
 SPT_API int spt_tiles_release_async(spt_tiles *t, uint64_t frame, void *stream);
+/* Give the transport up: every ready / consumed word of the shared segment set to the
+ * largest value from the host, so that no rank's stream stays blocked on a wait packet
+ * (then destroy it).  Used when the setup check (distributed.TileTransport.verify) fails. */
+SPT_API int spt_tiles_abort(spt_tiles *t);
 SPT_API void spt_tiles_destroy(spt_tiles *t);
 
 /* Per-(pixel, sample) colors of a rectangle, host memory: out[(p*spp + s)*4 + c]

@@ -144,6 +144,8 @@ def lib() -> ctypes.CDLL:
         "spt_tiles_recv_async": ([P, u64, P], I),
         "spt_tiles_release_async": ([P, u64, P], I),
         "spt_tiles_destroy": ([P], None),
+        "spt_tiles_abort": ([P], I),
+        "spt_service_set_full_grid": ([P, u32], I),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

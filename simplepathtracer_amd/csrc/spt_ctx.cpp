@@ -694,6 +694,7 @@ int spt_ctx_create(int device, spt_ctx **out)
     }
     int per_cu = 0;
     if (spt::render_occupancy(ctx->block, &per_cu) != hipSuccess || per_cu <= 0) per_cu = 1;
+    ctx->svc_per_cu = per_cu;
     ctx->svc_grid = (uint32_t)(std::max(1, per_cu - 1) * ctx->num_cu);
     // SPT_SVC_FULL_GRID=1: the session takes every block slot (folds and other streams'
     // kernels then wait for the session's end; for pipelines that end their sessions

@@ -262,6 +262,7 @@ struct spt_ctx {
     // folds, publish launches and other streams' kernels need the free slot)
     uint32_t svc_grid = 0;
     bool svc_full = false;  // SPT_SVC_FULL_GRID: sessions take every block slot (LDS-tree sessions too)
+    int svc_per_cu = 1;     // the occupancy's blocks per CU the session grids derive from
     uint32_t last_grid = 0, last_block = 0;  // shape of the most recent render launch
 
     // scene (Globals.hpp:31-37)

@@ -444,6 +444,18 @@ int spt_service_start(spt_ctx *ctx)
     });
 }
 
+int spt_service_set_full_grid(spt_ctx *ctx, uint32_t full)
+{
+    return for_members(ctx, [full](spt_ctx *c) -> int {
+        std::lock_guard<std::mutex> lk(c->mu);
+        if (c->svc.running || c->svc.draining)
+            return fail(c, SPT_ERR_STATE, "a render-service session is running (spt_service_stop first)");
+        c->svc_full = full != 0;
+        c->svc_grid = (uint32_t)((full ? c->svc_per_cu : std::max(1, c->svc_per_cu - 1)) * c->num_cu);
+        return SPT_OK;
+    });
+}
+
 int spt_service_stop(spt_ctx *ctx)
 {
     return for_members(ctx, [](spt_ctx *c) {

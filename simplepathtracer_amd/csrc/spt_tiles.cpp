@@ -240,6 +240,17 @@ int spt_tiles_release_async(spt_tiles *t, uint64_t frame, void *stream)
     return SPT_OK;
 }
 
+int spt_tiles_abort(spt_tiles *t)
+{
+    if (!t) return tiles_fail(t, SPT_ERR_ARG, "null tiles");
+    // every word to the largest generation, from the host: every wait packet of every rank
+    // on this segment is satisfied, so no stream stays blocked on a transport given up
+    if (t->host)
+        for (size_t w = 0; w < t->host_bytes / kLine; ++w)
+            __atomic_store_n((uint32_t *)((uint8_t *)t->host + w * kLine), 0xFFFFFFFFu, __ATOMIC_SEQ_CST);
+    return SPT_OK;
+}
+
 void spt_tiles_destroy(spt_tiles *t)
 {
     if (!t) return;

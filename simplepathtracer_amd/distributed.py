@@ -110,33 +110,58 @@ class TileTransport:
         from . import _native
         self._lib = _native.lib()
         self._ctx = ctx
+        self._group = group
         self.rank, self.world, self.nbuf = rank, split.world, nbuf
+        self.base = 0  # frames the setup check used (verify): caller frame f is transport frame base + f
         self.tile_bytes = split.slot_pixels(mode) * 16  # float4
         src = dist.get_global_rank(group, 0) if group is not None else 0
         name = [f"{os.getpid()}_{secrets.token_hex(6)}" if rank == 0 else None]
         dist.broadcast_object_list(name, src=src, group=group)
         self._h = ctypes.c_void_p()
+        # every rank runs every collective below whatever fails locally; the outcome is
+        # agreed at the end (a rank that raised midway would leave the others in a barrier)
+        err = []
+
+        def attempt(fn):
+            if not err:
+                try:
+                    fn()
+                except Exception as e:  # noqa: BLE001 -- reported after the agreement
+                    err.append(e)
 
         def create():
             _native.check(self._lib.spt_tiles_create(ctx.handle, name[0].encode(), rank, self.world,
                                                      self.tile_bytes, nbuf, ctypes.byref(self._h)), ctx.handle)
 
         if rank == 0:
-            create()  # the segment exists before the others open it
+            attempt(create)  # the segment exists before the others open it
         dist.barrier(group=group)
         if rank != 0:
-            create()
+            attempt(create)
         handle = [None]
-        if rank == 0:
+        if rank == 0 and not err:
             buf = (ctypes.c_uint8 * 64)()
-            self._check(self._lib.spt_tiles_handle(self._h, buf))
-            handle[0] = bytes(buf)
+
+            def export():
+                self._check(self._lib.spt_tiles_handle(self._h, buf))
+                handle[0] = bytes(buf)
+
+            attempt(export)
         dist.broadcast_object_list(handle, src=src, group=group)
         if rank != 0:
-            self._check(self._lib.spt_tiles_attach(self._h, (ctypes.c_uint8 * 64).from_buffer_copy(handle[0])))
+            if handle[0] is None:
+                err.append(RuntimeError("rank 0 exported no buffer handle"))
+            attempt(lambda: self._check(self._lib.spt_tiles_attach(
+                self._h, (ctypes.c_uint8 * 64).from_buffer_copy(handle[0]))))
         dist.barrier(group=group)
-        if rank == 0:
-            self._check(self._lib.spt_tiles_unlink(self._h))
+        if rank == 0 and self._h.value:
+            attempt(lambda: self._check(self._lib.spt_tiles_unlink(self._h)))
+        oks = [None] * self.world
+        dist.all_gather_object(oks, not err, group=group)
+        if not all(oks):
+            self.close()
+            raise RuntimeError(f"tile transport setup failed on ranks {[r for r, o in enumerate(oks) if not o]}"
+                               + (f": {err[0]}" if err else ""))
 
     def _check(self, code: int) -> None:
         from . import _native
@@ -145,30 +170,93 @@ class TileTransport:
     def buffer(self, frame: int) -> int:
         """Rank 0: device address of frame's gathered buffer (its own tile is slot 0)."""
         p = ctypes.c_void_p()
-        self._check(self._lib.spt_tiles_buffer(self._h, frame, ctypes.byref(p)))
+        self._check(self._lib.spt_tiles_buffer(self._h, self.base + frame, ctypes.byref(p)))
         return p.value
 
     def send(self, frame: int, d_tile: int, stream) -> None:
         """Ranks > 0: the tile at d_tile into the frame's buffer, then the ready word."""
-        self._check(self._lib.spt_tiles_send_async(self._h, frame, ctypes.c_void_p(d_tile), ctypes.c_void_p(stream)))
+        self._check(self._lib.spt_tiles_send_async(self._h, self.base + frame, ctypes.c_void_p(d_tile),
+                                                   ctypes.c_void_p(stream)))
 
     def send_range(self, frame: int, d_src: int, offset: int, nbytes: int, stream) -> None:
         """Ranks > 0: nbytes at d_src to byte `offset` of the frame's buffer, then the ready word."""
-        self._check(self._lib.spt_tiles_send_range_async(self._h, frame, ctypes.c_void_p(d_src), offset, nbytes,
-                                                         ctypes.c_void_p(stream)))
+        self._check(self._lib.spt_tiles_send_range_async(self._h, self.base + frame, ctypes.c_void_p(d_src), offset,
+                                                         nbytes, ctypes.c_void_p(stream)))
 
     def recv(self, frame: int, stream) -> None:
         """Rank 0: `stream` waits for every rank's ready word of the frame."""
-        self._check(self._lib.spt_tiles_recv_async(self._h, frame, ctypes.c_void_p(stream)))
+        self._check(self._lib.spt_tiles_recv_async(self._h, self.base + frame, ctypes.c_void_p(stream)))
 
     def release(self, frame: int, stream) -> None:
         """Rank 0, after its reads of the frame's buffer: the buffer's consumed word."""
-        self._check(self._lib.spt_tiles_release_async(self._h, frame, ctypes.c_void_p(stream)))
+        self._check(self._lib.spt_tiles_release_async(self._h, self.base + frame, ctypes.c_void_p(stream)))
+
+    def verify(self, local_tile, stream, timeout_s: float = 20.0) -> bool:
+        """Setup check (collective, before any frame): 2 x nbuf frames of a known pattern go
+        through the transport -- every buffer used twice, so the consumed-word handshake runs
+        -- and rank 0 compares each rank's slot with a device kernel reading the buffer (the
+        assemble's access path).  A wait that does not complete within timeout_s gives the
+        transport up (spt_tiles_abort unblocks every rank's streams).  True on every rank only
+        if every rank saw its part complete and every slot matched; the frames used are
+        skipped by later calls (self.base).  local_tile: a device float4 tensor of at least a
+        slot (ranks > 0); stream: the torch.cuda.Stream the transport's packets go on."""
+        import os
+        import time
+        import torch
+        import torch.distributed as dist
+        slot = self.tile_bytes // 16
+        ok, checks = True, []
+        with torch.cuda.stream(stream):
+            for f in range(2 * self.nbuf):
+                if self.rank != 0:
+                    # SPT_TILES_TEST_CORRUPT=1 (tests): a wrong pattern, so the check fails
+                    bad = os.environ.get("SPT_TILES_TEST_CORRUPT", "0") != "0"
+                    local_tile[:slot].fill_(float(self.rank * 64 + f + 1 + (7 if bad else 0)))
+                    self.send(f, local_tile.data_ptr(), stream.cuda_stream)
+                else:
+                    self.recv(f, stream.cuda_stream)
+                    try:
+                        view = torch.as_tensor(_DeviceArray(self.buffer(f), self.world * slot),
+                                               device=local_tile.device)
+                        for r in range(1, self.world):  # device results, read after the bounded wait
+                            checks.append(view[r * slot:(r + 1) * slot].eq(float(r * 64 + f + 1)).all())
+                    except Exception:  # no __cuda_array_interface__ support: no check possible
+                        checks.append(False)
+                    self.release(f, stream.cuda_stream)
+                ev = torch.cuda.Event()
+                ev.record(stream)
+                deadline = time.monotonic() + timeout_s
+                while not ev.query():
+                    if time.monotonic() > deadline:
+                        self._lib.spt_tiles_abort(self._h)
+                        ok = False
+                        break
+                    time.sleep(0.0005)
+                if not ok:
+                    break
+        stream.synchronize()
+        if self.rank == 0:
+            ok = ok and all(bool(c) for c in checks)
+        seen = [None] * self.world
+        dist.all_gather_object(seen, ok, group=self._group)
+        ok = all(seen)
+        if not ok:
+            self._lib.spt_tiles_abort(self._h)
+        else:
+            self.base = 2 * self.nbuf
+        return ok
 
     def close(self) -> None:
         if self._h.value:
             self._lib.spt_tiles_destroy(self._h)
             self._h = type(self._h)()
+
+
+class _DeviceArray:
+    """A float4 device array at a raw address, for torch.as_tensor (__cuda_array_interface__)."""
+
+    def __init__(self, ptr: int, n: int):
+        self.__cuda_array_interface__ = {"shape": (n, 4), "typestr": "<f4", "data": (ptr, False), "version": 2}
 
 
 def render_frame(ctx, split: FrameSplit, rank: int, mode: int, local_tile, gathered=None, frame=None,

@@ -215,6 +215,10 @@ class Context:
         renders run as jobs of one persistent launch, without a ramp and tail each."""
         self._check(_native.lib().spt_service_start(self._h))
 
+    def service_set_full_grid(self, full: bool) -> None:
+        """Sessions on every block slot (True) or one per CU left free (False, the default)."""
+        self._check(_native.lib().spt_service_set_full_grid(self._h, 1 if full else 0))
+
     def service_stop(self) -> None:
         """Drain and end the service session; renders launch per call again."""
         self._check(_native.lib().spt_service_stop(self._h))

@@ -550,7 +550,8 @@ def test_cpp_dropin_shim_renders_like_the_context(spt, golden_scenes, tmp_path, 
     (0, "rccl", 2, "segment", "c2"), (1, "rccl", 2, "segment", "c2"), (0, "ipc", 2, "segment", "c2"),
     (1, "ipc", 2, "segment", "c2"), (0, "rccl", 3, "task", "c2"), (0, "ipc", 3, "task", "c2"),
     (1, "rccl", 3, "task", "c2"), (1, "ipc", 3, "task", "c2"), (0, "ipc", 2, "segment", "c5"),
-    (0, "rccl", 2, "task", "c2w"), (0, "ipc", 2, "segment", "c3")])
+    (0, "rccl", 2, "task", "c2w"), (0, "ipc", 2, "segment", "c3"), (1, "auto", 2, "segment", "c2"),
+    (1, "auto-fail", 2, "segment", "c2")])
 def test_bench_two_ranks_on_one_gpu_matches_one_rank(spt, tmp_path, service, transport, world, mode, config):
     """bench.py's N>1 flow (strip split, gather to rank 0, rank-0 assemble)
     rehearsed with two gloo ranks sharing cuda:0, launched by bench.py itself
@@ -566,7 +567,9 @@ def test_bench_two_ranks_on_one_gpu_matches_one_rank(spt, tmp_path, service, tra
     186): split by output ranges (spt_task_range), gathered and placed end to end; and
     config 5's LDS-tree scene (1920 x 1080 x 256 spp) over the transport, and the
     ~500-sphere scene (its 89-node tree takes the LDS lane walk) in task mode, and config 3
-    (3840 x 2160 x 1024 spp: each rank share rendered in sample batches) over the transport."""
+    (3840 x 2160 x 1024 spp: each rank share rendered in sample batches) over the transport;
+    the default (--transport auto: the copy-engine transport once its setup check passes)
+    and its fallback to the RCCL-path gather when the check fails (a corrupted pattern)."""
     import json
     import os
     import subprocess
@@ -582,14 +585,21 @@ def test_bench_two_ranks_on_one_gpu_matches_one_rank(spt, tmp_path, service, tra
     if service:
         env["SPT_SVC_GRID_DIV"] = str(world)
         extra = ["--service", "1", "--steps", "3", "--warmup", "1"]
-    if transport == "ipc":
-        extra = ["--service", str(service), "--steps", "5", "--warmup", "2", "--transport", "ipc"]
+    if transport != "rccl":
+        extra = ["--service", str(service), "--steps", "5", "--warmup", "2"]
+    if transport == "auto-fail":
+        env["SPT_TILES_TEST_CORRUPT"] = "1"  # the setup check fails: bench falls back to RCCL
+    extra += ["--transport", transport.split("-")[0]]
     r = subprocess.run(base + ["--gpus", str(world), "--dump", str(two)] + extra, check=True, timeout=300, cwd=root,
                        env=env, capture_output=True, text=True)
     line = json.loads([s for s in r.stdout.splitlines() if s.startswith("{")][-1])
     assert line["n_gpus"] == world and line["world_size"] == world and line["backend"] == "gloo"
     assert line["config"]["render_service"] == bool(service)
-    assert line["config"]["transport"] == transport
+    want = {"rccl": ("rccl", None), "ipc": ("ipc", "passed"), "auto": ("ipc", "passed"),
+            "auto-fail": ("rccl", "failed")}[transport]
+    assert (line["config"]["transport"], line["config"]["transport_check"]) == want
+    # the session leaves a block slot free only beside the copy-engine transport
+    assert line["config"]["service_full_grid"] == (bool(service) and want[0] == "rccl")
     assert len(line["ranks"]["render_ms"]) == world and min(line["ranks"]["render_ms"]) > 0
     a, b = np.fromfile(one, np.uint8), np.fromfile(two, np.uint8)
     W, H = {"c5": (1920, 1080), "c3": (3840, 2160)}.get(config, (1200, 800))

@@ -881,6 +881,30 @@ def test_multi_device_frame_equals_one_device(spt, golden_scenes, devices, task,
         assert st["launches"] == len(devices) and st["samples"] == W * H * spp
 
 
+@pytest.mark.parametrize("scene_kind,task", [("stress", False), ("stress", True), ("random500", True)])
+def test_batched_concurrent_calls_on_lane_walk_scenes(spt, scene_kind, task):
+    """RenderImageParallelMain's concurrent calls (Renderer.hpp:257-302) batched into one
+    launch per batch (spt_batch.cpp) on scenes whose tree takes the LDS lane walk -- the
+    10 000-sphere stress scene (render_kernel_lds_batch, 1 024-thread blocks) and the
+    ~500-sphere one -- in both modes (task mode on its non-square tiles aliases): the same
+    g_data bytes as one call per tile in turn, and the calls really were batched."""
+    scene = spt.generate_stress(5, 10000) if scene_kind == "stress" else spt.generate_spheres(1, z_end=37.5)
+    W, H = 320, 180
+    g = spt.Globals(scene, width=W, height=H, samples=4, bounces=50)
+    g.ctx.reset_stats()
+    spt.RenderImageParallelMain(g, thread_count=4, task=task)
+    got = g.g_data.copy()
+    st = g.ctx.stats()
+    assert st["batches"] >= 1 and st["batched_calls"] == 16 and st["batches"] < 16
+    tiles = spt.Globals(scene, width=W, height=H, samples=4, bounces=50, context=g.ctx)
+    fn = spt.RenderSegmentTask if task else spt.RenderSegment
+    for j in range(4):
+        for i in range(4):
+            fn(spt.MakeRenderSegmentData(i, j, W // 4, H // 4, tiles), tiles)
+    assert np.array_equal(got, tiles.g_data)
+    g.ctx.close()
+
+
 def test_multi_device_context_serves_render_jobs(spt, golden_scenes):
     """RenderImageParallelMain's concurrent RenderJob tiles (Renderer.hpp:257-302) on a
     two-member context: tiles go to the least busy member, same g_data bytes."""

@@ -551,7 +551,7 @@ def test_cpp_dropin_shim_renders_like_the_context(spt, golden_scenes, tmp_path, 
     (1, "ipc", 2, "segment", "c2"), (0, "rccl", 3, "task", "c2"), (0, "ipc", 3, "task", "c2"),
     (1, "rccl", 3, "task", "c2"), (1, "ipc", 3, "task", "c2"), (0, "ipc", 2, "segment", "c5"),
     (0, "rccl", 2, "task", "c2w"), (0, "ipc", 2, "segment", "c3"), (1, "auto", 2, "segment", "c2"),
-    (1, "auto-fail", 2, "segment", "c2")])
+    (1, "auto-fail", 2, "segment", "c2"), (0, "ipc", 2, "task", "c2+wavefront")])
 def test_bench_two_ranks_on_one_gpu_matches_one_rank(spt, tmp_path, service, transport, world, mode, config):
     """bench.py's N>1 flow (strip split, gather to rank 0, rank-0 assemble)
     rehearsed with two gloo ranks sharing cuda:0, launched by bench.py itself
@@ -569,7 +569,8 @@ def test_bench_two_ranks_on_one_gpu_matches_one_rank(spt, tmp_path, service, tra
     ~500-sphere scene (its 89-node tree takes the LDS lane walk) in task mode, and config 3
     (3840 x 2160 x 1024 spp: each rank share rendered in sample batches) over the transport;
     the default (--transport auto: the copy-engine transport once its setup check passes)
-    and its fallback to the RCCL-path gather when the check fails (a corrupted pattern)."""
+    and its fallback to the RCCL-path gather when the check fails (a corrupted pattern);
+    the wavefront engine's rank shares in task mode."""
     import json
     import os
     import subprocess
@@ -577,7 +578,9 @@ def test_bench_two_ranks_on_one_gpu_matches_one_rank(spt, tmp_path, service, tra
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     one, two = tmp_path / "one.bin", tmp_path / "two.bin"
     base = [sys.executable, os.path.join(root, "bench.py"), "--steps", "1", "--warmup", "0", "--no-cpu-baseline",
-            "--no-dropin", "--mode", mode, "--config", config]
+            "--no-dropin", "--mode", mode, "--config", config.split("+")[0]]
+    if "+" in config:  # the render engine: "+wavefront" = the material-queue variant
+        base += ["--engine", config.split("+")[1]]
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     subprocess.run(base + ["--dump", str(one)], check=True, timeout=300, cwd=root, env=env)
     env["SPT_DIST_BACKEND"] = "gloo"
@@ -602,7 +605,7 @@ def test_bench_two_ranks_on_one_gpu_matches_one_rank(spt, tmp_path, service, tra
     assert line["config"]["service_full_grid"] == (bool(service) and want[0] == "rccl")
     assert len(line["ranks"]["render_ms"]) == world and min(line["ranks"]["render_ms"]) > 0
     a, b = np.fromfile(one, np.uint8), np.fromfile(two, np.uint8)
-    W, H = {"c5": (1920, 1080), "c3": (3840, 2160)}.get(config, (1200, 800))
+    W, H = {"c5": (1920, 1080), "c3": (3840, 2160)}.get(config.split("+")[0], (1200, 800))
     assert a.size == b.size == W * H * 3
     bad = np.nonzero(a != b)[0]
     rows = np.unique(H - 1 - (bad // 3) // W)  # g_data row r holds image row y = H-1-r

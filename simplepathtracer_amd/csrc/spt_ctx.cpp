@@ -468,9 +468,18 @@ int check_not_in_callback(spt_ctx *ctx)
 // even_strip, the same rule as the one-process-per-GPU path).
 uint32_t even_strip(uint32_t height, uint32_t parts)
 {
-    for (uint32_t s : {8u, 4u, 2u, 1u})
-        if (height % s == 0 && (height / s) % parts == 0) return s;
-    return 8u;
+    // the tallest strip (8, 4, 2, 1 rows) whose deal gives no part more than 6% over an
+    // even share: 8-row strips keep the 8x8 pixel blocks of the primary batches and
+    // candidate lists whole (round 6, tools/scaling_probe.py at N = 8: config 3 42.85 /
+    // 46.26 / 51.05 ms per share at 8 / 4 / 2 rows, config 2 5.9 / 6.2 / 6.9 us per row);
+    // distributed.even_strip is the same rule
+    if (parts <= 1) return 8u;
+    for (uint32_t s : {8u, 4u, 2u}) {
+        const uint64_t strips = (height + s - 1) / s;
+        const uint64_t rows = std::min<uint64_t>(height, (strips + parts - 1) / parts * s);
+        if ((double)rows <= 1.06 * (double)height / parts) return s;
+    }
+    return 1u;
 }
 
 // Setters of one context; the exported setters apply them to every member device.

@@ -22,12 +22,20 @@ MODE_TASK = 1  # spt_hip.h SPT_MODE_TASK
 
 
 def even_strip(height: int, world: int) -> int:
-    """Rows per strip: the largest of 8, 4, 2, 1 that deals the frame's strips
-    evenly over the ranks (config 2 at 8 ranks: 200 strips of 4 rows), else 8."""
-    for s in (8, 4, 2, 1):
-        if height % s == 0 and (height // s) % world == 0:
+    """Rows per strip: the tallest of 8, 4, 2 whose deal gives no rank more than 6% over an
+    even share, else 1.  8-row strips keep the 8x8 pixel blocks of the primary batches and
+    the candidate lists whole: at N = 8 (tools/scaling_probe.py, round 6) config 3's share
+    renders in 42.85 / 46.26 / 51.05 ms with 8- / 4- / 2-row strips and config 2's at 5.9 /
+    6.2 / 6.9 us per row, so config 2 at 8 ranks takes 13 or 12 strips of 8 rows (104 rows
+    at most) rather than 25 of 4.  The C++ host (spt_ctx.cpp even_strip) uses the same rule."""
+    if world <= 1:
+        return 8
+    for s in (8, 4, 2):
+        strips = -(-height // s)
+        rows = min(height, -(-strips // world) * s)
+        if rows <= 1.06 * height / world:
             return s
-    return 8
+    return 1
 
 
 @dataclass(frozen=True)

@@ -458,8 +458,9 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     st = ctx.stats()
-    # this rank's render device time per step (union of its launches' intervals)
-    rank_render_ms = st["render_busy_ms"] / args.steps
+    # this rank's render device time per step (union of its launches' intervals; the
+    # render service: its session kernel's time)
+    rank_render_ms = (st["svc_kernel_ms"] if use_svc else st["render_busy_ms"]) / args.steps
     rank_gather_ms = sum(a.elapsed_time(b) for a, b in gev) / max(len(gev), 1)
     per_rank = None
     if world > 1:
@@ -490,6 +491,11 @@ def main():
         # device time; the span average is reported beside it
         avg_ms = st["render_busy_ms"] / launches
         span_ms = st["render_ms"] / launches
+        if use_svc:
+            # the render service: one resident launch per timed region, one job per frame;
+            # the per-frame device time is the session kernel's time over its jobs
+            launches = max(st["svc_jobs"], 1)
+            avg_ms = span_ms = st["svc_kernel_ms"] / launches
         t_launch = avg_ms / 1e3
         rays_per_launch = st["casts"] / launches
         samples_per_launch = st["samples"] / launches
@@ -545,9 +551,11 @@ def main():
                          "slot_def": "the design's per-sample slots (a 4-byte sample word in segment mode, word + "
                                      "order key in task mode) written once by the render kernel and read back "
                                      "once by the fold",
-                         "kernel": "render_kernel", "avg_launch_ms": round(avg_ms, 4),
-                         "avg_launch_ms_def": "union of the render launches' HIP-event intervals (launch stream) "
-                                              "/ launches",
+                         "kernel": "render_kernel_svc" if use_svc else "render_kernel",
+                         "avg_launch_ms": round(avg_ms, 4),
+                         "avg_launch_ms_def": ("the session kernel's HIP-event interval / its jobs (one per frame)"
+                                               if use_svc else "union of the render launches' HIP-event intervals "
+                                                               "(launch stream) / launches"),
                          "avg_launch_span_ms": round(span_ms, 4)},
             "world_size": world_seen,
             "backend": backend_seen,

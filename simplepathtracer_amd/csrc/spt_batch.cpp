@@ -457,17 +457,26 @@ int spec_serve(spt_ctx *ctx, std::unique_lock<std::mutex> &lk, int mode, uint32_
                 sp.armed = false;
             }
             uint8_t &seen = sp.arm_seen[(size_t)(yB / h) * tc + xB / w];
+            // arm_first: the first call of a tiling (RenderImageParallelMain's detached
+            // threads reach the library in no fixed order) arms it and starts the read-ahead at
+            // once -- the one frame of the reference's MainLoop is then rendered whole
+            // 
+            const bool now = !seen && sp.arm_first && sp.arm_count == 0;
             if (!seen) {
                 seen = 1;
-                sp.armed = ++sp.arm_count == tc * tc;
+                sp.armed = ++sp.arm_count == tc * tc || now;
                 // the read-ahead's buffers now, while this frame's tiles render as usual
                 if (sp.armed) {
                     const int rc = spec_prepare(ctx, lk, mode, tc);
                     if (rc) return rc;
                 }
             }
-            return kSpecMiss;
+            if (!now) {
+                host_trace("spec_serve miss (not armed), tile", (void *)(uintptr_t)((yB / h) * tc + xB / w));
+                return kSpecMiss;
+            }
         }
+        host_trace("spec_serve launch for tile", (void *)(uintptr_t)((yB / h) * tc + xB / w));
         int rc = spec_launch(ctx, lk, mode, tc);
         if (rc) return rc;
         k = tile_of();

@@ -52,6 +52,23 @@ void warm_start(spt_ctx *ctx)
                                     : hipStreamCreateWithPriority(&s, hipStreamNonBlocking, prio);
         w.s[i] = e == hipSuccess ? s : nullptr;  // null: the taker creates its own
     }
+    // the process's first device-to-host hipMemcpy2D waits ~8.6 ms for the runtime's copy
+    // setup (round 6 API trace of the cold frame, gpurun r06bo: its first four tile copies
+    // out of the read-ahead frame took 8.6 ms each, the later ones 0.1-0.3 ms): one small
+    // 2D copy into page-locked (registered and allocated) and pageable memory now
+    uint8_t *d = nullptr;
+    if (hipMalloc((void **)&d, 4096) != hipSuccess) return;
+    (void)hipMemset(d, 0, 4096);
+    static thread_local uint8_t pageable[8192];
+    uint8_t *reg = (uint8_t *)(((uintptr_t)pageable + 4095) & ~(uintptr_t)4095);
+    const bool registered = hipHostRegister(reg, 4096, hipHostRegisterDefault) == hipSuccess;
+    uint8_t *pinned = nullptr;
+    if (hipHostMalloc((void **)&pinned, 4096) != hipSuccess) pinned = nullptr;
+    for (uint8_t *h : {reg, pinned})
+        if (h) (void)hipMemcpy2D(h, 64, d, 64, 48, 16, hipMemcpyDeviceToHost);
+    if (registered) (void)hipHostUnregister(reg);
+    if (pinned) (void)hipHostFree(pinned);
+    (void)hipFree(d);
 }
 
 // Warm stream i, or nullptr without a warm-up (or once taken)
@@ -932,9 +949,14 @@ int spt_set_cluster_tree(spt_ctx *ctx, uint32_t branching)
 
 int spt_prepare_dropin(spt_ctx *ctx)
 {
-    return for_members(ctx, [](spt_ctx *c) {
+    // the drop-in's caller renders whole tilings: the read-ahead may arm at a tiling's
+    // first tile (SPT_READAHEAD_FIRST=0: only after a whole tiling, as for other callers)
+    const char *e = env_var("SPT_READAHEAD_FIRST");
+    const bool first = !e || std::atoi(e) != 0;
+    return for_members(ctx, [&](spt_ctx *c) {
         std::lock_guard<std::mutex> lk(c->mu);
         warm_start(c);
+        c->spec.arm_first = first;
         return SPT_OK;
     });
 }

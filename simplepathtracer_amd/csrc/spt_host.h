@@ -96,7 +96,8 @@ struct BatchReq {
 // read-ahead"): RenderImageParallelMain (Renderer.hpp:257-302) calls RenderSegment on the
 // tc x tc tiles of MakeRenderSegmentData, at most tc at a time, from detached threads (so
 // in no fixed order).  Once a caller has called every tile of such a tiling (the tiling is
-// "armed": a caller rendering one tile alone never arms it), the first call of a tile of it
+// "armed": a caller rendering one tile alone never arms it; with arm_first, the drop-in's
+// setting, its first call arms it), the first call of a tile of it
 // renders every tile of the frame at once in `parts` batched launches of consecutive tile
 // rows (SPT_READAHEAD_PARTS, default 4) into a device copy of g_data; each tile's call then
 // waits for its part and copies its own rows to the caller's g_data.  Every tile is still
@@ -123,6 +124,10 @@ struct SpecFrame {
     uint32_t arm_tc = 0, arm_w = 0, arm_h = 0, arm_count = 0;
     std::vector<uint8_t> arm_seen;
     bool armed = false;
+    // arm at a tiling's first call instead of after a whole tiling (the drop-in,
+    // spt_prepare_dropin: its caller is RenderImageParallelMain, which renders every tile
+    // of every frame -- and MainLoop only one frame per process)
+    bool arm_first = false;
 };
 
 constexpr int kSpecMiss = 1;  // spec_serve: not a read-ahead tile (render it as usual)

@@ -102,8 +102,9 @@ class Context:
         self._check(_native.lib().spt_set_cluster_tree(self._h, int(branching)))
 
     def prepare_dropin(self) -> None:
-        """spt_prepare_dropin: create the drop-in's batch and read-ahead streams on a helper
-        thread (what the C++ shim does once after creating its context)."""
+        """spt_prepare_dropin (what the C++ shim does once after creating its context): create
+        the drop-in's batch and read-ahead streams now, and arm the tiling read-ahead at a
+        tiling's first call (SPT_READAHEAD_FIRST=0: only after a whole tiling)."""
         self._check(_native.lib().spt_prepare_dropin(self._h))
 
     def set_reserved_cus(self, n: int) -> None:

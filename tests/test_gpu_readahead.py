@@ -5,7 +5,9 @@ read-ahead render of the whole tiling, once the caller has called every tile of 
 tiling (the tiling is armed).  Every output byte must equal a plain render, a lone
 first-tile call must write only its own rows and start no read-ahead, a frame whose
 first call is another tile (the reference's detached threads keep no order) must be
-served too, and a setter between frames must not serve a stale frame."""
+served too, and a setter between frames must not serve a stale frame.  The drop-in's
+setting (spt_prepare_dropin) arms a tiling at its first call instead, so that the first
+frame is served too."""
 import threading
 
 import numpy as np
@@ -149,3 +151,52 @@ def test_readahead_starts_at_any_tile(spt, golden_scenes, first):
     ctx.close()
     assert np.array_equal(g, want), f"{np.count_nonzero(g != want)} bytes differ"
     assert st["batches"] == min(4, tc) and st["batched_calls"] == tc * tc and st["samples"] == W * H * spp
+
+
+@pytest.mark.parametrize("task", [False, True])
+def test_dropin_first_frame_served_from_readahead(spt, golden_scenes, monkeypatch, task):
+    """The drop-in (spt_prepare_dropin, which the C++ shim calls) arms the read-ahead at a
+    tiling's first call (RenderImageParallelMain's detached threads arrive in no fixed
+    order), so MainLoop's one frame per
+    process (Renderer.hpp:335-344) is rendered whole in the read-ahead's launches.  Its bytes
+    equal plain calls, whichever tile comes first; a lone tile (0, 0) still writes only its
+    own rows (the rest of the frame is rendered but not copied); SPT_READAHEAD_FIRST=0 keeps
+    the first frame tile by tile."""
+    W, H, spp, tc = 240, 160, 4, 4
+    monkeypatch.setenv("SPT_READAHEAD", "0")
+    plain = make_ctx(spt, golden_scenes, W, H, spp, seed=6)
+    want = np.zeros(W * H * 3, np.uint8)
+    for t in tiles(W, H, tc):
+        plain.render_segment(*t, g_data=want, task=task, rgba=False)
+    plain.close()
+    monkeypatch.delenv("SPT_READAHEAD")
+    ctx = make_ctx(spt, golden_scenes, W, H, spp, seed=6)
+    ctx.prepare_dropin()
+    ctx.reset_stats()
+    g = render_tiling(ctx, W, H, tc, task, 4)
+    st = ctx.stats()
+    ctx.close()
+    assert np.array_equal(g, want), f"{np.count_nonzero(g != want)} bytes differ"
+    assert st["batches"] == min(4, tc) and st["batched_calls"] == tc * tc and st["samples"] == W * H * spp
+    # a lone tile (0, 0): only its rows reach g_data
+    lone = make_ctx(spt, golden_scenes, W, H, spp, seed=6)
+    lone.prepare_dropin()
+    g1 = np.zeros(W * H * 3, np.uint8)
+    lone.render_segment(*tiles(W, H, tc)[0], g_data=g1, task=task, rgba=False)
+    lone.close()
+    img, ref = g1.reshape(H, W, 3), want.reshape(H, W, 3)
+    sw, sh = W // tc, H // tc
+    # tile (0, 0) = image rows [0, sh), columns [0, sw) = g_data rows H-sh.. H-1
+    assert np.array_equal(img[H - sh:, :sw], ref[H - sh:, :sw])
+    img2 = img.copy()
+    img2[H - sh:, :sw] = 0
+    assert not img2.any()
+    monkeypatch.setenv("SPT_READAHEAD_FIRST", "0")
+    off = make_ctx(spt, golden_scenes, W, H, spp, seed=6)
+    off.prepare_dropin()
+    off.reset_stats()
+    g2 = render_tiling(off, W, H, tc, task, 4)
+    st2 = off.stats()
+    off.close()
+    assert np.array_equal(g2, want)
+    assert st2["samples"] == W * H * spp and st2["batched_calls"] == tc * tc and st2["batches"] >= 1

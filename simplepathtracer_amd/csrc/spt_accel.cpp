@@ -722,7 +722,9 @@ PrimListTables build_prim_lists(const AccelTables &t, const Camera &cam, uint32_
     };
     const size_t work_units = sups.size() * t.slots.size();
     const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-    size_t nth = work_units < (1u << 20) ? 1 : std::min<size_t>({(size_t)hw, (size_t)16, sups.size()});
+    // config 2 (247 super-blocks x 160 slots) took 7.5 ms on one thread: threads from 2^14
+    // work units (a thread's start costs ~50 us)
+    size_t nth = work_units < (1u << 14) ? 1 : std::min<size_t>({(size_t)hw, (size_t)16, sups.size()});
     if (const char *ev = std::getenv("SPT_PRIM_THREADS"))  // tests: one thread vs many give the same tables
         if (*ev) nth = std::max(1, std::atoi(ev));
     if (nth <= 1) {

@@ -54,11 +54,16 @@ void warm_start(spt_ctx *ctx)
     }
     // the process's first device-to-host hipMemcpy2D waits ~8.6 ms for the runtime's copy
     // setup (round 6 API trace of the cold frame, gpurun r06bo: its first four tile copies
-    // out of the read-ahead frame took 8.6 ms each, the later ones 0.1-0.3 ms): one small
-    // 2D copy into page-locked (registered and allocated) and pageable memory now
+    // out of the read-ahead frame took 8.6 ms each, the later ones 0.1-0.3 ms), and so does
+    // its first host-to-device copy on a copy engine (the primary lists' upload, 8.5 ms for
+    // 120 KB; the smaller scene tables go through blit kernels): one small 2D copy into
+    // page-locked (registered and allocated) memory and one 256 KiB upload now
     uint8_t *d = nullptr;
-    if (hipMalloc((void **)&d, 4096) != hipSuccess) return;
-    (void)hipMemset(d, 0, 4096);
+    if (hipMalloc((void **)&d, 256 << 10) != hipSuccess) return;
+    {
+        std::vector<uint8_t> up((size_t)256 << 10, 0);
+        (void)hipMemcpy(d, up.data(), up.size(), hipMemcpyHostToDevice);
+    }
     static thread_local uint8_t pageable[8192];
     uint8_t *reg = (uint8_t *)(((uintptr_t)pageable + 4095) & ~(uintptr_t)4095);
     const bool registered = hipHostRegister(reg, 4096, hipHostRegisterDefault) == hipSuccess;
@@ -480,8 +485,7 @@ int check_not_in_callback(spt_ctx *ctx)
     return SPT_OK;
 }
 
-// Rows per strip of the multi-device frame split: the largest of 8, 4, 2, 1 that deals
-// the frame's strips evenly over the members, else 8 (simplepathtracer_amd/distributed.py
+// Rows per strip of the multi-device frame split (simplepathtracer_amd/distributed.py
 // even_strip, the same rule as the one-process-per-GPU path).
 uint32_t even_strip(uint32_t height, uint32_t parts)
 {

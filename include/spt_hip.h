@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define SPT_ABI_VERSION 10
+#define SPT_ABI_VERSION 11
 
 /* Only the functions below are exported from libspt_hip.so (built with
  * -fvisibility=hidden), so several builds can be loaded side by side. */
@@ -119,8 +119,6 @@ typedef struct spt_stats {
                                     accel tables, the camera or the frame size changed) */
     double accel_build_ms;       /* host time of the last traversal-table build + upload
                                     (spt_set_scene / cluster setters) */
-    uint64_t svc_inkernel_folds; /* service jobs folded inside the session by its fold waves
-                                    (the rest are fold launches on the caller's stream) */
 } spt_stats;
 
 SPT_API int spt_abi_version(void);

@@ -15,7 +15,7 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG_DIR, "lib", os.environ.get("SPT_LIB", "libspt_hip.so"))
 HEADER_PATH = os.path.join(os.path.dirname(PKG_DIR), "include", "spt_hip.h")
 
-ABI_VERSION = 10  # SPT_ABI_VERSION of include/spt_hip.h
+ABI_VERSION = 11  # SPT_ABI_VERSION of include/spt_hip.h
 SPT_OK = 0
 STATUS_NAMES = {0: "SPT_OK", 1: "SPT_ERR_ARG", 2: "SPT_ERR_STATE", 3: "SPT_ERR_HIP", 4: "SPT_ERR_NOMEM",
                 5: "SPT_ERR_NODEVICE", 6: "SPT_ERR_TIMEOUT"}
@@ -60,7 +60,6 @@ class Stats(ctypes.Structure):
         ("prim_list_build_ms", ctypes.c_double),
         ("prim_list_builds", ctypes.c_uint64),
         ("accel_build_ms", ctypes.c_double),
-        ("svc_inkernel_folds", ctypes.c_uint64),
     ]
 
 

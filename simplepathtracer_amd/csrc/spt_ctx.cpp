@@ -659,7 +659,6 @@ int stats_one(spt_ctx *ctx, spt_stats *out)
     out->prim_list_build_ms = ctx->prim_build_s * 1e3;
     out->prim_list_builds = ctx->prim_builds;
     out->accel_build_ms = ctx->accel_build_s * 1e3;
-    out->svc_inkernel_folds = ctx->svc.inkernel_folds;
     return SPT_OK;
 }
 
@@ -676,7 +675,6 @@ int reset_one(spt_ctx *ctx)
     ctx->batches = ctx->batched_calls = 0;
     ctx->svc.sessions = ctx->svc.jobs = ctx->svc.watchdog_exits = 0;
     ctx->svc.flow_restarts = ctx->svc.closing_restarts = 0;
-    ctx->svc.inkernel_folds = 0;
     ctx->svc.kernel_ms = 0;
     ctx->spans.clear();
     ctx->ref_recorded = false;
@@ -760,9 +758,7 @@ int spt_ctx_create(int device, spt_ctx **out)
     // SPT_SERVICE=1: the context starts with the render service on (spt_service_start)
     if (const char *e = env_var("SPT_SERVICE")) ctx->svc.enabled = std::atoi(e) != 0;
     if (const char *e = env_var("SPT_SVC_CLAIM")) ctx->svc.claim = (uint32_t)std::max(64, std::atoi(e) / 64 * 64);
-    if (const char *e = env_var("SPT_SVC_FOLD")) ctx->svc.fold_inkernel = std::atoi(e) != 0;
     if (const char *e = env_var("SPT_SVC_LDS")) ctx->svc.lds = std::atoi(e) != 0;
-    if (const char *e = env_var("SPT_SVC_FOLD_BLOCKS")) ctx->svc.fold_blocks = (uint32_t)std::max(1, std::atoi(e));
     if (const char *e = env_var("SPT_SVC_QUEUES"))
         ctx->svc.queues = (uint32_t)std::min<int>((int)spt::kMaxQueues, std::max(1, std::atoi(e)));
     if (const char *e = env_var("SPT_SVC_RING_MB")) {
@@ -904,8 +900,7 @@ void spt_ctx_destroy(spt_ctx *ctx)
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     {
         Service &v = ctx->svc;
-        for (void *b : {(void *)v.d_ctl, (void *)v.d_jobs, (void *)v.d_job_claim, (void *)v.d_done, (void *)v.d_ring,
-                        (void *)v.d_fold})
+        for (void *b : {(void *)v.d_ctl, (void *)v.d_jobs, (void *)v.d_job_claim, (void *)v.d_done, (void *)v.d_ring})
             if (b) (void)hipFree(b);
         for (const SvcInflight &e : v.inflight) (void)hipEventDestroy(e.ev);
         for (hipEvent_t e : v.ev_pool) (void)hipEventDestroy(e);

@@ -160,16 +160,9 @@ struct Service {
     uint32_t *d_ctl = nullptr;
     spt::SvcJob *d_jobs = nullptr;
     uint32_t *d_job_claim = nullptr, *d_done = nullptr, *d_ring = nullptr;
-    // in-kernel folds (round 6, SPT_SVC_FOLD=1): the session's fold block (spt_internal.h
-    // svc_fold_words).  Off by default: measured slower than fold launches
-    uint32_t *d_fold = nullptr;
-    bool fold_inkernel = false;
     // SPT_SVC_LDS=1: scenes whose tree takes the LDS lane walk run LDS-tree sessions
     // (render_kernel_svc_lds); off by default: measured slower than launches (§4.7)
     bool lds = false;
-    bool fold_session = false;  // the running session has fold waves
-    uint32_t fold_blocks = 64;  // SPT_SVC_FOLD_BLOCKS: blocks of fold waves per session
-    uint64_t inkernel_folds = 0;  // jobs published with an in-kernel fold
     uint64_t ring_words = 0;
     uint64_t ring_bytes = 4ull << 30;  // SPT_SVC_RING_MB, else sized at the first session (svc_start)
     bool ring_set = false;             // SPT_SVC_RING_MB given
@@ -187,9 +180,6 @@ struct Service {
     // is not ordered before the caller's wait); a total that would pass 2^32 restarts at
     // zero, with the caller's stream ordered after that publish
     std::vector<uint64_t> done_cum;
-    // per completion counter, the running total of samples folded in-kernel (the device's
-    // folded[] words count only in-kernel-fold jobs; zeroed with done_cum's restarts)
-    std::vector<uint64_t> folded_cum;
     std::vector<SvcInflight> inflight;
     std::vector<hipEvent_t> ev_pool;
     hipEvent_t ev_start = nullptr, ev_end = nullptr, ev_ctl = nullptr;
@@ -224,13 +214,6 @@ struct SvcJobSpec {
     spt::FastDiv div_band, div_tile, div_strip;
     uint64_t slot_local;
 };
-// A job folded inside the session (SvcJob::fold_*): its outputs (device pointers, either
-// nullable); the caller's stream then waits for the fold instead of launching it.
-struct SvcFold {
-    float4 *rgba;
-    uint8_t *rgb8;
-};
-
 // Render the rows of `map` and fold them into d_rgba (local pixel order) and/or
 // d_rgb8 (full frame).  keep_samples: leave the per-sample colours of a single
 // batch in d_samples (debug path).
@@ -467,8 +450,8 @@ EventPair get_pair(spt_ctx *ctx);
 int check_on_device(spt_ctx *ctx, const void *p, const char *what);
 int fail(spt_ctx *ctx, int code, const char *fmt, ...);
 int svc_retire(spt_ctx *ctx, hipStream_t s, uint64_t w0, uint64_t words, uint32_t idx);
-int svc_submit(spt_ctx *ctx, const spt::RenderArgs &ra, int mode, hipStream_t s, uint64_t *w0_out, uint32_t *idx_out, const SvcFold *fold = nullptr);
-int svc_submit_jobs(spt_ctx *ctx, int mode, const SvcJobSpec *jobs, size_t n, uint64_t total_slots, hipStream_t s, uint64_t *w0_out, uint32_t *idx_out, const SvcFold *fold = nullptr);
+int svc_submit(spt_ctx *ctx, const spt::RenderArgs &ra, int mode, hipStream_t s, uint64_t *w0_out, uint32_t *idx_out);
+int svc_submit_jobs(spt_ctx *ctx, int mode, const SvcJobSpec *jobs, size_t n, uint64_t total_slots, hipStream_t s, uint64_t *w0_out, uint32_t *idx_out);
 bool svc_eligible(const spt_ctx *ctx, uint64_t words, bool keep_samples);
 // SPT_HOST_TRACE=1: a line on stderr with the ms since the process's first trace point
 // (where host time goes in a cold frame: allocations, stream creation, first launches)
@@ -476,7 +459,6 @@ void host_trace(const char *what, const void *arg = nullptr);
 void warm_start(spt_ctx *ctx);
 hipStream_t warm_take(spt_ctx *ctx, int i);
 void warm_join(spt_ctx *ctx);
-bool svc_folds_in_kernel(const spt_ctx *ctx);
 uint32_t svc_session_grid(const spt_ctx *ctx);
 int svc_begin(spt_ctx *ctx, int mode, const std::vector<hipEvent_t> &waits, int64_t reset_idx, hipStream_t s);
 int svc_end(spt_ctx *ctx);

@@ -336,14 +336,6 @@ struct RenderArgs {
     uint32_t *svc_host;
     const struct SvcJob *svc_host_jobs;
     const uint32_t *svc_host_job_claim;
-    // in-kernel folds: the session's fold block (svc_fold_words), its capacities, and the
-    // sample-code divisor the fold decodes with (FoldArgs::code_div)
-    uint32_t *svc_fold;
-    uint32_t svc_job_cap, svc_done_cap;
-    FastDiv fold_code_div;
-    // blocks [0, svc_fold_blocks) of the session: their waves (but the forwarder, wave 0 of
-    // block 0) fold published jobs instead of rendering (spt_kernels.hip svc_fold_loop)
-    uint32_t svc_fold_blocks;
     // primary-ray candidate lists (PrimLists; on = 0: every primary batch walks the tree)
     PrimLists prim;
 };
@@ -379,24 +371,11 @@ struct SvcJob {
     RowMap map;                   // region (rows or interleaved strips, columns)
     FastDiv div_band, div_tile, div_strip;  // ts_item / row_of_fast divisors
     uint32_t claim_first;         // its first claim (item_off / claim)
-    // in-kernel fold (fold_flags & kSvcFoldInKernel; round 6): the job's
-    // completion counter reaches fold_target with its last sample; the session's waves then
-    // fold it into fold_rgba (local float4, nullable) / fold_rgb8 (g_data layout, nullable)
-    // and add its samples to the counter's folded total, which the caller's stream waits on
-    uint32_t fold_target;
-    uint64_t fold_rgba, fold_rgb8;
-    uint32_t fold_flags;
-    uint32_t pad;
+    uint32_t pad[7];
 };
 static_assert(sizeof(SvcJob) == 128, "SvcJob: 32 words, one per lane of the loading wave");
 constexpr uint32_t kSvcJobWords = 32;
-constexpr uint32_t kSvcFoldInKernel = 1u;
-
-// word offsets of the fold fields (the fold step loads them by lane)
-constexpr uint32_t kSvcJobFoldTarget = 25, kSvcJobFoldRgba = 26, kSvcJobFoldRgb8 = 28, kSvcJobFoldFlags = 30;
-static_assert(offsetof(SvcJob, claim_first) == 24 * 4 && offsetof(SvcJob, fold_target) == kSvcJobFoldTarget * 4 &&
-                  offsetof(SvcJob, fold_rgba) == kSvcJobFoldRgba * 4 && offsetof(SvcJob, fold_rgb8) == kSvcJobFoldRgb8 * 4 &&
-                  offsetof(SvcJob, fold_flags) == kSvcJobFoldFlags * 4 && offsetof(SvcJob, map) == 8 * 4 &&
+static_assert(offsetof(SvcJob, claim_first) == 24 * 4 && offsetof(SvcJob, map) == 8 * 4 &&
                   offsetof(SvcJob, div_strip) == 21 * 4,
               "SvcJob word offsets (the service kernel reads the record by word)");
 // SvcCtl words (device memory, svc_ctl): claim counters head[q * kQueueStride]
@@ -406,23 +385,7 @@ static_assert(offsetof(SvcJob, claim_first) == 24 * 4 && offsetof(SvcJob, fold_t
 constexpr uint32_t kSvcPub = kMaxQueues * kQueueStride;  // uint64_t: claims | jobs << 32
 constexpr uint32_t kSvcStop = kSvcPub + 64;
 constexpr uint32_t kSvcLive = kSvcStop + 64;
-// in-kernel folds: entries published to the fold ring (the waves that complete a job's
-// counter add them), in-kernel-fold jobs forwarded (the forwarder stores the total before
-// the pair that publishes them), and such jobs whose fold has finished
-constexpr uint32_t kSvcFoldTail = kSvcLive + 64;
-constexpr uint32_t kSvcFoldJobs = kSvcFoldTail + 64;
-constexpr uint32_t kSvcFoldsDone = kSvcFoldJobs + 64;
-constexpr uint32_t kSvcCtlWords = kSvcFoldsDone + 64;
-// The session's fold block (RenderArgs::svc_fold), zeroed per session but for `folded`:
-// ring[job_cap] (job + 1 per published fold, in publication order), next[job_cap] (a
-// job's fold chunks taken), fin[job_cap] (its chunks finished), cjob[done_cap] (the last
-// job forwarded on each completion counter), then folded[done_cap] (per counter, the
-// running total of folded samples: like the completion counters, zeroed at allocation
-// and when a total restarts)
-__host__ __device__ inline uint32_t svc_fold_words(uint32_t job_cap, uint32_t done_cap)
-{
-    return 3u * job_cap + 2u * done_cap;
-}
+constexpr uint32_t kSvcCtlWords = kSvcLive + 64;
 // A wave with no work for 0.5 s (s_memrealtime, 100 MHz) may leave, but only through the
 // closing handshake with the host (SvcHost words):
 //   wave:  closing = 1; fence; c = committed; read the published pair; leave iff every one

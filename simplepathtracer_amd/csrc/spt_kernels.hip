@@ -184,12 +184,6 @@ __device__ __forceinline__ uint32_t svc_reserve(uint32_t q, uint32_t lane, uint3
 // current job and the first claim after it, the fold-ring entries it is done taking from
 constexpr uint32_t kSvcSt = 28;
 constexpr uint32_t kSvcRecWords = 40;  // LDS words per wave: job record (32) + state
-// the sample words a fold lane loads ahead (svc_fold_loop; sc1 loads: deep runs keep a fold
-// wave's loads in flight)
-#ifndef SPT_SVC_FOLD_RUN
-#define SPT_SVC_FOLD_RUN 8
-#endif
-constexpr int kSvcFoldRun = SPT_SVC_FOLD_RUN;
 
 // The published pair {claims, jobs} (one 64-bit sc1 load: the forwarder stores it after
 // its records, sc1, with its stores drained -- MI355X_MICROARCH.md, hand-off table)
@@ -217,8 +211,7 @@ __device__ __forceinline__ void svc_forward(uint32_t lane)
 {
     kargs_t &k = *kernarg_args();
     const gu32 *hw = (const gu32 *)k.svc_host;
-    uint32_t fwd = 0;    // records forwarded
-    uint32_t nfold = 0;  // lane 33: in-kernel-fold jobs among them
+    uint32_t fwd = 0;  // records forwarded
     for (uint32_t idle = 0;; ++idle) {
         const uint32_t st = lane == 0 ? __hip_atomic_load(hw + kSvcHostStop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0u;
         const bool stop = __builtin_amdgcn_readfirstlane(st) != 0u;
@@ -231,8 +224,7 @@ __device__ __forceinline__ void svc_forward(uint32_t lane)
         const uint32_t phi = __builtin_amdgcn_readfirstlane((uint32_t)(pv >> 32));
         if (phi > fwd) {
             // records [fwd, phi): lanes 0-31 one record's words, lane 32 its first claim,
-            // lane 33 the record's counter -> job entry (in-kernel folds) and the count of
-            // in-kernel-fold jobs, stored before the pair that publishes them
+            // stored before the pair that publishes them
             const gu32 *hj = (const gu32 *)k.svc_host_jobs;
             const gu32 *hc = (const gu32 *)k.svc_host_job_claim;
             for (uint32_t j = fwd; j < phi; ++j) {
@@ -243,19 +235,8 @@ __device__ __forceinline__ void svc_forward(uint32_t lane)
                 } else if (lane == kSvcJobWords) {
                     const uint32_t c = __hip_atomic_load(hc + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                     __hip_atomic_store((gu32 *)(k.svc_job_claim + j), c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                } else if (lane == kSvcJobWords + 1u && k.svc_fold) {
-                    const uint32_t di = __hip_atomic_load(hj + (size_t)j * kSvcJobWords + 3u, __ATOMIC_RELAXED,
-                                                          __HIP_MEMORY_SCOPE_SYSTEM);
-                    const uint32_t fl = __hip_atomic_load(hj + (size_t)j * kSvcJobWords + kSvcJobFoldFlags,
-                                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                    __hip_atomic_store((gu32 *)(k.svc_fold + 3u * k.svc_job_cap + di), j, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-                    nfold += (fl & kSvcFoldInKernel) ? 1u : 0u;
                 }
             }
-            const uint32_t nf = __builtin_amdgcn_readlane(nfold, (int)kSvcJobWords + 1);
-            if (k.svc_fold && lane == 0)
-                __hip_atomic_store((gu32 *)(k.svc_ctl + kSvcFoldJobs), nf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             if (lane == 0)
                 __hip_atomic_store((gu64 *)(k.svc_ctl + kSvcPub), (unsigned long long)plo | ((unsigned long long)phi << 32),
@@ -450,26 +431,10 @@ __device__ __forceinline__ void alias_accumulate(const FoldArgs &a, const uint32
 // (map, `rows` rows, alias: task mode on a non-square tile) whose slots start at
 // `samples` (item order of a batch of a.spp_batch samples: ts_slot_base); local float4
 // output at out_rgba[lr * width + col].
-// SC1 (the render service's in-kernel fold): the sample words are loaded with sc1 loads
-// (another XCD's L2 may hold stale lines of the ring) and the outputs stored write-through
-// (sc1), so that the counter add after the wave's drain publishes them (MI355X_MICROARCH.md
-// hand-off table, R1).  Segment mode and square task tiles only (no aliasing).
-template <bool SC1 = false, int RUN = SPT_FOLD_RUN>
 __device__ __forceinline__ void fold_pixel(const FoldArgs &a, const uint32_t *samples, const RowMap &map,
                                            uint32_t rows, int alias, uint32_t lr, uint32_t col, float4 *out_rgba,
                                            uint8_t *out_rgb8)
 {
-    typedef __attribute__((address_space(1))) uint32_t g32;
-    typedef __attribute__((address_space(1))) unsigned long long g64;
-    typedef __attribute__((address_space(1))) uint8_t g8;
-    auto ldw = [&](const uint32_t *q) -> uint32_t {
-        return SC1 ? __hip_atomic_load((g32 *)q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : *q;
-    };
-    auto ldw2 = [&](const uint2 *q) -> uint2 {
-        if (!SC1) return *q;
-        const unsigned long long v = __hip_atomic_load((g64 *)q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return make_uint2((uint32_t)v, (uint32_t)(v >> 32));
-    };
     const uint32_t W = map.width, S = a.spp_batch;
     const uint32_t p = lr * W + col;
     float4 acc = a.first ? make_float4(0.f, 0.f, 0.f, 0.f) : a.acc[p];
@@ -479,12 +444,12 @@ __device__ __forceinline__ void fold_pixel(const FoldArgs &a, const uint32_t *sa
         // RenderSegment: one word per slot, every sample counts.  Runs of kFoldRun words
         // are loaded before any is decoded (the loads of a run are in flight together),
         // then decoded eight at a time
-        constexpr int kFoldRun = RUN;
+        constexpr int kFoldRun = SPT_FOLD_RUN;
         uint32_t k = 0;
         for (; k + kFoldRun <= S; k += kFoldRun) {
             uint32_t w[kFoldRun];
 #pragma unroll
-            for (int i = 0; i < kFoldRun; ++i) w[i] = ldw(samples + q0 + (k + i) * step);
+            for (int i = 0; i < kFoldRun; ++i) w[i] = samples[q0 + (k + i) * step];
 #pragma unroll
             for (int g = 0; g < kFoldRun; g += 8) {
                 uint32_t w8[8];
@@ -502,7 +467,7 @@ __device__ __forceinline__ void fold_pixel(const FoldArgs &a, const uint32_t *sa
             }
         }
         for (; k < S; ++k) {
-            const f3 c = decode_sample(a, ldw(samples + q0 + k * step));
+            const f3 c = decode_sample(a, samples[q0 + k * step]);
             acc.x = acc.x + c.x;
             acc.y = acc.y + c.y;
             acc.z = acc.z + c.z;
@@ -512,7 +477,7 @@ __device__ __forceinline__ void fold_pixel(const FoldArgs &a, const uint32_t *sa
         // RenderSegmentTask on a square tile: pixel p is colors[p]; key 0 marks a dropped path
         const uint2 *s2 = (const uint2 *)samples;
         for (uint32_t k = 0; k < S; ++k) {
-            const uint2 v = ldw2(s2 + q0 + k * step);
+            const uint2 v = s2[q0 + k * step];
             if (v.y != 0u) {
                 const f3 c = decode_sample(a, v.x);
                 acc.x = acc.x + c.x;
@@ -521,7 +486,7 @@ __device__ __forceinline__ void fold_pixel(const FoldArgs &a, const uint32_t *sa
                 acc.w = acc.w + 1.f;
             }
         }
-    } else if (!SC1) {
+    } else {
         alias_accumulate(a, samples, p, W, rows, 0u, rows, S, acc);
     }
     if (!a.last) {
@@ -533,29 +498,14 @@ __device__ __forceinline__ void fold_pixel(const FoldArgs &a, const uint32_t *sa
     // s_done samples is the render at g_samples = s_done, bit for bit (keyed samples).
     const float scale = a.mode == 0 ? 1.f / (float)a.s_done : 1.f / acc.w;
     const float r = acc.x * scale, g = acc.y * scale, b = acc.z * scale;
-    if (out_rgba) {
-        if (SC1) {
-            g64 *o = (g64 *)(out_rgba + p);
-            __hip_atomic_store(o, (unsigned long long)__float_as_uint(r) | ((unsigned long long)__float_as_uint(g) << 32),
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(o + 1, (unsigned long long)__float_as_uint(b), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            out_rgba[p] = make_float4(r, g, b, 0.f);
-        }
-    }
+    if (out_rgba) out_rgba[p] = make_float4(r, g, b, 0.f);
     if (out_rgb8) {
         const uint32_t x = map.x0 + col;
         const uint32_t y = row_of(map, lr);
         const size_t gi = (size_t)3 * ((size_t)(a.height - 1u - y) * a.width + x);
-        if (SC1) {
-            __hip_atomic_store((g8 *)(out_rgb8 + gi + 0), gamma_byte(r), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store((g8 *)(out_rgb8 + gi + 1), gamma_byte(g), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store((g8 *)(out_rgb8 + gi + 2), gamma_byte(b), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            out_rgb8[gi + 0] = gamma_byte(r);
-            out_rgb8[gi + 1] = gamma_byte(g);
-            out_rgb8[gi + 2] = gamma_byte(b);
-        }
+        out_rgb8[gi + 0] = gamma_byte(r);
+        out_rgb8[gi + 1] = gamma_byte(g);
+        out_rgb8[gi + 2] = gamma_byte(b);
     }
 }
 
@@ -571,11 +521,6 @@ __device__ __forceinline__ void fold_pixel(const FoldArgs &a, const uint32_t *sa
 // an agent release: the fold runs on any XCD) before the add (MI355X_MICROARCH.md
 // hand-off table, each storing wave signalling for itself; Compiler hazard: the asm wait
 // after the fence).
-//
-// In-kernel folds (SvcJob::fold_flags): the add that brings the counter to the job's
-// fold_target -- the job's last samples, whichever wave holds them -- publishes the job to
-// the session's fold ring (svc_fold_step then folds it, any wave, 64 pixels at a time).
-template <bool FOLD>
 __device__ __forceinline__ void svc_flush(uint32_t idx, uint32_t cnt, uint32_t lane)
 {
     if (cnt == 0u) return;
@@ -585,165 +530,15 @@ __device__ __forceinline__ void svc_flush(uint32_t idx, uint32_t cnt, uint32_t l
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-    uint32_t old = 0;
-    if (lane == 0) old = __hip_atomic_fetch_add((gu32 *)(k.svc_done + idx), cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (lane == 0) __hip_atomic_fetch_add((gu32 *)(k.svc_done + idx), cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (k.svc_trace && lane == 0) atomicMax(k.svc_trace + 4u * idx + 2u, __builtin_amdgcn_s_memrealtime());
-    if (FOLD && k.svc_fold) {
-        uint32_t *const fb = k.svc_fold;
-        const uint32_t j = __builtin_amdgcn_readfirstlane(
-            lane == 0 ? __hip_atomic_load((gu32 *)(fb + 3u * k.svc_job_cap + idx), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                      : 0u);
-        const gu32 *jr = (const gu32 *)(k.svc_jobs + j);
-        const uint32_t w = lane == 0   ? __hip_atomic_load(jr + kSvcJobFoldTarget, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                           : lane == 1 ? __hip_atomic_load(jr + kSvcJobFoldFlags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                       : 0u;
-        const uint32_t target = __builtin_amdgcn_readlane(w, 0), flags = __builtin_amdgcn_readlane(w, 1);
-        if ((flags & kSvcFoldInKernel) && __builtin_amdgcn_readfirstlane(old) + cnt == target) {
-            uint32_t e = 0;
-            if (lane == 0) e = __hip_atomic_fetch_add((gu32 *)(k.svc_ctl + kSvcFoldTail), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            e = __builtin_amdgcn_readfirstlane(e);
-            if (lane == 0) __hip_atomic_store((gu32 *)(fb + e), j + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
 }
 
-// One chunk of in-kernel fold work (64 pixels of one job) for a fold wave (svc_fold_loop):
-// the first fold-ring entry from the wave's position st[4] whose chunks are not all taken;
-// false when there is none.  Ring entries are written right after their slot is taken; an entry not written
-// yet is left for the next visit.  The chunk's samples are loaded after this wave's own sc1
-// poll of the job's completion counter has matched (R1: every storing wave drained its
-// write-through sample stores before its add), its outputs stored write-through and
-// drained before the chunk is counted; the wave that finishes a job's last chunk adds the
-// job's samples to the counter's folded total, the value the caller's stream waits for.
-// Wave-uniform; `tail` = published ring entries as last read.
-// k: the kernel's arguments (passed in: svc_fold_loop is a real call, and a callee's
-// kernarg segment pointer is null)
-__device__ __forceinline__ bool svc_fold_step(kargs_t &k, uint32_t lane, uint32_t *st, uint32_t tail)
-{
-    uint32_t *const ring = k.svc_fold;
-    const uint32_t jc = k.svc_job_cap;
-    uint32_t seen = __builtin_amdgcn_readfirstlane(st[4]);
-    while (seen < tail) {
-        const uint32_t j1 = __builtin_amdgcn_readfirstlane(
-            lane == 0 ? __hip_atomic_load((gu32 *)(ring + seen), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u);
-        if (j1 == 0u) return false;
-        const uint32_t j = j1 - 1u;
-        const uint32_t w = lane < kSvcJobWords
-                               ? __hip_atomic_load((const gu32 *)(k.svc_jobs + j) + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                               : 0u;
-        auto f = [&](int i) -> uint32_t { return __builtin_amdgcn_readlane(w, i); };
-        const RowMap map{f(8), f(9), f(10), f(11), f(12), f(13), f(14)};
-        const uint32_t rows = f(4), S = f(5), idx = f(3), npix = rows * map.width;
-        const uint32_t nch = (npix + 63u) / 64u;
-        uint32_t c = 0;
-        if (lane == 0) c = __hip_atomic_fetch_add((gu32 *)(ring + jc + j), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        c = __builtin_amdgcn_readfirstlane(c);
-        if (c >= nch) {
-            // every chunk of this entry is taken: move on
-            ++seen;
-            if (lane == 0) st[4] = seen;
-            continue;
-        }
-        const uint32_t target = f(kSvcJobFoldTarget);
-        for (;;) {
-            const uint32_t v = __builtin_amdgcn_readfirstlane(
-                lane == 0 ? __hip_atomic_load((gu32 *)(k.svc_done + idx), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u);
-            if ((int32_t)(v - target) >= 0) break;
-            __builtin_amdgcn_s_sleep(1);
-        }
-        FoldArgs fa{};
-        fa.slot_words = k.mode == 0u ? 1u : 2u;
-        fa.samples = k.samples + (size_t)fa.slot_words * f(2);
-        fa.shade = k.scene.shade;
-        fa.sky[0] = k.cam.sky[0];
-        fa.sky[1] = k.cam.sky[1];
-        fa.sky[2] = k.cam.sky[2];
-        fa.code_div = FastDiv{k.fold_code_div.d, k.fold_code_div.m, k.fold_code_div.s};
-        fa.map = map;
-        fa.width = k.width;
-        fa.height = k.height;
-        fa.npix = npix;
-        fa.spp_batch = fa.spp_total = fa.s_done = S;
-        fa.first = fa.last = 1;
-        fa.mode = (int)k.mode;
-        float4 *const rgba = (float4 *)((unsigned long long)f(kSvcJobFoldRgba) | ((unsigned long long)f(kSvcJobFoldRgba + 1) << 32));
-        uint8_t *const rgb8 = (uint8_t *)((unsigned long long)f(kSvcJobFoldRgb8) | ((unsigned long long)f(kSvcJobFoldRgb8 + 1) << 32));
-        const uint32_t i = c * 64u + lane;
-        if (i < npix) {
-            uint32_t lr, col;
-            tile_pixel(i, map.width, rows, lr, col);
-            fold_pixel<true, kSvcFoldRun>(fa, fa.samples, map, rows, 0, lr, col, rgba, rgb8);
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        uint32_t fin = 0;
-        if (lane == 0) fin = __hip_atomic_fetch_add((gu32 *)(ring + 2u * jc + j), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (__builtin_amdgcn_readfirstlane(fin) + 1u == nch && lane == 0) {
-            __hip_atomic_fetch_add((gu32 *)(ring + 3u * jc + k.svc_done_cap + idx), f(1) - f(0), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_fetch_add((gu32 *)(k.svc_ctl + kSvcFoldsDone), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        return true;
-    }
-    return false;
-}
-
-// The session's fold-ring tail (lane 0; 0 when the session has no fold block)
-__device__ __forceinline__ uint32_t svc_fold_tail(kargs_t &k, uint32_t lane)
-{
-    return k.svc_fold && lane == 0 ? __hip_atomic_load((gu32 *)(k.svc_ctl + kSvcFoldTail), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                   : 0u;
-}
-
-// Every in-kernel fold of the session finished (read after the stop flag or with no render
-// wave left: the forwarder stored the fold-job count before the pair that published them)
-__device__ __forceinline__ bool svc_folds_done(kargs_t &k, uint32_t lane)
-{
-    const uint32_t v = lane == 0 ? __hip_atomic_load((gu32 *)(k.svc_ctl + kSvcFoldJobs), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                     : lane == 1 ? __hip_atomic_load((gu32 *)(k.svc_ctl + kSvcFoldsDone), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                 : 0u;
-    return __builtin_amdgcn_readlane(v, 1) >= __builtin_amdgcn_readlane(v, 0);
-}
-
-// A fold wave of the session (waves of blocks < svc_fold_blocks but the forwarder): folds
-// published jobs chunk by chunk; leaves once the stop flag is seen or no render wave is
-// left, and every in-kernel fold of the session has finished (the render waves' last
-// flushes publish the last folds before those waves leave).  Dedicated waves keep the fold
-// code out of the render loop's registers; 31 of them fold a config-2 frame's 384 MB of
-// sample words at well above a frame's rate.
-__device__ __attribute__((noinline)) void svc_fold_loop(kargs_t *kp, uint32_t lane, uint32_t *st)
-{
-    kargs_t &k = *kp;
-    for (uint32_t idle = 0;; ++idle) {
-        const uint32_t tail = __builtin_amdgcn_readfirstlane(svc_fold_tail(k, lane));
-        if (tail > __builtin_amdgcn_readfirstlane(st[4]) && svc_fold_step(k, lane, st, tail)) {
-            idle = 0;
-            continue;
-        }
-        const bool stop =
-            __hip_atomic_load((gu32 *)(k.svc_ctl + kSvcStop), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
-        const uint32_t live = __builtin_amdgcn_readfirstlane(
-            lane == 0 ? __hip_atomic_load((gu32 *)(k.svc_ctl + kSvcLive), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 1u);
-        if (stop || live == 0u) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (svc_folds_done(k, lane)) return;
-        }
-        // ~0.1 us between polls while folds arrive, ~3 us once idle for a while
-        if (idle < 256u)
-            __builtin_amdgcn_s_sleep(2);
-        else
-            __builtin_amdgcn_s_sleep(127);
-    }
-}
-
-// SVCF: the session may fold jobs in-kernel (SPT_SVC_FOLD; its own instantiation, so that
-// the default session kernel keeps round 5's register allocation)
-template <bool TREE, int LEAF, bool LDSN, uint32_t BLOCK, bool BATCH = false, bool GLANE = false, bool SVC = false,
-          bool SVCF = false>
+template <bool TREE, int LEAF, bool LDSN, uint32_t BLOCK, bool BATCH = false, bool GLANE = false, bool SVC = false>
 __device__ __forceinline__ void render_body(const RenderArgs &a)
 {
     static_assert(!SVC || (!GLANE && !BATCH && (LDSN || SPT_PRIM)),
                   "the render service runs the wave-walk kernel or the LDS lane walk");
-    static_assert(!SVCF || (SVC && !LDSN), "in-kernel folds: the wave-walk session only");
     const uint32_t lane = __lane_id();
     const uint32_t rows = SVC ? 0u : a.npix / a.map.width;  // region rows (uniform; SVC: per job)
 
@@ -769,15 +564,10 @@ __device__ __forceinline__ void render_body(const RenderArgs &a)
     __shared__ uint32_t s_rec[SVC ? (BLOCK / 64u) * kSvcRecWords : 1];
     uint32_t *const rec = s_rec + (SVC ? (threadIdx.x >> 6) * kSvcRecWords : 0u);
     if (SVC && lane < kSvcRecWords - kSvcSt) rec[kSvcSt + lane] = 0u;
-    // the session's forwarder: wave 0 of block 0 (before any claim is reserved); the other
-    // waves of the first svc_fold_blocks blocks are its fold waves (in-kernel folds).  The
+    // the session's forwarder: wave 0 of block 0 (before any claim is reserved).  The
     // LDS-tree session's forwarder first joins its block's node-table copy (its barrier)
     if (SVC && !LDSN && blockIdx.x == 0u && (threadIdx.x >> 6) == 0u) {
         svc_forward(lane);
-        return;
-    }
-    if (SVCF && kernarg_args()->svc_fold && blockIdx.x < kernarg_args()->svc_fold_blocks) {
-        svc_fold_loop(kernarg_args(), lane, rec + kSvcSt);
         return;
     }
     uint32_t q_n = 0, q_pos = 0;  // the wave's queue: rows [q_pos, q_n) hold parked paths
@@ -1037,7 +827,7 @@ __device__ __forceinline__ void render_body(const RenderArgs &a)
                 // published pair: jobs are published before the stop).  After kSvcIdleTicks
                 // without work the wave may leave through the closing handshake with the
                 // host (spt_internal.h kSvcIdleTicks), then the watchdog word tells the host.
-                svc_flush<SVCF>(acc_idx, acc_cnt, lane);
+                svc_flush(acc_idx, acc_cnt, lane);
                 acc_cnt = 0;
                 unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
                 bool leave = false;
@@ -1201,7 +991,7 @@ __device__ __forceinline__ void render_body(const RenderArgs &a)
                 const uint32_t j = __builtin_amdgcn_readlane(ps.job, (int)__builtin_ctzll(fm));
                 const unsigned long long m = __ballot(fin && ps.job == j);
                 if (j != acc_idx) {
-                    svc_flush<SVCF>(acc_idx, acc_cnt, lane);
+                    svc_flush(acc_idx, acc_cnt, lane);
                     acc_idx = j;
                     acc_cnt = 0;
                 }
@@ -1226,7 +1016,7 @@ __device__ __forceinline__ void render_body(const RenderArgs &a)
     }
 
     if (SVC) {
-        svc_flush<SVCF>(acc_idx, acc_cnt, lane);
+        svc_flush(acc_idx, acc_cnt, lane);
         // one render wave fewer (the forwarder leaves when none is left)
         kargs_t &k = *kernarg_args();
         if (lane == 0) __hip_atomic_fetch_add((gu32 *)(k.svc_ctl + kSvcLive), 0xFFFFFFFFu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1291,10 +1081,10 @@ __global__ __launch_bounds__(kRenderBlock) SPT_RENDER_ATTR void render_kernel_ba
 
 // the render service: one resident launch over a stream of published jobs (RenderArgs
 // svc_*)
-template <bool TREE, int LEAF, bool FOLD>
+template <bool TREE, int LEAF>
 __global__ __launch_bounds__(kRenderBlock) SPT_RENDER_ATTR void render_kernel_svc(RenderArgs a)
 {
-    render_body<TREE, LEAF, false, kRenderBlock, false, false, true, FOLD>(a);
+    render_body<TREE, LEAF, false, kRenderBlock, false, false, true>(a);
 }
 
 // trees of kLdsNodeRecords to kGlaneMaxNodes nodes: the lane walk reading layout 0 from
@@ -1328,7 +1118,7 @@ __global__ __launch_bounds__(kLdsBlock)
 __global__ __launch_bounds__(kLdsBlock)
     __attribute__((amdgpu_num_sgpr(SPT_LDS_NUM_SGPR), amdgpu_waves_per_eu(2 * kLdsBlock / 256))) void render_kernel_svc_lds(RenderArgs a)
 {
-    render_body<true, (int)kClusterSlots, true, kLdsBlock, false, false, true, false>(a);
+    render_body<true, (int)kClusterSlots, true, kLdsBlock, false, false, true>(a);
 }
 
 // Threads take the region's pixels in 8x8-tile order (tile_pixel), so the 64 lanes of
@@ -1568,27 +1358,15 @@ hipError_t launch_render_svc(const RenderArgs &a, uint32_t grid, hipStream_t s)
 {
     if (!svc_supported(a.scene.accel) || !a.svc_host) return hipErrorInvalidValue;
     if (svc_lds(a.scene.accel)) {
-        if (a.svc_fold) return hipErrorInvalidValue;  // no fold waves in the LDS-tree session
         hipLaunchKernelGGL(render_kernel_svc_lds, dim3(grid), dim3(kLdsBlock), 0, s, a);
         return hipGetLastError();
     }
-    // sessions that fold in-kernel (a.svc_fold) run the kernel built with the fold waves
-    if (a.scene.accel.tree) {
-        if (a.svc_fold)
-            hipLaunchKernelGGL((render_kernel_svc<true, (int)kClusterSlots, true>), dim3(grid), dim3(kRenderBlock), 0, s, a);
-        else
-            hipLaunchKernelGGL((render_kernel_svc<true, (int)kClusterSlots, false>), dim3(grid), dim3(kRenderBlock), 0, s, a);
-    } else if (a.scene.accel.leaf_slots == kFlatLeafSlots) {
-        if (a.svc_fold)
-            hipLaunchKernelGGL((render_kernel_svc<false, (int)kFlatLeafSlots, true>), dim3(grid), dim3(kRenderBlock), 0, s, a);
-        else
-            hipLaunchKernelGGL((render_kernel_svc<false, (int)kFlatLeafSlots, false>), dim3(grid), dim3(kRenderBlock), 0, s, a);
-    } else {
-        if (a.svc_fold)
-            hipLaunchKernelGGL((render_kernel_svc<false, (int)kClusterSlots, true>), dim3(grid), dim3(kRenderBlock), 0, s, a);
-        else
-            hipLaunchKernelGGL((render_kernel_svc<false, (int)kClusterSlots, false>), dim3(grid), dim3(kRenderBlock), 0, s, a);
-    }
+    if (a.scene.accel.tree)
+        hipLaunchKernelGGL((render_kernel_svc<true, (int)kClusterSlots>), dim3(grid), dim3(kRenderBlock), 0, s, a);
+    else if (a.scene.accel.leaf_slots == kFlatLeafSlots)
+        hipLaunchKernelGGL((render_kernel_svc<false, (int)kFlatLeafSlots>), dim3(grid), dim3(kRenderBlock), 0, s, a);
+    else
+        hipLaunchKernelGGL((render_kernel_svc<false, (int)kClusterSlots>), dim3(grid), dim3(kRenderBlock), 0, s, a);
     return hipGetLastError();
 }
 

@@ -116,10 +116,6 @@ int render_impl(spt_ctx *ctx, int mode, const spt::RowMap &map, float4 *d_rgba, 
 
     spt::FoldArgs fa = fold_args(ctx, w->d_samples, slot_words);
     fa.acc = w->d_acc;
-    // the service folds a single-batch job without aliasing inside its session (SvcFold)
-    const bool svc_fold = use_svc && !pg && !ar && !keep_samples && spp_batch == ctx->spp && svc_folds_in_kernel(ctx) &&
-                          !(mode == SPT_MODE_TASK && map.parts == 1u && rows != map.width);
-    const SvcFold fold_in{d_rgba, d_rgb8};
     fa.out_rgba = d_rgba;
     fa.out_rgb8 = d_rgb8;
     fa.map = map;
@@ -172,7 +168,7 @@ int render_impl(spt_ctx *ctx, int mode, const spt::RowMap &map, float4 *d_rgba, 
                 ctx->ref_recorded = true;
             }
             HIP_TRY(ctx, hipEventRecord(ev.a, s));
-            if ((rc = svc_submit(ctx, ra, mode, s, &svc_w0, &svc_idx, svc_fold ? &fold_in : nullptr))) return rc;
+            if ((rc = svc_submit(ctx, ra, mode, s, &svc_w0, &svc_idx))) return rc;
             HIP_TRY(ctx, hipEventRecord(ev.b, s));
             fa.samples = ctx->svc.d_ring + svc_w0;
         } else if (ctx->engine == SPT_ENGINE_WAVEFRONT) {
@@ -207,11 +203,6 @@ int render_impl(spt_ctx *ctx, int mode, const spt::RowMap &map, float4 *d_rgba, 
         ctx->pending_render.push_back(ev);
         ctx->launches++;
         if (keep_samples) continue;
-        if (svc_fold) {
-            // folded inside the session: the stream has waited for the fold's completion
-            if ((rc = svc_retire(ctx, s, svc_w0, (uint64_t)npix * b * slot_words, svc_idx))) return rc;
-            continue;
-        }
         fa.spp_batch = b;
         fa.first = s0 == 0;
         fa.last = s0 + b >= ctx->spp;

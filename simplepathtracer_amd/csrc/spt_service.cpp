@@ -169,17 +169,12 @@ int svc_begin(spt_ctx *ctx, int mode, const std::vector<hipEvent_t> &waits, int6
                         hipMalloc((void **)&v.d_jobs, (size_t)v.job_cap * sizeof(spt::SvcJob)) == hipSuccess &&
                         hipMalloc((void **)&v.d_job_claim, (size_t)v.job_cap * sizeof(uint32_t)) == hipSuccess &&
                         hipMalloc((void **)&v.d_done, (size_t)v.done_cap * sizeof(uint32_t)) == hipSuccess &&
-                        hipMalloc((void **)&v.d_ring, (size_t)v.ring_words * sizeof(uint32_t)) == hipSuccess &&
-                        hipMalloc((void **)&v.d_fold, (size_t)spt::svc_fold_words(v.job_cap, v.done_cap) * sizeof(uint32_t)) ==
-                            hipSuccess;
+                        hipMalloc((void **)&v.d_ring, (size_t)v.ring_words * sizeof(uint32_t)) == hipSuccess;
         if (!ok) return fail(ctx, SPT_ERR_NOMEM, "render service buffers (%llu MiB ring) allocation failed",
                              (unsigned long long)(v.ring_bytes >> 20));
         HIP_TRY(ctx, hipMemsetAsync(v.d_done, 0, (size_t)v.done_cap * sizeof(uint32_t), v.stream));
-        // the folded totals (the block's last done_cap words), like the completion counters
-        HIP_TRY(ctx, hipMemsetAsync(v.d_fold + 3u * v.job_cap + v.done_cap, 0, (size_t)v.done_cap * sizeof(uint32_t), v.stream));
     }
     const uint32_t grid = svc_session_grid(ctx);
-    v.fold_session = svc_folds_in_kernel(ctx);
     spt::RenderArgs ra{};
     ra.scene = device_scene(ctx);
     ra.prim = ctx->prim;
@@ -201,13 +196,6 @@ int svc_begin(spt_ctx *ctx, int mode, const std::vector<hipEvent_t> &waits, int6
     ra.svc_host = v.d_host;
     ra.svc_host_jobs = v.dh_jobs;
     ra.svc_host_job_claim = v.dh_job_claim;
-    if (v.fold_session) {
-        ra.svc_fold = v.d_fold;
-        ra.svc_job_cap = v.job_cap;
-        ra.svc_done_cap = v.done_cap;
-        ra.fold_code_div = spt::make_fastdiv(ctx->code_stride);
-        ra.svc_fold_blocks = v.fold_blocks;
-    }
     if (env_var("SPT_SVC_TRACE")) {
         const size_t n = (size_t)v.done_cap * 4 + spt::kSvcTraceClaims;
         if (!v.d_trace) HIP_TRY(ctx, hipMalloc((void **)&v.d_trace, n * sizeof(unsigned long long)));
@@ -224,21 +212,16 @@ int svc_begin(spt_ctx *ctx, int mode, const std::vector<hipEvent_t> &waits, int6
     __atomic_store_n(v.h_host + spt::kSvcHostStop, 0u, __ATOMIC_SEQ_CST);
     __atomic_store_n(v.h_host + spt::kSvcHostWatchdog, 0u, __ATOMIC_SEQ_CST);
     for (hipEvent_t e : waits) HIP_TRY(ctx, hipStreamWaitEvent(v.stream, e, 0));
-    // control words zeroed, the render-wave count set (every wave but the forwarder and the
-    // fold waves), before the kernel; the fold ring and its chunk counters zeroed
+    // control words zeroed, the render-wave count set (every wave but the forwarder), before
+    // the kernel
     HIP_TRY(ctx, hipMemsetAsync(v.d_ctl, 0, spt::kSvcCtlWords * sizeof(uint32_t), v.stream));
     const uint32_t bw = spt::svc_block(ctx->accel) / 64u;  // waves per block of the session kernel
-    const uint32_t waves = grid * bw;
-    const uint32_t render_waves = v.fold_session ? waves - v.fold_blocks * bw : waves - 1u;
+    const uint32_t render_waves = grid * bw - 1u;
     HIP_TRY(ctx, hipMemsetD32Async((hipDeviceptr_t)(v.d_ctl + spt::kSvcLive), (int)render_waves, 1, v.stream));
-    if (v.fold_session)
-        HIP_TRY(ctx, hipMemsetAsync(v.d_fold, 0, (size_t)(3u * v.job_cap + v.done_cap) * sizeof(uint32_t), v.stream));
     if (reset_idx >= 0) {
         // a completion counter whose running total restarts: zeroed after the folds that
-        // waited on it (waits), and the caller's stream ordered after the zeroing (its
-        // folded total with it)
+        // waited on it (waits), and the caller's stream ordered after the zeroing
         HIP_TRY(ctx, hipMemsetAsync(v.d_done + reset_idx, 0, sizeof(uint32_t), v.stream));
-        HIP_TRY(ctx, hipMemsetAsync(v.d_fold + 3u * v.job_cap + v.done_cap + reset_idx, 0, sizeof(uint32_t), v.stream));
         HIP_TRY(ctx, hipEventRecord(v.ev_ctl, v.stream));
         HIP_TRY(ctx, hipStreamWaitEvent(s, v.ev_ctl, 0));
     }
@@ -253,14 +236,6 @@ int svc_begin(spt_ctx *ctx, int mode, const std::vector<hipEvent_t> &waits, int6
     v.sessions++;
     SVC_DBG(ctx, "begin session %llu, grid %u, %zu waits", (unsigned long long)v.sessions, grid, waits.size());
     return SPT_OK;
-}
-
-// Does the service fold single-job publications inside the session (fold waves)?  It
-// needs the fold waves' blocks and at least one block of render waves.
-bool svc_folds_in_kernel(const spt_ctx *ctx)
-{
-    const Service &v = ctx->svc;
-    return v.fold_inkernel && !spt::svc_lds(ctx->accel) && svc_session_grid(ctx) > 2u * v.fold_blocks;
 }
 
 // Blocks of a session over the context's scene: the wave-walk kernel's svc_grid, or the
@@ -285,7 +260,7 @@ bool svc_eligible(const spt_ctx *ctx, uint64_t words, bool keep_samples)
 // and make stream s wait for all their samples.  Out: the ring word of the publication's
 // first slot and its counter (svc_retire after the folds).
 int svc_submit_jobs(spt_ctx *ctx, int mode, const SvcJobSpec *jobs, size_t n, uint64_t total_slots, hipStream_t s,
-                    uint64_t *w0_out, uint32_t *idx_out, const SvcFold *fold)
+                    uint64_t *w0_out, uint32_t *idx_out)
 {
     Service &v = ctx->svc;
     const uint32_t slot_words = mode == SPT_MODE_SEGMENT ? 1u : 2u;
@@ -303,10 +278,8 @@ int svc_submit_jobs(spt_ctx *ctx, int mode, const SvcJobSpec *jobs, size_t n, ui
     const uint64_t w0 = v.ring_head + words > v.ring_words ? 0 : v.ring_head, w1 = w0 + words;
     const uint32_t idx = v.next_done;
     if (v.done_cum.empty()) v.done_cum.assign(v.done_cap, 0);  // counters zeroed with their allocation
-    if (v.folded_cum.empty()) v.folded_cum.assign(v.done_cap, 0);
     uint64_t target = v.done_cum[idx] + items;
-    uint64_t ftarget = v.folded_cum[idx] + (fold ? items : 0u);
-    const bool reset = target > 0xFFFFFFFFull || ftarget > 0xFFFFFFFFull;
+    const bool reset = target > 0xFFFFFFFFull;
     // Flow control: earlier jobs whose folds still read these ring words or still wait on
     // this counter (or the oldest, with 1024 jobs in flight) must be folded first.  Folds
     // found finished are retired; an unfinished one is never waited for inside the running
@@ -352,17 +325,11 @@ int svc_submit_jobs(spt_ctx *ctx, int mode, const SvcJobSpec *jobs, size_t n, ui
         if (rc) return rc;
         __atomic_store_n(v.h_host + spt::kSvcHostCommitted, (uint32_t)n, __ATOMIC_SEQ_CST);
     }
-    if (fold && !v.fold_session)
-        return fail(ctx, SPT_ERR_STATE, "render service: an in-kernel fold for a session without fold waves");
     v.ring_head = w1;
     v.session_items += items;
     v.next_done = (v.next_done + 1u) % v.done_cap;
-    if (reset) {
-        target = items;
-        ftarget = fold ? items : 0u;
-    }
+    if (reset) target = items;
     v.done_cum[idx] = target;
-    v.folded_cum[idx] = ftarget;
     // SPT_SVC_TEST_PUB_DELAY_US (fault injection): committed, not yet published
     if (v.pub_delay_us) std::this_thread::sleep_for(std::chrono::microseconds(v.pub_delay_us));
     // the records and first claims (host tables, the forwarder copies them), then the pair
@@ -384,13 +351,6 @@ int svc_submit_jobs(spt_ctx *ctx, int mode, const SvcJobSpec *jobs, size_t n, ui
         j.div_tile = js.div_tile;
         j.div_strip = js.div_strip;
         j.claim_first = (uint32_t)v.claims;
-        if (fold && n == 1) {
-            v.inkernel_folds++;
-            j.fold_flags = spt::kSvcFoldInKernel;
-            j.fold_target = (uint32_t)target;
-            j.fold_rgba = (uint64_t)(uintptr_t)fold->rgba;
-            j.fold_rgb8 = (uint64_t)(uintptr_t)fold->rgb8;
-        }
         std::memcpy(&v.h_jobs[v.n_jobs], &j, sizeof j);
         v.h_job_claim[v.n_jobs] = j.claim_first;
         v.claims += nc;
@@ -400,12 +360,8 @@ int svc_submit_jobs(spt_ctx *ctx, int mode, const SvcJobSpec *jobs, size_t n, ui
     // x86 keeps stores in order: the device sees the pair only after the records it covers
     __atomic_store_n((uint64_t *)(v.h_host + spt::kSvcHostPub), (uint64_t)(uint32_t)v.claims | ((uint64_t)v.n_jobs << 32),
                      __ATOMIC_RELEASE);
-    // the caller's stream waits for the job's samples -- or, folded in the session, for its fold
-    if (fold && n == 1)
-        HIP_TRY(ctx, hipStreamWaitValue32(s, v.d_fold + 3u * v.job_cap + v.done_cap + idx, (uint32_t)ftarget,
-                                          hipStreamWaitValueGte, 0xFFFFFFFFu));
-    else
-        HIP_TRY(ctx, hipStreamWaitValue32(s, v.d_done + idx, (uint32_t)target, hipStreamWaitValueGte, 0xFFFFFFFFu));
+    // the caller's stream waits for the job's samples
+    HIP_TRY(ctx, hipStreamWaitValue32(s, v.d_done + idx, (uint32_t)target, hipStreamWaitValueGte, 0xFFFFFFFFu));
     SVC_DBG(ctx, "submitted, %u jobs in session", v.n_jobs);
     *w0_out = w0;
     *idx_out = idx;
@@ -413,11 +369,10 @@ int svc_submit_jobs(spt_ctx *ctx, int mode, const SvcJobSpec *jobs, size_t n, ui
 }
 
 // One render_impl launch (`ra`: map, npix, spp_batch, s0, divisors) as one job.
-int svc_submit(spt_ctx *ctx, const spt::RenderArgs &ra, int mode, hipStream_t s, uint64_t *w0_out, uint32_t *idx_out,
-               const SvcFold *fold)
+int svc_submit(spt_ctx *ctx, const spt::RenderArgs &ra, int mode, hipStream_t s, uint64_t *w0_out, uint32_t *idx_out)
 {
     SvcJobSpec js{ra.map, ra.npix / ra.map.width, ra.spp_batch, ra.s0, ra.div_band, ra.div_tile, ra.div_strip, 0};
-    return svc_submit_jobs(ctx, mode, &js, 1, (uint64_t)ra.n_items, s, w0_out, idx_out, fold);
+    return svc_submit_jobs(ctx, mode, &js, 1, (uint64_t)ra.n_items, s, w0_out, idx_out);
 }
 
 // After the job's fold was enqueued on s: its ring words and counter are free once the

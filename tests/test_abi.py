@@ -12,7 +12,7 @@ def test_library_exports_every_declared_symbol(native):
     L = native.lib()
     missing = [n for n in names if not hasattr(L, n)]
     assert not missing, missing
-    assert L.spt_abi_version() == native.ABI_VERSION == 10
+    assert L.spt_abi_version() == native.ABI_VERSION == 11
 
 
 def test_ctx_create_reports_no_device_without_gpu(native):

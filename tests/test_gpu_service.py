@@ -68,17 +68,14 @@ def render_frames(ctx, jobs, W, H, mode, streams, service):
     return [(a.cpu().numpy(), b.cpu().numpy()) for a, b in outs]
 
 
-@pytest.mark.parametrize("fold", [1, 0])
 @pytest.mark.parametrize("full", [0, 1])
 @pytest.mark.parametrize("mode", [0, 1])
-def test_service_frames_equal_launched_frames(spt, golden_scenes, monkeypatch, mode, full, fold):
+def test_service_frames_equal_launched_frames(spt, golden_scenes, monkeypatch, mode, full):
     """K consecutive frames through the queue, each compared with a one-shot render; also
-    with the session on every block slot (SPT_SVC_FULL_GRID, bench.py's N > 1 regions);
-    folded inside the session by its fold waves (default) or by fold launches on the
-    caller's streams (SPT_SVC_FOLD=0: with the full grid those run after the session ends)."""
+    with the session on every block slot (SPT_SVC_FULL_GRID, bench.py's N > 1 regions),
+    whose fold launches on the caller's streams then run after the session ends."""
     import torch
     monkeypatch.setenv("SPT_SVC_FULL_GRID", str(full))
-    monkeypatch.setenv("SPT_SVC_FOLD", str(fold))
     W, H = 320, 200
     ctx = make_ctx(spt, golden_scenes, W, H, 16, 50, seed=3)
     streams = [torch.cuda.Stream(), torch.cuda.Stream()]
@@ -94,9 +91,6 @@ def test_service_frames_equal_launched_frames(spt, golden_scenes, monkeypatch, m
     assert st["svc_jobs"] == len(jobs) and st["svc_sessions"] >= 1 and st["svc_running"] == 0
     assert st["samples"] == len(jobs) * W * H * 16
     assert st["launches"] == len(jobs)
-    # task mode on this non-square frame aliases pixels (RenderSegmentTask's colorIndex):
-    # those jobs keep the fold launch
-    assert st["svc_inkernel_folds"] == (len(jobs) if fold and mode == 0 else 0)
 
 
 @pytest.mark.parametrize("full", [0, 1])
@@ -133,14 +127,10 @@ def test_service_lds_tree_sessions_equal_launched_frames(spt, monkeypatch, mode,
     assert st["svc_grid_blocks"] == (2 if full else 1) * n_cu
 
 
-@pytest.mark.parametrize("fold", [1, 0])
-def test_service_rank_shares_and_regions(spt, golden_scenes, monkeypatch, fold):
+def test_service_rank_shares_and_regions(spt, golden_scenes):
     """Interleaved strips (the bench's rank shares), odd rectangles and tiny regions, many
-    jobs in flight at once (more than 64 of them: the job search's second step); folded in
-    the session (its fold waves take 64-pixel chunks: ragged tiles, 1-pixel jobs) or by
-    fold launches."""
+    jobs in flight at once (more than 64 of them: the job search's second step)."""
     import torch
-    monkeypatch.setenv("SPT_SVC_FOLD", str(fold))
     W, H = 240, 160
     ctx = make_ctx(spt, golden_scenes, W, H, 8, 50, seed=7)
     streams = [torch.cuda.Stream(), torch.cuda.Stream(), torch.cuda.Stream()]
@@ -158,7 +148,6 @@ def test_service_rank_shares_and_regions(spt, golden_scenes, monkeypatch, fold):
         assert not len(bad), (f"job {k} {jobs[k]} g_data: {len(bad)} bytes differ, rows "
                               f"{sorted(set((H - 1 - bad // (3 * W)).tolist()))[:12]}, got {b[bad[:8]]} want {rb[bad[:8]]}")
     assert st["svc_watchdog_exits"] == 0
-    assert st["svc_inkernel_folds"] == (len(jobs) if fold else 0)
 
 
 @pytest.mark.parametrize("mode", [0, 1])

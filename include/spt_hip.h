@@ -186,7 +186,10 @@ SPT_API int spt_set_cluster_tree(spt_ctx *ctx, uint32_t branching);
 /* The drop-in's warm-up (the C++ shim calls it once, right after creating its
  * context): creates the streams of the second batch set and of the tiling read-ahead
  * now, so that the first frame does not pay for them (a HIP stream costs ~9.5 ms to
- * create on MI355X and stalls the device's other queues meanwhile), and lets the tiling
+ * create on MI355X and stalls the device's other queues meanwhile), runs one small
+ * device-to-host 2D copy and one host-to-device upload (the process's first of each waits
+ * ~8.5 ms for the runtime's copy setup: the first frame's tile copies, the setup's list
+ * upload), and lets the tiling
  * read-ahead arm at a tiling's first call (RenderImageParallelMain's first tile to arrive)
  * rather than after one whole tiling, so that the reference app's one frame per process
  * (Renderer.hpp:335-344) is rendered whole at its first tile (SPT_READAHEAD_FIRST=0: not).

@@ -20,6 +20,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <memory>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -75,30 +76,40 @@ int main(int argc, char **argv)
     // RenderJob (242-255: it takes a free slot when it starts and returns it when its tile
     // is done, then notifies) is spawned and detached, and the main thread waits for a free
     // slot before the next; at the end it waits until all tc slots are free.  Two changes
-    // keep the harness itself defined: the count, condition variable and mutex outlive the
-    // frame (the reference's are locals while detached threads may still notify them),
-    // and the slot is returned under the mutex (the reference's unlocked fetch_add +
-    // notify can be lost and leave the final wait asleep).  `alive` lets main return only
-    // after every detached thread has finished touching them.
+    // keep the harness itself defined: the count, condition variable and mutex of a frame
+    // outlive it (the reference's are locals while detached threads may still notify them:
+    // here each frame's live in a block its threads share), and the slot is returned under
+    // the mutex (the reference's unlocked fetch_add + notify can be lost and leave the final
+    // wait asleep).  As in the reference, a thread takes its slot only when it starts, so the
+    // final wait can end while a spawned thread has not started yet: that thread then works
+    // on its own frame's count (one count shared by all frames and reset per frame drifted
+    // when such a thread straddled the reset, and a later frame's final wait never ended).
+    // `alive` lets main return only after every detached thread has finished.
     // SPT_HARNESS_COLD=2 also prints every tile's RenderJob span (ms from the frame's start)
+    struct FrameSync {
+        std::atomic<int> free_threads{0};
+        std::condition_variable cv;
+        std::mutex mu;
+    };
     static std::vector<std::pair<double, double>> spans((size_t)tc * tc);
     static std::chrono::steady_clock::time_point frame_t0;
-    static std::atomic<int> free_threads, alive{0};
-    static std::condition_variable cv;
-    static std::mutex mu;
+    static std::atomic<int> alive{0};
+    static std::mutex spans_mu;
     auto frame_once = [&]() {
         const uint32_t sw = g_width / tc, sh = g_height / tc;
-        free_threads = (int)tc;
+        auto fs = std::make_shared<FrameSync>();
+        fs->free_threads = (int)tc;
         frame_t0 = std::chrono::steady_clock::now();
-        std::unique_lock<std::mutex> lk(mu);
+        std::unique_lock<std::mutex> lk(fs->mu);
         for (uint32_t j = 0; j < tc; ++j)
             for (uint32_t i = 0; i < tc; ++i) {
                 RenderSegmentData seg{sh * j, sh * j + sh > g_height ? g_height : sh * j + sh, sw * i,
                                       sw * i + sw > g_width ? g_width : sw * i + sw};
                 alive.fetch_add(1);
                 const size_t k = (size_t)j * tc + i;
-                std::thread thread([seg, task, noop, k] {
-                    free_threads.fetch_sub(1);
+                const auto t_frame = frame_t0;
+                std::thread thread([seg, task, noop, k, fs, t_frame] {
+                    fs->free_threads.fetch_sub(1);
                     const auto ts = std::chrono::steady_clock::now();
                     if (noop) {
                     } else if (task) {
@@ -107,19 +118,22 @@ int main(int argc, char **argv)
                         RenderSegment(seg);
                     }
                     {
-                        std::lock_guard<std::mutex> g(mu);
+                        std::lock_guard<std::mutex> g(fs->mu);
                         const auto te = std::chrono::steady_clock::now();
-                        spans[k] = {std::chrono::duration<double, std::milli>(ts - frame_t0).count(),
-                                    std::chrono::duration<double, std::milli>(te - frame_t0).count()};
-                        free_threads.fetch_add(1);
+                        {
+                            std::lock_guard<std::mutex> gs(spans_mu);
+                            spans[k] = {std::chrono::duration<double, std::milli>(ts - t_frame).count(),
+                                        std::chrono::duration<double, std::milli>(te - t_frame).count()};
+                        }
+                        fs->free_threads.fetch_add(1);
                     }
-                    cv.notify_one();
+                    fs->cv.notify_one();
                     alive.fetch_sub(1);
                 });
                 thread.detach();
-                cv.wait(lk, [] { return free_threads.load() > 0; });
+                fs->cv.wait(lk, [&] { return fs->free_threads.load() > 0; });
             }
-        cv.wait(lk, [&] { return free_threads.load() == (int)tc; });
+        fs->cv.wait(lk, [&] { return fs->free_threads.load() == (int)tc; });
     };
     const bool cold = std::getenv("SPT_HARNESS_COLD") && std::atoi(std::getenv("SPT_HARNESS_COLD")) != 0;
     if (cold && !noop) {

@@ -390,6 +390,16 @@ int spec_launch(spt_ctx *ctx, std::unique_lock<std::mutex> &lk, int mode, uint32
     if (rc) return rc;
     const uint32_t W = ctx->W, H = ctx->H, sw = W / tc, sh = H / tc;
     if ((rc = ensure(ctx, &sp.d8, &sp.d8_cap, (size_t)W * H * 3))) return rc;
+    // the frame being replaced: its unserved tiles are owed to late callers (at most 4 per
+    // tile, so a caller that never asks for a tile does not accumulate them)
+    const size_t ntiles = (size_t)tc * tc;
+    if (sp.active && sp.mode == mode && sp.tc == tc && sp.gen == ctx->gen && sp.owed.size() == ntiles &&
+        sp.served.size() == ntiles) {
+        for (size_t k = 0; k < ntiles; ++k)
+            if (!sp.served[k] && sp.owed[k] < 4) sp.owed[k]++;
+    } else {
+        sp.owed.assign(ntiles, 0);
+    }
     std::vector<BatchReq> reqs((size_t)tc * tc);
     for (uint32_t j = 0; j < tc; ++j)
         for (uint32_t i = 0; i < tc; ++i)
@@ -434,7 +444,13 @@ int spec_serve(spt_ctx *ctx, std::unique_lock<std::mutex> &lk, int mode, uint32_
         const uint32_t i = xB / sp.sw, j = yB / sp.sh;
         if (i >= sp.tc || j >= sp.tc) return -1;
         const size_t k = (size_t)j * sp.tc + i;
-        return sp.served[k] ? -1 : (int64_t)k;
+        if (!sp.served[k]) return (int64_t)k;
+        if (k < sp.owed.size() && sp.owed[k] > 0) {
+            // a call an earlier frame still owed (late RenderJob thread): same bytes
+            --sp.owed[k];
+            return (int64_t)k;
+        }
+        return -1;
     };
     int64_t k = tile_of();
     if (k < 0) {

@@ -108,6 +108,11 @@ struct SpecFrame {
     uint32_t tc = 0, sw = 0, sh = 0;
     uint64_t gen = 0;            // spt_ctx::gen when launched
     std::vector<uint8_t> served; // per tile (row-major over tile rows j, columns i)
+    // per tile, calls still owed by an earlier frame of this tiling: tiles that frame had
+    // not served when the next one began -- a RenderJob thread that starts only after its
+    // frame's final wait ended (Renderer.hpp:242-255, 282-292) -- served from the current
+    // frame (same state, the same bytes) instead of starting another one
+    std::vector<uint8_t> owed;
     static constexpr int kParts = 4;
     uint32_t parts = 4, rows_per_part = 1;  // tile rows per launch
     hipEvent_t ev[kParts] = {};

@@ -340,6 +340,24 @@ int spec_stream(spt_ctx *ctx, int p)
     return SPT_OK;
 }
 
+// The read-ahead frame's page-locked bytes (SpecFrame::h8), at least `bytes` of them.
+int spec_frame_bytes(spt_ctx *ctx, size_t bytes)
+{
+    SpecFrame &sp = ctx->spec;
+    if (sp.h8_cap >= bytes) return SPT_OK;
+    // hipHostFree synchronises the device, which a resident service session would hold
+    if (int rc = svc_end(ctx)) return rc;
+    if (sp.h8) HIP_TRY(ctx, hipHostFree(sp.h8));
+    sp.h8 = sp.h8_dev = nullptr;
+    sp.h8_cap = 0;
+    HIP_TRY(ctx, hipHostMalloc((void **)&sp.h8, bytes));
+    void *dp = nullptr;
+    HIP_TRY(ctx, hipHostGetDevicePointer(&dp, sp.h8, 0));
+    sp.h8_dev = (uint8_t *)dp;
+    sp.h8_cap = bytes;
+    return SPT_OK;
+}
+
 // The buffers the read-ahead of a tc x tc tiling will use (its parts' streams, rectangle
 // tables and sample-word workspaces, the frame's device bytes), allocated when the tiling
 // arms: allocated by the first read-ahead itself, each part's first allocations held its
@@ -354,8 +372,8 @@ int spec_prepare(spt_ctx *ctx, std::unique_lock<std::mutex> &lk, int mode, uint3
     host_trace("spec_prepare begin");
     (void)mode;
     const uint32_t W = ctx->W, H = ctx->H;
-    int rc = ensure(ctx, &sp.d8, &sp.d8_cap, (size_t)W * H * 3);
-    host_trace("spec_prepare d8");
+    int rc = spec_frame_bytes(ctx, (size_t)W * H * 3);
+    host_trace("spec_prepare frame bytes");
     if (rc) return rc;
     const uint32_t np = std::min(sp.parts, tc), rpp = (tc + np - 1) / np;
     // the parts' streams and sample workspaces come with the first read-ahead (spec_launch):
@@ -389,7 +407,7 @@ int spec_launch(spt_ctx *ctx, std::unique_lock<std::mutex> &lk, int mode, uint32
     int rc = spec_drain(ctx);
     if (rc) return rc;
     const uint32_t W = ctx->W, H = ctx->H, sw = W / tc, sh = H / tc;
-    if ((rc = ensure(ctx, &sp.d8, &sp.d8_cap, (size_t)W * H * 3))) return rc;
+    if ((rc = spec_frame_bytes(ctx, (size_t)W * H * 3))) return rc;
     // the frame being replaced: its unserved tiles are owed to late callers (at most 4 per
     // tile, so a caller that never asks for a tile does not accumulate them)
     const size_t ntiles = (size_t)tc * tc;
@@ -404,7 +422,7 @@ int spec_launch(spt_ctx *ctx, std::unique_lock<std::mutex> &lk, int mode, uint32
     for (uint32_t j = 0; j < tc; ++j)
         for (uint32_t i = 0; i < tc; ++i)
             reqs[(size_t)j * tc + i] = BatchReq{mode,    sh * j,    std::min(sh * j + sh, H), sw * i, std::min(sw * i + sw, W),
-                                                nullptr, sp.d8,    SPT_OK,                   true,   false};
+                                                nullptr, sp.h8,    SPT_OK,                   true,   false};
     const uint32_t np = std::min(sp.parts, tc), rpp = (tc + np - 1) / np;  // launches, tile rows each
     sp.rows_per_part = rpp;
     for (uint32_t p = 0; p * rpp < tc; ++p) {
@@ -413,7 +431,7 @@ int spec_launch(spt_ctx *ctx, std::unique_lock<std::mutex> &lk, int mode, uint32
             for (uint32_t i = 0; i < tc; ++i) part.push_back(&reqs[(size_t)j * tc + i]);
         BatchSet *bs = &sp.bs[p];
         if ((rc = spec_stream(ctx, (int)p))) return rc;
-        if ((rc = launch_batch(ctx, bs, part, sp.d8))) return rc;
+        if ((rc = launch_batch(ctx, bs, part, sp.h8_dev))) return rc;
         HIP_TRY(ctx, hipEventRecord(sp.ev[p], bs->stream));
         sp.launched[p] = true;
         ctx->batches++;
@@ -501,14 +519,16 @@ int spec_serve(spt_ctx *ctx, std::unique_lock<std::mutex> &lk, int mode, uint32_
     sp.served[(size_t)k] = 1;
     const uint32_t part = (uint32_t)k / sp.tc / sp.rows_per_part;
     const hipEvent_t ev = sp.ev[part];
-    uint8_t *const src = sp.d8;
+    const uint8_t *const src = sp.h8;
     sp.readers++;
     lk.unlock();
-    // rows y in [yB, yE) live at g_data rows H-1-y: one band, xB.. per row
+    // rows y in [yB, yE) live at g_data rows H-1-y: one band, xB.. per row; the part's fold
+    // wrote them into the page-locked frame (its event completes after the kernel's writes)
     const size_t pitch = (size_t)W * 3, off = (size_t)(H - yE) * pitch + (size_t)xB * 3;
-    hipError_t e = hipEventSynchronize(ev);
+    const hipError_t e = hipEventSynchronize(ev);
     if (e == hipSuccess)
-        e = hipMemcpy2D(g_data + off, pitch, src + off, pitch, (size_t)(xE - xB) * 3, yE - yB, hipMemcpyDeviceToHost);
+        for (uint32_t r = 0; r < yE - yB; ++r)
+            std::memcpy(g_data + off + r * pitch, src + off + r * pitch, (size_t)(xE - xB) * 3);
     lk.lock();
     if (--sp.readers == 0) sp.readers_cv.notify_all();
     if (e != hipSuccess) return fail(ctx, SPT_ERR_HIP, "read-ahead tile copy failed: %s", hipGetErrorString(e));

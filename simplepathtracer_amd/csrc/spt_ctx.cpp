@@ -569,6 +569,10 @@ int spt_set_params_one(spt_ctx *ctx, uint32_t width, uint32_t height, uint32_t s
     ctx->seed = seed;
     ctx->params_set = true;
     HIP_TRY(ctx, hipSetDevice(ctx->device));
+    // the drop-in (spt_prepare_dropin) renders its first frame through the tiling read-ahead:
+    // its page-locked frame now, with the setup, not in that frame
+    if (ctx->spec.arm_first && ctx->readahead)
+        if (int rc = spec_frame_bytes(ctx, (size_t)width * height * 3)) return rc;
     return rebuild_prim(ctx);
 }
 
@@ -879,7 +883,7 @@ void spt_ctx_destroy(spt_ctx *ctx)
     }
     for (hipEvent_t e : ctx->spec.ev)
         if (e) (void)hipEventDestroy(e);
-    if (ctx->spec.d8) (void)hipFree(ctx->spec.d8);
+    if (ctx->spec.h8) (void)hipHostFree(ctx->spec.h8);
     for (BatchSet &b : ctx->bsets) {
         if (b.d_rects) (void)hipFree(b.d_rects);
         if (b.h_rects) (void)hipHostFree(b.h_rects);

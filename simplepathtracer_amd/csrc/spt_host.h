@@ -118,10 +118,13 @@ struct SpecFrame {
     hipEvent_t ev[kParts] = {};
     bool launched[kParts] = {};
     BatchSet bs[kParts];
-    uint8_t *d8 = nullptr;  // the frame's RGB8 bytes (g_data layout), device
-    size_t d8_cap = 0;
-    // serves copying out of d8 with the context unlocked: the next read-ahead neither
-    // rewrites nor reallocates d8 before they are done (readers_cv, ctx->mu)
+    // the frame's RGB8 bytes (g_data layout) in page-locked host memory: the parts' folds
+    // write them through its device view, each serve copies its tile's rows on the host
+    // (a hipMemcpy2D per tile cost ~10 us of runtime time each: 1 024 per frame at tc = 32)
+    uint8_t *h8 = nullptr, *h8_dev = nullptr;
+    size_t h8_cap = 0;
+    // serves copying out of h8 with the context unlocked: the next read-ahead neither
+    // rewrites nor reallocates h8 before they are done (readers_cv, ctx->mu)
     uint32_t readers = 0;
     std::condition_variable readers_cv;
     // arming: the tiles of one tiling (mode, tc, frame size) called so far by plain calls
@@ -478,6 +481,7 @@ int render_impl(spt_ctx *ctx, int mode, const spt::RowMap &map, float4 *d_rgba, 
 int render_task_range(spt_ctx *ctx, uint32_t i0, uint32_t i1, float4 *d_out, hipStream_t s);
 spt::FoldArgs fold_args(const spt_ctx *ctx, const uint32_t *samples, uint32_t slot_words);
 int spec_serve(spt_ctx *ctx, std::unique_lock<std::mutex> &lk, int mode, uint32_t yB, uint32_t yE, uint32_t xB, uint32_t xE, uint8_t *g_data);
+int spec_frame_bytes(spt_ctx *ctx, size_t bytes);
 int spec_launch(spt_ctx *ctx, std::unique_lock<std::mutex> &lk, int mode, uint32_t tc);
 int spec_prepare(spt_ctx *ctx, std::unique_lock<std::mutex> &lk, int mode, uint32_t tc);
 int spec_stream(spt_ctx *ctx, int p);

@@ -54,7 +54,8 @@ void warm_start(spt_ctx *ctx)
     }
     // the process's first device-to-host hipMemcpy2D waits ~8.6 ms for the runtime's copy
     // setup (round 6 API trace of the cold frame, gpurun r06bo: its first four tile copies
-    // out of the read-ahead frame took 8.6 ms each, the later ones 0.1-0.3 ms), and so does
+    // out of the read-ahead frame took 8.6 ms each, the later ones 0.1-0.3 ms; the read-ahead
+    // now serves from page-locked memory, batches copy back unpinned g_data so), and so does
     // its first host-to-device copy on a copy engine (the primary lists' upload, 8.5 ms for
     // 120 KB; the smaller scene tables go through blit kernels): one small 2D copy into
     // page-locked (registered and allocated) memory and one 256 KiB upload now

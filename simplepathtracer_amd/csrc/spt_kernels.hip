@@ -1123,7 +1123,11 @@ __global__ __launch_bounds__(kLdsBlock)
 
 // Threads take the region's pixels in 8x8-tile order (tile_pixel), so the 64 lanes of
 // a wave read 64 consecutive slots per sample.
-__global__ __launch_bounds__(256) void fold_kernel(FoldArgs a)
+// threads per fold block (its blocks run beside the next frame's render)
+#ifndef SPT_FOLD_BLOCK
+#define SPT_FOLD_BLOCK 256
+#endif
+__global__ __launch_bounds__(SPT_FOLD_BLOCK) void fold_kernel(FoldArgs a)
 {
     // a launched render's fold runs beside the next frame's persistent render launch, whose
     // waves are older and win the SIMDs' issue arbitration: at the default priority the
@@ -1379,7 +1383,7 @@ hipError_t launch_fold(const FoldArgs &a, hipStream_t s)
     else if (a.rects)
         hipLaunchKernelGGL(fold_kernel_batch, dim3((a.npix + 255) / 256), dim3(256), 0, s, a);
     else
-        hipLaunchKernelGGL(fold_kernel, dim3((a.npix + 255) / 256), dim3(256), 0, s, a);
+        hipLaunchKernelGGL(fold_kernel, dim3((a.npix + SPT_FOLD_BLOCK - 1) / SPT_FOLD_BLOCK), dim3(SPT_FOLD_BLOCK), 0, s, a);
     return hipGetLastError();
 }
 

@@ -1123,6 +1123,10 @@ __global__ __launch_bounds__(kLdsBlock)
 
 // Threads take the region's pixels in 8x8-tile order (tile_pixel), so the 64 lanes of
 // a wave read 64 consecutive slots per sample.
+// the launched fold's wave priority (s_setprio) when FoldArgs::prio is set
+#ifndef SPT_FOLD_PRIO
+#define SPT_FOLD_PRIO 3
+#endif
 // threads per fold block (its blocks run beside the next frame's render)
 #ifndef SPT_FOLD_BLOCK
 #define SPT_FOLD_BLOCK 256
@@ -1135,7 +1139,7 @@ __global__ __launch_bounds__(SPT_FOLD_BLOCK) void fold_kernel(FoldArgs a)
     // at priority 3 the fold takes 0.6 ms and the bench gains 0.8%.  Beside
     // the render service nothing waits to start after a fold, and the raised priority only
     // took issue cycles from the service's waves (-1.5%): FoldArgs::prio is 0 there.
-    if (a.prio) __builtin_amdgcn_s_setprio(3);
+    if (a.prio) __builtin_amdgcn_s_setprio(SPT_FOLD_PRIO);
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= a.npix) return;
     const uint32_t rows = a.npix / a.map.width;

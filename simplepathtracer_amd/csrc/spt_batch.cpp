@@ -404,15 +404,17 @@ int spec_launch(spt_ctx *ctx, std::unique_lock<std::mutex> &lk, int mode, uint32
 {
     SpecFrame &sp = ctx->spec;
     sp.readers_cv.wait(lk, [&] { return sp.readers == 0; });
+    // the frame being replaced (before spec_drain retires it): its unserved tiles are owed to
+    // late callers (at most 4 per tile, so a caller that never asks for a tile does not
+    // accumulate them)
+    const size_t ntiles = (size_t)tc * tc;
+    const bool replaces = sp.active && sp.mode == mode && sp.tc == tc && sp.gen == ctx->gen &&
+                          sp.owed.size() == ntiles && sp.served.size() == ntiles;
     int rc = spec_drain(ctx);
     if (rc) return rc;
     const uint32_t W = ctx->W, H = ctx->H, sw = W / tc, sh = H / tc;
     if ((rc = spec_frame_bytes(ctx, (size_t)W * H * 3))) return rc;
-    // the frame being replaced: its unserved tiles are owed to late callers (at most 4 per
-    // tile, so a caller that never asks for a tile does not accumulate them)
-    const size_t ntiles = (size_t)tc * tc;
-    if (sp.active && sp.mode == mode && sp.tc == tc && sp.gen == ctx->gen && sp.owed.size() == ntiles &&
-        sp.served.size() == ntiles) {
+    if (replaces) {
         for (size_t k = 0; k < ntiles; ++k)
             if (!sp.served[k] && sp.owed[k] < 4) sp.owed[k]++;
     } else {

@@ -200,3 +200,28 @@ def test_dropin_first_frame_served_from_readahead(spt, golden_scenes, monkeypatc
     off.close()
     assert np.array_equal(g2, want)
     assert st2["samples"] == W * H * spp and st2["batched_calls"] == tc * tc and st2["batches"] >= 1
+
+
+def test_late_call_is_served_without_another_frame(spt, golden_scenes):
+    """A RenderJob thread that starts after its frame's final wait (Renderer.hpp:242-255,
+    282-292) calls its tile after the next frame has begun: that frame's read-ahead serves
+    it, and the next frame's own call of the same tile is served as an owed tile -- two
+    read-ahead frames for the two frames, not three -- with the bytes of plain calls."""
+    W, H, spp, tc = 160, 96, 4, 2
+    ctx = make_ctx(spt, golden_scenes, W, H, spp, seed=9)
+    want = render_tiling(ctx, W, H, tc, False, 2)  # plain calls: arms the tiling
+    ctx.reset_stats()
+    a, b, c, d = tiles(W, H, tc)
+    g1 = np.zeros(W * H * 3, np.uint8)
+    g2 = np.zeros(W * H * 3, np.uint8)
+    for t in (a, b, c):  # frame 1 without its late tile d
+        ctx.render_segment(*t, g_data=g1, rgba=False)
+    ctx.render_segment(*a, g_data=g2, rgba=False)  # frame 2 begins
+    ctx.render_segment(*d, g_data=g1, rgba=False)  # frame 1's late call
+    for t in (b, c, d):
+        ctx.render_segment(*t, g_data=g2, rgba=False)
+    st = ctx.stats()
+    ctx.close()
+    assert np.array_equal(g1, want) and np.array_equal(g2, want)
+    parts = min(4, tc)
+    assert st["batches"] == 2 * parts and st["batched_calls"] == 2 * tc * tc, st

@@ -436,6 +436,7 @@ int spec_launch(spt_ctx *ctx, std::unique_lock<std::mutex> &lk, int mode, uint32
         if ((rc = launch_batch(ctx, bs, part, sp.h8_dev))) return rc;
         HIP_TRY(ctx, hipEventRecord(sp.ev[p], bs->stream));
         sp.launched[p] = true;
+        sp.finished[p] = false;
         ctx->batches++;
         ctx->batched_calls += part.size();
     }
@@ -521,17 +522,21 @@ int spec_serve(spt_ctx *ctx, std::unique_lock<std::mutex> &lk, int mode, uint32_
     sp.served[(size_t)k] = 1;
     const uint32_t part = (uint32_t)k / sp.tc / sp.rows_per_part;
     const hipEvent_t ev = sp.ev[part];
+    const bool finished = sp.finished[part];
     const uint8_t *const src = sp.h8;
     sp.readers++;
     lk.unlock();
     // rows y in [yB, yE) live at g_data rows H-1-y: one band, xB.. per row; the part's fold
-    // wrote them into the page-locked frame (its event completes after the kernel's writes)
+    // wrote them into the page-locked frame (its event completes after the kernel's writes;
+    // once one serve has seen it complete, the part's other serves skip the sync: 1 024
+    // serves per frame at tc = 32)
     const size_t pitch = (size_t)W * 3, off = (size_t)(H - yE) * pitch + (size_t)xB * 3;
-    const hipError_t e = hipEventSynchronize(ev);
+    const hipError_t e = finished ? hipSuccess : hipEventSynchronize(ev);
     if (e == hipSuccess)
         for (uint32_t r = 0; r < yE - yB; ++r)
             std::memcpy(g_data + off + r * pitch, src + off + r * pitch, (size_t)(xE - xB) * 3);
     lk.lock();
+    if (e == hipSuccess && sp.ev[part] == ev && sp.launched[part]) sp.finished[part] = true;
     if (--sp.readers == 0) sp.readers_cv.notify_all();
     if (e != hipSuccess) return fail(ctx, SPT_ERR_HIP, "read-ahead tile copy failed: %s", hipGetErrorString(e));
     return SPT_OK;

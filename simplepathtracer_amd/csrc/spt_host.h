@@ -117,6 +117,7 @@ struct SpecFrame {
     uint32_t parts = 4, rows_per_part = 1;  // tile rows per launch
     hipEvent_t ev[kParts] = {};
     bool launched[kParts] = {};
+    bool finished[kParts] = {};  // a serve saw the part's event complete (later serves skip the sync)
     BatchSet bs[kParts];
     // the frame's RGB8 bytes (g_data layout) in page-locked host memory: the parts' folds
     // write them through its device view, each serve copies its tile's rows on the host

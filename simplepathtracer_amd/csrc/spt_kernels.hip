@@ -345,7 +345,9 @@ __device__ __forceinline__ void decode_run(const FoldArgs &a, const uint32_t (&w
 #ifndef SPT_FOLD_RUN
 #define SPT_FOLD_RUN 8
 #endif
-static_assert(SPT_FOLD_RUN % 8 == 0, "fold runs are decoded eight words at a time");
+// words decoded together (their shading-table reads in flight at once)
+constexpr int kFoldDecode = SPT_FOLD_RUN < 8 ? SPT_FOLD_RUN : 8;
+static_assert(SPT_FOLD_RUN % kFoldDecode == 0, "fold runs are decoded kFoldDecode words at a time");
 
 // RenderSegmentTask's colorIndex aliasing (TaskBasedPathTracer.hpp:103,186,196-205) for
 // output index p of a W x H call: colors[p] collects every pixel (dx, dy) of the call with
@@ -443,7 +445,7 @@ __device__ __forceinline__ void fold_pixel(const FoldArgs &a, const uint32_t *sa
     if (a.mode == 0) {
         // RenderSegment: one word per slot, every sample counts.  Runs of kFoldRun words
         // are loaded before any is decoded (the loads of a run are in flight together),
-        // then decoded eight at a time
+        // then decoded kFoldDecode (8) at a time
         constexpr int kFoldRun = SPT_FOLD_RUN;
         uint32_t k = 0;
         for (; k + kFoldRun <= S; k += kFoldRun) {
@@ -451,14 +453,14 @@ __device__ __forceinline__ void fold_pixel(const FoldArgs &a, const uint32_t *sa
 #pragma unroll
             for (int i = 0; i < kFoldRun; ++i) w[i] = samples[q0 + (k + i) * step];
 #pragma unroll
-            for (int g = 0; g < kFoldRun; g += 8) {
-                uint32_t w8[8];
+            for (int g = 0; g < kFoldRun; g += kFoldDecode) {
+                uint32_t w8[kFoldDecode];
 #pragma unroll
-                for (int i = 0; i < 8; ++i) w8[i] = w[g + i];
-                f3 c[8];
-                decode_run<8>(a, w8, c);
+                for (int i = 0; i < kFoldDecode; ++i) w8[i] = w[g + i];
+                f3 c[kFoldDecode];
+                decode_run<kFoldDecode>(a, w8, c);
 #pragma unroll
-                for (int i = 0; i < 8; ++i) {
+                for (int i = 0; i < kFoldDecode; ++i) {
                     acc.x = acc.x + c[i].x;
                     acc.y = acc.y + c[i].y;
                     acc.z = acc.z + c[i].z;

@@ -482,6 +482,12 @@ int spec_serve(spt_ctx *ctx, std::unique_lock<std::mutex> &lk, int mode, uint32_
               batch_slot_bytes(ctx, mode, (uint64_t)w * h * tc * tc) <= ctx->ws_bytes &&
               (uint64_t)w * h * (tc * tc + tc) * ctx->spp < 0x7FFF0000ull))
             return kSpecMiss;
+        // the read-ahead frame's page-locked bytes (grown only once no serve copies out of the
+        // old ones): without them the call renders as usual
+        if (sp.h8_cap < (size_t)W * H * 3) {
+            sp.readers_cv.wait(lk, [&] { return sp.readers == 0; });
+            if (spec_frame_bytes(ctx, (size_t)W * H * 3) != SPT_OK) return kSpecMiss;
+        }
         if (!(sp.armed && sp.arm_mode == mode && sp.arm_tc == tc && sp.arm_w == W && sp.arm_h == H)) {
             // not armed: note the tile; the tiling arms once all its tiles have been called
             if (sp.arm_mode != mode || sp.arm_tc != tc || sp.arm_w != W || sp.arm_h != H) {

@@ -573,7 +573,7 @@ int spt_set_params_one(spt_ctx *ctx, uint32_t width, uint32_t height, uint32_t s
     // the drop-in (spt_prepare_dropin) renders its first frame through the tiling read-ahead:
     // its page-locked frame now, with the setup, not in that frame
     if (ctx->spec.arm_first && ctx->readahead)
-        if (int rc = spec_frame_bytes(ctx, (size_t)width * height * 3)) return rc;
+        (void)spec_frame_bytes(ctx, (size_t)width * height * 3);  // best effort: else at arming
     return rebuild_prim(ctx);
 }
 
